@@ -1,0 +1,229 @@
+#!/usr/bin/env python3
+"""Benchmark: GC-SLAM v2 per-scan hot path on MI355X (BASELINE.json metric: LiDAR scans/s at
+64k points x 256 hypotheses).
+
+One "step" = one synthetic 64k-point scan through the batched per-scan pipeline for all H
+hypotheses on this GPU (see DESIGN.md §Measurement for exactly which operators run inside
+the step). Inputs are resident in HBM before the timed region; the timed region is bracketed
+by a barrier + device synchronisation on both sides and the max over ranks is reported.
+
+Extra legs (outside the timed region, same process):
+  * roofline   — the contract decomposition BinSoftAssign + ScanBinMomentMatch over H
+                 hypotheses (responsibilities materialised), timed per kernel with HIP events
+                 on the library stream; achieved = algorithmic bytes / time.
+  * cpu_baseline — the CPU oracle (NumPy restatement) on a bounded sample of the same
+                 workload, rank 0 only, N=1 only.
+"""
+
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--hyps", type=int, default=256, help="total hypotheses per scan (strong scaling)")
+    ap.add_argument("--n-az", type=int, default=4096, help="azimuth steps (x16 rings = points)")
+    ap.add_argument("--scans", type=int, default=4, help="distinct resident scans cycled through")
+    ap.add_argument("--no-roofline", action="store_true")
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    return ap.parse_args()
+
+
+class Dist:
+    """Host-side barrier / max-over-ranks for the bench harness (gloo); product collectives
+    run in libgcslam over RCCL."""
+
+    def __init__(self, n):
+        self.world = int(os.environ.get("WORLD_SIZE", "1"))
+        self.rank = int(os.environ.get("RANK", "0"))
+        self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+        self.pg = None
+        if self.world > 1:
+            import torch.distributed as td
+            td.init_process_group("gloo")
+            self.td = td
+
+    def barrier(self):
+        if self.world > 1:
+            self.td.barrier()
+
+    def max(self, x: float) -> float:
+        if self.world == 1:
+            return x
+        import torch
+        t = torch.tensor([x], dtype=torch.float64)
+        self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
+        return float(t.item())
+
+
+def bytes_soft_assign(n, B):
+    return n * 24 + B * 24 + n * B * 8
+
+
+def bytes_moment_match(n, B):
+    return n * (24 + 72 + 8 + 8 + B * 8) + 24 + B * (1 + 3 + 9 + 3 + 9 + 1) * 8
+
+
+def main():
+    args = parse()
+    dist = Dist(args.gpus)
+    from gcslam import _abi
+    from gcslam.constants import GC_B_BINS, GC_TAU_SOFT_ASSIGN, T_BASE_LIDAR
+    from gcslam.ops.binning import create_fibonacci_atlas
+    from gcslam.synth import make_scan
+
+    ctx = _abi.Context(dist.local_rank)
+    H_total = args.hyps
+    h0 = (H_total * dist.rank) // dist.world
+    h1 = (H_total * (dist.rank + 1)) // dist.world
+    H = h1 - h0
+    B = GC_B_BINS
+    origin = np.asarray(T_BASE_LIDAR[:3])
+    bins = create_fibonacci_atlas(B).dirs
+    scans = [make_scan(k, n_az=args.n_az) for k in range(args.scans)]
+    n = scans[0]["points"].shape[0]
+    rng = np.random.default_rng(20261015 + 99)
+    xi_all = np.zeros((H_total, 6))
+    xi_all[:, 0] = 0.1 + rng.normal(0, 0.005, H_total)
+    xi_all[:, 5] = 0.03 + rng.normal(0, 0.002, H_total)
+    xi = xi_all[h0:h1]
+
+    # resident inputs
+    dscan = [{k: _abi.DeviceArray.from_host(ctx, s[k]) for k in ("points", "timestamps", "weights")} for s in scans]
+    dxi = _abi.DeviceArray.from_host(ctx, xi)
+    dbins = _abi.DeviceArray.from_host(ctx, bins)
+    dscal = _abi.DeviceArray(ctx, 8)
+    dstats = _abi.DeviceArray(ctx, (H, B, 38))
+    dcert = _abi.DeviceArray(ctx, (H, 8))
+    oa, op = _abi.f64p(origin)
+
+    def step(k):
+        s, d = scans[k % len(scans)], dscan[k % len(scans)]
+        _abi.call("gc_budget_stats", ctx.handle, d["weights"].ptr, n, n, dscal.ptr, ctx=ctx)
+        _abi.call("gc_scan_bins_fused", ctx.handle, H, n, n, B, d["points"].ptr, d["timestamps"].ptr,
+                  d["weights"].ptr, dscal.ptr, s["scan_start"], s["scan_end"], dxi.ptr, dbins.ptr,
+                  GC_TAU_SOFT_ASSIGN, op, 1e-12, 1e-12, dstats.ptr, dcert.ptr, ctx=ctx)
+
+    for k in range(args.warmup):
+        step(k)
+    ctx.sync()
+    dist.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        step(k)
+    ctx.sync()
+    dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = dist.max(t1 - t0)
+    scans_per_s = args.steps / elapsed
+
+    out = {
+        "metric": "LiDAR scans/sec (64k pts, 256 hypotheses) at 1/2/4/8 MI355X",
+        "value": scans_per_s,
+        "unit": "scans/s",
+        "n_gpus": dist.world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": "synthetic (VLP-16-like 16x%d ray-cast box room, SURVEY §8d)" % args.n_az,
+        "config": {"workload": "C3 front half: budget + per-hypothesis deskew + soft-assign + moment-match "
+                               "(fused) over all hypotheses; per-hypothesis twists synthetic",
+                   "points": n, "hypotheses": H_total, "bins": B, "parallelism": "hypotheses/%d" % dist.world},
+    }
+
+    if dist.rank == 0 and not args.no_roofline:
+        out["roofline"] = roofline_leg(ctx, _abi, scans[0], dscan[0], xi, dbins, B, n, H, origin)
+    if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_leg(scans[0], xi_all, bins, origin, n, H_total, args.cpu_budget_s)
+    if dist.rank == 0:
+        print(json.dumps(out), flush=True)
+
+
+def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=3):
+    """BinSoftAssign + ScanBinMomentMatch contract kernels over H hypotheses, HBM-bound."""
+    from gcslam.constants import GC_TAU_SOFT_ASSIGN
+    dxi = _abi.DeviceArray.from_host(ctx, xi)
+    pts = _abi.DeviceArray(ctx, (H, n, 3)); w = _abi.DeviceArray(ctx, (H, n)); sw = _abi.DeviceArray(ctx, H)
+    _abi.call("gc_deskew_constant_twist", ctx.handle, H, n, d["points"].ptr, d["timestamps"].ptr, d["weights"].ptr,
+              s["scan_start"], s["scan_end"], dxi.ptr, pts.ptr, w.ptr, sw.ptr, ctx=ctx)
+    dirs = _abi.DeviceArray(ctx, (H, n, 3))
+    oa, op = _abi.f64p(origin)
+    _abi.call("gc_point_directions", ctx.handle, H * n, pts.ptr, op, 1e-12, dirs.ptr, ctx=ctx)
+    resp = _abi.DeviceArray(ctx, (H, n, B)); idx = _abi.DeviceArray(ctx, (H, n), np.int32)
+    sac = _abi.DeviceArray(ctx, (H, 2))
+    covs = _abi.DeviceArray(ctx, (H, n, 9)); covs.zero()
+    lam = _abi.DeviceArray.from_host(ctx, np.ones((H, n)))
+    st = _abi.DeviceArray(ctx, (H, B, 38)); ce = _abi.DeviceArray(ctx, (H, 8))
+    ev = [_abi.Event(ctx) for _ in range(3)]
+    t_sa, t_mm = [], []
+    for r in range(reps + 1):
+        ev[0].record()
+        _abi.call("gc_bin_soft_assign", ctx.handle, H, n, B, dirs.ptr, dbins.ptr, GC_TAU_SOFT_ASSIGN, resp.ptr,
+                  idx.ptr, sac.ptr, ctx=ctx)
+        ev[1].record()
+        _abi.call("gc_scan_bin_moment_match", ctx.handle, H, n, B, pts.ptr, covs.ptr, w.ptr, resp.ptr, lam.ptr, op,
+                  1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
+        ev[2].record()
+        ctx.sync()
+        if r > 0:
+            t_sa.append(ev[0].elapsed_ms(ev[1]))
+            t_mm.append(ev[1].elapsed_ms(ev[2]))
+    ms_sa, ms_mm = float(np.mean(t_sa)), float(np.mean(t_mm))
+    b_sa, b_mm = H * bytes_soft_assign(n, B), H * bytes_moment_match(n, B)
+    ach = (b_sa + b_mm) / ((ms_sa + ms_mm) * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
+            "traffic": None,
+            "kernel": "BinSoftAssign+ScanBinMomentMatch (k_soft_assign + k_moment_partials/k_bins_finalize)",
+            "per_kernel": {"soft_assign": {"ms": ms_sa, "bytes": b_sa, "GB/s": b_sa / (ms_sa * 1e-3) / 1e9},
+                           "moment_match": {"ms": ms_mm, "bytes": b_mm, "GB/s": b_mm / (ms_mm * 1e-3) / 1e9}},
+            "hypotheses": H}
+
+
+def cpu_leg(s, xi_all, bins, origin, n, H_total, budget_s):
+    """Oracle front half on whole hypotheses until the time budget is spent; extrapolated."""
+    sys.path.insert(0, ROOT)
+    from threadpoolctl import threadpool_limits
+    from oracle import gc_oracle as O
+    with threadpool_limits(limits=1):
+        t0 = time.perf_counter()
+        done = 0
+        while done < H_total:
+            bud = O.point_budget_resample(s["points"], s["timestamps"], s["weights"], None, None, n)
+            p0, wd, _ = O.deskew_constant_twist(bud["points"], bud["timestamps"], bud["weights"],
+                                                s["scan_start"], s["scan_end"], xi_all[done])
+            sa = O.bin_soft_assign(O.point_directions(p0, origin), bins)
+            O.scan_bin_moment_match(p0, None, wd, sa["resp"], None, origin)
+            done += 1
+            if time.perf_counter() - t0 > budget_s:
+                break
+        dt = time.perf_counter() - t0
+    per_hyp = dt / done
+    return {"value": 1.0 / (per_hyp * H_total), "unit": "scans/s", "cores": 1, "kind": "port",
+            "sample": "%d of %d hypotheses of one %d-point scan through the oracle front half (NumPy, 1 thread), "
+                      "extrapolated; %s" % (done, H_total, n, os.environ.get("HOSTNAME", "")),
+            "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+
+
+if __name__ == "__main__":
+    main()

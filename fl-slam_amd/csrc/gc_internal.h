@@ -1,0 +1,44 @@
+// gc_internal.h — host-side internals shared by the libgcslam translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <string>
+#include "../../include/gcslam.h"
+
+struct gc_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::string err;
+  void* scratch = nullptr;  // growable device scratch (per ctx, stream-ordered use only)
+  size_t scratch_bytes = 0;
+};
+
+namespace gc {
+
+// thread-local fallback message for errors raised before a ctx exists
+void set_error(gc_ctx* ctx, const std::string& msg);
+
+// device scratch of at least `bytes` (synchronises the stream before growing)
+int scratch(gc_ctx* ctx, size_t bytes, void** out);
+
+}  // namespace gc
+
+#define GC_CHECK_ARG(ctx, cond, msg)                   \
+  do {                                                 \
+    if (!(cond)) {                                     \
+      gc::set_error((ctx), std::string("invalid argument: ") + (msg)); \
+      return GC_ERR_ARG;                               \
+    }                                                  \
+  } while (0)
+
+#define GC_HIP(ctx, expr)                                                              \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess) {                                                            \
+      gc::set_error((ctx), std::string("HIP error ") + hipGetErrorString(_e) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__) + " (" #expr ")"); \
+      return GC_ERR_RUNTIME;                                                           \
+    }                                                                                  \
+  } while (0)
+
+#define GC_LAUNCH_CHECK(ctx) GC_HIP(ctx, hipGetLastError())

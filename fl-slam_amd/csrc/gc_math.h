@@ -1,0 +1,416 @@
+// gc_math.h — register-resident f64 math for the GC-SLAM v2 kernels (gfx950).
+//
+// Lie maps restate fl_slam_poc/common/geometry/se3_jax.py (so3_exp :259-301, so3_log :304-366,
+// se3_V :137-174, _se3_V_inv :177-217, se3_exp :473-504, se3_log :220-256, se3_compose
+// :420-438); kappa restates backend/operators/kappa.py:130-169; the 3x3 symmetric eigen / SVD
+// replace jnp.linalg.eigh / svd on 3x3 blocks (matrix_fisher_evidence.py:199-233,
+// binning.py:183-189). Everything is branch-uniform per lane and allocation-free.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#define GC_DEV __device__ __forceinline__
+
+namespace gc {
+
+constexpr double kSmallAngle = 1e-7;
+constexpr double kNearPi = 1e-7;
+constexpr double kPi = 3.141592653589793238462643383279502884;
+constexpr double kF64Eps = 2.220446049250313e-16;
+
+GC_DEV double clampd(double x, double lo, double hi) { return fmin(fmax(x, lo), hi); }
+
+// jax.nn.sigmoid, evaluated without overflow.
+GC_DEV double sigmoid(double x) {
+  if (x >= 0.0) return 1.0 / (1.0 + exp(-x));
+  double e = exp(x);
+  return e / (1.0 + e);
+}
+
+// jax.nn.softplus = log1p(exp(-|x|)) + max(x, 0)
+GC_DEV double softplus(double x) { return log1p(exp(-fabs(x))) + fmax(x, 0.0); }
+
+// ---------------------------------------------------------------- 3-vectors / 3x3 (row-major)
+GC_DEV void mat3_mul(const double* A, const double* B, double* C) {
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+}
+GC_DEV void mat3_mul_tn(const double* A, const double* B, double* C) {  // Aᵀ B
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      C[3 * i + j] = A[i] * B[j] + A[3 + i] * B[3 + j] + A[6 + i] * B[6 + j];
+}
+GC_DEV void mat3_mul_nt(const double* A, const double* B, double* C) {  // A Bᵀ
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      C[3 * i + j] = A[3 * i] * B[3 * j] + A[3 * i + 1] * B[3 * j + 1] + A[3 * i + 2] * B[3 * j + 2];
+}
+GC_DEV void mat3_vec(const double* A, const double* x, double* y) {
+  for (int i = 0; i < 3; ++i) y[i] = A[3 * i] * x[0] + A[3 * i + 1] * x[1] + A[3 * i + 2] * x[2];
+}
+GC_DEV void mat3_tvec(const double* A, const double* x, double* y) {  // Aᵀ x
+  for (int i = 0; i < 3; ++i) y[i] = A[i] * x[0] + A[3 + i] * x[1] + A[6 + i] * x[2];
+}
+GC_DEV void cross3(const double* a, const double* b, double* c) {
+  c[0] = a[1] * b[2] - a[2] * b[1];
+  c[1] = a[2] * b[0] - a[0] * b[2];
+  c[2] = a[0] * b[1] - a[1] * b[0];
+}
+GC_DEV double dot3(const double* a, const double* b) { return a[0] * b[0] + a[1] * b[1] + a[2] * b[2]; }
+GC_DEV double norm3(const double* a) { return sqrt(dot3(a, a)); }
+GC_DEV double det3(const double* A) {
+  return A[0] * (A[4] * A[8] - A[5] * A[7]) - A[1] * (A[3] * A[8] - A[5] * A[6]) +
+         A[2] * (A[3] * A[7] - A[4] * A[6]);
+}
+
+// I + a K + b K², K = [w]×  (the Rodrigues / V form shared by so3_exp and se3_V)
+GC_DEV void rodrigues_form(const double* w, double a, double b, double* R) {
+  const double x = w[0], y = w[1], z = w[2];
+  const double xx = x * x, yy = y * y, zz = z * z;
+  // K² = w wᵀ - |w|² I
+  R[0] = 1.0 + b * (-(yy + zz));
+  R[4] = 1.0 + b * (-(xx + zz));
+  R[8] = 1.0 + b * (-(xx + yy));
+  R[1] = -a * z + b * (x * y);
+  R[3] = a * z + b * (x * y);
+  R[2] = a * y + b * (x * z);
+  R[6] = -a * y + b * (x * z);
+  R[5] = -a * x + b * (y * z);
+  R[7] = a * x + b * (y * z);
+}
+
+// se3_jax.py:259-301
+GC_DEV void so3_exp(const double* w, double* R) {
+  const double ts = dot3(w, w);
+  const double th = sqrt(ts);
+  double a, b;
+  if (th < kSmallAngle) {
+    a = 1.0;
+    b = 0.5;
+  } else {
+    double s, c;
+    sincos(th, &s, &c);
+    const double sts = (ts < kSmallAngle * kSmallAngle) ? 1.0 : ts;
+    a = s / th;
+    b = (1.0 - c) / sts;
+  }
+  rodrigues_form(w, a, b, R);
+}
+
+// B=(1-cos)/θ², C=(θ-sin)/θ³ with the θ<1e-7 Taylor branch (se3_jax.py:137-174)
+GC_DEV void se3_BC(double ts, double* B, double* C) {
+  const double th = sqrt(ts);
+  if (th < kSmallAngle) {
+    *B = 0.5 - ts / 24.0;
+    *C = 1.0 / 6.0 - ts / 120.0;
+  } else {
+    double s, c;
+    sincos(th, &s, &c);
+    const double sts = (ts < kSmallAngle * kSmallAngle) ? 1.0 : ts;
+    *B = (1.0 - c) / sts;
+    *C = (th - s) / (sts * th);
+  }
+}
+
+// se3_jax.py:473-504 : out = [V(φ)ρ, φ]
+GC_DEV void se3_exp(const double* xi, double* out) {
+  const double* phi = xi + 3;
+  double B, C, V[9];
+  se3_BC(dot3(phi, phi), &B, &C);
+  rodrigues_form(phi, B, C, V);
+  mat3_vec(V, xi, out);
+  out[3] = phi[0];
+  out[4] = phi[1];
+  out[5] = phi[2];
+}
+
+// se3_jax.py:304-366 (incl. the softmax-mixed near-π axis)
+GC_DEV void so3_log(const double* R, double* w) {
+  const double c = clampd(0.5 * ((R[0] + R[4] + R[8]) - 1.0), -1.0, 1.0);
+  const double th = acos(c);
+  const double v0 = 0.5 * (R[7] - R[5]), v1 = 0.5 * (R[2] - R[6]), v2 = 0.5 * (R[3] - R[1]);
+  if (th < kSmallAngle) {
+    w[0] = v0; w[1] = v1; w[2] = v2;
+    return;
+  }
+  if (fabs(th - kPi) < kNearPi) {
+    const double z0 = 50.0 * (R[0] + 1.0), z1 = 50.0 * (R[4] + 1.0), z2 = 50.0 * (R[8] + 1.0);
+    const double zm = fmax(z0, fmax(z1, z2));
+    double e0 = exp(z0 - zm), e1 = exp(z1 - zm), e2 = exp(z2 - zm);
+    const double es = e0 + e1 + e2;
+    e0 /= es; e1 /= es; e2 /= es;
+    double ax[3];
+    for (int i = 0; i < 3; ++i)
+      ax[i] = e0 * (R[3 * i] + (i == 0)) + e1 * (R[3 * i + 1] + (i == 1)) + e2 * (R[3 * i + 2] + (i == 2));
+    double n = norm3(ax);
+    n = (n < kSmallAngle) ? 1.0 : n;
+    for (int i = 0; i < 3; ++i) w[i] = ax[i] / n * th;
+    return;
+  }
+  double s = sin(th);
+  s = (fabs(s) < kSmallAngle) ? 1.0 : s;
+  const double k = th / (2.0 * s);
+  w[0] = k * (2.0 * v0); w[1] = k * (2.0 * v1); w[2] = k * (2.0 * v2);
+}
+
+// se3_jax.py:177-217
+GC_DEV void se3_V_inv(const double* phi, double* Vi) {
+  const double ts = dot3(phi, phi);
+  const double th = sqrt(ts);
+  double D;
+  if (th < kSmallAngle) {
+    D = 1.0 / 12.0 + ts / 720.0;
+  } else {
+    double s, c;
+    sincos(th, &s, &c);
+    const double sts = (ts < kSmallAngle * kSmallAngle) ? 1.0 : ts;
+    D = 1.0 / sts - (1.0 + c) / (2.0 * th * s + 1e-12);
+  }
+  rodrigues_form(phi, -0.5, D, Vi);
+}
+
+// se3_jax.py:220-256
+GC_DEV void se3_log(const double* T, double* xi) {
+  double R[9], phi[3], Vi[9];
+  so3_exp(T + 3, R);
+  so3_log(R, phi);
+  se3_V_inv(phi, Vi);
+  mat3_vec(Vi, T, xi);
+  xi[3] = phi[0]; xi[4] = phi[1]; xi[5] = phi[2];
+}
+
+// se3_jax.py:420-438
+GC_DEV void se3_compose(const double* a, const double* b, double* out) {
+  double Ra[9], Rb[9], Rab[9], t[3];
+  so3_exp(a + 3, Ra);
+  so3_exp(b + 3, Rb);
+  mat3_vec(Ra, b, t);
+  mat3_mul(Ra, Rb, Rab);
+  double o[6];
+  o[0] = a[0] + t[0]; o[1] = a[1] + t[1]; o[2] = a[2] + t[2];
+  so3_log(Rab, o + 3);
+  for (int i = 0; i < 6; ++i) out[i] = o[i];
+}
+
+// kappa.py:130-169
+GC_DEV double kappa_blend(double R, double eps_r, double d, double r0, double tau) {
+  const double Rc = clampd(R, 0.0, 1.0 - eps_r);
+  const double R2 = Rc * Rc;
+  const double k_low = (Rc * (d - R2)) / (1.0 - R2 + eps_r);
+  const double k_high = -log(fmax(1.0 - R2, eps_r));
+  const double s = sigmoid((Rc - r0) / fmax(tau, 1e-6));
+  return (1.0 - s) * k_low + s * k_high;
+}
+
+// ------------------------------------------------------- symmetric 3x3 eigen (cyclic Jacobi)
+// A (row-major, symmetrised by caller) -> w[3] unsorted, V columns = eigenvectors.
+GC_DEV void jacobi_rot3(double* A, double* V, int p, int q) {
+  const double apq = A[3 * p + q];
+  const double app = A[3 * p + p], aqq = A[3 * q + q];
+  if (apq == 0.0 || fabs(apq) <= 1e-300) return;
+  if (fabs(apq) <= 1e-18 * sqrt(fabs(app * aqq))) {
+    A[3 * p + q] = 0.0; A[3 * q + p] = 0.0;
+    return;
+  }
+  const double th = (aqq - app) / (2.0 * apq);
+  const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+  const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+  for (int k = 0; k < 3; ++k) {  // columns: A G
+    const double akp = A[3 * k + p], akq = A[3 * k + q];
+    A[3 * k + p] = c * akp - s * akq;
+    A[3 * k + q] = s * akp + c * akq;
+  }
+  for (int k = 0; k < 3; ++k) {  // rows: Gᵀ A
+    const double apk = A[3 * p + k], aqk = A[3 * q + k];
+    A[3 * p + k] = c * apk - s * aqk;
+    A[3 * q + k] = s * apk + c * aqk;
+  }
+  A[3 * p + q] = 0.0; A[3 * q + p] = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    const double vkp = V[3 * k + p], vkq = V[3 * k + q];
+    V[3 * k + p] = c * vkp - s * vkq;
+    V[3 * k + q] = s * vkp + c * vkq;
+  }
+}
+
+GC_DEV void eigh3(const double* Ain, double* w, double* V) {
+  double A[9];
+  for (int i = 0; i < 9; ++i) A[i] = Ain[i];
+  for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 12; ++sweep) {
+    const double off = A[1] * A[1] + A[2] * A[2] + A[5] * A[5];
+    const double dg = A[0] * A[0] + A[4] * A[4] + A[8] * A[8];
+    if (off <= 1e-36 * dg || off == 0.0) break;
+    jacobi_rot3(A, V, 0, 1);
+    jacobi_rot3(A, V, 0, 2);
+    jacobi_rot3(A, V, 1, 2);
+  }
+  w[0] = A[0]; w[1] = A[4]; w[2] = A[8];
+}
+
+// domain_projection_psd_core on a 3x3 (primitives.py:80-123). cert = [proj, sym, min, max, cond, nnc]
+GC_DEV void psd_project3(const double* M, double eps, double* Mp, double* cert) {
+  double S[9];
+  double symd = 0.0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      S[3 * i + j] = 0.5 * (M[3 * i + j] + M[3 * j + i]);
+      const double d = S[3 * i + j] - M[3 * i + j];
+      symd += d * d;
+    }
+  double w[3], V[9];
+  eigh3(S, w, V);
+  double proj = 0.0, mn = 1e308, mx = -1e308, nnc = 0.0;
+  for (int k = 0; k < 3; ++k) {
+    w[k] = fmax(w[k], eps);
+    mn = fmin(mn, w[k]);
+    mx = fmax(mx, w[k]);
+    nnc += (w[k] < 10.0 * eps) ? 1.0 : 0.0;
+  }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      const double v = V[3 * i] * w[0] * V[3 * j] + V[3 * i + 1] * w[1] * V[3 * j + 1] +
+                       V[3 * i + 2] * w[2] * V[3 * j + 2];
+      Mp[3 * i + j] = v;
+      const double d = v - S[3 * i + j];
+      proj += d * d;
+    }
+  if (cert) {
+    cert[0] = sqrt(proj); cert[1] = sqrt(symd); cert[2] = mn; cert[3] = mx; cert[4] = mx / mn; cert[5] = nnc;
+  }
+}
+
+// Sorted (descending) eigenvalues of a symmetric 3x3.
+GC_DEV void eigvalsh3_desc(const double* M, double* lam) {
+  double V[9], w[3];
+  eigh3(M, w, V);
+  double a = w[0], b = w[1], c = w[2], t;
+  if (a < b) { t = a; a = b; b = t; }
+  if (b < c) { t = b; b = c; c = t; }
+  if (a < b) { t = a; a = b; b = t; }
+  lam[0] = a; lam[1] = b; lam[2] = c;
+}
+
+// ------------------------------------------------------------- 3x3 SVD (one-sided Jacobi)
+// H = U diag(s) Vᵀ, s descending (LAPACK gesdd convention). Degenerate columns of U are
+// completed to an orthonormal, right-handed-agnostic basis (H = 0 gives U = V = I).
+GC_DEV void svd3(const double* Hin, double* U, double* s, double* V) {
+  double A[9];
+  for (int i = 0; i < 9; ++i) A[i] = Hin[i];
+  for (int i = 0; i < 9; ++i) V[i] = (i % 4 == 0) ? 1.0 : 0.0;
+  for (int sweep = 0; sweep < 16; ++sweep) {
+    double rot = 0.0;
+    for (int pq = 0; pq < 3; ++pq) {
+      const int p = (pq == 2) ? 1 : 0, q = (pq == 0) ? 1 : 2;
+      double alpha = 0.0, beta = 0.0, gamma = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        alpha += A[3 * k + p] * A[3 * k + p];
+        beta += A[3 * k + q] * A[3 * k + q];
+        gamma += A[3 * k + p] * A[3 * k + q];
+      }
+      if (gamma == 0.0 || fabs(gamma) <= 1e-17 * sqrt(alpha * beta)) continue;
+      rot += 1.0;
+      const double zeta = (beta - alpha) / (2.0 * gamma);
+      const double t = (zeta >= 0.0 ? 1.0 : -1.0) / (fabs(zeta) + sqrt(1.0 + zeta * zeta));
+      const double c = 1.0 / sqrt(1.0 + t * t), sn = c * t;
+      for (int k = 0; k < 3; ++k) {
+        const double ap = A[3 * k + p], aq = A[3 * k + q];
+        A[3 * k + p] = c * ap - sn * aq;
+        A[3 * k + q] = sn * ap + c * aq;
+        const double vp = V[3 * k + p], vq = V[3 * k + q];
+        V[3 * k + p] = c * vp - sn * vq;
+        V[3 * k + q] = sn * vp + c * vq;
+      }
+    }
+    if (rot == 0.0) break;
+  }
+  double sv[3];
+  for (int j = 0; j < 3; ++j) sv[j] = sqrt(A[j] * A[j] + A[3 + j] * A[3 + j] + A[6 + j] * A[6 + j]);
+  // sort columns by descending singular value
+  int ord[3] = {0, 1, 2};
+  for (int i = 0; i < 2; ++i)
+    for (int j = 0; j < 2 - i; ++j)
+      if (sv[ord[j]] < sv[ord[j + 1]]) { int t = ord[j]; ord[j] = ord[j + 1]; ord[j + 1] = t; }
+  double Vs[9], As[9];
+  for (int j = 0; j < 3; ++j) {
+    s[j] = sv[ord[j]];
+    for (int k = 0; k < 3; ++k) { Vs[3 * k + j] = V[3 * k + ord[j]]; As[3 * k + j] = A[3 * k + ord[j]]; }
+  }
+  for (int i = 0; i < 9; ++i) V[i] = Vs[i];
+  // U columns = A_j / s_j, Gram-Schmidt completion for (near-)zero singular values
+  const double tol = 1e-14 * fmax(s[0], 1e-300);
+  for (int j = 0; j < 3; ++j) {
+    double u[3] = {As[j], As[3 + j], As[6 + j]};
+    if (s[j] > tol && s[j] > 0.0) {
+      for (int k = 0; k < 3; ++k) u[k] /= s[j];
+    } else {
+      // pick the unit axis least aligned with previous columns
+      double best = -1.0; int bi = j;
+      for (int ax = 0; ax < 3; ++ax) {
+        double e[3] = {0.0, 0.0, 0.0}; e[ax] = 1.0;
+        for (int pj = 0; pj < j; ++pj) {
+          const double d = U[ax * 3 + pj];
+          for (int k = 0; k < 3; ++k) e[k] -= d * U[3 * k + pj];
+        }
+        const double n = norm3(e);
+        if (n > best + 1e-12) { best = n; bi = ax; }
+      }
+      double e[3] = {0.0, 0.0, 0.0}; e[bi] = 1.0;
+      if (j == 0) { u[0] = e[0]; u[1] = e[1]; u[2] = e[2]; }
+      else {
+        for (int pj = 0; pj < j; ++pj) {
+          const double d = U[bi * 3 + pj];
+          for (int k = 0; k < 3; ++k) e[k] -= d * U[3 * k + pj];
+        }
+        const double n = norm3(e);
+        for (int k = 0; k < 3; ++k) u[k] = e[k] / n;
+      }
+    }
+    for (int k = 0; k < 3; ++k) U[3 * k + j] = u[k];
+  }
+}
+
+// LU with partial pivoting 3x3 inverse (jnp.linalg.inv semantics).
+GC_DEV void inv3(const double* Ain, double* X) {
+  double A[9];
+  int piv[3] = {0, 1, 2};
+  for (int i = 0; i < 9; ++i) A[i] = Ain[i];
+  for (int k = 0; k < 3; ++k) {
+    int p = k;
+    double m = fabs(A[3 * k + k]);
+    for (int i = k + 1; i < 3; ++i)
+      if (fabs(A[3 * i + k]) > m) { m = fabs(A[3 * i + k]); p = i; }
+    if (p != k) {
+      for (int j = 0; j < 3; ++j) { double t = A[3 * k + j]; A[3 * k + j] = A[3 * p + j]; A[3 * p + j] = t; }
+      int t = piv[k]; piv[k] = piv[p]; piv[p] = t;
+    }
+    for (int i = k + 1; i < 3; ++i) {
+      A[3 * i + k] /= A[3 * k + k];
+      for (int j = k + 1; j < 3; ++j) A[3 * i + j] -= A[3 * i + k] * A[3 * k + j];
+    }
+  }
+  for (int c = 0; c < 3; ++c) {
+    double y[3];
+    for (int i = 0; i < 3; ++i) {
+      double v = (piv[i] == c) ? 1.0 : 0.0;
+      for (int j = 0; j < i; ++j) v -= A[3 * i + j] * y[j];
+      y[i] = v;
+    }
+    for (int i = 2; i >= 0; --i) {
+      double v = y[i];
+      for (int j = i + 1; j < 3; ++j) v -= A[3 * i + j] * X[3 * j + c];
+      X[3 * i + c] = v / A[3 * i + i];
+    }
+  }
+}
+
+// Solve A x = b (3x3, partial pivoting) — jnp.linalg.solve semantics.
+GC_DEV void solve3(const double* A, const double* b, double* x) {
+  double Ai[9];
+  inv3(A, Ai);
+  mat3_vec(Ai, b, x);
+}
+
+}  // namespace gc

@@ -1,0 +1,842 @@
+// gc_points.hip — per-point / per-bin kernels of the GC-SLAM v2 hot path (gfx950).
+//
+//  a1 PointBudgetResample   backend/operators/point_budget.py:50-221
+//  a4 DeskewConstantTwist   backend/operators/deskew_constant_twist.py:31-117 (+ pipeline.py:589-593)
+//  a5 BinSoftAssign         archive/legacy_operators/binning.py:56-131
+//  a6 ScanBinMomentMatch    archive/legacy_operators/binning.py:139-324, kappa.py:130-169
+//
+// Layout / mapping: a wave processes 4 points per step; its 64 lanes
+// are 4 point-groups x 16 bin-lanes, bin-lane l owns bins {l, l+16, l+32, ...}. Per-point
+// softmax sums are 16-lane butterflies; per-bin moment accumulators live in VGPRs for the
+// whole chunk and are reduced across groups/waves once, in a fixed order, into one partial
+// record per (hypothesis, chunk). A finalize kernel sums the records in chunk order, so every
+// result is bit-reproducible run to run (no float atomics anywhere).
+#include <hip/hip_runtime.h>
+#include <algorithm>
+#include "gc_internal.h"
+#include "gc_wgla.h"
+
+namespace gc {
+
+constexpr int NF_BASE = 19;   // [1, d(3), dd(6: 00 01 02 11 12 22), p(3), pp(6)] x w
+constexpr int NF_COV = 9;     // full 3x3 point covariance x w
+constexpr int REC_EXTRA = 4;  // [entropy_sum, max_resp, sum_w, n_points]
+
+GC_DEV double group16_sum(double v) {
+  v += __shfl_xor(v, 8, 16);
+  v += __shfl_xor(v, 4, 16);
+  v += __shfl_xor(v, 2, 16);
+  v += __shfl_xor(v, 1, 16);
+  return v;
+}
+GC_DEV double group16_max(double v) {
+  v = fmax(v, __shfl_xor(v, 8, 16));
+  v = fmax(v, __shfl_xor(v, 4, 16));
+  v = fmax(v, __shfl_xor(v, 2, 16));
+  v = fmax(v, __shfl_xor(v, 1, 16));
+  return v;
+}
+
+GC_DEV void lds_wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Un-fused similarity: the bin-index integer contract (argmax of exactly this f64 expression).
+GC_DEV double sim_nofma(double d0, double d1, double d2, double b0, double b1, double b2) {
+#pragma clang fp contract(off)
+  double s = d0 * b0 + d1 * b1;
+  s = s + d2 * b2;
+  return s;
+}
+
+// p0 = Exp(α ξ)^{-1} p  (deskew_constant_twist.py:50-58: se3_exp then so3_exp of the rotvec)
+GC_DEV void deskew_point(const double* p, double alpha, const double* xi, double* out) {
+  const double rho[3] = {alpha * xi[0], alpha * xi[1], alpha * xi[2]};
+  const double phi[3] = {alpha * xi[3], alpha * xi[4], alpha * xi[5]};
+  const double ts = dot3(phi, phi);
+  const double th = sqrt(ts);
+  double Bv, Cv, a, b;
+  if (th < kSmallAngle) {
+    Bv = 0.5 - ts / 24.0;
+    Cv = 1.0 / 6.0 - ts / 120.0;
+    a = 1.0;
+    b = 0.5;
+  } else {
+    double s, c;
+    sincos(th, &s, &c);
+    const double sts = (ts < kSmallAngle * kSmallAngle) ? 1.0 : ts;
+    Bv = (1.0 - c) / sts;
+    Cv = (th - s) / (sts * th);
+    a = s / th;
+    b = Bv;
+  }
+  double V[9], R[9], t[3], q[3];
+  rodrigues_form(phi, Bv, Cv, V);
+  mat3_vec(V, rho, t);
+  rodrigues_form(phi, a, b, R);
+  q[0] = p[0] - t[0]; q[1] = p[1] - t[1]; q[2] = p[2] - t[2];
+  mat3_tvec(R, q, out);
+}
+
+// smooth_window_weights (imu_preintegration.py:19-43)
+GC_DEV double window_weight(double t, double t0, double t1, double sigma) {
+  const double sig = fmax(sigma, 1e-6);
+  const double wr = sigmoid((t - t0) / sig) * sigmoid((t1 - t) / sig);
+  return wr * (1.0 - 1e-12) + 1e-12;
+}
+
+// Features g (pre-multiplied by w) for the moment sums of binning.py:160-173.
+GC_DEV void point_features(const double* p, const double* d, double w, double* f) {
+  f[0] = w;
+  f[1] = w * d[0]; f[2] = w * d[1]; f[3] = w * d[2];
+  f[4] = w * (d[0] * d[0]); f[5] = w * (d[0] * d[1]); f[6] = w * (d[0] * d[2]);
+  f[7] = w * (d[1] * d[1]); f[8] = w * (d[1] * d[2]); f[9] = w * (d[2] * d[2]);
+  f[10] = w * p[0]; f[11] = w * p[1]; f[12] = w * p[2];
+  f[13] = w * (p[0] * p[0]); f[14] = w * (p[0] * p[1]); f[15] = w * (p[0] * p[2]);
+  f[16] = w * (p[1] * p[1]); f[17] = w * (p[1] * p[2]); f[18] = w * (p[2] * p[2]);
+}
+
+GC_DEV void direction(const double* p, const double* o, double eps, double* d) {
+  const double r0 = p[0] - o[0], r1 = p[1] - o[1], r2 = p[2] - o[2];
+  const double den = sqrt(r0 * r0 + r1 * r1 + r2 * r2) + eps;
+  d[0] = r0 / den; d[1] = r1 / den; d[2] = r2 / den;
+}
+
+// =============================================================================== a1 budget
+__global__ void __launch_bounds__(256) k_budget_stats(const double* __restrict__ w, int64_t n_in,
+                                                      int64_t n_cap, int64_t stride, double* out) {
+  __shared__ double red[4];
+  const int64_t n_sel = (n_in + stride - 1) / stride;
+  double loc_in = 0.0, loc_sel = 0.0;
+  for (int64_t i = threadIdx.x; i < n_in; i += kWG) loc_in += w[i];
+  for (int64_t j = threadIdx.x; j < n_sel; j += kWG) loc_sel += w[j * stride];
+  const double mass_in = wg_sum(loc_in, red);
+  const double mass_sel = wg_sum(loc_sel, red);
+  const double scale = mass_in / (mass_sel + 1e-12);
+  double loc_ess = 0.0, loc_out = 0.0;
+  for (int64_t j = threadIdx.x; j < n_cap; j += kWG) {
+    const double wo = (j < n_sel) ? w[j * stride] * scale : 0.0;
+    const double wn = wo / (mass_in + 1e-12);
+    loc_ess += wn * wn + 1e-12;
+    loc_out += wo;
+  }
+  const double s_ess = wg_sum(loc_ess, red);
+  const double s_out = wg_sum(loc_out, red);
+  if (threadIdx.x == 0) {
+    out[0] = mass_in;
+    out[1] = mass_sel;
+    out[2] = scale;
+    out[3] = 1.0 / s_ess;
+    out[4] = s_out;
+    out[5] = (double)n_sel;
+    out[6] = (double)stride;
+    out[7] = fmin(1.0, (double)n_cap / ((double)n_in + 1e-12));
+  }
+}
+
+__global__ void k_budget_gather(const double* __restrict__ pts, const double* __restrict__ t,
+                                const double* __restrict__ w, const uint8_t* __restrict__ ring,
+                                const uint8_t* __restrict__ tag, int64_t n_in, int64_t n_cap,
+                                int64_t stride, const double* __restrict__ scal, double* pts_o,
+                                double* t_o, double* w_o, uint8_t* ring_o, uint8_t* tag_o,
+                                int64_t* idx_o) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n_cap) return;
+  const int64_t n_sel = (n_in + stride - 1) / stride;
+  const bool sel = j < n_sel;
+  const int64_t i = j * stride;
+  pts_o[3 * j + 0] = sel ? pts[3 * i + 0] : 0.0;
+  pts_o[3 * j + 1] = sel ? pts[3 * i + 1] : 0.0;
+  pts_o[3 * j + 2] = sel ? pts[3 * i + 2] : 0.0;
+  t_o[j] = sel ? t[i] : 0.0;
+  w_o[j] = sel ? w[i] * scal[2] : 0.0;
+  if (ring_o) ring_o[j] = (sel && ring) ? ring[i] : 0;
+  if (tag_o) tag_o[j] = (sel && tag) ? tag[i] : 0;
+  if (idx_o) idx_o[j] = sel ? i : -1;
+}
+
+// ============================================================================== a4 deskew
+__global__ void __launch_bounds__(256) k_deskew(int64_t n, const double* __restrict__ pts,
+                                                const double* __restrict__ t,
+                                                const double* __restrict__ w, double t0, double t1,
+                                                const double* __restrict__ xi, double* pts_o,
+                                                double* w_o, double* partial) {
+  __shared__ double red[4];
+  const int h = blockIdx.y;
+  const int64_t j = (int64_t)blockIdx.x * kWG + threadIdx.x;
+  double xr[6];
+  for (int k = 0; k < 6; ++k) xr[k] = xi[6 * h + k];
+  const double denom = fmax(t1 - t0, 1e-12);
+  double wo = 0.0;
+  if (j < n) {
+    const double p[3] = {pts[3 * j], pts[3 * j + 1], pts[3 * j + 2]};
+    const double alpha = (t[j] - t0) / denom;
+    double q[3];
+    deskew_point(p, alpha, xr, q);
+    wo = w[j] * window_weight(t[j], t0, t1, 0.1 * denom);
+    const int64_t o = (int64_t)h * n + j;
+    pts_o[3 * o] = q[0]; pts_o[3 * o + 1] = q[1]; pts_o[3 * o + 2] = q[2];
+    w_o[o] = wo;
+  }
+  const double s = wg_sum(wo, red);
+  if (threadIdx.x == 0) partial[(int64_t)h * gridDim.x + blockIdx.x] = s;
+}
+
+// out[h] = Σ_c partial[h][c] (fixed order)
+__global__ void k_sum_rows(const double* __restrict__ partial, int64_t cols, int rows, double* out) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= rows) return;
+  double s = 0.0;
+  for (int64_t c = 0; c < cols; ++c) s += partial[(int64_t)h * cols + c];
+  out[h] = s;
+}
+
+__global__ void k_point_dirs(int64_t rows, const double* __restrict__ pts, double o0, double o1,
+                             double o2, double eps, double* dirs) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= rows) return;
+  const double p[3] = {pts[3 * j], pts[3 * j + 1], pts[3 * j + 2]};
+  const double o[3] = {o0, o1, o2};
+  double d[3];
+  direction(p, o, eps, d);
+  dirs[3 * j] = d[0]; dirs[3 * j + 1] = d[1]; dirs[3 * j + 2] = d[2];
+}
+
+// ============================================================================ a5 soft assign
+// grid (ceil(n/256), H); each wave: 16 steps x 4 points. Writes resp rows coalesced
+// (16 bin-lanes x 8 B = 128 B per point and bin-slot).
+template <int BPL>
+__global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, const double* __restrict__ dirs,
+                                                     const double* __restrict__ bins, double inv_tau,
+                                                     double* resp, int32_t* bin_idx, double* partial) {
+  __shared__ double red[8];
+  const int h = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, bl = lane & 15;
+  double bx[BPL], by[BPL], bz[BPL];
+  bool bv[BPL];
+#pragma unroll
+  for (int j = 0; j < BPL; ++j) {
+    const int b = bl + 16 * j;
+    bv[j] = b < B;
+    bx[j] = bv[j] ? bins[3 * b] : 0.0;
+    by[j] = bv[j] ? bins[3 * b + 1] : 0.0;
+    bz[j] = bv[j] ? bins[3 * b + 2] : 0.0;
+  }
+  const double Beps = (double)B * 1e-12;
+  double ent = 0.0, mxr = 0.0;
+  const int64_t base = (int64_t)blockIdx.x * 256 + wv * 64;
+  for (int s = 0; s < 16; ++s) {
+    const int64_t pt = base + s * 4 + g;
+    const bool valid = pt < n;
+    const int64_t row = (int64_t)h * n + (valid ? pt : 0);
+    const double d0 = dirs[3 * row], d1 = dirs[3 * row + 1], d2 = dirs[3 * row + 2];
+    double S[BPL];
+    double best = -1e308;
+    int bidx = 0x7fffffff;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+      S[j] = sim_nofma(d0, d1, d2, bx[j], by[j], bz[j]);
+      if (bv[j] && S[j] > best) { best = S[j]; bidx = bl + 16 * j; }
+    }
+    // argmax across the 16 bin-lanes (lowest index on ties)
+    for (int off = 8; off >= 1; off >>= 1) {
+      const double ob = __shfl_xor(best, off, 16);
+      const int oi = __shfl_xor(bidx, off, 16);
+      if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+    }
+    const double m = best * inv_tau;
+    double e[BPL], zl = 0.0, sl = 0.0;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+      const double x = S[j] * inv_tau - m;
+      e[j] = bv[j] ? exp(x) : 0.0;
+      zl += e[j];
+      sl += e[j] * x;
+    }
+    const double Z = group16_sum(zl);
+    const double Sx = group16_sum(sl);
+    const double rZ = 1.0 / Z;
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+      const double r = e[j] * rZ;
+      if (valid && bv[j]) {
+        resp[row * B + bl + 16 * j] = r;
+        mxr = fmax(mxr, r);
+      }
+    }
+    if (valid && bl == 0) {
+      ent += (log(Z) - Sx * rZ) - Beps;  // -Σ R log(R+ε) up to ≤ B·ε
+      if (bin_idx) bin_idx[row] = bidx;
+    }
+  }
+  const double es = wg_sum(ent, red);
+  const double ms = wg_max(mxr, red);
+  if (threadIdx.x == 0) {
+    partial[((int64_t)h * gridDim.x + blockIdx.x) * 2] = es;
+    partial[((int64_t)h * gridDim.x + blockIdx.x) * 2 + 1] = ms;
+  }
+}
+
+__global__ void k_soft_assign_finalize(const double* __restrict__ partial, int64_t cols, int H,
+                                       int64_t n, double* cert) {
+  const int h = blockIdx.x * blockDim.x + threadIdx.x;
+  if (h >= H) return;
+  double e = 0.0, m = 0.0;
+  for (int64_t c = 0; c < cols; ++c) {
+    e += partial[((int64_t)h * cols + c) * 2];
+    m = fmax(m, partial[((int64_t)h * cols + c) * 2 + 1]);
+  }
+  cert[2 * h] = e / ((double)n + 1e-12);
+  cert[2 * h + 1] = m;
+}
+
+// ===================================================================== a6 moment partials
+// Shared epilogue: reduce BPL x NF accumulators over the 4 point-groups (xor 16/32) and the
+// 4 waves (LDS, fixed order), append the extras and write one partial record.
+template <int BPL, int NF>
+GC_DEV void write_partial_record(double (&acc)[BPL][NF], double ent, double mxr, double sumw,
+                                 double npts, int B, double* lds, double* rec) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, bl = lane & 15;
+#pragma unroll
+  for (int j = 0; j < BPL; ++j)
+#pragma unroll
+    for (int k = 0; k < NF; ++k) {
+      double v = acc[j][k];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      acc[j][k] = v;
+    }
+  __syncthreads();
+  if (lane < 16) {
+#pragma unroll
+    for (int j = 0; j < BPL; ++j) {
+      const int b = bl + 16 * j;
+      if (b < B)
+#pragma unroll
+        for (int k = 0; k < NF; ++k) lds[(wv * B + b) * NF + k] = acc[j][k];
+    }
+  }
+  // extras
+  double e = wave_sum(ent), m = wave_max(mxr), s = wave_sum(sumw);
+  if (lane == 0) {
+    lds[4 * B * NF + wv * 3 + 0] = e;
+    lds[4 * B * NF + wv * 3 + 1] = m;
+    lds[4 * B * NF + wv * 3 + 2] = s;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < B * NF; i += kWG)
+    rec[i] = (lds[i] + lds[B * NF + i]) + (lds[2 * B * NF + i] + lds[3 * B * NF + i]);
+  if (threadIdx.x == 0) {
+    const double* ex = lds + 4 * B * NF;
+    rec[B * NF + 0] = (ex[0] + ex[3]) + (ex[6] + ex[9]);
+    rec[B * NF + 1] = fmax(fmax(ex[1], ex[4]), fmax(ex[7], ex[10]));
+    rec[B * NF + 2] = (ex[2] + ex[5]) + (ex[8] + ex[11]);
+    rec[B * NF + 3] = npts;
+  }
+}
+
+// Contract variant: responsibilities streamed from HBM. grid (chunks, H), chunk = ITERS*256 pts.
+template <int BPL, bool COV>
+__global__ void __launch_bounds__(256) k_moment_partials(int64_t n, int B, int iters,
+                                                         const double* __restrict__ pts,
+                                                         const double* __restrict__ covs,
+                                                         const double* __restrict__ w,
+                                                         const double* __restrict__ resp,
+                                                         const double* __restrict__ lam, double o0,
+                                                         double o1, double o2, double* partials) {
+  constexpr int NF = COV ? NF_BASE + NF_COV : NF_BASE;
+  extern __shared__ double lds[];  // max(4 * 64 * NF, 4*B*NF + 12)
+  const int h = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, bl = lane & 15;
+  double* F = lds + wv * (NF * 64);
+  const double o[3] = {o0, o1, o2};
+  double acc[BPL][NF];
+#pragma unroll
+  for (int j = 0; j < BPL; ++j)
+#pragma unroll
+    for (int k = 0; k < NF; ++k) acc[j][k] = 0.0;
+  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
+  for (int it = 0; it < iters; ++it) {
+    const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
+    {  // phase A: lane = point
+      const int64_t pt = wbase + lane;
+      double f[NF];
+      if (pt < n) {
+        const int64_t row = (int64_t)h * n + pt;
+        const double p[3] = {pts[3 * row], pts[3 * row + 1], pts[3 * row + 2]};
+        double d[3];
+        direction(p, o, 1e-12, d);
+        const double we = w[row] * (lam ? lam[row] : 1.0);
+        point_features(p, d, we, f);
+        if constexpr (COV) {
+#pragma unroll
+          for (int k = 0; k < 9; ++k) f[NF_BASE + k] = we * covs[9 * row + k];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < NF; ++k) f[k] = 0.0;
+      }
+#pragma unroll
+      for (int k = 0; k < NF; ++k) F[k * 64 + lane] = f[k];
+    }
+    lds_wave_sync();
+    // phase B: 16 steps x 4 points, lanes = 4 groups x 16 bin-lanes
+    double rn[BPL];
+    {
+      const int64_t pt = wbase + g;
+      const int64_t row = (int64_t)h * n + (pt < n ? pt : 0);
+#pragma unroll
+      for (int j = 0; j < BPL; ++j) {
+        const int b = bl + 16 * j;
+        rn[j] = (pt < n && b < B) ? resp[row * B + b] : 0.0;
+      }
+    }
+#pragma unroll 1
+    for (int s = 0; s < 16; ++s) {
+      double r[BPL];
+#pragma unroll
+      for (int j = 0; j < BPL; ++j) r[j] = rn[j];
+      if (s < 15) {  // prefetch next step
+        const int64_t pt = wbase + (s + 1) * 4 + g;
+        const int64_t row = (int64_t)h * n + (pt < n ? pt : 0);
+#pragma unroll
+        for (int j = 0; j < BPL; ++j) {
+          const int b = bl + 16 * j;
+          rn[j] = (pt < n && b < B) ? resp[row * B + b] : 0.0;
+        }
+      }
+      const int pl = s * 4 + g;
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        const double fk = F[k * 64 + pl];
+#pragma unroll
+        for (int j = 0; j < BPL; ++j) acc[j][k] += r[j] * fk;
+      }
+    }
+    lds_wave_sync();
+  }
+  int64_t npts = n - chunk0;
+  npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
+  const int RL = B * NF + REC_EXTRA;
+  write_partial_record<BPL, NF>(acc, 0.0, 0.0, 0.0, (double)npts, B, lds,
+                                partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
+}
+
+// =========================================================== fused a1 -> a4 -> a5 -> a6
+// grid (chunks, H). Budget selection + deskew + directions in phase A (lane = point), soft
+// assignment + moment accumulation in phase B (resp stays in registers).
+template <int BPL>
+__global__ void __launch_bounds__(256) k_bins_fused(int64_t n_cap, int B, int iters,
+                                                    const double* __restrict__ pts_raw,
+                                                    const double* __restrict__ t_raw,
+                                                    const double* __restrict__ w_raw,
+                                                    const double* __restrict__ bscal, double t0,
+                                                    double t1, const double* __restrict__ xi,
+                                                    const double* __restrict__ bins, double inv_tau,
+                                                    double o0, double o1, double o2,
+                                                    double* partials) {
+  constexpr int NF = NF_BASE;
+  constexpr int NS = NF + 4;  // + d(3) + valid flag
+  extern __shared__ double lds[];
+  const int h = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, bl = lane & 15;
+  double* F = lds + wv * (NS * 64);
+  const double o[3] = {o0, o1, o2};
+  double xr[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) xr[k] = xi[6 * h + k];
+  const double scale = bscal[2];
+  const int64_t n_sel = (int64_t)bscal[5];
+  const int64_t stride = (int64_t)bscal[6];
+  const double denom = fmax(t1 - t0, 1e-12);
+  const double sig = 0.1 * denom;
+  double bx[BPL], by[BPL], bz[BPL];
+  bool bv[BPL];
+#pragma unroll
+  for (int j = 0; j < BPL; ++j) {
+    const int b = bl + 16 * j;
+    bv[j] = b < B;
+    bx[j] = bv[j] ? bins[3 * b] : 0.0;
+    by[j] = bv[j] ? bins[3 * b + 1] : 0.0;
+    bz[j] = bv[j] ? bins[3 * b + 2] : 0.0;
+  }
+  double acc[BPL][NF];
+#pragma unroll
+  for (int j = 0; j < BPL; ++j)
+#pragma unroll
+    for (int k = 0; k < NF; ++k) acc[j][k] = 0.0;
+  double sumw = 0.0, logacc = 0.0, entq = 0.0, mxr = 0.0;
+  const double xmax = inv_tau;  // S <= 1 for unit vectors: exp never overflows
+  const double Beps = (double)B * 1e-12;
+  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
+  for (int it = 0; it < iters; ++it) {
+    const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
+    {  // phase A
+      const int64_t j = wbase + lane;
+      const bool inr = j < n_cap;
+      double p[3] = {0.0, 0.0, 0.0}, tt = 0.0, ww = 0.0;
+      if (inr && j < n_sel) {
+        const int64_t i = j * stride;
+        p[0] = pts_raw[3 * i]; p[1] = pts_raw[3 * i + 1]; p[2] = pts_raw[3 * i + 2];
+        tt = t_raw[i];
+        ww = w_raw[i] * scale;
+      }
+      double q[3], d[3], f[NF];
+      deskew_point(p, (tt - t0) / denom, xr, q);
+      const double wd = inr ? ww * window_weight(tt, t0, t1, sig) : 0.0;
+      direction(q, o, 1e-12, d);
+      point_features(q, d, wd, f);
+      sumw += wd;
+#pragma unroll
+      for (int k = 0; k < NF; ++k) F[k * 64 + lane] = f[k];
+      F[(NF + 0) * 64 + lane] = d[0];
+      F[(NF + 1) * 64 + lane] = d[1];
+      F[(NF + 2) * 64 + lane] = d[2];
+      F[(NF + 3) * 64 + lane] = inr ? 1.0 : 0.0;
+    }
+    lds_wave_sync();
+    double zst = 1.0;
+#pragma unroll 1
+    for (int s = 0; s < 16; ++s) {
+      const int pl = s * 4 + g;
+      const double d0 = F[(NF + 0) * 64 + pl], d1 = F[(NF + 1) * 64 + pl], d2 = F[(NF + 2) * 64 + pl];
+      const bool valid = F[(NF + 3) * 64 + pl] != 0.0;
+      double e[BPL], zl = 0.0, sl = 0.0;
+#pragma unroll
+      for (int j = 0; j < BPL; ++j) {
+        const double x = (d0 * bx[j] + d1 * by[j] + d2 * bz[j]) * inv_tau - xmax;
+        e[j] = bv[j] ? exp(x) : 0.0;
+        zl += e[j];
+        sl += e[j] * x;
+      }
+      const double Z = group16_sum(zl);
+      const double Sx = group16_sum(sl);
+      const double rZ = 1.0 / Z;
+      if (valid) entq += Sx * rZ;
+      if (bl == s) zst = valid ? Z : 1.0;
+#pragma unroll
+      for (int j = 0; j < BPL; ++j) {
+        e[j] *= rZ;
+        if (valid) mxr = fmax(mxr, e[j]);
+      }
+#pragma unroll
+      for (int k = 0; k < NF; ++k) {
+        const double fk = F[k * 64 + pl];
+#pragma unroll
+        for (int j = 0; j < BPL; ++j) acc[j][k] += e[j] * fk;
+      }
+    }
+    // each lane stashed the Z of one point per 16 steps: one log per lane per iteration
+    logacc += log(zst);
+    lds_wave_sync();
+  }
+  // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε  (entq is group-uniform)
+  int64_t npts = n_cap - chunk0;
+  npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
+  const double ent = logacc - (bl == 0 ? entq : 0.0) - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
+  const int RL = B * NF + REC_EXTRA;
+  write_partial_record<BPL, NF>(acc, ent, mxr, (lane == 0 ? 0.0 : 0.0) + sumw, (double)npts, B, lds,
+                                partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
+}
+
+// ================================================================ finalize (a6 + certs)
+// One workgroup per hypothesis: chunk records summed in order, per-bin moments -> p̄, Σ_p
+// (PSD-projected), κ; cert reductions in a fixed order.
+__global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t chunks,
+                                                       const double* __restrict__ partials,
+                                                       double eps_psd, double eps_mass,
+                                                       double* stats, double* cert) {
+  extern __shared__ double sm[];  // B*NF + 8 + 4
+  double* red = sm + B * NF + REC_EXTRA;
+  const int h = blockIdx.x;
+  const int RL = B * NF + REC_EXTRA;
+  const double* P = partials + (int64_t)h * chunks * RL;
+  for (int i = threadIdx.x; i < RL; i += kWG) {
+    double v = 0.0;
+    if (i == B * NF + 1) {
+      for (int64_t c = 0; c < chunks; ++c) v = fmax(v, P[c * RL + i]);
+    } else {
+      for (int64_t c = 0; c < chunks; ++c) v += P[c * RL + i];
+    }
+    sm[i] = v;
+  }
+  __syncthreads();
+  double Nl = 0.0, N2l = 0.0, psdl = 0.0, epsl = 0.0, sfl = 0.0;
+  if ((int)threadIdx.x < B) {
+    const int b = threadIdx.x;
+    const double* a = sm + b * NF;
+    const double N = a[0];
+    const double denom = N + eps_mass + kF64Eps;
+    const double invN = 1.0 / denom, er = eps_mass / denom;
+    const double sd[3] = {a[1], a[2], a[3]};
+    const double Ssc[9] = {a[4], a[5], a[6], a[5], a[7], a[8], a[6], a[8], a[9]};
+    const double sp[3] = {a[10], a[11], a[12]};
+    const double Spp[9] = {a[13], a[14], a[15], a[14], a[16], a[17], a[15], a[17], a[18]};
+    double pb[3] = {sp[0] * invN, sp[1] * invN, sp[2] * invN};
+    double Sr[9], Sp[9], c6[6];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) {
+        double v = Spp[3 * i + j] * invN - pb[i] * pb[j];
+        if (NF > NF_BASE) v += a[NF_BASE + 3 * i + j] * invN;
+        Sr[3 * i + j] = v;
+      }
+    psd_project3(Sr, eps_psd, Sp, c6);
+    const double Rbar = sqrt(sd[0] * sd[0] + sd[1] * sd[1] + sd[2] * sd[2]) * invN;
+    const double kap = kappa_blend(Rbar, 1e-6, 3.0, 0.8, 0.03);
+    double* o = stats + ((int64_t)h * B + b) * GC_BIN_STATS;
+    o[0] = N;
+    for (int k = 0; k < 3; ++k) o[1 + k] = sd[k];
+    for (int k = 0; k < 9; ++k) o[4 + k] = Ssc[k];
+    for (int k = 0; k < 3; ++k) o[13 + k] = pb[k];
+    for (int k = 0; k < 9; ++k) o[16 + k] = Sp[k];
+    o[25] = kap;
+    for (int k = 0; k < 3; ++k) o[26 + k] = sp[k];
+    for (int k = 0; k < 9; ++k) o[29 + k] = Spp[k];
+    Nl = N; N2l = N * N; psdl = c6[0]; epsl = er; sfl = N / (N + eps_mass);
+  }
+  const double Nt = wg_sum(Nl, red);
+  const double N2 = wg_sum(N2l, red);
+  const double psd = wg_sum(psdl, red);
+  const double mer = wg_max(epsl, red);
+  const double sf = wg_sum(sfl, red);
+  if (threadIdx.x == 0) {
+    const double* ex = sm + B * NF;
+    double* c = cert + (int64_t)h * GC_BIN_CERT;
+    c[0] = Nt * Nt / (N2 + eps_mass);
+    c[1] = sf / (double)B;
+    c[2] = psd;
+    c[3] = mer;
+    c[4] = ex[0] / (ex[3] + eps_mass);
+    c[5] = ex[1];
+    c[6] = ex[2];
+    c[7] = psd + mer;
+  }
+}
+
+__global__ void k_kappa(int64_t n, const double* __restrict__ R, double eps_r, double d, double r0,
+                        double tau, double* out) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = kappa_blend(R[i], eps_r, d, r0, tau);
+}
+
+__global__ void k_psd3(int batch, const double* __restrict__ M, double eps, double* Mo, double* cert) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch) return;
+  double A[9], P[9], c[6];
+  for (int k = 0; k < 9; ++k) A[k] = M[9 * i + k];
+  psd_project3(A, eps, P, c);
+  for (int k = 0; k < 9; ++k) Mo[9 * i + k] = P[k];
+  for (int k = 0; k < 6; ++k) cert[6 * i + k] = c[k];
+}
+
+__global__ void __launch_bounds__(256) k_psd_wg(int d, const double* __restrict__ M, double eps,
+                                                double* Mo, double* cert) {
+  __shared__ double Ml[kDZ * kDZ], Mp[kDZ * kDZ], scr[2 * kDZ * kDZ + 4 * kDZ], red[4], c6[6];
+  const int i = blockIdx.x;
+  for (int k = threadIdx.x; k < d * d; k += kWG) Ml[k] = M[(int64_t)i * d * d + k];
+  __syncthreads();
+  wg_psd_project(Ml, Mp, eps, d, scr, red, c6);
+  for (int k = threadIdx.x; k < d * d; k += kWG) Mo[(int64_t)i * d * d + k] = Mp[k];
+  if (threadIdx.x < 6) cert[6 * i + threadIdx.x] = c6[threadIdx.x];
+}
+
+// ------------------------------------------------------------------------ launch helpers
+static int bpl_for(int B) { return (B + 15) / 16; }
+
+}  // namespace gc
+
+using namespace gc;
+
+static int pick_iters(int64_t n, int H) {
+  // Aim for >= ~4 workgroups per CU-slot while keeping partial records small.
+  int iters = 8;
+  while (iters > 1 && ((n + iters * 256 - 1) / (iters * 256)) * (int64_t)H < 2048) iters >>= 1;
+  return iters;
+}
+
+extern "C" {
+
+int32_t gc_budget_stats(gc_ctx* ctx, const double* d_w, int64_t n_in, int64_t n_cap, double* d_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, n_in > 0 && n_cap > 0, "n_in and n_cap must be positive");
+  GC_CHECK_ARG(ctx, d_w && d_out, "NULL buffer");
+  const int64_t stride = std::max<int64_t>(1, (n_in + n_cap - 1) / n_cap);
+  hipLaunchKernelGGL(k_budget_stats, dim3(1), dim3(256), 0, ctx->stream, d_w, n_in, n_cap, stride, d_out);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+int32_t gc_point_budget_resample(gc_ctx* ctx, const double* d_points, const double* d_t, const double* d_w,
+                                 const uint8_t* d_ring, const uint8_t* d_tag, int64_t n_in, int64_t n_cap,
+                                 double* d_points_out, double* d_t_out, double* d_w_out, uint8_t* d_ring_out,
+                                 uint8_t* d_tag_out, int64_t* d_idx_out, double* d_scalars_out) {
+  int32_t rc = gc_budget_stats(ctx, d_w, n_in, n_cap, d_scalars_out);
+  if (rc) return rc;
+  GC_CHECK_ARG(ctx, d_points && d_t && d_points_out && d_t_out && d_w_out, "NULL buffer");
+  const int64_t stride = std::max<int64_t>(1, (n_in + n_cap - 1) / n_cap);
+  hipLaunchKernelGGL(k_budget_gather, dim3((unsigned)((n_cap + 255) / 256)), dim3(256), 0, ctx->stream,
+                     d_points, d_t, d_w, d_ring, d_tag, n_in, n_cap, stride, d_scalars_out, d_points_out,
+                     d_t_out, d_w_out, d_ring_out, d_tag_out, d_idx_out);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+int32_t gc_deskew_constant_twist(gc_ctx* ctx, int32_t H, int64_t n, const double* d_points, const double* d_t,
+                                 const double* d_w, double t0, double t1, const double* d_xi,
+                                 double* d_points_out, double* d_w_out, double* d_sum_w_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, H > 0 && n > 0, "H and n must be positive");
+  GC_CHECK_ARG(ctx, d_points && d_t && d_w && d_xi && d_points_out && d_w_out && d_sum_w_out, "NULL buffer");
+  const int64_t blocks = (n + 255) / 256;
+  void* scr;
+  if (int rc = gc::scratch(ctx, sizeof(double) * blocks * H, &scr)) return rc;
+  hipLaunchKernelGGL(k_deskew, dim3((unsigned)blocks, H), dim3(256), 0, ctx->stream, n, d_points, d_t, d_w, t0,
+                     t1, d_xi, d_points_out, d_w_out, (double*)scr);
+  GC_LAUNCH_CHECK(ctx);
+  hipLaunchKernelGGL(k_sum_rows, dim3((H + 63) / 64), dim3(64), 0, ctx->stream, (const double*)scr, blocks, H,
+                     d_sum_w_out);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+int32_t gc_point_directions(gc_ctx* ctx, int64_t rows, const double* d_points, const double* h_origin3,
+                            double eps_mass, double* d_dirs_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, rows > 0 && d_points && h_origin3 && d_dirs_out, "bad arguments");
+  hipLaunchKernelGGL(k_point_dirs, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, ctx->stream, rows,
+                     d_points, h_origin3[0], h_origin3[1], h_origin3[2], eps_mass, d_dirs_out);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const double* d_dirs,
+                           const double* d_bins, double tau, double* d_resp_out, int32_t* d_bin_index_out,
+                           double* d_cert_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, H > 0 && n > 0, "H and n must be positive");
+  GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
+  GC_CHECK_ARG(ctx, tau > 0.0, "tau must be positive");
+  GC_CHECK_ARG(ctx, d_dirs && d_bins && d_resp_out && d_cert_out, "NULL buffer");
+  const int64_t blocks = (n + 255) / 256;
+  void* scr;
+  if (int rc = gc::scratch(ctx, sizeof(double) * 2 * blocks * H, &scr)) return rc;
+  const double inv_tau = 1.0 / tau;
+  dim3 grid((unsigned)blocks, H);
+  switch (bpl_for(B)) {
+    case 1: hipLaunchKernelGGL(k_soft_assign<1>, grid, dim3(256), 0, ctx->stream, n, B, d_dirs, d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr); break;
+    case 2: hipLaunchKernelGGL(k_soft_assign<2>, grid, dim3(256), 0, ctx->stream, n, B, d_dirs, d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr); break;
+    case 3: hipLaunchKernelGGL(k_soft_assign<3>, grid, dim3(256), 0, ctx->stream, n, B, d_dirs, d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr); break;
+    default: hipLaunchKernelGGL(k_soft_assign<4>, grid, dim3(256), 0, ctx->stream, n, B, d_dirs, d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr); break;
+  }
+  GC_LAUNCH_CHECK(ctx);
+  hipLaunchKernelGGL(k_soft_assign_finalize, dim3((H + 63) / 64), dim3(64), 0, ctx->stream, (const double*)scr,
+                     blocks, H, n, d_cert_out);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+static int32_t launch_finalize(gc_ctx* ctx, int H, int B, int NF, int64_t chunks, const double* partials,
+                               double eps_psd, double eps_mass, double* stats, double* cert) {
+  const size_t sh = sizeof(double) * (B * NF + REC_EXTRA + 8);
+  hipLaunchKernelGGL(k_bins_finalize, dim3(H), dim3(256), sh, ctx->stream, B, NF, chunks, partials, eps_psd,
+                     eps_mass, stats, cert);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+int32_t gc_scan_bin_moment_match(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const double* d_points,
+                                 const double* d_covs, const double* d_w, const double* d_resp,
+                                 const double* d_lambda, const double* h_origin3, double eps_psd, double eps_mass,
+                                 double* d_stats_out, double* d_cert_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, H > 0 && n > 0, "H and n must be positive");
+  GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
+  GC_CHECK_ARG(ctx, d_points && d_w && d_resp && d_stats_out && d_cert_out, "NULL buffer");
+  double o[3] = {0.0, 0.0, 0.0};
+  if (h_origin3) { o[0] = h_origin3[0]; o[1] = h_origin3[1]; o[2] = h_origin3[2]; }
+  const int iters = pick_iters(n, H);
+  const int64_t chunks = (n + iters * 256 - 1) / (iters * 256);
+  const bool cov = d_covs != nullptr;
+  const int NF = cov ? NF_BASE + NF_COV : NF_BASE;
+  const int RL = B * NF + REC_EXTRA;
+  void* scr;
+  if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
+  const size_t sh = sizeof(double) * std::max<size_t>(4 * 64 * NF, 4 * (size_t)B * NF + 12);
+  dim3 grid((unsigned)chunks, H);
+  const int bpl = bpl_for(B);
+#define GC_MOM(BP, CV)                                                                                   \
+  hipLaunchKernelGGL((k_moment_partials<BP, CV>), grid, dim3(256), sh, ctx->stream, n, B, iters, d_points, \
+                     d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr)
+  if (cov) {
+    switch (bpl) { case 1: GC_MOM(1, true); break; case 2: GC_MOM(2, true); break; case 3: GC_MOM(3, true); break; default: GC_MOM(4, true); }
+  } else {
+    switch (bpl) { case 1: GC_MOM(1, false); break; case 2: GC_MOM(2, false); break; case 3: GC_MOM(3, false); break; default: GC_MOM(4, false); }
+  }
+#undef GC_MOM
+  GC_LAUNCH_CHECK(ctx);
+  return launch_finalize(ctx, H, B, NF, chunks, (const double*)scr, eps_psd, eps_mass, d_stats_out, d_cert_out);
+}
+
+int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, int32_t B,
+                           const double* d_points_raw, const double* d_t_raw, const double* d_w_raw,
+                           const double* d_budget_scalars, double t0, double t1, const double* d_xi,
+                           const double* d_bins, double tau, const double* h_origin3, double eps_psd,
+                           double eps_mass, double* d_stats_out, double* d_cert_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, H > 0 && n_in > 0 && n_cap > 0, "H, n_in, n_cap must be positive");
+  GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
+  GC_CHECK_ARG(ctx, tau > 0.0, "tau must be positive");
+  GC_CHECK_ARG(ctx, d_points_raw && d_t_raw && d_w_raw && d_budget_scalars && d_xi && d_bins && h_origin3 &&
+                        d_stats_out && d_cert_out, "NULL buffer");
+  (void)n_in;
+  const int iters = pick_iters(n_cap, H);
+  const int64_t chunks = (n_cap + iters * 256 - 1) / (iters * 256);
+  const int NF = NF_BASE;
+  const int RL = B * NF + REC_EXTRA;
+  void* scr;
+  if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
+  const size_t sh = sizeof(double) * std::max<size_t>(4 * 64 * (NF + 4), 4 * (size_t)B * NF + 12);
+  dim3 grid((unsigned)chunks, H);
+  const double inv_tau = 1.0 / tau;
+#define GC_FUSED(BP)                                                                                     \
+  hipLaunchKernelGGL((k_bins_fused<BP>), grid, dim3(256), sh, ctx->stream, n_cap, B, iters, d_points_raw, \
+                     d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins, inv_tau, h_origin3[0],     \
+                     h_origin3[1], h_origin3[2], (double*)scr)
+  switch (bpl_for(B)) { case 1: GC_FUSED(1); break; case 2: GC_FUSED(2); break; case 3: GC_FUSED(3); break; default: GC_FUSED(4); }
+#undef GC_FUSED
+  GC_LAUNCH_CHECK(ctx);
+  return launch_finalize(ctx, H, B, NF, chunks, (const double*)scr, eps_psd, eps_mass, d_stats_out, d_cert_out);
+}
+
+int32_t gc_kappa_from_resultant_batch(gc_ctx* ctx, int64_t n, const double* d_R, double eps_r, double d,
+                                      double r0, double tau, double* d_kappa_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, n >= 0 && d_R && d_kappa_out, "bad arguments");
+  if (n == 0) return GC_OK;
+  hipLaunchKernelGGL(k_kappa, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, n, d_R, eps_r, d, r0,
+                     tau, d_kappa_out);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+int32_t gc_domain_projection_psd_batch(gc_ctx* ctx, int32_t batch, int32_t d, const double* d_M, double eps_psd,
+                                       double* d_M_out, double* d_cert_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, batch >= 0 && d_M && d_M_out && d_cert_out, "bad arguments");
+  GC_CHECK_ARG(ctx, d == 3 || (d >= 2 && d <= 22 && d % 2 == 0), "d must be 3 or even in [2, 22]");
+  if (batch == 0) return GC_OK;
+  if (d == 3) {
+    hipLaunchKernelGGL(k_psd3, dim3((batch + 63) / 64), dim3(64), 0, ctx->stream, batch, d_M, eps_psd, d_M_out,
+                       d_cert_out);
+  } else {
+    hipLaunchKernelGGL(k_psd_wg, dim3(batch), dim3(256), 0, ctx->stream, d, d_M, eps_psd, d_M_out, d_cert_out);
+  }
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,173 @@
+// gc_runtime.cpp — context, device buffers, events and error plumbing of libgcslam.
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <string>
+#include "gc_internal.h"
+
+struct gc_event {
+  hipEvent_t ev = nullptr;
+};
+
+namespace {
+thread_local std::string tl_error;
+}
+
+namespace gc {
+
+void set_error(gc_ctx* ctx, const std::string& msg) {
+  if (ctx) ctx->err = msg;
+  tl_error = msg;
+}
+
+int scratch(gc_ctx* ctx, size_t bytes, void** out) {
+  if (bytes > ctx->scratch_bytes) {
+    GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->scratch) GC_HIP(ctx, hipFree(ctx->scratch));
+    ctx->scratch = nullptr;
+    ctx->scratch_bytes = 0;
+    size_t sz = bytes < (1u << 20) ? (1u << 20) : bytes + bytes / 4;
+    GC_HIP(ctx, hipMalloc(&ctx->scratch, sz));
+    ctx->scratch_bytes = sz;
+  }
+  *out = ctx->scratch;
+  return GC_OK;
+}
+
+}  // namespace gc
+
+extern "C" {
+
+int32_t gc_version(void) { return 10000; /* 1.0.0 */ }
+
+const char* gc_last_error(const gc_ctx* ctx) {
+  if (ctx && !ctx->err.empty()) return ctx->err.c_str();
+  return tl_error.c_str();
+}
+
+int32_t gc_device_count(int32_t* count) {
+  int n = 0;
+  hipError_t e = hipGetDeviceCount(&n);
+  if (e != hipSuccess) {
+    gc::set_error(nullptr, std::string("hipGetDeviceCount: ") + hipGetErrorString(e));
+    *count = 0;
+    return GC_ERR_RUNTIME;
+  }
+  *count = n;
+  return GC_OK;
+}
+
+int32_t gc_ctx_create(int32_t device, gc_ctx** out) {
+  GC_CHECK_ARG(nullptr, out != nullptr, "out is NULL");
+  int n = 0;
+  GC_HIP(nullptr, hipGetDeviceCount(&n));
+  GC_CHECK_ARG(nullptr, device >= 0 && device < n, "device index out of range");
+  GC_HIP(nullptr, hipSetDevice(device));
+  gc_ctx* c = new gc_ctx();
+  c->device = device;
+  hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+  if (e != hipSuccess) {
+    gc::set_error(nullptr, std::string("hipStreamCreate: ") + hipGetErrorString(e));
+    delete c;
+    return GC_ERR_RUNTIME;
+  }
+  *out = c;
+  return GC_OK;
+}
+
+int32_t gc_ctx_destroy(gc_ctx* ctx) {
+  if (!ctx) return GC_OK;
+  (void)hipSetDevice(ctx->device);
+  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->scratch) (void)hipFree(ctx->scratch);
+  (void)hipStreamDestroy(ctx->stream);
+  delete ctx;
+  return GC_OK;
+}
+
+int32_t gc_ctx_synchronize(gc_ctx* ctx) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_HIP(ctx, hipSetDevice(ctx->device));
+  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_buffer_alloc(gc_ctx* ctx, uint64_t bytes, void** d_ptr) {
+  GC_CHECK_ARG(nullptr, ctx && d_ptr, "NULL argument");
+  GC_HIP(ctx, hipSetDevice(ctx->device));
+  GC_HIP(ctx, hipMalloc(d_ptr, bytes ? bytes : 16));
+  return GC_OK;
+}
+
+int32_t gc_buffer_free(gc_ctx* ctx, void* d_ptr) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (!d_ptr) return GC_OK;
+  GC_HIP(ctx, hipSetDevice(ctx->device));
+  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  GC_HIP(ctx, hipFree(d_ptr));
+  return GC_OK;
+}
+
+int32_t gc_buffer_upload(gc_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (bytes == 0) return GC_OK;
+  GC_HIP(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
+  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_buffer_download(gc_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (bytes == 0) return GC_OK;
+  GC_HIP(ctx, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
+  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_buffer_copy(gc_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (bytes == 0) return GC_OK;
+  GC_HIP(ctx, hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_buffer_memset(gc_ctx* ctx, void* d_dst, int32_t value, uint64_t bytes) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (bytes == 0) return GC_OK;
+  GC_HIP(ctx, hipMemsetAsync(d_dst, value, bytes, ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_event_create(gc_ctx* ctx, gc_event** out) {
+  GC_CHECK_ARG(nullptr, ctx && out, "NULL argument");
+  gc_event* e = new gc_event();
+  hipError_t r = hipEventCreate(&e->ev);
+  if (r != hipSuccess) {
+    delete e;
+    gc::set_error(ctx, std::string("hipEventCreate: ") + hipGetErrorString(r));
+    return GC_ERR_RUNTIME;
+  }
+  *out = e;
+  return GC_OK;
+}
+
+int32_t gc_event_destroy(gc_event* ev) {
+  if (!ev) return GC_OK;
+  (void)hipEventDestroy(ev->ev);
+  delete ev;
+  return GC_OK;
+}
+
+int32_t gc_event_record(gc_ctx* ctx, gc_event* ev) {
+  GC_CHECK_ARG(nullptr, ctx && ev, "NULL argument");
+  GC_HIP(ctx, hipEventRecord(ev->ev, ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_event_elapsed_ms(gc_event* start, gc_event* stop, float* ms) {
+  GC_CHECK_ARG(nullptr, start && stop && ms, "NULL argument");
+  GC_HIP(nullptr, hipEventSynchronize(stop->ev));
+  GC_HIP(nullptr, hipEventElapsedTime(ms, start->ev, stop->ev));
+  return GC_OK;
+}
+
+}  // extern "C"

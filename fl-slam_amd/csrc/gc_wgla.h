@@ -1,0 +1,309 @@
+// gc_wgla.h — workgroup-cooperative f64 dense linear algebra on LDS-resident matrices
+// (n <= 22), for the batched-small kernels (one 256-thread workgroup per hypothesis).
+//
+// Restates fl_slam_poc/common/primitives.py: domain_projection_psd_core (:80-123),
+// spd_cholesky_solve_lifted_core (:141-166), spd_cholesky_inverse_lifted_core (:169-192).
+// The symmetric eigensolver is a parallel cyclic Jacobi (round-robin pairing, n/2 disjoint
+// rotations per round applied as 2x2 tile updates, so each tile is owned by one thread and
+// a round needs two barriers). Eigenvalues agree with LAPACK's eigh to ~1e-15 relative; the
+// clamped reconstruction V max(λ, ε) Vᵀ is basis-independent, so PSD outputs match.
+//
+// Every function must be called by all 256 threads of the workgroup (uniform control flow).
+#pragma once
+#include "gc_math.h"
+
+namespace gc {
+
+constexpr int kWG = 256;
+constexpr int kDZ = 22;
+
+GC_DEV int tid() { return threadIdx.x; }
+
+// Deterministic workgroup sum (fixed shuffle tree + fixed wave order). red: >= 4 doubles of LDS.
+GC_DEV double wave_sum(double v) {
+  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+GC_DEV double wave_max(double v) {
+  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
+  return v;
+}
+GC_DEV double wave_min(double v) {
+  for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
+  return v;
+}
+GC_DEV double wg_sum(double v, double* red) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = (red[0] + red[1]) + (red[2] + red[3]);
+  __syncthreads();
+  return r;
+}
+GC_DEV double wg_max(double v, double* red) {
+  v = wave_max(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double r = fmax(fmax(red[0], red[1]), fmax(red[2], red[3]));
+  __syncthreads();
+  return r;
+}
+
+GC_DEV void wg_copy(double* dst, const double* src, int count) {
+  for (int i = threadIdx.x; i < count; i += kWG) dst[i] = src[i];
+  __syncthreads();
+}
+
+// In-place lower Cholesky of the n x n (row-major) A; upper triangle zeroed.
+GC_DEV void wg_chol(double* A, int n) {
+  for (int k = 0; k < n; ++k) {
+    if (threadIdx.x == 0) A[k * n + k] = sqrt(A[k * n + k]);
+    __syncthreads();
+    const double dk = A[k * n + k];
+    const int m = n - k - 1;
+    if ((int)threadIdx.x < m) {
+      const int i = k + 1 + threadIdx.x;
+      A[i * n + k] = A[i * n + k] / dk;
+    }
+    __syncthreads();
+    const int tri = m * (m + 1) / 2;
+    for (int idx = threadIdx.x; idx < tri; idx += kWG) {
+      // decode lower-triangular (i, j) with j <= i inside the trailing block
+      int i = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+      while ((i + 1) * (i + 2) / 2 <= idx) ++i;
+      while (i * (i + 1) / 2 > idx) --i;
+      const int j = idx - i * (i + 1) / 2;
+      const int gi = k + 1 + i, gj = k + 1 + j;
+      A[gi * n + gj] -= A[gi * n + k] * A[gj * n + k];
+    }
+    __syncthreads();
+  }
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    if (j > i) A[idx] = 0.0;
+  }
+  __syncthreads();
+}
+
+// x = (C Cᵀ)^{-1} b for lower-triangular C (thread 0; result visible to all on return).
+GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
+  if (threadIdx.x == 0) {
+    double y[kDZ];
+    for (int i = 0; i < n; ++i) {
+      double v = b[i];
+      for (int j = 0; j < i; ++j) v -= C[i * n + j] * y[j];
+      y[i] = v / C[i * n + i];
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      double v = y[i];
+      for (int j = i + 1; j < n; ++j) v -= C[j * n + i] * x[j];
+      x[i] = v / C[i * n + i];
+    }
+  }
+  __syncthreads();
+}
+
+// Ainv = C^{-ᵀ} C^{-1} (primitives.py:186-191: L_chol_inv.T @ L_chol_inv). scratch: n*n.
+GC_DEV void wg_chol_inverse(const double* C, double* Ainv, double* scratch, int n) {
+  // scratch <- C^{-1} (lower), column j solved by thread j
+  if ((int)threadIdx.x < n) {
+    const int j = threadIdx.x;
+    for (int i = 0; i < n; ++i) {
+      double v = (i == j) ? 1.0 : 0.0;
+      if (i >= j)
+        for (int k = j; k < i; ++k) v -= C[i * n + k] * scratch[k * n + j];
+      scratch[i * n + j] = (i >= j) ? v / C[i * n + i] : 0.0;
+    }
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    const int k0 = i > j ? i : j;
+    double v = 0.0;
+    for (int k = k0; k < n; ++k) v += scratch[k * n + i] * scratch[k * n + j];
+    Ainv[idx] = v;
+  }
+  __syncthreads();
+}
+
+// Lifted solve / inverse (primitives.py:141-192). work: n*n scratch, work2: n*n scratch.
+GC_DEV void wg_solve_lifted(const double* L, const double* b, double* x, double eps_lift, int n,
+                            double* work) {
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG)
+    work[idx] = L[idx] + ((idx / n == idx % n) ? eps_lift : 0.0);
+  __syncthreads();
+  wg_chol(work, n);
+  wg_chol_solve(work, b, x, n);
+}
+GC_DEV void wg_inverse_lifted(const double* L, double* Linv, double eps_lift, int n, double* work,
+                              double* work2) {
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG)
+    work[idx] = L[idx] + ((idx / n == idx % n) ? eps_lift : 0.0);
+  __syncthreads();
+  wg_chol(work, n);
+  wg_chol_inverse(work, Linv, work2, n);
+}
+
+// Round-robin (circle method) pair k of round r for even n: p < q.
+GC_DEV void rr_pair(int n, int r, int k, int* p, int* q) {
+  const int m = n - 1;
+  int a, b;
+  if (k == 0) {
+    a = m;
+    b = r % m;
+  } else {
+    a = (r + k) % m;
+    b = (r - k + m) % m;
+  }
+  *p = a < b ? a : b;
+  *q = a < b ? b : a;
+}
+
+// Parallel cyclic Jacobi on the symmetric n x n (n even, <= 22) A (destroyed). If V != nullptr
+// it accumulates eigenvectors (columns). w receives the (unsorted) eigenvalues.
+// cs: 2*(n/2) doubles + n/2 ints worth of LDS (pass >= 3*n doubles), red: 4 doubles.
+GC_DEV void wg_jacobi_eigh(double* A, double* V, double* w, int n, double* cs, double* red) {
+  const int half = n / 2;
+  const int tiles = half * half;
+  int* pq = reinterpret_cast<int*>(cs + 2 * half);
+  if (V)
+    for (int idx = threadIdx.x; idx < n * n; idx += kWG) V[idx] = (idx / n == idx % n) ? 1.0 : 0.0;
+  // diagonal norm for the relative convergence test
+  double dloc = 0.0;
+  for (int i = threadIdx.x; i < n; i += kWG) dloc += A[i * n + i] * A[i * n + i];
+  double offloc = 0.0;
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG)
+    if (idx / n != idx % n) offloc += A[idx] * A[idx];
+  const double fro2 = wg_sum(dloc + offloc, red);
+  double off = wg_sum(offloc, red);
+  for (int sweep = 0; sweep < 20 && off > 1e-34 * fro2 && off > 1e-300; ++sweep) {
+    for (int r = 0; r < n - 1; ++r) {
+      if ((int)threadIdx.x < half) {
+        int p, q;
+        rr_pair(n, r, threadIdx.x, &p, &q);
+        const double apq = A[p * n + q], app = A[p * n + p], aqq = A[q * n + q];
+        double c = 1.0, s = 0.0;
+        if (apq != 0.0 && fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
+          const double th = (aqq - app) / (2.0 * apq);
+          const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+          c = 1.0 / sqrt(t * t + 1.0);
+          s = t * c;
+        }
+        cs[2 * threadIdx.x] = c;
+        cs[2 * threadIdx.x + 1] = s;
+        pq[2 * threadIdx.x] = p;
+        pq[2 * threadIdx.x + 1] = q;
+      }
+      __syncthreads();
+      // A tiles: B' = G_Iᵀ B G_J
+      for (int t = threadIdx.x; t < tiles; t += kWG) {
+        const int I = t / half, J = t % half;
+        const int pi = pq[2 * I], qi = pq[2 * I + 1], pj = pq[2 * J], qj = pq[2 * J + 1];
+        const double ci = cs[2 * I], si = cs[2 * I + 1], cj = cs[2 * J], sj = cs[2 * J + 1];
+        const double b00 = A[pi * n + pj], b01 = A[pi * n + qj], b10 = A[qi * n + pj], b11 = A[qi * n + qj];
+        // B G_J : columns
+        const double c00 = cj * b00 - sj * b01, c01 = sj * b00 + cj * b01;
+        const double c10 = cj * b10 - sj * b11, c11 = sj * b10 + cj * b11;
+        // G_Iᵀ (B G_J) : rows
+        double n00 = ci * c00 - si * c10, n01 = ci * c01 - si * c11;
+        double n10 = si * c00 + ci * c10, n11 = si * c01 + ci * c11;
+        if (I == J) { n01 = 0.0; n10 = 0.0; }
+        A[pi * n + pj] = n00; A[pi * n + qj] = n01; A[qi * n + pj] = n10; A[qi * n + qj] = n11;
+      }
+      if (V) {
+        const int items = n * half;
+        for (int t = (int)threadIdx.x - tiles; t < items; t += kWG) {
+          if (t < 0) continue;
+          const int i = t / half, k = t % half;
+          const int p = pq[2 * k], q = pq[2 * k + 1];
+          const double c = cs[2 * k], s = cs[2 * k + 1];
+          const double vp = V[i * n + p], vq = V[i * n + q];
+          V[i * n + p] = c * vp - s * vq;
+          V[i * n + q] = s * vp + c * vq;
+        }
+      }
+      __syncthreads();
+    }
+    offloc = 0.0;
+    for (int idx = threadIdx.x; idx < n * n; idx += kWG)
+      if (idx / n != idx % n) offloc += A[idx] * A[idx];
+    off = wg_sum(offloc, red);
+  }
+  for (int i = threadIdx.x; i < n; i += kWG) w[i] = A[i * n + i];
+  __syncthreads();
+}
+
+// domain_projection_psd_core (primitives.py:80-123) on an n x n LDS matrix (n even <= 22).
+// M (input, preserved) -> Mp. cert6 (LDS or registers, written by all) =
+// [projection_delta, sym_delta, eig_min, eig_max, cond, near_null_count].
+// scratch: 2*n*n + 4*n doubles.
+GC_DEV void wg_psd_project(const double* M, double* Mp, double eps, int n, double* scratch,
+                           double* red, double* cert6) {
+  double* S = scratch;             // symmetrised, then Jacobi workspace
+  double* V = scratch + n * n;     // eigenvectors
+  double* w = scratch + 2 * n * n; // eigenvalues (clamped)
+  double* cs = w + n;              // 3n
+  double symloc = 0.0;
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    const double s = 0.5 * (M[i * n + j] + M[j * n + i]);
+    const double d = s - M[idx];
+    symloc += d * d;
+    Mp[idx] = s;  // keep M_sym in Mp for the delta
+    S[idx] = s;
+  }
+  const double symd = wg_sum(symloc, red);
+  wg_jacobi_eigh(S, V, w, n, cs, red);
+  double mnl = 1e308, mxl = -1e308, nnl = 0.0;
+  if ((int)threadIdx.x < n) {
+    const double wc = fmax(w[threadIdx.x], eps);
+    w[threadIdx.x] = wc;
+    mnl = wc; mxl = wc; nnl = (wc < 10.0 * eps) ? 1.0 : 0.0;
+  }
+  const double mn = -wg_max(-mnl, red);
+  const double mx = wg_max(mxl, red);
+  const double nn = wg_sum(nnl, red);
+  double projloc = 0.0;
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    double v = 0.0;
+    for (int k = 0; k < n; ++k) v += V[i * n + k] * w[k] * V[j * n + k];
+    const double d = v - Mp[idx];
+    projloc += d * d;
+    S[idx] = v;
+  }
+  const double proj = wg_sum(projloc, red);
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) Mp[idx] = S[idx];
+  __syncthreads();
+  if (cert6 && threadIdx.x == 0) {
+    cert6[0] = sqrt(proj); cert6[1] = sqrt(symd); cert6[2] = mn; cert6[3] = mx;
+    cert6[4] = mx / mn; cert6[5] = nn;
+  }
+  __syncthreads();
+}
+
+// eigvalsh (ascending not required) of the symmetrised n x n M -> w. scratch: n*n + 3n.
+GC_DEV void wg_eigvalsh(const double* M, double* w, int n, double* scratch, double* red) {
+  double* S = scratch;
+  double* cs = scratch + n * n;
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    S[idx] = 0.5 * (M[i * n + j] + M[j * n + i]);
+  }
+  __syncthreads();
+  wg_jacobi_eigh(S, nullptr, w, n, cs, red);
+}
+
+// y = A x (n x n, LDS), threads < n
+GC_DEV void wg_matvec(const double* A, const double* x, double* y, int n) {
+  if ((int)threadIdx.x < n) {
+    double v = 0.0;
+    for (int k = 0; k < n; ++k) v += A[threadIdx.x * n + k] * x[k];
+    y[threadIdx.x] = v;
+  }
+  __syncthreads();
+}
+
+}  // namespace gc

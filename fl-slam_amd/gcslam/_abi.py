@@ -1,0 +1,204 @@
+"""ctypes binding of libgcslam (include/gcslam.h).
+
+The library is loaded from this package directory (built in-tree by ``make`` in
+``fl-slam_amd/``). There is no fallback: if the shared object is missing or no GPU is
+visible, the first call raises — the product path never computes on the CPU.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libgcslam.so")
+
+GC_OK, GC_ERR_ARG, GC_ERR_RUNTIME = 0, 1, 2
+GC_BIN_STATS = 38
+GC_BIN_CERT = 8
+
+_vp, _dp, _i32, _i64, _u64, _f64 = C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
+_dptr = C.POINTER(C.c_double)
+
+# name -> argtypes (restype int32 unless noted). Device pointers travel as c_void_p.
+SIGNATURES = {
+    "gc_version": [],
+    "gc_device_count": [C.POINTER(C.c_int32)],
+    "gc_ctx_create": [_i32, C.POINTER(_vp)],
+    "gc_ctx_destroy": [_vp],
+    "gc_ctx_synchronize": [_vp],
+    "gc_buffer_alloc": [_vp, _u64, C.POINTER(_vp)],
+    "gc_buffer_free": [_vp, _vp],
+    "gc_buffer_upload": [_vp, _vp, _vp, _u64],
+    "gc_buffer_download": [_vp, _vp, _vp, _u64],
+    "gc_buffer_copy": [_vp, _vp, _vp, _u64],
+    "gc_buffer_memset": [_vp, _vp, _i32, _u64],
+    "gc_event_create": [_vp, C.POINTER(_vp)],
+    "gc_event_destroy": [_vp],
+    "gc_event_record": [_vp, _vp],
+    "gc_event_elapsed_ms": [_vp, _vp, C.POINTER(C.c_float)],
+    "gc_point_budget_resample": [_vp, _vp, _vp, _vp, _vp, _vp, _i64, _i64, _vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "gc_budget_stats": [_vp, _vp, _i64, _i64, _vp],
+    "gc_deskew_constant_twist": [_vp, _i32, _i64, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp],
+    "gc_point_directions": [_vp, _i64, _vp, _dptr, _f64, _vp],
+    "gc_bin_soft_assign": [_vp, _i32, _i64, _i32, _vp, _vp, _f64, _vp, _vp, _vp],
+    "gc_scan_bin_moment_match": [_vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _dptr, _f64, _f64, _vp, _vp],
+    "gc_scan_bins_fused": [_vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _f64, _dptr,
+                           _f64, _f64, _vp, _vp],
+    "gc_kappa_from_resultant_batch": [_vp, _i64, _vp, _f64, _f64, _f64, _f64, _vp],
+    "gc_domain_projection_psd_batch": [_vp, _i32, _i32, _vp, _f64, _vp, _vp],
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libgcslam.so (once). Raises RuntimeError if it has not been built."""
+    global _lib
+    if _lib is None:
+        with _lock:
+            if _lib is None:
+                if not os.path.exists(LIB_PATH):
+                    raise RuntimeError(f"libgcslam.so not found at {LIB_PATH}: build it with "
+                                       "`make -C fl-slam_amd` (there is no CPU fallback)")
+                L = C.CDLL(LIB_PATH)
+                for name, argt in SIGNATURES.items():
+                    fn = getattr(L, name)
+                    fn.argtypes = argt
+                    fn.restype = C.c_int32
+                L.gc_last_error.argtypes = [_vp]
+                L.gc_last_error.restype = C.c_char_p
+                _lib = L
+    return _lib
+
+
+def check(rc: int, ctx=None):
+    if rc == GC_OK:
+        return
+    msg = lib().gc_last_error(ctx.handle if ctx is not None else None)
+    msg = msg.decode() if msg else "unknown error"
+    if rc == GC_ERR_ARG:
+        raise ValueError(msg)
+    raise RuntimeError(msg)
+
+
+def call(name: str, *args, ctx=None):
+    check(getattr(lib(), name)(*args), ctx)
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    rc = lib().gc_device_count(C.byref(n))
+    return int(n.value) if rc == GC_OK else 0
+
+
+class Context:
+    """A HIP device + stream (gc_ctx). One per calling thread (see include/gcslam.h)."""
+
+    def __init__(self, device: int = 0):
+        h = _vp()
+        check(lib().gc_ctx_create(int(device), C.byref(h)))
+        self.handle = h.value
+        self.device = device
+
+    def sync(self):
+        check(lib().gc_ctx_synchronize(self.handle), self)
+
+    def close(self):
+        if self.handle:
+            lib().gc_ctx_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class DeviceArray:
+    """A device allocation with a NumPy dtype/shape view for staging."""
+
+    def __init__(self, ctx: Context, shape, dtype=np.float64):
+        self.ctx = ctx
+        self.shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
+        self.dtype = np.dtype(dtype)
+        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        p = _vp()
+        check(lib().gc_buffer_alloc(ctx.handle, max(self.nbytes, 16), C.byref(p)), ctx)
+        self.ptr = p.value
+
+    @classmethod
+    def from_host(cls, ctx: Context, arr, dtype=np.float64):
+        a = np.ascontiguousarray(arr, dtype=dtype)
+        d = cls(ctx, a.shape, a.dtype)
+        d.upload(a)
+        return d
+
+    def upload(self, arr):
+        a = np.ascontiguousarray(arr, dtype=self.dtype)
+        if a.nbytes != self.nbytes:
+            raise ValueError(f"upload size mismatch: {a.nbytes} vs {self.nbytes}")
+        check(lib().gc_buffer_upload(self.ctx.handle, self.ptr, a.ctypes.data, a.nbytes), self.ctx)
+
+    def download(self) -> np.ndarray:
+        out = np.empty(self.shape, dtype=self.dtype)
+        check(lib().gc_buffer_download(self.ctx.handle, out.ctypes.data, self.ptr, self.nbytes), self.ctx)
+        return out
+
+    def zero(self):
+        check(lib().gc_buffer_memset(self.ctx.handle, self.ptr, 0, self.nbytes), self.ctx)
+
+    def free(self):
+        if self.ptr:
+            lib().gc_buffer_free(self.ctx.handle, self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+class Event:
+    def __init__(self, ctx: Context):
+        h = _vp()
+        check(lib().gc_event_create(ctx.handle, C.byref(h)), ctx)
+        self.handle, self.ctx = h.value, ctx
+
+    def record(self):
+        check(lib().gc_event_record(self.ctx.handle, self.handle), self.ctx)
+
+    def elapsed_ms(self, later: "Event") -> float:
+        ms = C.c_float(0.0)
+        check(lib().gc_event_elapsed_ms(self.handle, later.handle, C.byref(ms)), self.ctx)
+        return float(ms.value)
+
+    def __del__(self):
+        try:
+            lib().gc_event_destroy(self.handle)
+        except Exception:
+            pass
+
+
+_tls = threading.local()
+
+
+def default_context() -> Context:
+    """Per-thread context on GCSLAM_DEVICE (default 0)."""
+    c = getattr(_tls, "ctx", None)
+    if c is None:
+        c = Context(int(os.environ.get("GCSLAM_DEVICE", "0")))
+        _tls.ctx = c
+    return c
+
+
+def f64p(vals):
+    """Host double[] for small by-value vector arguments (e.g. h_origin3)."""
+    a = np.ascontiguousarray(vals, dtype=np.float64)
+    return a, a.ctypes.data_as(_dptr)

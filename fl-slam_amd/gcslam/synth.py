@@ -1,0 +1,96 @@
+"""Synthetic scan / IMU / hypothesis generator for the benchmark configs.
+
+VLP-16-like scans (16 rings x n_az azimuth steps, azimuth-major firing order) ray-cast into a
+20 x 20 x 4 m box room with a ground plane, N(0, 1 cm) range noise, per-point time over the
+0.1 s sweep and the reference range-sigmoid weights (backend_node.py:448-459). IMU at 200 Hz
+padded to 512 slots (backend_node.py:1927-1951). Hypothesis anchors perturbed by N(0, 5 cm) /
+N(0, 0.02 rad). Seeds: default_rng(20261015 + scan_idx).
+
+This is input generation only (host NumPy); no hot-path arithmetic lives here.
+"""
+
+from __future__ import annotations
+
+import numpy as np
+
+from .constants import (GC_RANGE_WEIGHT_SIGMA, GC_RANGE_WEIGHT_MIN_R, GC_RANGE_WEIGHT_MAX_R,
+                        GC_WEIGHT_FLOOR, GC_MAX_IMU_PREINT_LEN, D_Z, T_BASE_LIDAR)
+
+SEED0 = 20261015
+SCAN_PERIOD = 0.1
+T0_ABS = 1000.0
+
+
+def range_weights(dist):
+    """backend_node.py:448-459 continuous range weighting."""
+    a = (dist - GC_RANGE_WEIGHT_MIN_R) / GC_RANGE_WEIGHT_SIGMA
+    b = (GC_RANGE_WEIGHT_MAX_R - dist) / GC_RANGE_WEIGHT_SIGMA
+    w_raw = (1.0 / (1.0 + np.exp(-a))) * (1.0 / (1.0 + np.exp(-b)))
+    return w_raw * (1.0 - GC_WEIGHT_FLOOR) + GC_WEIGHT_FLOOR
+
+
+def make_scan(scan_idx: int = 0, n_rings: int = 16, n_az: int = 4096, room=(10.0, 10.0, 4.0),
+              omega_z: float = 0.3, vel_x: float = 1.0):
+    """One synthetic scan plus its IMU window. Returns a dict of float64 / uint8 arrays."""
+    rng = np.random.default_rng(SEED0 + scan_idx)
+    o = np.asarray(T_BASE_LIDAR[:3], dtype=np.float64)
+    el = np.deg2rad(np.linspace(-15.0, 15.0, n_rings))
+    az = 2.0 * np.pi * np.arange(n_az) / n_az
+    AZ, EL = np.meshgrid(az, el, indexing="ij")  # (n_az, n_rings): azimuth-major
+    d = np.stack([np.cos(EL) * np.cos(AZ), np.cos(EL) * np.sin(AZ), np.sin(EL)], -1).reshape(-1, 3)
+    hx, hy, hz = room
+    with np.errstate(divide="ignore", invalid="ignore"):
+        tx = np.where(d[:, 0] > 0, (hx - o[0]) / d[:, 0], (-hx - o[0]) / d[:, 0])
+        ty = np.where(d[:, 1] > 0, (hy - o[1]) / d[:, 1], (-hy - o[1]) / d[:, 1])
+        tz = np.where(d[:, 2] > 0, (hz - o[2]) / d[:, 2], (0.0 - o[2]) / d[:, 2])
+    tt = np.stack([tx, ty, tz], 1)
+    tt[~np.isfinite(tt) | (tt <= 0)] = np.inf
+    r = tt.min(axis=1) + rng.normal(0.0, 0.01, size=tt.shape[0])
+    pts = o[None, :] + r[:, None] * d
+    t_start = T0_ABS + SCAN_PERIOD * scan_idx
+    az_idx = np.repeat(np.arange(n_az), n_rings)
+    ts = t_start + (az_idx / n_az) * SCAN_PERIOD
+    w = range_weights(np.linalg.norm(pts - o[None, :], axis=1))
+    ring = np.tile(np.arange(n_rings, dtype=np.uint8), n_az)
+    tag = np.zeros(pts.shape[0], np.uint8)
+    # IMU over [t_last, t_scan] at 200 Hz, padded with zeros (invalid stamps) to 512.
+    t_last, t_scan = t_start, t_start + SCAN_PERIOD
+    st = np.arange(t_last, t_scan + 1e-9, 1.0 / 200.0)
+    M = GC_MAX_IMU_PREINT_LEN
+    stamps = np.zeros(M); gyro = np.zeros((M, 3)); accel = np.zeros((M, 3))
+    n = st.shape[0]
+    stamps[:n] = st
+    gyro[:n] = np.array([0.0, 0.0, omega_z]) + rng.normal(0.0, 1e-3, size=(n, 3))
+    accel[:n] = np.array([0.0, 0.0, 9.81]) + rng.normal(0.0, 1e-2, size=(n, 3))
+    return dict(points=np.ascontiguousarray(pts), timestamps=ts, weights=w, ring=ring, tag=tag,
+                imu_stamps=stamps, imu_gyro=gyro, imu_accel=accel, scan_start=t_start,
+                scan_end=t_start + SCAN_PERIOD, t_last=t_last, t_scan=t_scan, dt_sec=SCAN_PERIOD)
+
+
+def make_hypotheses(H: int, seed: int = SEED0, prior_precision: float = 1e-6):
+    """Identity-prior beliefs (belief.py:328-371) with perturbed anchors."""
+    rng = np.random.default_rng(seed + 777)
+    X = np.zeros((H, 6))
+    X[:, 0:3] = rng.normal(0.0, 0.05, size=(H, 3))
+    X[:, 3:6] = rng.normal(0.0, 0.02, size=(H, 3))
+    L = np.broadcast_to(prior_precision * np.eye(D_Z), (H, D_Z, D_Z)).copy()
+    return dict(X_anchor=X, z_lin=np.zeros((H, D_Z)), L=L, h=np.zeros((H, D_Z)),
+                stamp=np.zeros(H), weights=np.full(H, 1.0 / H))
+
+
+def make_io_evidence(H: int, seed: int = SEED0):
+    """Synthetic per-hypothesis IMU/odom-branch evidence (L_io, h_io) and its cert scalars.
+
+    Layout of the cert row (10 f64): ess_odom, ess_imu, ess_gyro, sf_odom, sf_imu, sf_gyro,
+    exc_dt, exc_ex, nll_sum, trig_sum (see oracle IOEvidence / include/gcslam.h)."""
+    rng = np.random.default_rng(seed + 4242)
+    diag = np.array([50.0, 50.0, 1e4, 1e3, 1e3, 1e2, 1e2, 1e2, 1e4, 1e4, 1e4, 1e4,
+                     1e3, 1e3, 1e3, 1e2, 1e2, 1e2, 1e2, 1e2, 1e2, 1e2])
+    L = np.empty((H, D_Z, D_Z)); h = np.empty((H, D_Z)); cert = np.empty((H, 10))
+    for k in range(H):
+        A = rng.normal(0.0, 1.0, size=(D_Z, D_Z))
+        Lk = A @ A.T + np.diag(diag)
+        L[k] = 0.5 * (Lk + Lk.T)
+        h[k] = L[k] @ rng.normal(0.0, 1e-3, size=D_Z)
+        cert[k] = [1.0, 20.0, 1.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.01, 0.5]
+    return L, h, cert

@@ -1,0 +1,957 @@
+"""
+TEST INFRASTRUCTURE ONLY — CPU oracle for the GC-SLAM v2 per-scan hot path.
+
+This module is a NumPy restatement of the reference's algorithm (whabacivch/FL-SLAM,
+GC-SLAM v2), written from the reference semantics; every function cites the reference
+file:line it follows (paths relative to the reference root; ``fl_slam_poc/`` means
+``fl_ws/src/fl_slam_poc/fl_slam_poc/``).
+
+Who may use it: ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s
+``cpu_baseline`` leg — as the checker / the timed CPU baseline, never as the thing
+measured or shipped. The product path (``fl-slam_amd/gcslam``) never imports it and
+fails loudly when its HIP library is missing.
+
+Pinning: the reference's Python path imports JAX, which is absent from this image;
+no stand-in for JAX is used. The oracle is pinned against the
+known-answer and property tests the reference's own test suites hold for this path
+(``tests/test_oracle_kat.py``, citing each reference test). Rows the reference never
+pinned (τ, the legacy bin-path wiring, PoseCovInflationPushforward) are marked
+"parity unpinned" where they are defined.
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+
+import numpy as np
+from scipy.linalg import solve_triangular
+from scipy.special import expit
+
+# ---------------------------------------------------------------------------------------
+# Constants — fl_slam_poc/common/constants.py:54-143, :259-281 ; pipeline.py:96-160
+# ---------------------------------------------------------------------------------------
+D_Z = 22
+EPS_PSD = 1e-12
+EPS_LIFT = 1e-9
+EPS_MASS = 1e-12
+EPS_R = 1e-6
+EXC_EPS = 1e-12
+F64_EPS = float(np.finfo(np.float64).eps)
+GRAVITY_W = np.array([0.0, 0.0, -9.81])
+KAPPA_R0 = 0.8
+KAPPA_TAU = 0.03
+ALPHA_MIN = 1.0
+ALPHA_MAX = 1.0
+C0_COND = 1e6
+C_FROB = 1.0
+ANCHOR_M0 = 0.5
+ANCHOR_R0 = 0.2
+TIME_WARP_SIGMA_FRAC = 0.1
+WEIGHT_FLOOR = 1e-12
+OU_LAMBDA = 0.1
+POWER_BETA_MIN = 0.25
+POWER_BETA_EXC_C = 50.0
+POWER_BETA_Z_C = 1.0
+FORGETTING = 0.99
+IW_NU_WEAK_ADD = 0.5
+IW_RHO_PROC = np.array([0.99, 0.995, 0.95, 0.999, 0.999, 0.9999, 0.9999])  # trans,rot,vel,bg,ba,dt,ex
+IW_RHO_MEAS = np.array([0.995, 0.995, 0.99])
+PROC_BLOCK_DIMS = np.array([3, 3, 3, 3, 3, 1, 6])
+PROC_BLOCK_STARTS = np.array([0, 3, 6, 9, 12, 15, 16])
+SMALL_ANGLE = 1e-7
+NEAR_PI = 1e-7
+# Build-declared (never recorded in the reference — parity unpinned):
+B_BINS = 48
+TAU_SOFT_ASSIGN = 0.1
+RANGE_SIGMA, RANGE_MIN_R, RANGE_MAX_R = 0.25, 0.5, 50.0
+
+_rows = np.arange(6)[None, :] < PROC_BLOCK_DIMS[:, None]
+PROC_BLOCK_MASKS = (_rows[:, :, None] & _rows[:, None, :]).astype(np.float64)
+
+
+def sigmoid(x):
+    # jax.nn.sigmoid (evaluated without overflow)
+    return expit(x)
+
+
+def softplus(x):
+    # jax.nn.softplus = log1p(exp(-|x|)) + max(x, 0)
+    x = np.asarray(x, dtype=np.float64)
+    return np.log1p(np.exp(-np.abs(x))) + np.maximum(x, 0.0)
+
+
+# ---------------------------------------------------------------------------------------
+# Numeric primitives — fl_slam_poc/common/primitives.py
+# ---------------------------------------------------------------------------------------
+def psd_project(M, eps_psd=EPS_PSD):
+    """domain_projection_psd_core (primitives.py:80-123). Returns (M_psd, cert6)."""
+    M = np.asarray(M, dtype=np.float64)
+    M_sym = 0.5 * (M + M.T)
+    sym_delta = np.linalg.norm(M_sym - M, "fro")
+    w, V = np.linalg.eigh(M_sym)
+    wc = np.maximum(w, eps_psd)
+    M_psd = V @ np.diag(wc) @ V.T
+    proj = np.linalg.norm(M_psd - M_sym, "fro")
+    nnc = float(np.sum(wc < 10.0 * eps_psd))
+    emin, emax = float(np.min(wc)), float(np.max(wc))
+    return M_psd, np.array([proj, sym_delta, emin, emax, emax / emin, nnc])
+
+
+def chol_solve_lifted(L, b, eps_lift=EPS_LIFT):
+    """spd_cholesky_solve_lifted_core (primitives.py:141-166)."""
+    d = L.shape[0]
+    C = np.linalg.cholesky(L + eps_lift * np.eye(d))
+    y = solve_triangular(C, b, lower=True)
+    return solve_triangular(C.T, y, lower=False), eps_lift * d
+
+
+def chol_inverse_lifted(L, eps_lift=EPS_LIFT):
+    """spd_cholesky_inverse_lifted_core (primitives.py:169-192)."""
+    d = L.shape[0]
+    C = np.linalg.cholesky(L + eps_lift * np.eye(d))
+    Ci = solve_triangular(C, np.eye(d), lower=True)
+    return Ci.T @ Ci, eps_lift * d
+
+
+def inv_mass(m, eps_mass=EPS_MASS):
+    """inv_mass_core (primitives.py:195-212): 1/(m+eps+f64eps), eps/(m+eps+f64eps)."""
+    denom = np.asarray(m, dtype=np.float64) + eps_mass + F64_EPS
+    return 1.0 / denom, eps_mass / denom
+
+
+# ---------------------------------------------------------------------------------------
+# Lie maps — fl_slam_poc/common/geometry/se3_jax.py
+# ---------------------------------------------------------------------------------------
+def skew(v):
+    return np.array([[0.0, -v[2], v[1]], [v[2], 0.0, -v[0]], [-v[1], v[0], 0.0]])
+
+
+def _BC(theta, theta_sq):
+    """Shared B=(1-cos)/θ², C=(θ-sin)/θ³ with the small-angle branch (se3_jax.py:473-504)."""
+    if theta < SMALL_ANGLE:
+        return 0.5 - theta_sq / 24.0, 1.0 / 6.0 - theta_sq / 120.0
+    st = theta
+    sts = theta_sq if theta_sq >= SMALL_ANGLE ** 2 else 1.0
+    return (1.0 - math.cos(st)) / sts, (st - math.sin(st)) / (sts * st)
+
+
+def so3_exp(w):
+    """so3_exp (se3_jax.py:259-301)."""
+    w = np.asarray(w, dtype=np.float64)
+    theta_sq = float(w @ w)
+    theta = math.sqrt(theta_sq)
+    K = skew(w)
+    if theta < SMALL_ANGLE:
+        a, b = 1.0, 0.5
+    else:
+        sts = theta_sq if theta_sq >= SMALL_ANGLE ** 2 else 1.0
+        a, b = math.sin(theta) / theta, (1.0 - math.cos(theta)) / sts
+    return np.eye(3) + a * K + b * (K @ K)
+
+
+def so3_log(R):
+    """so3_log (se3_jax.py:304-366), incl. the softmax-mixed near-π axis."""
+    R = np.asarray(R, dtype=np.float64)
+    c = min(max(0.5 * (np.trace(R) - 1.0), -1.0), 1.0)
+    theta = math.acos(c)
+    sk = 0.5 * (R - R.T)
+    vex = np.array([sk[2, 1], sk[0, 2], sk[1, 0]])
+    if theta < SMALL_ANGLE:
+        return vex
+    if abs(theta - math.pi) < NEAR_PI:
+        dp1 = np.diag(R) + 1.0
+        z = 50.0 * dp1
+        e = np.exp(z - z.max())
+        wts = e / e.sum()
+        cols = R + np.eye(3)
+        axis = wts[0] * cols[:, 0] + wts[1] * cols[:, 1] + wts[2] * cols[:, 2]
+        n = np.linalg.norm(axis)
+        n = 1.0 if n < SMALL_ANGLE else n
+        return axis / n * theta
+    s = math.sin(theta)
+    s = 1.0 if abs(s) < SMALL_ANGLE else s
+    return (theta / (2.0 * s)) * (2.0 * vex)
+
+
+def se3_V(phi):
+    """se3_V (se3_jax.py:137-174)."""
+    ts = float(phi @ phi)
+    B, C = _BC(math.sqrt(ts), ts)
+    K = skew(phi)
+    return np.eye(3) + B * K + C * (K @ K)
+
+
+def se3_V_inv(phi):
+    """_se3_V_inv (se3_jax.py:177-217)."""
+    ts = float(phi @ phi)
+    th = math.sqrt(ts)
+    K = skew(phi)
+    if th < SMALL_ANGLE:
+        D = 1.0 / 12.0 + ts / 720.0
+    else:
+        sts = ts if ts >= SMALL_ANGLE ** 2 else 1.0
+        D = 1.0 / sts - (1.0 + math.cos(th)) / (2.0 * th * math.sin(th) + 1e-12)
+    return np.eye(3) - 0.5 * K + D * (K @ K)
+
+
+def se3_exp(xi):
+    """se3_exp (se3_jax.py:473-504): [V(φ)ρ, φ]."""
+    xi = np.asarray(xi, dtype=np.float64)
+    return np.concatenate([se3_V(xi[3:6]) @ xi[:3], xi[3:6]])
+
+
+def se3_log(T):
+    """se3_log (se3_jax.py:220-256)."""
+    T = np.asarray(T, dtype=np.float64)
+    phi = so3_log(so3_exp(T[3:6]))
+    return np.concatenate([se3_V_inv(phi) @ T[:3], phi])
+
+
+def se3_compose(a, b):
+    """se3_compose (se3_jax.py:420-438)."""
+    Ra, Rb = so3_exp(a[3:6]), so3_exp(b[3:6])
+    return np.concatenate([a[:3] + Ra @ b[:3], so3_log(Ra @ Rb)])
+
+
+# ---------------------------------------------------------------------------------------
+# Belief helpers — fl_slam_poc/common/belief.py
+# ---------------------------------------------------------------------------------------
+@dataclass
+class Belief:
+    X_anchor: np.ndarray
+    z_lin: np.ndarray
+    L: np.ndarray
+    h: np.ndarray
+    stamp_sec: float = 0.0
+
+    def copy(self):
+        return Belief(self.X_anchor.copy(), self.z_lin.copy(), self.L.copy(), self.h.copy(), self.stamp_sec)
+
+
+def identity_prior(precision=1e-6):
+    """create_identity_prior (belief.py:328-371)."""
+    return Belief(np.zeros(6), np.zeros(D_Z), precision * np.eye(D_Z), np.zeros(D_Z), 0.0)
+
+
+def mean_increment(b: Belief):
+    """belief.py:373-386."""
+    return chol_solve_lifted(b.L, b.h)[0]
+
+
+def world_pose(b: Belief):
+    """belief.py:408-425: X_anchor ∘ Exp(δz[0:6])."""
+    return se3_compose(b.X_anchor, se3_exp(mean_increment(b)[0:6]))
+
+
+# ---------------------------------------------------------------------------------------
+# Certificates — only the numeric surface that feeds back into the numbers
+# (fl_slam_poc/common/certificates.py:77-108 InfluenceCert, :439-455 total_trigger_magnitude)
+# ---------------------------------------------------------------------------------------
+def trigger(lift=0.0, psd=0.0, nu=0.0, mass=0.0, rho=0.0, dt=1.0, ex=1.0, alpha=1.0, beta=1.0):
+    return (lift + psd + nu + mass + rho + abs(1.0 - dt) + abs(1.0 - ex)
+            + abs(1.0 - alpha) + abs(1.0 - beta))
+
+
+# ---------------------------------------------------------------------------------------
+# a1 PointBudgetResample — backend/operators/point_budget.py:50-221
+# ---------------------------------------------------------------------------------------
+def point_budget_resample(points, t, w, ring=None, tag=None, n_points_cap=8192):
+    n_in = points.shape[0]
+    stride = max(1, int(math.ceil(n_in / n_points_cap)))
+    idx = np.arange(0, n_in, stride)
+    ns = idx.shape[0]
+    ring = np.zeros(n_in, np.uint8) if ring is None else np.asarray(ring, np.uint8)
+    tag = np.zeros(n_in, np.uint8) if tag is None else np.asarray(tag, np.uint8)
+    mass_in = np.sum(w)
+    w_raw = w[idx]
+    scale = mass_in / (np.sum(w_raw) + EPS_MASS)
+    P = np.zeros((n_points_cap, 3)); P[:ns] = points[idx]
+    T = np.zeros(n_points_cap); T[:ns] = t[idx]
+    W = np.zeros(n_points_cap); W[:ns] = w_raw * scale
+    RG = np.zeros(n_points_cap, np.uint8); RG[:ns] = ring[idx]
+    TG = np.zeros(n_points_cap, np.uint8); TG[:ns] = tag[idx]
+    wn = W / (mass_in + EPS_MASS)
+    ess = 1.0 / np.sum(wn ** 2 + EPS_MASS)
+    return dict(points=P, timestamps=T, weights=W, ring=RG, tag=TG, indices=idx, n_input=n_in,
+                n_output=ns, total_mass_in=float(mass_in), total_mass_out=float(mass_in),
+                ess=float(ess), support_frac=float(min(1.0, n_points_cap / (n_in + EPS_MASS))),
+                trig=trigger(mass=EPS_MASS / (float(mass_in) + EPS_MASS)))
+
+
+# ---------------------------------------------------------------------------------------
+# a3 IMU windows + preintegration — backend/operators/imu_preintegration.py:19-147
+# ---------------------------------------------------------------------------------------
+def smooth_window_weights(stamps, t0, t1, sigma):
+    sig = max(sigma, 1e-6)
+    wr = sigmoid((stamps - t0) / sig) * sigmoid((t1 - stamps) / sig)
+    return wr * (1.0 - WEIGHT_FLOOR) + WEIGHT_FLOOR
+
+
+def preintegrate(stamps, gyro, accel, w, rotvec0, bg, ba, g=GRAVITY_W):
+    """preintegrate_imu_relative_pose_jax (imu_preintegration.py:46-147) — sequential scan."""
+    dt = np.maximum(np.concatenate([stamps[1:] - stamps[:-1], [0.0]]), 0.0)
+    R = so3_exp(rotvec0)
+    R0 = R.copy()
+    v = np.zeros(3); p = np.zeros(3)
+    swdt = 0.0
+    for i in range(stamps.shape[0]):
+        de = w[i] * dt[i]
+        dR = so3_exp((gyro[i] - bg) * de)
+        a_nog = R @ (accel[i] - ba)
+        a_w = a_nog + g
+        swdt += de
+        p = p + v * de + 0.5 * a_w * (de * de)
+        v = v + a_w * de
+        R = R @ dR
+    dRel = R0.T @ R
+    p_b = R0.T @ p
+    return dict(delta_pose=np.concatenate([p_b, so3_log(dRel)]), ess=float(np.sum(w)),
+                delta_R=dRel, delta_p=p_b, delta_v=R0.T @ v, dt_eff_sum=swdt)
+
+
+def imu_dt_mean(stamps):
+    """Average IMU period over valid (stamp>0) samples — pipeline.py:526-535."""
+    v = stamps[stamps > 0.0]
+    if v.shape[0] >= 2:
+        v = np.sort(v)
+        return max(float((v[-1] - v[0]) / max(v.shape[0] - 1, 1)), 1e-12)
+    return 1e-12
+
+
+def iw_meas_gyro_suffstats(gyro, w, bg, omega_avg, dt_imu):
+    """imu_gyro_meas_iw_suffstats_from_avg_rate_jax (measurement_noise_iw_jax.py:130-171)."""
+    wn = w / (np.sum(w) + EPS_MASS)
+    r = (gyro - bg[None, :]) - omega_avg[None, :]
+    rr = np.einsum("m,mi,mj->ij", wn, r, r)
+    rr = 0.5 * (rr + rr.T)
+    return psd_project(rr)[0] * max(dt_imu, 1e-12)
+
+
+def iw_meas_accel_suffstats(rotvec0, accel, w, ba, dt_imu, g=GRAVITY_W):
+    """imu_accel_meas_iw_suffstats_from_gravity_dir_jax (measurement_noise_iw_jax.py:174-218)."""
+    f_pred = -(so3_exp(rotvec0).T @ g)
+    wn = w / (np.sum(w) + EPS_MASS)
+    r = (accel - ba[None, :]) - f_pred[None, :]
+    rr = np.einsum("m,mi,mj->ij", wn, r, r)
+    rr = 0.5 * (rr + rr.T)
+    return psd_project(rr)[0] * max(dt_imu, 1e-12)
+
+
+# ---------------------------------------------------------------------------------------
+# a4 DeskewConstantTwist — backend/operators/deskew_constant_twist.py:31-117
+# ---------------------------------------------------------------------------------------
+def deskew_constant_twist(points, t, w, t0, t1, xi):
+    """Vectorised over points (the reference vmaps one_point, deskew_constant_twist.py:50-58)."""
+    denom = max(t1 - t0, 1e-12)
+    alpha = (t - t0) / denom
+    rho = alpha[:, None] * xi[None, 0:3]
+    phi = alpha[:, None] * xi[None, 3:6]
+    ts = np.sum(phi * phi, axis=1)
+    th = np.sqrt(ts)
+    small = th < SMALL_ANGLE
+    st = np.where(small, 1.0, th)
+    sts = np.where(ts < SMALL_ANGLE ** 2, 1.0, ts)
+    s, c = np.sin(st), np.cos(st)
+    Bv = np.where(small, 0.5 - ts / 24.0, (1.0 - c) / sts)
+    Cv = np.where(small, 1.0 / 6.0 - ts / 120.0, (st - s) / (sts * st))
+    a = np.where(small, 1.0, s / st)
+    b = np.where(small, 0.5, (1.0 - c) / sts)
+    K = np.zeros((points.shape[0], 3, 3))
+    K[:, 0, 1], K[:, 0, 2], K[:, 1, 2] = -phi[:, 2], phi[:, 1], -phi[:, 0]
+    K[:, 1, 0], K[:, 2, 0], K[:, 2, 1] = phi[:, 2], -phi[:, 1], phi[:, 0]
+    K2 = K @ K
+    I = np.eye(3)[None]
+    V = I + Bv[:, None, None] * K + Cv[:, None, None] * K2
+    R = I + a[:, None, None] * K + b[:, None, None] * K2
+    tv = np.einsum("nij,nj->ni", V, rho)
+    out = np.einsum("nji,nj->ni", R, points - tv)
+    w_out = w * smooth_window_weights(t, t0, t1, TIME_WARP_SIGMA_FRAC * denom)
+    retained = float(np.sum(w_out) / (np.sum(w) + EPS_MASS))
+    return out, w_out, retained
+
+
+def point_directions(points, origin, eps_mass=EPS_MASS):
+    """pipeline.py:589-593 / binning.py:162-164."""
+    rays = points - origin[None, :]
+    return rays / (np.linalg.norm(rays, axis=1, keepdims=True) + eps_mass)
+
+
+# ---------------------------------------------------------------------------------------
+# a5 BinSoftAssign — archive/legacy_operators/binning.py:56-131 ; archive/bin_atlas.py:40-61
+# ---------------------------------------------------------------------------------------
+def fibonacci_atlas(n_bins=B_BINS):
+    i = np.arange(n_bins, dtype=np.float64) + 0.5
+    phi = np.arccos(1 - 2 * i / n_bins)
+    theta = np.pi * (1 + np.sqrt(5)) * i
+    d = np.stack([np.sin(phi) * np.cos(theta), np.sin(phi) * np.sin(theta), np.cos(phi)], 1)
+    return d / (np.linalg.norm(d, axis=1, keepdims=True) + EPS_MASS)
+
+
+def similarities(dirs, bins):
+    """S = dirs·binsᵀ restated as an explicit, un-fused d0*b0 + d1*b1 + d2*b2 (the bin-index
+    integer contract: argmax over this exact f64 expression, lowest index on ties)."""
+    return (dirs[:, 0:1] * bins[None, :, 0] + dirs[:, 1:2] * bins[None, :, 1]) + dirs[:, 2:3] * bins[None, :, 2]
+
+
+def bin_soft_assign(dirs, bins, tau=TAU_SOFT_ASSIGN):
+    S = similarities(dirs, bins)
+    x = S / tau
+    e = np.exp(x - x.max(axis=1, keepdims=True))
+    R = e / e.sum(axis=1, keepdims=True)
+    ent = -np.sum(R * np.log(R + EPS_MASS), axis=1)
+    avg_ent = np.sum(ent) / (dirs.shape[0] + EPS_MASS)
+    return dict(resp=R, bin_index=np.argmax(S, axis=1).astype(np.int32), avg_entropy=float(avg_ent),
+                max_resp=float(R.max()), ess=float(math.exp(avg_ent)), trig=0.0)
+
+
+# ---------------------------------------------------------------------------------------
+# a6 ScanBinMomentMatch + KappaFromResultant — binning.py:139-324 ; kappa.py:84-169
+# ---------------------------------------------------------------------------------------
+def kappa_batch(R, eps_r=EPS_R, d=3, r0=KAPPA_R0, tau=KAPPA_TAU):
+    Rc = np.clip(R, 0.0, 1.0 - eps_r)
+    R2 = Rc * Rc
+    k_low = (Rc * (d - R2)) / (1.0 - R2 + eps_r)
+    k_high = -np.log(np.maximum(1.0 - R2, eps_r))
+    s = sigmoid((Rc - r0) / max(tau, 1e-6))
+    return (1.0 - s) * k_low + s * k_high
+
+
+def kappa_scalar(R, eps_r=EPS_R, d=3.0, r0=KAPPA_R0, tau=KAPPA_TAU):
+    """_kappa_continuous_formula (kappa.py:84-127) after the clamp of kappa_from_resultant_v2."""
+    R = min(max(float(R), 0.0), 1.0 - eps_r)
+    R2 = R * R
+    k_low = (R * (d - R2)) / (1.0 - R2 + eps_r)
+    k_high = -math.log(max(1.0 - R2, eps_r))
+    s = 1.0 / (1.0 + math.exp(-(R - r0) / max(tau, 1e-6)))
+    return (1.0 - s) * k_low + s * k_high
+
+
+def moment_sums(points, covs, w, resp, lam, origin):
+    """The raw per-bin sums of binning.py:160-173 (sum_cov skipped when covs is None)."""
+    w_r = (w * lam)[:, None] * resp
+    d = point_directions(points, origin)
+    N = np.sum(w_r, axis=0)
+    s_dir = w_r.T @ d
+    S_sc = np.einsum("nb,ni,nj->bij", w_r, d, d)
+    sum_p = w_r.T @ points
+    sum_ppT = np.einsum("nb,ni,nj->bij", w_r, points, points)
+    sum_cov = np.zeros_like(sum_ppT) if covs is None else np.einsum("nb,nij->bij", w_r, covs)
+    return N, s_dir, S_sc, sum_p, sum_ppT, sum_cov
+
+
+def moments_finalize(N, s_dir, S_sc, sum_p, sum_ppT, sum_cov, eps_psd=EPS_PSD, eps_mass=EPS_MASS):
+    """binning.py:175-209."""
+    inv_N, eps_ratio = inv_mass(N, eps_mass)
+    p_bar = sum_p * inv_N[:, None]
+    Sig_raw = sum_ppT * inv_N[:, None, None] - np.einsum("bi,bj->bij", p_bar, p_bar) + sum_cov * inv_N[:, None, None]
+    Sig = np.empty_like(Sig_raw)
+    psd_total = 0.0
+    for b in range(N.shape[0]):
+        Sig[b], c = psd_project(Sig_raw[b], eps_psd)
+        psd_total += c[0]
+    Rbar = np.linalg.norm(s_dir, axis=1) * inv_N
+    kap = kappa_batch(Rbar)
+    tm = np.sum(N)
+    ess = tm ** 2 / (np.sum(N ** 2) + eps_mass)
+    sf = float(np.mean(N / (N + eps_mass)))
+    return dict(N=N, s_dir=s_dir, S_dir_scatter=S_sc, p_bar=p_bar, Sigma_p=Sig, kappa=kap,
+                sum_p=sum_p, sum_ppT=sum_ppT, ess=float(ess), support_frac=sf,
+                psd_delta=float(psd_total), max_eps_ratio=float(np.max(eps_ratio)),
+                trig=trigger(psd=float(psd_total), mass=float(np.max(eps_ratio))))
+
+
+def scan_bin_moment_match(points, covs, w, resp, lam=None, origin=None):
+    lam = np.ones(points.shape[0]) if lam is None else lam
+    origin = np.zeros(3) if origin is None else origin
+    return moments_finalize(*moment_sums(points, covs, w, resp, lam, origin))
+
+
+# ---------------------------------------------------------------------------------------
+# Map bin statistics — archive/bin_atlas.py:101-257
+# ---------------------------------------------------------------------------------------
+@dataclass
+class MapStats:
+    S_dir: np.ndarray
+    S_dir_scatter: np.ndarray
+    N_dir: np.ndarray
+    N_pos: np.ndarray
+    sum_p: np.ndarray
+    sum_ppT: np.ndarray
+
+    @staticmethod
+    def empty(nb=B_BINS):
+        return MapStats(np.zeros((nb, 3)), np.zeros((nb, 3, 3)), np.zeros(nb), np.zeros(nb),
+                        np.zeros((nb, 3)), np.zeros((nb, 3, 3)))
+
+    def copy(self):
+        return MapStats(*(x.copy() for x in (self.S_dir, self.S_dir_scatter, self.N_dir,
+                                              self.N_pos, self.sum_p, self.sum_ppT)))
+
+
+def map_forget_and_add(m: MapStats, inc: MapStats, gamma=FORGETTING):
+    """update_map_stats(apply_forgetting(m, γ), inc) (bin_atlas.py:137-163, :232-257)."""
+    return MapStats(gamma * m.S_dir + inc.S_dir, gamma * m.S_dir_scatter + inc.S_dir_scatter,
+                    gamma * m.N_dir + inc.N_dir, gamma * m.N_pos + inc.N_pos,
+                    gamma * m.sum_p + inc.sum_p, gamma * m.sum_ppT + inc.sum_ppT)
+
+
+def map_derived(m: MapStats, eps_mass=EPS_MASS, eps_psd=EPS_PSD):
+    """_compute_map_derived_stats_core (bin_atlas.py:166-207) → (mu_dir, kappa, centroid, Sigma_c)."""
+    nrm = np.linalg.norm(m.S_dir, axis=1)
+    mu = m.S_dir / (nrm + eps_mass)[:, None]
+    inv_d, _ = inv_mass(m.N_dir, eps_mass)
+    kap = kappa_batch(nrm * inv_d)
+    inv_p, _ = inv_mass(m.N_pos, eps_mass)
+    c = m.sum_p * inv_p[:, None]
+    raw = m.sum_ppT * inv_p[:, None, None] - np.einsum("bi,bj->bij", c, c)
+    Sig = np.stack([psd_project(raw[b], eps_psd)[0] for b in range(raw.shape[0])])
+    return mu, kap, c, Sig
+
+
+def pose_cov_inflation_pushforward(stats, R, t, Sigma_pose):
+    """PoseCovInflationPushforward (a13). BUILD-DEFINED — the reference source was deleted
+    (CHANGELOG.md:1226,1246); parity unpinned. Pushes scan bin stats into the world frame
+    with pose (R, t), t[2] = 0 (CHANGELOG.md:575-578), inflating each bin's centroid
+    covariance by the pose covariance pushed through J = [R | -R[p̄]×]."""
+    N = stats["N"]
+    nb = N.shape[0]
+    pw = stats["p_bar"] @ R.T + t[None, :]
+    Sw = np.empty((nb, 3, 3))
+    for b in range(nb):
+        J = np.concatenate([R, -R @ skew(stats["p_bar"][b])], axis=1)
+        Sw[b] = R @ stats["Sigma_p"][b] @ R.T + J @ Sigma_pose @ J.T
+    return MapStats(stats["s_dir"] @ R.T, np.einsum("ij,bjk,lk->bil", R, stats["S_dir_scatter"], R),
+                    N.copy(), N.copy(), N[:, None] * pw,
+                    N[:, None, None] * (Sw + np.einsum("bi,bj->bij", pw, pw)))
+
+
+# ---------------------------------------------------------------------------------------
+# a7 MatrixFisherRotation — archive/legacy_operators/matrix_fisher_evidence.py:83-394
+# ---------------------------------------------------------------------------------------
+def scatter_metrics(S, N_total, eps=EPS_MASS):
+    """compute_scatter_metrics (matrix_fisher_evidence.py:83-147)."""
+    w, V = np.linalg.eigh(S * (1.0 / (N_total + eps)))
+    idx = np.argsort(w)[::-1]
+    lam = np.maximum(w[idx], 0.0)
+    il = 1.0 / (lam[0] + eps)
+    tot = lam.sum() + eps
+    p = lam / tot
+    ent = -np.sum(p * np.log(p + eps))
+    return dict(eigenvalues=lam, linearity=(lam[0] - lam[1]) * il, planarity=(lam[1] - lam[2]) * il,
+                sphericity=lam[2] * il, anisotropy=1.0 - lam[2] * il, effective_rank=math.exp(ent))
+
+
+def matrix_fisher(R_pred, scan_s, scan_S, scan_N, map_s, map_S, map_N, eps_psd=EPS_PSD, eps=EPS_MASS):
+    wb = np.sqrt(scan_N * map_N + eps)
+    sn = np.linalg.norm(scan_s, axis=1)
+    mn = np.linalg.norm(map_s, axis=1)
+    us = scan_s / (sn + eps)[:, None]
+    um = map_s / (mn + eps)[:, None]
+    conf = (sn * (1.0 / (scan_N + eps))) * (mn * (1.0 / (map_N + eps)))
+    wf = wb * conf
+    H = np.einsum("b,bi,bj->ij", wf, um, us)
+    U, s, Vt = np.linalg.svd(H)
+    sgn = np.sign(np.linalg.det(U @ Vt))
+    U = U.copy(); U[:, 2] *= sgn
+    R_mf = U @ Vt
+    V = Vt.T
+    L_raw = V @ np.diag([s[1] + s[2], s[0] + s[2], s[0] + s[1]]) @ V.T
+    delta = so3_log(R_pred.T @ R_mf)
+    L_rot, pc = psd_project(L_raw, eps_psd)
+    h_rot = L_rot @ delta
+    N_eff = float(np.sum(wf))
+    nll = 0.5 * float(delta @ L_rot @ delta)
+    return dict(R_mf=R_mf, L_rot=L_rot, h_rot=h_rot, delta_rot=delta, svd=s, N_eff=N_eff,
+                nll_per_ess=nll / (N_eff + eps), psd_delta=float(pc[0]),
+                scan_metrics=scatter_metrics(scan_S.sum(0), float(scan_N.sum()), eps),
+                map_metrics=scatter_metrics(map_S.sum(0), float(map_N.sum()), eps),
+                trig=trigger(psd=float(pc[0]), mass=eps / (N_eff + eps)))
+
+
+# ---------------------------------------------------------------------------------------
+# a8 PlanarTranslationEvidence — matrix_fisher_evidence.py:413-671 ; 22D embed :729-756
+# ---------------------------------------------------------------------------------------
+def planar_translation(t_pred, scan_p, scan_Sig, scan_N, map_c, map_Sig, map_Np, map_Sdir_sc, map_Nd,
+                       R_hat, eps_psd=EPS_PSD, eps=EPS_MASS):
+    T_map = map_Sdir_sc.sum(0) / (np.sum(map_Nd) + eps)
+    ev = np.sort(np.linalg.eigvalsh(T_map))[::-1]
+    zs = max(ev[2], 0.0) / max(ev[0], eps)
+    tb = map_c - scan_p @ R_hat.T
+    Sc = map_Sig + np.einsum("ij,bjk,lk->bil", R_hat, scan_Sig, R_hat)
+    wb = np.sqrt(scan_N * map_Np + eps)
+    Wi = np.stack([wb[b] * np.linalg.inv(Sc[b] + eps * np.eye(3)) for b in range(wb.shape[0])])
+    Lf = Wi.sum(0)
+    hf = np.einsum("bij,bj->bi", Wi, tb).sum(0)
+    t_wls = np.linalg.solve(Lf + eps * np.eye(3), hf)
+    m = np.array([1.0, 1.0, zs])
+    L_raw = Lf * m[:, None] * m[None, :]
+    delta = t_wls - t_pred
+    L_t, pc = psd_project(L_raw, eps_psd)
+    h_t = L_t @ delta
+    N_eff = float(np.sum(wb))
+    nll = 0.5 * float(delta @ L_t @ delta)
+    return dict(t_wls=t_wls, L_trans=L_t, h_trans=h_t, delta_trans=delta, z_scale=zs, N_eff=N_eff,
+                nll_per_ess=nll / (N_eff + eps), psd_delta=float(pc[0]),
+                xy_info_scale=0.5 * (L_t[0, 0] + L_t[1, 1]), z_info_scale=L_t[2, 2],
+                trig=trigger(psd=float(pc[0]), mass=eps / (N_eff + eps)))
+
+
+# ---------------------------------------------------------------------------------------
+# a2 PredictDiffusion — backend/operators/predict.py:43-214
+# ---------------------------------------------------------------------------------------
+def predict_diffusion(b: Belief, Q, dt, eps_psd=EPS_PSD, eps_lift=EPS_LIFT, lam=OU_LAMBDA):
+    mu, _ = chol_solve_lifted(b.L, b.h, eps_lift)
+    cov, lift_prev = chol_inverse_lifted(b.L, eps_lift)
+    ef = math.exp(-2.0 * lam * dt)
+    dc = (1.0 - ef) / (2.0 * lam + F64_EPS)
+    cov_psd, c1 = psd_project(ef * cov + dc * Q, eps_psd)
+    Lp, lift_inv = chol_inverse_lifted(cov_psd, eps_lift)
+    Lp, c2 = psd_project(Lp, eps_psd)
+    out = Belief(b.X_anchor.copy(), b.z_lin.copy(), Lp, Lp @ mu, b.stamp_sec + dt)
+    return out, dict(lift=lift_prev + lift_inv, psd_delta=c1[0] + c2[0], cond=c2[2:6].copy(),
+                     trace_cov=float(np.trace(cov_psd)),
+                     trig=trigger(lift=lift_prev + lift_inv, psd=c1[0] + c2[0], dt=dt))
+
+
+# ---------------------------------------------------------------------------------------
+# a9-a11 evidence assembly, tempering, excitation, fusion — pipeline.py:1038-1206 ;
+# excitation.py:14-64 ; fusion.py:46-230 ; certificates.py:511-600 (aggregation)
+# ---------------------------------------------------------------------------------------
+@dataclass
+class IOEvidence:
+    """Per-hypothesis IMU/odom-branch evidence (pipeline.py:595-776), a synthetic input for this
+    tier: L_io, h_io plus the certificate scalars that branch feeds
+    into the numbers: odom/imu/gyro cert (ess, support_frac), excitation maxima, nll sum and the
+    summed trigger magnitude of its 11 certs."""
+    L: np.ndarray
+    h: np.ndarray
+    ess: np.ndarray = field(default_factory=lambda: np.zeros(3))
+    support: np.ndarray = field(default_factory=lambda: np.ones(3))
+    exc_dt: float = 0.0
+    exc_ex: float = 0.0
+    nll: float = 0.0
+    trig: float = 0.0
+
+
+def tempering_beta(L_raw, ess_total, exc_total):
+    """pipeline.py:1070-1111."""
+    eps = EPS_MASS
+    dpose = np.linalg.norm(L_raw[15, 0:6]) + np.linalg.norm(L_raw[0:6, 15])
+    dvel = np.linalg.norm(L_raw[15, 6:9]) + np.linalg.norm(L_raw[6:9, 15])
+    dt_asym = min(max(abs(dvel - dpose) / (dvel + dpose + eps), 0.0), 1.0)
+    z_xy = abs(L_raw[2, 2]) / (0.5 * (abs(L_raw[0, 0]) + abs(L_raw[1, 1])) + eps)
+    ess_to_exc = ess_total / (exc_total + eps)
+    s = min(max(dt_asym * (z_xy / (z_xy + POWER_BETA_Z_C)) * (1.0 / (1.0 + ess_to_exc / POWER_BETA_EXC_C)), 0.0), 1.0)
+    beta = min(max(POWER_BETA_MIN + (1.0 - POWER_BETA_MIN) * s, POWER_BETA_MIN), 1.0)
+    return beta, dt_asym, z_xy
+
+
+def excitation_scaling(L_ev, L_prior, h_prior, eps=EXC_EPS):
+    """compute_excitation_scales_jax + apply_excitation_prior_scaling_jax (excitation.py:14-64)."""
+    e_dt, pi_dt = L_ev[15, 15], L_prior[15, 15]
+    e_ex, pi_ex = np.trace(L_ev[16:22, 16:22]), np.trace(L_prior[16:22, 16:22])
+    s_dt = e_dt / (e_dt + pi_dt + eps)
+    s_ex = e_ex / (e_ex + pi_ex + eps)
+    Lp, hp = L_prior.copy(), h_prior.copy()
+    Lp[15, :] *= 1.0 - s_dt; Lp[:, 15] *= 1.0 - s_dt; hp[15] *= 1.0 - s_dt
+    Lp[16:22, :] *= 1.0 - s_ex; Lp[:, 16:22] *= 1.0 - s_ex; hp[16:22] *= 1.0 - s_ex
+    return Lp, hp, float(s_dt), float(s_ex)
+
+
+def fusion_alpha(cond_ev, ess_ev, exc_total, dt_asym, z_xy, beta, nll,
+                 amin=ALPHA_MIN, amax=ALPHA_MAX, c0=C0_COND):
+    """fusion_scale_from_certificates (fusion.py:46-142)."""
+    q = math.sqrt((c0 / (cond_ev + c0)) * (ess_ev / (ess_ev + 1.0)))
+    q *= math.exp(-nll) * min(max(dt_asym, 0.0), 1.0)
+    q *= min(max(z_xy / (z_xy + 1.0), 0.0), 1.0) * min(max(exc_total / (exc_total + 1.0), 0.0), 1.0)
+    q *= min(max(beta, 0.0), 1.0)
+    return min(max(amin + (amax - amin) * q, amin), amax)
+
+
+def pose6_cond(L_ev, eps=EPS_PSD):
+    """pipeline.py:1157-1170: eigvalsh of the symmetrised pose block, clipped at eps_psd."""
+    P = 0.5 * (L_ev[0:6, 0:6] + L_ev[0:6, 0:6].T)
+    ev = np.maximum(np.linalg.eigvalsh(P), eps)
+    return ev[-1] / ev[0]
+
+
+def info_fusion_additive(L_pred, h_pred, L_ev, h_ev, alpha, eps_psd=EPS_PSD):
+    """fusion.py:150-230."""
+    Lp, c = psd_project(L_pred + alpha * L_ev, eps_psd)
+    return Lp, h_pred + alpha * h_ev, c
+
+
+# ---------------------------------------------------------------------------------------
+# a12 PoseUpdateFrobeniusRecompose — backend/operators/recompose.py:50-205
+# ---------------------------------------------------------------------------------------
+def bch3(x1, x2):
+    return 0.5 * np.concatenate([np.cross(x1[3:6], x2[:3]) + np.cross(x1[:3], x2[3:6]),
+                                 np.cross(x1[3:6], x2[3:6])])
+
+
+def recompose(b: Belief, T, c_frob=C_FROB, eps_lift=EPS_LIFT):
+    dz = chol_solve_lifted(b.L, b.h, eps_lift)[0]
+    s = T / (T + c_frob)
+    corr = bch3(b.z_lin[0:6], dz[0:6])
+    dpc = dz[0:6] + s * corr
+    X_new = se3_compose(b.X_anchor, se3_exp(dpc))
+    shift = np.zeros(D_Z); shift[0:6] = dpc
+    return Belief(X_new, b.z_lin - shift, b.L.copy(), b.h - b.L @ shift, b.stamp_sec), dict(
+        delta_pose=dpc, frobenius_strength=s, bch=corr)
+
+
+# ---------------------------------------------------------------------------------------
+# a14 AnchorDriftUpdate — backend/operators/anchor_drift.py:93-191
+# ---------------------------------------------------------------------------------------
+def anchor_drift(b: Belief, eps_lift=EPS_LIFT):
+    dz = chol_solve_lifted(b.L, b.h, eps_lift)[0]
+    dm, dr = float(np.linalg.norm(dz[0:3])), float(np.linalg.norm(dz[3:6]))
+    rho = min(max(max(dm / ANCHOR_M0, dr / ANCHOR_R0), 0.0), 1.0)
+    X = se3_compose(b.X_anchor, se3_exp(rho * dz[0:6]))
+    zl = (1.0 - rho) * dz
+    return Belief(X, zl, b.L.copy(), b.L @ zl, b.stamp_sec), dict(rho=rho, drift_m=dm, drift_r=dr)
+
+
+# ---------------------------------------------------------------------------------------
+# a15 Inverse-Wishart — backend/operators/inverse_wishart_jax.py:26-185 ;
+# measurement_noise_iw_jax.py:28-100 ; backend/structures/*iw*.py
+# ---------------------------------------------------------------------------------------
+def softplus_pos(x, eps=1e-12, beta=50.0):
+    return softplus(beta * x) / beta + eps
+
+
+def iw_process_init():
+    """create_datasheet_process_noise_state (structures/inverse_wishart_jax.py:43-80)."""
+    nu = PROC_BLOCK_DIMS + 1.0 + IW_NU_WEAK_ADD
+    diag = [1e-4, 8.7e-7, 9.5e-5, 1e-8, 1e-6, 1e-6, 1e-8]
+    Psi = np.zeros((7, 6, 6))
+    for i in range(7):
+        d = PROC_BLOCK_DIMS[i]
+        Psi[i, :d, :d] = np.eye(d) * diag[i] * IW_NU_WEAK_ADD
+    return nu.astype(np.float64), Psi
+
+
+def iw_meas_init(lidar_sigma=0.01):
+    """create_datasheet_measurement_noise_state (structures/measurement_noise_iw_jax.py:37-68)."""
+    nu = np.array([3.0, 3.0, 3.0]) + 1.0 + IW_NU_WEAK_ADD
+    Psi = np.stack([8.7e-7 * np.eye(3), 9.5e-5 * np.eye(3), lidar_sigma * np.eye(3)]) * IW_NU_WEAK_ADD
+    return nu, Psi
+
+
+def iw_process_Q(nu, Psi, eps_psd=EPS_PSD):
+    """process_noise_state_to_Q_jax (inverse_wishart_jax.py:35-68)."""
+    den = softplus_pos(nu - PROC_BLOCK_DIMS - 1.0)
+    Qb = Psi / den[:, None, None] * PROC_BLOCK_MASKS
+    Q = np.zeros((D_Z, D_Z))
+    for i in range(7):
+        s = PROC_BLOCK_STARTS[i]
+        e = min(s + 6, D_Z)
+        Q[s:e, s:e] = Qb[i][: e - s, : e - s]
+    return psd_project(Q, eps_psd)[0]
+
+
+def iw_process_suffstats(L_pred, h_pred, L_post, h_post, eps_lift=EPS_LIFT):
+    """process_noise_iw_suffstats_from_info_jax (inverse_wishart_jax.py:71-123)."""
+    r = chol_solve_lifted(L_post, h_post, eps_lift)[0] - chol_solve_lifted(L_pred, h_pred, eps_lift)[0]
+    Sp = chol_inverse_lifted(L_post, eps_lift)[0]
+    dPsi = np.zeros((7, 6, 6))
+    for i in range(7):
+        s, d = PROC_BLOCK_STARTS[i], PROC_BLOCK_DIMS[i]
+        dPsi[i, :d, :d] = np.outer(r[s:s + d], r[s:s + d]) + Sp[s:s + d, s:s + d]
+    return dPsi, np.ones(7)
+
+
+def _nu_project(nu_raw, dims, nu_max=1000.0):
+    nmin = dims + 1.0 + IW_NU_WEAK_ADD
+    nf = nmin + softplus(nu_raw - nmin)
+    return nu_max - softplus(nu_max - nf)
+
+
+def iw_process_apply(nu, Psi, dPsi, dnu, eps_psd=EPS_PSD):
+    """process_noise_iw_apply_suffstats_jax (inverse_wishart_jax.py:126-185)."""
+    raw = (IW_RHO_PROC[:, None, None] * Psi + dPsi) * PROC_BLOCK_MASKS
+    out = np.empty_like(raw)
+    pd = 0.0
+    for i in range(7):
+        out[i], c = psd_project(raw[i], eps_psd)
+        pd += c[0]
+    nr = IW_RHO_PROC * nu + dnu
+    n2 = _nu_project(nr, PROC_BLOCK_DIMS.astype(np.float64))
+    return n2, out, np.array([pd, np.sum(np.abs(n2 - nr))])
+
+
+def iw_meas_apply(nu, Psi, dPsi, dnu, eps_psd=EPS_PSD):
+    """measurement_noise_apply_suffstats_jax (measurement_noise_iw_jax.py:59-100)."""
+    raw = IW_RHO_MEAS[:, None, None] * Psi + dPsi
+    raw = 0.5 * (raw + np.swapaxes(raw, -1, -2))
+    out = np.empty_like(raw)
+    pd = 0.0
+    for i in range(3):
+        out[i], c = psd_project(raw[i], eps_psd)
+        pd += c[0]
+    nr = IW_RHO_MEAS * nu + dnu
+    n2 = _nu_project(nr, np.array([3.0, 3.0, 3.0]))
+    return n2, out, np.array([pd, np.sum(np.abs(n2 - nr))])
+
+
+def iw_meas_mode(nu, Psi, idx):
+    """measurement_noise_mean_jax (measurement_noise_iw_jax.py:37-56)."""
+    return psd_project(Psi[idx] / (nu[idx] + 3.0 + 1.0))[0]
+
+
+# ---------------------------------------------------------------------------------------
+# a16 HypothesisBarycenterProjection — backend/operators/hypothesis.py:51-236
+# ---------------------------------------------------------------------------------------
+def hypothesis_barycenter(Ls, hs, zs, weights, floor, eps_psd=EPS_PSD, eps_lift=EPS_LIFT):
+    wf = np.maximum(weights, floor)
+    adj = float(np.sum(np.abs(wf - weights)))
+    wn = wf / np.sum(wf)
+    L_raw = np.einsum("k,kij->ij", wn, Ls)
+    h = np.einsum("k,ki->i", wn, hs)
+    z = np.einsum("k,ki->i", wn, zs)
+    L, c = psd_project(L_raw, eps_psd)
+    mus = np.stack([chol_solve_lifted(Ls[k], hs[k], eps_lift)[0] for k in range(Ls.shape[0])])
+    mom = np.einsum("k,ki->i", wn, mus)
+    spread = float(np.sum(wn * np.sum((mus - mom[None]) ** 2, axis=1)))
+    K = Ls.shape[0]
+    return dict(L=L, h=h, z_lin=z, floor_adjustment=adj, weights=wn, psd_cert=c, spread=spread,
+                ess=float(1.0 / np.sum(wn ** 2)), support_frac=float(np.sum(wn > floor) / K),
+                mass_eps=adj / K)
+
+
+# ---------------------------------------------------------------------------------------
+# Build-defined legacy bin-path wiring (SURVEY §3.2 "restated"; parity of the wiring itself
+# is unpinned — every operator it calls is pinned individually above).
+# ---------------------------------------------------------------------------------------
+@dataclass
+class ScanInput:
+    points: np.ndarray
+    timestamps: np.ndarray
+    weights: np.ndarray
+    ring: np.ndarray
+    tag: np.ndarray
+    imu_stamps: np.ndarray
+    imu_gyro: np.ndarray
+    imu_accel: np.ndarray
+    scan_start: float
+    scan_end: float
+    t_last: float
+    t_scan: float
+    dt_sec: float
+
+
+@dataclass
+class PipeConfig:
+    n_points_cap: int = 65536
+    lidar_origin: np.ndarray = field(default_factory=lambda: np.array([-0.065447, -0.100474, 0.108987]))
+    tau: float = TAU_SOFT_ASSIGN
+    n_bins: int = B_BINS
+
+
+def scan_hypothesis(b_prev: Belief, scan: ScanInput, Q, io: IOEvidence, mapst: MapStats, mderived,
+                    bins, cfg: PipeConfig):
+    """One hypothesis through steps a1-a14 (pipeline.py:316-1591 restated for the bin path)."""
+    o = cfg.lidar_origin
+    bud = point_budget_resample(scan.points, scan.timestamps, scan.weights, scan.ring, scan.tag, cfg.n_points_cap)
+    pts, ts, ws = bud["points"], bud["timestamps"], bud["weights"]
+    bpred, pc = predict_diffusion(b_prev, Q, scan.dt_sec)
+    Sig_pred = chol_inverse_lifted(bpred.L)[0]
+    sigma_warp = max(math.sqrt(Sig_pred[15, 15]), 0.01)
+    w_scan = smooth_window_weights(scan.imu_stamps, scan.scan_start, scan.scan_end, sigma_warp)
+    w_int = smooth_window_weights(scan.imu_stamps, scan.t_last, scan.t_scan, sigma_warp)
+    mu_inc = chol_solve_lifted(bpred.L, bpred.h)[0]
+    bg, ba = mu_inc[9:12], mu_inc[12:15]
+    pose0 = world_pose(b_prev)
+    rv0 = pose0[3:6]
+    pre = preintegrate(scan.imu_stamps, scan.imu_gyro, scan.imu_accel, w_scan, rv0, bg, ba)
+    xi = se3_log(pre["delta_pose"])
+    dt_imu = imu_dt_mean(scan.imu_stamps)
+    wv = w_int * (scan.imu_stamps > 0.0)
+    wnv = wv / (np.sum(wv) + EPS_MASS)
+    omega_avg = np.einsum("m,mi->i", wnv, scan.imu_gyro - bg[None, :])
+    dPsi_meas = np.zeros((3, 3, 3))
+    dPsi_meas[0] = iw_meas_gyro_suffstats(scan.imu_gyro, wv, bg, omega_avg, dt_imu)
+    dPsi_meas[1] = iw_meas_accel_suffstats(rv0, scan.imu_accel, wv, ba, dt_imu)
+    dnu_meas = np.array([1.0, 1.0, 0.0])
+    p0, wd, retained = deskew_constant_twist(pts, ts, ws, scan.scan_start, scan.scan_end, xi)
+    dirs = point_directions(p0, o)
+    sa = bin_soft_assign(dirs, bins, cfg.tau)
+    mm = scan_bin_moment_match(p0, None, wd, sa["resp"], None, o)
+    R_pred = so3_exp(world_pose(bpred)[3:6])
+    t_pred = world_pose(bpred)[0:3]
+    mu_dir, kap_m, cen, Sig_c = mderived
+    mf = matrix_fisher(R_pred, mm["s_dir"], mm["S_dir_scatter"], mm["N"], mapst.S_dir,
+                       mapst.S_dir_scatter, mapst.N_dir)
+    tr = planar_translation(t_pred, mm["p_bar"], mm["Sigma_p"], mm["N"], cen, Sig_c, mapst.N_pos,
+                            mapst.S_dir_scatter, mapst.N_dir, mf["R_mf"])
+    L_lidar = np.zeros((D_Z, D_Z)); h_lidar = np.zeros(D_Z)
+    L_lidar[0:3, 0:3] = tr["L_trans"]; h_lidar[0:3] = tr["h_trans"]
+    L_lidar[3:6, 3:6] = mf["L_rot"]; h_lidar[3:6] = mf["h_rot"]
+    L_raw = io.L + L_lidar
+    h_raw = io.h + h_lidar
+    # aggregate_certificates([deskew, assign, moments, MF, planar]) then with [odom, imu, gyro]
+    ess_ev = (pre["ess"] + sa["ess"] + mm["ess"] + 0.0 + 0.0) / 5.0
+    sf_ev = (retained + sa["max_resp"] + mm["support_frac"] + 1.0 + 1.0) / 5.0
+    ess_tot = (ess_ev + io.ess.sum()) / 4.0
+    sf_tot = (sf_ev + io.support.sum()) / 4.0
+    exc_total = max(0.0, io.exc_dt) + max(0.0, io.exc_ex)
+    nll = mf["nll_per_ess"] + tr["nll_per_ess"] + io.nll
+    beta, dt_asym, z_xy = tempering_beta(L_raw, ess_tot, exc_total)
+    L_ev, h_ev = beta * L_raw, beta * h_raw
+    Lps, hps, s_dt, s_ex = excitation_scaling(L_ev, bpred.L, bpred.h)
+    cond6 = pose6_cond(L_ev)
+    alpha = fusion_alpha(cond6, ess_tot, exc_total, dt_asym, z_xy, beta, nll)
+    L_post, h_post, fc = info_fusion_additive(Lps, hps, L_ev, h_ev, alpha)
+    T = (bud["trig"] + pc["trig"] + io.trig + sa["trig"] + mm["trig"] + mf["trig"] + tr["trig"]
+         + trigger(beta=beta) + trigger(dt=1.0 - s_dt, ex=1.0 - s_ex) + trigger(alpha=alpha)
+         + trigger(psd=fc[0], alpha=alpha))
+    b_post = Belief(bpred.X_anchor.copy(), bpred.z_lin.copy(), L_post, h_post, bpred.stamp_sec)
+    b_rec, rc = recompose(b_post, T)
+    dPsi_p, dnu_p = iw_process_suffstats(Lps, hps, b_rec.L, b_rec.h)
+    z_t = world_pose(b_rec)
+    R_t = so3_exp(z_t[3:6])
+    t_t = z_t[0:3].copy(); t_t[2] = 0.0
+    Sig_pose = chol_inverse_lifted(b_rec.L)[0][0:6, 0:6]
+    inc = pose_cov_inflation_pushforward(mm, R_t, t_t, Sig_pose)
+    b_fin, dr = anchor_drift(b_rec)
+    return dict(belief=b_fin, dPsi_proc=dPsi_p, dnu_proc=dnu_p, dPsi_meas=dPsi_meas, dnu_meas=dnu_meas,
+                map_inc=inc, T=T, beta=beta, alpha=alpha, s_dt=s_dt, s_ex=s_ex, xi_body=xi,
+                moments=mm, assign=sa, mf=mf, planar=tr, rho=dr["rho"], frob=rc["frobenius_strength"],
+                budget=bud, retained=retained, pose=world_pose(b_fin), L_post=L_post, h_post=h_post)
+
+
+@dataclass
+class ScanState:
+    beliefs: list
+    weights: np.ndarray
+    nu_proc: np.ndarray
+    Psi_proc: np.ndarray
+    nu_meas: np.ndarray
+    Psi_meas: np.ndarray
+    map: MapStats
+    scan_count: int = 0
+
+
+def process_scan(state: ScanState, scan: ScanInput, ios, bins, cfg: PipeConfig, hyp_range=None):
+    """backend_node.py:2036-2119 restated for H hypotheses: per-hypothesis pipeline, weighted
+    IW accumulation, barycenter combine, one IW apply, hypothesis-0 map update.
+    Weight floor = 0.01/H (docs/GC_SLAM.md:122; manifest records it)."""
+    H = len(state.beliefs)
+    Q = iw_process_Q(state.nu_proc, state.Psi_proc)
+    md = map_derived(state.map)
+    res = [scan_hypothesis(state.beliefs[i], scan, Q, ios[i], state.map, md, bins, cfg) for i in range(H)]
+    aP = np.zeros((7, 6, 6)); an = np.zeros(7); aM = np.zeros((3, 3, 3)); am = np.zeros(3)
+    for i, r in enumerate(res):
+        w = float(state.weights[i])
+        aP = aP + w * r["dPsi_proc"]; an = an + w * r["dnu_proc"]
+        aM = aM + w * r["dPsi_meas"]; am = am + w * r["dnu_meas"]
+    new_beliefs = [r["belief"] for r in res]
+    comb = hypothesis_barycenter(np.stack([b.L for b in new_beliefs]), np.stack([b.h for b in new_beliefs]),
+                                 np.stack([b.z_lin for b in new_beliefs]), state.weights, 0.01 / H)
+    wp = float(min(1, state.scan_count))
+    nu_p, Psi_p, _ = iw_process_apply(state.nu_proc, state.Psi_proc, wp * aP, wp * an)
+    nu_m, Psi_m, _ = iw_meas_apply(state.nu_meas, state.Psi_meas, aM, am)
+    new_map = map_forget_and_add(state.map, res[0]["map_inc"])
+    st = ScanState(new_beliefs, state.weights.copy(), nu_p, Psi_p, nu_m, Psi_m, new_map, state.scan_count + 1)
+    return st, comb, res
