@@ -1,0 +1,276 @@
+// gc_belief.hip — batched-small per-hypothesis kernels of the GC-SLAM v2 scan pipeline.
+// One 256-thread workgroup per hypothesis; 22x22 information-form algebra in LDS.
+//
+//  a2  PredictDiffusion            backend/operators/predict.py:43-98
+//  a3  IMU windows + preintegration backend/operators/imu_preintegration.py:19-147,
+//                                   pipeline.py:436-566 (scan window, ξ_body, meas-IW stats)
+//  a7  MatrixFisherRotation         archive/legacy_operators/matrix_fisher_evidence.py:155-394
+//  a8  PlanarTranslationEvidence    matrix_fisher_evidence.py:413-671, 22D embed :729-756
+//  a9  evidence sum, tempering β, excitation scaling   pipeline.py:1038-1148, excitation.py
+//  a10 FusionScaleFromCertificates  fusion.py:46-142 (+ pose-6 conditioning pipeline.py:1157-1177)
+//  a11 InfoFusionAdditive           fusion.py:150-230
+//  a12 PoseUpdateFrobeniusRecompose recompose.py:50-205
+//  a13 PoseCovInflationPushforward  build-defined (source deleted, CHANGELOG.md:1246) — unpinned
+//  a14 AnchorDriftUpdate            anchor_drift.py:93-191
+//  a15 IW suffstats/apply, Q        inverse_wishart_jax.py:35-185, measurement_noise_iw_jax.py
+//  a16 HypothesisBarycenter         hypothesis.py:51-236 (fixed-order partial sums + final)
+#include <hip/hip_runtime.h>
+#include "gc_internal.h"
+#include "gc_pipe.h"
+#include "gc_wgla.h"
+
+namespace gc {
+
+constexpr int N2 = kDZ * kDZ;
+constexpr double kG[3] = {0.0, 0.0, -9.81};
+
+// ------------------------------------------------------------------ small shared helpers
+// X ∘ Exp(δ[0:6]) (belief.py:408-425), thread-local.
+GC_DEV void compose_exp(const double* X, const double* d6, double* out) {
+  double e[6];
+  se3_exp(d6, e);
+  se3_compose(X, e, out);
+}
+
+// Lower-triangular solve of one column: y = C^{-1} e_j; returns Σ_k y_k² (= (A^{-1})_jj).
+GC_DEV double inv_diag_from_chol(const double* C, int n, int j) {
+  double y[kDZ];
+  double s = 0.0;
+  for (int i = 0; i < n; ++i) {
+    double v = (i == j) ? 1.0 : 0.0;
+    if (i >= j)
+      for (int k = j; k < i; ++k) v -= C[i * n + k] * y[k];
+    y[i] = (i >= j) ? v / C[i * n + i] : 0.0;
+    s += y[i] * y[i];
+  }
+  return s;
+}
+
+// ========================================================================= a2 + a3
+// Per hypothesis: predict (OU diffusion, 2 PSD projections), predicted moments, IMU soft
+// windows, parallel-scan preintegration (prefix products of the 512 Exp(ω dt) factors),
+// ξ_body = se3_log(Δpose), and the gyro/accel measurement-noise IW statistics.
+__global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
+  extern __shared__ double sm[];
+  double* Lp = sm;
+  double* W1 = Lp + N2;
+  double* W2 = W1 + N2;
+  double* W3 = W2 + N2;
+  double* W4 = W3 + N2;
+  double* Sx = W4 + N2;                 // 2 N2 + 4*22
+  double* vec = Sx + 2 * N2 + 4 * kDZ;  // 6 x 22
+  double* red = vec + 6 * kDZ;          // 8
+  double* c1 = red + 8;                 // 6
+  double* c2 = c1 + 6;                  // 6
+  double* misc = c2 + 6;                // 64
+  double* A = misc + 64;                // 256 x 9
+  double* Bm = A + 256 * 9;             // 256 x 9
+  double* V1 = Bm + 256 * 9;            // 256 x 3
+  double* V2 = V1 + 256 * 3;            // 256 x 3
+  const int h = blockIdx.x;
+  const int t = threadIdx.x;
+  const int n = kDZ;
+  double* hprev = vec;
+  double* mu_prev = vec + kDZ;
+  double* hpred = vec + 2 * kDZ;
+  double* mu_inc = vec + 3 * kDZ;
+
+  for (int i = t; i < N2; i += kWG) Lp[i] = P.L[(int64_t)h * N2 + i];
+  if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
+  __syncthreads();
+  // --- mu_prev and cov_prev from one lifted Cholesky (predict.py:66-67)
+  wg_solve_lifted(Lp, hprev, mu_prev, P.eps_lift, n, W1);
+  wg_chol_inverse(W1, W2, W3, n);
+  if (t == 0) compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);  // pose0 = world pose of belief_prev
+  // --- OU propagation (predict.py:69-72)
+  const double ef = exp(-2.0 * P.lambda_ou * S.dt);
+  const double dc = (1.0 - ef) / (2.0 * P.lambda_ou + kF64Eps);
+  for (int i = t; i < N2; i += kWG) W2[i] = ef * W2[i] + dc * P.Q[i];
+  __syncthreads();
+  wg_psd_project(W2, W3, P.eps_psd, n, Sx, red, c1);  // cov_psd -> W3
+  double trl = (t < n) ? W3[t * n + t] : 0.0;
+  const double trace_cov = wg_sum(trl, red);
+  wg_inverse_lifted(W3, W2, P.eps_lift, n, W4, W1);   // L_pred raw -> W2
+  wg_psd_project(W2, W1, P.eps_psd, n, Sx, red, c2);  // L_pred -> W1
+  wg_matvec(W1, mu_prev, hpred, n);                   // h_pred = L_pred mu_prev
+  for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
+  if (t < n) P.hpred[(int64_t)h * n + t] = hpred[t];
+  if (t == 0) {
+    double* pc = P.pred_cert + (int64_t)h * kPredCert;
+    const double lift = 2.0 * P.eps_lift * n;
+    pc[0] = lift; pc[1] = c1[0] + c2[0]; pc[2] = c2[2]; pc[3] = c2[3]; pc[4] = c2[4]; pc[5] = c2[5];
+    pc[6] = trace_cov;
+    pc[7] = lift + (c1[0] + c2[0]) + fabs(1.0 - S.dt);  // dt_scale = dt (predict.py:185-189)
+  }
+  // --- predicted moments: Σ_pred[15,15] and mu_inc (pipeline.py:436-453) from chol(L_pred+εI)
+  for (int i = t; i < N2; i += kWG) W4[i] = W1[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
+  __syncthreads();
+  wg_chol(W4, n);
+  wg_chol_solve(W4, hpred, mu_inc, n);
+  if (t == 0) {
+    const double s1515 = inv_diag_from_chol(W4, n, 15);
+    misc[6] = fmax(sqrt(s1515), 0.01);                  // sigma_warp
+    compose_exp(P.X + (int64_t)h * 6, mu_inc, misc + 8);  // pose_pred (for MF / planar)
+    for (int k = 0; k < 6; ++k) P.pose_pred[(int64_t)h * 6 + k] = misc[8 + k];
+    double R0[9];
+    so3_exp(misc + 3, R0);
+    for (int k = 0; k < 9; ++k) misc[16 + k] = R0[k];
+  }
+  __syncthreads();
+  // ------------------------------------------------------------------ IMU (a3)
+  const double sigma_warp = misc[6];
+  const double bg[3] = {mu_inc[9], mu_inc[10], mu_inc[11]};
+  const double ba[3] = {mu_inc[12], mu_inc[13], mu_inc[14]};
+  const int M = P.M;
+  // dt_imu over valid (stamp > 0) samples (pipeline.py:526-535)
+  double cnt = 0.0, tmin = 1e308, tmax = -1e308;
+  for (int i = t; i < M; i += kWG) {
+    const double ti = S.imu_t[i];
+    if (ti > 0.0) { cnt += 1.0; tmin = fmin(tmin, ti); tmax = fmax(tmax, ti); }
+  }
+  const double nvalid = wg_sum(cnt, red);
+  tmin = -wg_max(-tmin, red);
+  tmax = wg_max(tmax, red);
+  const double dt_imu = fmax(nvalid >= 2.0 ? (tmax - tmin) / fmax(nvalid - 1.0, 1.0) : 0.0, 1e-12);
+  // two samples per thread: a = 2t, b = 2t+1
+  const int ia = 2 * t, ib = 2 * t + 1;
+  auto stamp = [&](int i) { return i < M ? S.imu_t[i] : 0.0; };
+  const double ta = stamp(ia), tb = stamp(ib);
+  // dt_i = max(t_{i+1} - t_i, 0), last slot 0 (imu_preintegration.py:84-85)
+  const double dta = (ib < M) ? fmax(tb - ta, 0.0) : 0.0;
+  const double dtb = ib < M ? ((ib + 1 < M) ? fmax(stamp(ib + 1) - tb, 0.0) : 0.0) : 0.0;
+  const double wa = ia < M ? window_weight(ta, S.t0, S.t1, sigma_warp) : 0.0;
+  const double wb = ib < M ? window_weight(tb, S.t0, S.t1, sigma_warp) : 0.0;
+  const double dea = wa * dta, deb = wb * dtb;
+  double ga[3] = {0, 0, 0}, gb[3] = {0, 0, 0}, aa[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
+  for (int k = 0; k < 3; ++k) {
+    if (ia < M) { ga[k] = S.imu_g[3 * ia + k]; aa[k] = S.imu_a[3 * ia + k]; }
+    if (ib < M) { gb[k] = S.imu_g[3 * ib + k]; ab[k] = S.imu_a[3 * ib + k]; }
+  }
+  double dRa[9], dRb[9], Pl[9];
+  {
+    double wv[3] = {(ga[0] - bg[0]) * dea, (ga[1] - bg[1]) * dea, (ga[2] - bg[2]) * dea};
+    so3_exp(wv, dRa);
+    double wv2[3] = {(gb[0] - bg[0]) * deb, (gb[1] - bg[1]) * deb, (gb[2] - bg[2]) * deb};
+    so3_exp(wv2, dRb);
+    mat3_mul(dRa, dRb, Pl);
+  }
+  for (int k = 0; k < 9; ++k) A[t * 9 + k] = Pl[k];
+  __syncthreads();
+  // inclusive Hillis-Steele scan of 3x3 products: X_t = Pl_0 ... Pl_t
+  double* src = A;
+  double* dst = Bm;
+  for (int off = 1; off < kWG; off <<= 1) {
+    double Xn[9];
+    if (t >= off) {
+      mat3_mul(src + (t - off) * 9, src + t * 9, Xn);
+    } else {
+      for (int k = 0; k < 9; ++k) Xn[k] = src[t * 9 + k];
+    }
+    for (int k = 0; k < 9; ++k) dst[t * 9 + k] = Xn[k];
+    __syncthreads();
+    double* tmp = src; src = dst; dst = tmp;
+  }
+  const double* R0 = misc + 16;
+  double Ea[9], Rb[9];
+  if (t == 0) {
+    for (int k = 0; k < 9; ++k) Ea[k] = R0[k];
+  } else {
+    mat3_mul(R0, src + (t - 1) * 9, Ea);
+  }
+  mat3_mul(Ea, dRa, Rb);
+  double awa[3], awb[3], tmp3[3];
+  const double aba[3] = {aa[0] - ba[0], aa[1] - ba[1], aa[2] - ba[2]};
+  const double abb[3] = {ab[0] - ba[0], ab[1] - ba[1], ab[2] - ba[2]};
+  mat3_vec(Ea, aba, tmp3);
+  for (int k = 0; k < 3; ++k) awa[k] = tmp3[k] + kG[k];
+  mat3_vec(Rb, abb, tmp3);
+  for (int k = 0; k < 3; ++k) awb[k] = tmp3[k] + kG[k];
+  // exclusive prefix sum of velocity increments
+  for (int k = 0; k < 3; ++k) V1[t * 3 + k] = awa[k] * dea + awb[k] * deb;
+  __syncthreads();
+  double* vs = V1;
+  double* vd = V2;
+  for (int off = 1; off < kWG; off <<= 1) {
+    double v[3];
+    for (int k = 0; k < 3; ++k) v[k] = vs[t * 3 + k] + ((t >= off) ? vs[(t - off) * 3 + k] : 0.0);
+    for (int k = 0; k < 3; ++k) vd[t * 3 + k] = v[k];
+    __syncthreads();
+    double* tp = vs; vs = vd; vd = tp;
+  }
+  double va[3], pc[3];
+  for (int k = 0; k < 3; ++k) {
+    va[k] = (t > 0) ? vs[(t - 1) * 3 + k] : 0.0;
+    const double vb = va[k] + awa[k] * dea;
+    pc[k] = va[k] * dea + 0.5 * awa[k] * (dea * dea) + vb * deb + 0.5 * awb[k] * (deb * deb);
+  }
+  const double pe0 = wg_sum(pc[0], red), pe1 = wg_sum(pc[1], red), pe2 = wg_sum(pc[2], red);
+  const double ess_scan = wg_sum(wa + wb, red);
+  if (t == 0) {
+    double Rend[9], dR[9], dpose[6], xi[6];
+    mat3_mul(R0, src + (kWG - 1) * 9, Rend);
+    mat3_mul_tn(R0, Rend, dR);
+    const double pe[3] = {pe0, pe1, pe2};
+    mat3_tvec(R0, pe, dpose);
+    so3_log(dR, dpose + 3);
+    se3_log(dpose, xi);
+    for (int k = 0; k < 6; ++k) P.xi[(int64_t)h * 6 + k] = xi[k];
+  }
+  // --- scan-to-scan window: omega_avg and measurement-noise IW statistics
+  //     (pipeline.py:537-566, measurement_noise_iw_jax.py:130-218)
+  auto wint = [&](int i) {
+    const double ti = stamp(i);
+    return (i < M) ? window_weight(ti, S.t_last, S.t_scan, sigma_warp) * (ti > 0.0 ? 1.0 : 0.0) : 0.0;
+  };
+  const double wia = wint(ia), wib = wint(ib);
+  const double wsum = wg_sum(wia + wib, red) + P.eps_mass;
+  double om[3];
+  for (int k = 0; k < 3; ++k)
+    om[k] = wg_sum(wia * (ga[k] - bg[k]) + wib * (gb[k] - bg[k]), red) / wsum;
+  double rr[12];
+  {
+    const double f0 = -(R0[0] * kG[0] + R0[3] * kG[1] + R0[6] * kG[2]);
+    const double f1 = -(R0[1] * kG[0] + R0[4] * kG[1] + R0[7] * kG[2]);
+    const double f2 = -(R0[2] * kG[0] + R0[5] * kG[1] + R0[8] * kG[2]);
+    const double fp[3] = {f0, f1, f2};
+    double rga[3], rgb[3], raa[3], rab[3];
+    for (int k = 0; k < 3; ++k) {
+      rga[k] = (ga[k] - bg[k]) - om[k]; rgb[k] = (gb[k] - bg[k]) - om[k];
+      raa[k] = (aa[k] - ba[k]) - fp[k]; rab[k] = (ab[k] - ba[k]) - fp[k];
+    }
+    int q = 0;
+    for (int i = 0; i < 3; ++i)
+      for (int j = i; j < 3; ++j, ++q) {
+        rr[q] = (wia / wsum) * rga[i] * rga[j] + (wib / wsum) * rgb[i] * rgb[j];
+        rr[6 + q] = (wia / wsum) * raa[i] * raa[j] + (wib / wsum) * rab[i] * rab[j];
+      }
+  }
+  for (int q = 0; q < 12; ++q) rr[q] = wg_sum(rr[q], red);
+  if (t == 0) {
+    double* out = P.dPsiM + (int64_t)h * 27;
+    for (int blk = 0; blk < 2; ++blk) {
+      const double* r = rr + 6 * blk;
+      const double M3[9] = {r[0], r[1], r[2], r[1], r[3], r[4], r[2], r[4], r[5]};
+      double Pp[9];
+      psd_project3(M3, P.eps_psd, Pp, nullptr);
+      for (int k = 0; k < 9; ++k) out[9 * blk + k] = Pp[k] * dt_imu;
+    }
+    for (int k = 0; k < 9; ++k) out[18 + k] = 0.0;
+    double* io = P.imu_out + (int64_t)h * kImuOut;
+    io[0] = ess_scan; io[1] = sigma_warp; io[2] = dt_imu;
+    io[3] = om[0]; io[4] = om[1]; io[5] = om[2]; io[6] = 0.0; io[7] = 0.0;
+  }
+}
+
+static size_t lds_predict() {
+  return sizeof(double) * (5 * N2 + 2 * N2 + 4 * kDZ + 6 * kDZ + 8 + 12 + 64 + 256 * 24);
+}
+
+hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
+  (void)hipFuncSetAttribute((const void*)k_predict_imu, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)lds_predict());
+  hipLaunchKernelGGL(k_predict_imu, dim3(P.Hl), dim3(256), lds_predict(), st, P, S);
+  return hipGetLastError();
+}
+
+}  // namespace gc

@@ -1,0 +1,671 @@
+// gc_evidence.hip — per-hypothesis evidence, fusion and recompose (a7-a14), the IW process
+// statistics (a15), and the per-scan combine (a16) + IW apply + map update, as batched
+// one-workgroup-per-hypothesis kernels. See gc_belief.hip for the reference map.
+#include <hip/hip_runtime.h>
+#include "gc_internal.h"
+#include "gc_pipe.h"
+#include "gc_wgla.h"
+
+namespace gc {
+
+constexpr int NN = kDZ * kDZ;
+constexpr int kBlockStart[7] = {0, 3, 6, 9, 12, 15, 16};
+constexpr int kBlockDim[7] = {3, 3, 3, 3, 3, 1, 6};
+constexpr double kRhoProc[7] = {0.99, 0.995, 0.95, 0.999, 0.999, 0.9999, 0.9999};
+constexpr double kRhoMeas[3] = {0.995, 0.995, 0.99};
+
+GC_DEV void compose_exp2(const double* X, const double* d6, double* out) {
+  double e[6];
+  se3_exp(d6, e);
+  se3_compose(X, e, out);
+}
+
+// Sum a per-bin table [B][W] over bins (fixed order) into out[W] (threads < W).
+GC_DEV void sum_bins(const double* tab, int B, int W, double* out) {
+  if ((int)threadIdx.x < W) {
+    double s = 0.0;
+    for (int b = 0; b < B; ++b) s += tab[b * W + threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+  __syncthreads();
+}
+
+// ==================================================================== a7 .. a15 per hypothesis
+__global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
+  extern __shared__ double sm[];
+  double* Lpr = sm;          // L_pred
+  double* Lev = Lpr + NN;    // L_raw -> L_ev
+  double* Lps = Lev + NN;    // excitation-scaled prior
+  double* Lpo = Lps + NN;    // L_post
+  double* Wc = Lpo + NN;     // chol(L_post + εI)
+  double* W2 = Wc + NN;      // scratch / Σ_post
+  double* W3 = W2 + NN;      // scratch
+  double* Sx = W3 + NN;      // 2NN + 4*22
+  double* vec = Sx + 2 * NN + 4 * kDZ;  // 10 x 22
+  double* red = vec + 10 * kDZ;         // 8
+  double* tab = red + 8;                // 64 x 16 per-bin table
+  double* acc = tab + 64 * 16;          // 32
+  double* sc = acc + 32;                // 128 scalars
+  double* c6 = sc + 128;                // 6
+  const int hl = blockIdx.x;
+  const int t = threadIdx.x;
+  const int n = kDZ, B = P.B;
+  double* hev = vec;
+  double* hps = vec + kDZ;
+  double* hpo = vec + 2 * kDZ;
+  double* dz = vec + 3 * kDZ;
+  double* hrec = vec + 4 * kDZ;
+  double* mupo = vec + 5 * kDZ;
+  double* mups = vec + 6 * kDZ;
+  double* hfin = vec + 7 * kDZ;
+  double* zl = vec + 8 * kDZ;
+  double* mufin = vec + 9 * kDZ;
+  const double eps = P.eps_mass;
+
+  for (int i = t; i < NN; i += kWG) {
+    Lpr[i] = P.Lpred[(int64_t)hl * NN + i];
+    Lev[i] = P.io_L[(int64_t)hl * NN + i];
+  }
+  if (t < n) {
+    hev[t] = P.io_h[(int64_t)hl * n + t];
+    zl[t] = P.z[(int64_t)hl * n + t];
+  }
+  const double* st = P.stats + (int64_t)hl * B * 38;
+  // ---------------------------------------------- a7 MatrixFisher: per-bin cross-covariance
+  if (t < B) {
+    const double* s = st + t * 38;
+    const double* m = P.map + t * kMapRec;
+    const double sN = s[0], mN = m[12];
+    const double wb = sqrt(sN * mN + eps);
+    const double sn = sqrt(s[1] * s[1] + s[2] * s[2] + s[3] * s[3]);
+    const double mn = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+    double us[3], um[3];
+    for (int k = 0; k < 3; ++k) { us[k] = s[1 + k] / (sn + eps); um[k] = m[k] / (mn + eps); }
+    const double conf = (sn * (1.0 / (sN + eps))) * (mn * (1.0 / (mN + eps)));
+    const double wf = wb * conf;
+    double* r = tab + t * 10;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) r[3 * i + j] = wf * um[i] * us[j];
+    r[9] = wf;
+  }
+  __syncthreads();
+  sum_bins(tab, B, 10, acc);
+  if (t == 0) {
+    double U[9], s3[3], V[9];
+    svd3(acc, U, s3, V);
+    double UVt[9];
+    mat3_mul_nt(U, V, UVt);
+    const double dsg = det3(UVt);
+    const double sgn = (dsg > 0.0) ? 1.0 : ((dsg < 0.0) ? -1.0 : 0.0);
+    for (int k = 0; k < 3; ++k) U[3 * k + 2] *= sgn;
+    double Rmf[9];
+    mat3_mul_nt(U, V, Rmf);
+    const double ld[3] = {s3[1] + s3[2], s3[0] + s3[2], s3[0] + s3[1]};
+    double Lr[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j)
+        Lr[3 * i + j] = V[3 * i] * ld[0] * V[3 * j] + V[3 * i + 1] * ld[1] * V[3 * j + 1] +
+                        V[3 * i + 2] * ld[2] * V[3 * j + 2];
+    double Rp[9], Rerr[9], dl[3], Lrot[9], cc[6];
+    so3_exp(P.pose_pred + (int64_t)hl * 6 + 3, Rp);
+    mat3_mul_tn(Rp, Rmf, Rerr);
+    so3_log(Rerr, dl);
+    psd_project3(Lr, P.eps_psd, Lrot, cc);
+    double hr[3];
+    mat3_vec(Lrot, dl, hr);
+    const double Neff = acc[9];
+    const double nll = 0.5 * (dl[0] * hr[0] + dl[1] * hr[1] + dl[2] * hr[2]);
+    for (int k = 0; k < 9; ++k) { sc[k] = Rmf[k]; sc[9 + k] = Lrot[k]; }
+    for (int k = 0; k < 3; ++k) sc[18 + k] = hr[k];
+    sc[21] = nll / (Neff + eps);               // MF nll_per_ess
+    sc[22] = cc[0] + eps / (Neff + eps);       // MF trigger
+    sc[23] = s3[0]; sc[24] = s3[1]; sc[25] = s3[2];
+  }
+  __syncthreads();
+  // ---------------------------------------------- a8 planar translation WLS (R_hat = R_mf)
+  if (t < B) {
+    const double* s = st + t * 38;
+    const double* m = P.map + t * kMapRec;
+    const double* md = P.map_der + t * kMapDer;
+    const double* R = sc;
+    double RS[9], RSR[9], Sc[9], Si[9], rp[3], tb[3];
+    mat3_mul(R, s + 16, RS);
+    mat3_mul_nt(RS, R, RSR);
+    for (int k = 0; k < 9; ++k) Sc[k] = md[7 + k] + RSR[k] + ((k % 4 == 0) ? eps : 0.0);
+    inv3(Sc, Si);
+    const double wb = sqrt(s[0] * m[13] + eps);
+    mat3_vec(R, s + 13, rp);
+    for (int k = 0; k < 3; ++k) tb[k] = md[4 + k] - rp[k];
+    double* r = tab + t * 13;
+    for (int k = 0; k < 9; ++k) r[k] = wb * Si[k];
+    double hb[3];
+    mat3_vec(r, tb, hb);
+    r[9] = hb[0]; r[10] = hb[1]; r[11] = hb[2];
+    r[12] = wb;
+  }
+  __syncthreads();
+  sum_bins(tab, B, 13, acc);
+  if (t == 0) {
+    double Lr[9];
+    for (int k = 0; k < 9; ++k) Lr[k] = acc[k] + ((k % 4 == 0) ? eps : 0.0);
+    double tw[3];
+    solve3(Lr, acc + 9, tw);
+    const double zsc = P.map_misc[0];
+    const double msk[3] = {1.0, 1.0, zsc};
+    double Lm[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Lm[3 * i + j] = acc[3 * i + j] * msk[i] * msk[j];
+    const double* tp = P.pose_pred + (int64_t)hl * 6;
+    const double dl[3] = {tw[0] - tp[0], tw[1] - tp[1], tw[2] - tp[2]};
+    double Lt[9], cc[6], ht[3];
+    psd_project3(Lm, P.eps_psd, Lt, cc);
+    mat3_vec(Lt, dl, ht);
+    const double Neff = acc[12];
+    const double nll = 0.5 * (dl[0] * ht[0] + dl[1] * ht[1] + dl[2] * ht[2]);
+    for (int k = 0; k < 9; ++k) sc[30 + k] = Lt[k];
+    for (int k = 0; k < 3; ++k) { sc[39 + k] = ht[k]; sc[42 + k] = tw[k]; }
+    sc[45] = nll / (Neff + eps);
+    sc[46] = cc[0] + eps / (Neff + eps);
+  }
+  __syncthreads();
+  // ---------------------------------------------- a9 evidence sum: L_raw = L_io + L_lidar
+  if (t < 9) {
+    const int i = t / 3, j = t % 3;
+    Lev[i * n + j] += sc[30 + t];                 // translation block [0:3, 0:3]
+    Lev[(3 + i) * n + (3 + j)] += sc[9 + t];      // rotation block [3:6, 3:6]
+  }
+  if (t < 3) { hev[t] += sc[39 + t]; hev[3 + t] += sc[18 + t]; }
+  __syncthreads();
+  if (t == 0) {
+    // aggregate_certificates([deskew, assign, moments, MF, planar]) then [ev, odom, imu, gyro]
+    const double* bc = P.bincert + (int64_t)hl * 8;
+    const double* io = P.io_cert + (int64_t)hl * kIoCert;
+    const double* im = P.imu_out + (int64_t)hl * kImuOut;
+    const double retained = bc[6] / (P.budget[4] + eps);
+    const double ess_ev = (im[0] + exp(bc[4]) + bc[0] + 0.0 + 0.0) / 5.0;
+    const double sf_ev = (retained + bc[5] + bc[1] + 1.0 + 1.0) / 5.0;
+    const double ess_tot = (ess_ev + io[0] + io[1] + io[2]) / 4.0;
+    const double sf_tot = (sf_ev + io[3] + io[4] + io[5]) / 4.0;
+    const double exc = fmax(0.0, io[6]) + fmax(0.0, io[7]);
+    const double nll = sc[21] + sc[45] + io[8];
+    // tempering β from raw-evidence sentinels (pipeline.py:1070-1111)
+    double dp = 0.0, dp2 = 0.0, dv = 0.0, dv2 = 0.0;
+    for (int k = 0; k < 6; ++k) { dp += Lev[15 * n + k] * Lev[15 * n + k]; dp2 += Lev[k * n + 15] * Lev[k * n + 15]; }
+    for (int k = 6; k < 9; ++k) { dv += Lev[15 * n + k] * Lev[15 * n + k]; dv2 += Lev[k * n + 15] * Lev[k * n + 15]; }
+    const double dpose = sqrt(dp) + sqrt(dp2), dvel = sqrt(dv) + sqrt(dv2);
+    const double dt_asym = clampd(fabs(dvel - dpose) / (dvel + dpose + eps), 0.0, 1.0);
+    const double zxy = fabs(Lev[2 * n + 2]) / (0.5 * (fabs(Lev[0]) + fabs(Lev[n + 1])) + eps);
+    const double e2x = ess_tot / (exc + eps);
+    const double s_all = clampd(dt_asym * (zxy / (zxy + P.power_beta_z_c)) * (1.0 / (1.0 + e2x / P.power_beta_exc_c)), 0.0, 1.0);
+    const double beta = clampd(P.power_beta_min + (1.0 - P.power_beta_min) * s_all, P.power_beta_min, 1.0);
+    sc[50] = beta; sc[51] = dt_asym; sc[52] = zxy; sc[53] = ess_tot; sc[54] = sf_tot; sc[55] = exc; sc[56] = nll;
+  }
+  __syncthreads();
+  const double beta = sc[50];
+  for (int i = t; i < NN; i += kWG) Lev[i] *= beta;
+  if (t < n) hev[t] *= beta;
+  __syncthreads();
+  // excitation scales (excitation.py:14-64) and the scaled prior
+  if (t == 0) {
+    double eex = 0.0, pex = 0.0;
+    for (int k = 16; k < 22; ++k) { eex += Lev[k * n + k]; pex += Lpr[k * n + k]; }
+    const double edt = Lev[15 * n + 15], pdt = Lpr[15 * n + 15];
+    sc[57] = edt / (edt + pdt + 1e-12);
+    sc[58] = eex / (eex + pex + 1e-12);
+  }
+  __syncthreads();
+  const double s_dt = sc[57], s_ex = sc[58];
+  auto afac = [&](int i) { return i == 15 ? 1.0 - s_dt : (i >= 16 ? 1.0 - s_ex : 1.0); };
+  for (int idx = t; idx < NN; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    double v = Lpr[idx];
+    if (i == 15 || i >= 16) v = afac(i) * v;
+    if (j == 15 || j >= 16) v = afac(j) * v;
+    Lps[idx] = v;
+  }
+  if (t < n) hps[t] = afac(t) * P.hpred[(int64_t)hl * n + t];
+  __syncthreads();
+  // a10: pose-6 conditioning of L_ev and the fusion scale α
+  {
+    double* P6 = W3;
+    for (int idx = t; idx < 36; idx += kWG) {
+      const int i = idx / 6, j = idx % 6;
+      double v = 0.5 * (Lev[i * n + j] + Lev[j * n + i]);
+      P6[idx] = isfinite(v) ? v : 0.0;
+    }
+    __syncthreads();
+    double* w6 = acc;
+    wg_eigvalsh(P6, w6, 6, Sx, red);
+    if (t == 0) {
+      double mn = 1e308, mx = -1e308;
+      for (int k = 0; k < 6; ++k) {
+        double e = isfinite(w6[k]) ? w6[k] : P.eps_psd;
+        e = fmax(e, P.eps_psd);
+        mn = fmin(mn, e); mx = fmax(mx, e);
+      }
+      const double cond6 = mx / mn;
+      const double ess_ev = sc[53], exc = sc[55];
+      double q = sqrt((P.c0_cond / (cond6 + P.c0_cond)) * (ess_ev / (ess_ev + 1.0)));
+      q *= exp(-sc[56]) * clampd(sc[51], 0.0, 1.0);
+      q *= clampd(sc[52] / (sc[52] + 1.0), 0.0, 1.0) * clampd(exc / (exc + 1.0), 0.0, 1.0);
+      q *= clampd(sc[50], 0.0, 1.0);
+      sc[59] = clampd(P.alpha_min + (P.alpha_max - P.alpha_min) * q, P.alpha_min, P.alpha_max);
+      sc[60] = cond6;
+    }
+    __syncthreads();
+  }
+  const double alpha = sc[59];
+  // a11 InfoFusionAdditive
+  for (int i = t; i < NN; i += kWG) W2[i] = Lps[i] + alpha * Lev[i];
+  if (t < n) hpo[t] = hps[t] + alpha * hev[t];
+  __syncthreads();
+  wg_psd_project(W2, Lpo, P.eps_psd, n, Sx, red, c6);
+  // a12 recompose: T from every operator's trigger magnitude (pipeline.py:1211)
+  if (t == 0) {
+    const double* bc = P.bincert + (int64_t)hl * 8;
+    const double trig_budget = 1e-12 / (P.budget[0] + 1e-12);
+    double T = trig_budget + P.pred_cert[(int64_t)hl * kPredCert + 7] + P.io_cert[(int64_t)hl * kIoCert + 9];
+    T += 0.0 + bc[7] + sc[22] + sc[46];                // deskew, assign (exact), moments, MF, planar
+    T += fabs(1.0 - sc[50]);                           // PowerTempering
+    T += fabs(1.0 - (1.0 - s_dt)) + fabs(1.0 - (1.0 - s_ex));  // ExcitationPriorScaling
+    T += fabs(1.0 - alpha);                            // FusionScale
+    T += c6[0] + fabs(1.0 - alpha);                    // InfoFusionAdditive
+    sc[61] = T;
+    sc[62] = c6[0];
+  }
+  for (int i = t; i < NN; i += kWG) Wc[i] = Lpo[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
+  __syncthreads();
+  wg_chol(Wc, n);
+  wg_chol_solve(Wc, hpo, dz, n);
+  if (t == 0) {
+    const double T = sc[61];
+    const double s = T / (T + P.c_frob);
+    const double* x1 = zl;  // z_lin pose slice
+    double c1[3], c2[3], c3[3];
+    cross3(x1 + 3, dz, c1);
+    cross3(x1, dz + 3, c2);
+    cross3(x1 + 3, dz + 3, c3);
+    double dpc[6];
+    for (int k = 0; k < 3; ++k) {
+      dpc[k] = dz[k] + s * (0.5 * (c1[k] + c2[k]));
+      dpc[3 + k] = dz[3 + k] + s * (0.5 * c3[k]);
+    }
+    compose_exp2(P.X + (int64_t)hl * 6, dpc, sc + 64);  // X_new
+    for (int k = 0; k < 6; ++k) sc[70 + k] = dpc[k];
+    sc[63] = s;
+  }
+  __syncthreads();
+  if (t < n) {
+    const double sh = (t < 6) ? sc[70 + t] : 0.0;
+    double v = hpo[t];
+    for (int k = 0; k < 6; ++k) v -= Lpo[t * n + k] * sc[70 + k];
+    hrec[t] = v;
+    zl[t] = zl[t] - sh;
+  }
+  __syncthreads();
+  // a15 process-noise IW statistics (inverse_wishart_jax.py:71-123)
+  wg_chol_solve(Wc, hrec, mupo, n);
+  for (int i = t; i < NN; i += kWG) W3[i] = Lps[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
+  __syncthreads();
+  wg_chol(W3, n);
+  wg_chol_solve(W3, hps, mups, n);
+  wg_chol_inverse(Wc, W2, Sx, n);  // Σ_post -> W2
+  for (int idx = t; idx < 7 * 36; idx += kWG) {
+    const int b = idx / 36, i = (idx % 36) / 6, j = idx % 6;
+    const int d = kBlockDim[b], s0 = kBlockStart[b];
+    double v = 0.0;
+    if (i < d && j < d) {
+      const double r_i = mupo[s0 + i] - mups[s0 + i], r_j = mupo[s0 + j] - mups[s0 + j];
+      v = r_i * r_j + W2[(s0 + i) * n + (s0 + j)];
+    }
+    P.dPsiP[(int64_t)hl * 252 + idx] = v;
+  }
+  // a13 map increment from hypothesis 0 only (backend_node.py:2081-2083), build-defined pushforward
+  if (P.h_begin + hl == 0) {
+    if (t == 0) {
+      double zt[6], R[9];
+      compose_exp2(sc + 64, mupo, zt);
+      so3_exp(zt + 3, R);
+      for (int k = 0; k < 9; ++k) sc[80 + k] = R[k];
+      sc[89] = zt[0]; sc[90] = zt[1]; sc[91] = 0.0;  // planar map: t[2] = 0 (CHANGELOG.md:575-578)
+    }
+    __syncthreads();
+    if (t < B) {
+      const double* s = st + t * 38;
+      const double* R = sc + 80;
+      const double* tt = sc + 89;
+      double* o = P.map_inc + t * kMapRec;
+      const double N = s[0];
+      double v3[3], M3[9], M4[9];
+      mat3_vec(R, s + 1, v3);
+      for (int k = 0; k < 3; ++k) o[k] = v3[k];
+      mat3_mul(R, s + 4, M3);
+      mat3_mul_nt(M3, R, M4);
+      for (int k = 0; k < 9; ++k) o[3 + k] = M4[k];
+      o[12] = N; o[13] = N;
+      double pw[3];
+      mat3_vec(R, s + 13, pw);
+      for (int k = 0; k < 3; ++k) pw[k] += tt[k];
+      // Σ_w = R Σ_p Rᵀ + J Σ_pose Jᵀ, J = [R | -R [p̄]×]
+      mat3_mul(R, s + 16, M3);
+      mat3_mul_nt(M3, R, M4);
+      const double* pb = s + 13;
+      const double K[9] = {0.0, -pb[2], pb[1], pb[2], 0.0, -pb[0], -pb[1], pb[0], 0.0};
+      double RK[9], J[18];
+      mat3_mul(R, K, RK);
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) { J[i * 6 + j] = R[3 * i + j]; J[i * 6 + 3 + j] = -RK[3 * i + j]; }
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) {
+          double v = 0.0;
+          for (int a = 0; a < 6; ++a) {
+            double ja = 0.0;
+            for (int c = 0; c < 6; ++c) ja += W2[a * n + c] * J[j * 6 + c];
+            v += J[i * 6 + a] * ja;
+          }
+          M4[3 * i + j] += v;
+        }
+      for (int k = 0; k < 3; ++k) o[14 + k] = N * pw[k];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) o[17 + 3 * i + j] = N * (M4[3 * i + j] + pw[i] * pw[j]);
+    }
+  }
+  // a14 anchor drift (anchor_drift.py:93-191): δz = μ_post of the recomposed belief
+  if (t == 0) {
+    const double dm = sqrt(mupo[0] * mupo[0] + mupo[1] * mupo[1] + mupo[2] * mupo[2]);
+    const double dr = sqrt(mupo[3] * mupo[3] + mupo[4] * mupo[4] + mupo[5] * mupo[5]);
+    const double rho = clampd(fmax(dm / 0.5, dr / 0.2), 0.0, 1.0);
+    double d6[6];
+    for (int k = 0; k < 6; ++k) d6[k] = rho * mupo[k];
+    compose_exp2(sc + 64, d6, sc + 92);  // X_fin
+    sc[98] = rho;
+  }
+  __syncthreads();
+  const double rho = sc[98];
+  if (t < n) zl[t] = (1.0 - rho) * mupo[t];
+  __syncthreads();
+  wg_matvec(Lpo, zl, hfin, n);
+  wg_chol_solve(Wc, hfin, mufin, n);
+  // write the final belief and per-hypothesis outputs
+  for (int i = t; i < NN; i += kWG) P.L[(int64_t)hl * NN + i] = Lpo[i];
+  if (t < n) {
+    P.z[(int64_t)hl * n + t] = zl[t];
+    P.h[(int64_t)hl * n + t] = hfin[t];
+    P.mu_fin[(int64_t)hl * n + t] = mufin[t];
+  }
+  if (t == 0) {
+    for (int k = 0; k < 6; ++k) P.X[(int64_t)hl * 6 + k] = sc[92 + k];
+    P.stamp[hl] += S.dt;
+    double* dg = P.diag + (int64_t)hl * kHypDiag;
+    double pose[6];
+    compose_exp2(sc + 92, mufin, pose);
+    for (int k = 0; k < 6; ++k) dg[k] = pose[k];
+    dg[6] = sc[61]; dg[7] = sc[50]; dg[8] = alpha; dg[9] = s_dt; dg[10] = s_ex; dg[11] = rho;
+    dg[12] = sc[63]; dg[13] = sc[60]; dg[14] = sc[53]; dg[15] = sc[51]; dg[16] = sc[52]; dg[17] = sc[56];
+    dg[18] = sc[22]; dg[19] = sc[46]; dg[20] = sc[62];
+    for (int k = 0; k < 3; ++k) dg[21 + k] = sc[42 + k];  // t_wls
+    double wmf[3];
+    so3_log(sc, wmf);
+    for (int k = 0; k < 3; ++k) dg[24 + k] = wmf[k];      // log R_mf
+    for (int k = 0; k < 3; ++k) dg[27 + k] = sc[23 + k];  // MF singular values
+    for (int k = 0; k < 6; ++k) dg[30 + k] = P.xi[(int64_t)hl * 6 + k];
+    dg[36] = sc[54]; dg[37] = sc[55]; dg[38] = 0.0; dg[39] = 0.0;
+  }
+}
+
+// ==================================================================== a16 partial sums (local)
+__global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
+  __shared__ double wn_s[1024];
+  __shared__ double red[8];
+  const int t = threadIdx.x;
+  // floored / renormalised weights over ALL hypotheses (hypothesis.py:77-82), replicated
+  double loc = 0.0;
+  for (int k = t; k < P.H; k += kWG) loc += fmax(P.weights[k], P.weight_floor);
+  const double wsum = wg_sum(loc, red);
+  double* out = P.send;
+  const int Hl = P.Hl, n = kDZ;
+  for (int k = t; k < Hl && k < 1024; k += kWG) wn_s[k] = fmax(P.weights[P.h_begin + k], P.weight_floor) / wsum;
+  __syncthreads();
+  for (int e = t; e < kPMAP; e += kWG) {
+    double s = 0.0;
+    if (e < kPH) {
+      for (int k = 0; k < Hl; ++k) s += wn_s[k] * P.L[(int64_t)k * NN + e];
+    } else if (e < kPZ) {
+      for (int k = 0; k < Hl; ++k) s += wn_s[k] * P.h[(int64_t)k * n + (e - kPH)];
+    } else if (e < kPMU) {
+      for (int k = 0; k < Hl; ++k) s += wn_s[k] * P.z[(int64_t)k * n + (e - kPZ)];
+    } else if (e < kPMU2) {
+      for (int k = 0; k < Hl; ++k) s += wn_s[k] * P.mu_fin[(int64_t)k * n + (e - kPMU)];
+    } else if (e == kPMU2) {
+      for (int k = 0; k < Hl; ++k) {
+        double q = 0.0;
+        for (int i = 0; i < n; ++i) q += P.mu_fin[(int64_t)k * n + i] * P.mu_fin[(int64_t)k * n + i];
+        s += wn_s[k] * q;
+      }
+    } else if (e < kPDNUP) {
+      for (int k = 0; k < Hl; ++k) s += P.weights[P.h_begin + k] * P.dPsiP[(int64_t)k * 252 + (e - kPDPSIP)];
+    } else if (e < kPDPSIM) {
+      for (int k = 0; k < Hl; ++k) s += P.weights[P.h_begin + k] * 1.0;
+    } else if (e < kPDNUM) {
+      for (int k = 0; k < Hl; ++k) s += P.weights[P.h_begin + k] * P.dPsiM[(int64_t)k * 27 + (e - kPDPSIM)];
+    } else if (e < kPDNUM + 3) {
+      const double dn = (e - kPDNUM < 2) ? 1.0 : 0.0;
+      for (int k = 0; k < Hl; ++k) s += P.weights[P.h_begin + k] * dn;
+    } else if (e >= kPX0 && e < kPX0 + 6) {
+      s = (P.h_begin == 0) ? P.X[e - kPX0] : 0.0;
+    } else if (e == kPSTAMP0) {
+      s = (P.h_begin == 0) ? P.stamp[0] : 0.0;
+    }
+    out[e] = s;
+  }
+  for (int e = t; e < P.B * kMapRec; e += kWG) out[kPMAP + e] = (P.h_begin == 0) ? P.map_inc[e] : 0.0;
+}
+
+// Map-derived statistics for the evidence of the next scan (bin_atlas.py:166-207) and the
+// self-adaptive planar z-scale (matrix_fisher_evidence.py:572-589).
+GC_DEV void map_derive_wg(const PipeDev& P, double* red, double* tab) {
+  const int t = threadIdx.x, B = P.B;
+  const double eps = P.eps_mass;
+  if (t < B) {
+    const double* m = P.map + t * kMapRec;
+    double* d = P.map_der + t * kMapDer;
+    const double nr = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+    for (int k = 0; k < 3; ++k) d[k] = m[k] / (nr + eps);
+    const double invd = 1.0 / (m[12] + eps + kF64Eps);
+    d[3] = kappa_blend(nr * invd, 1e-6, 3.0, 0.8, 0.03);
+    const double invp = 1.0 / (m[13] + eps + kF64Eps);
+    double c[3], Sr[9], Sp[9];
+    for (int k = 0; k < 3; ++k) c[k] = m[14 + k] * invp;
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Sr[3 * i + j] = m[17 + 3 * i + j] * invp - c[i] * c[j];
+    psd_project3(Sr, P.eps_psd, Sp, nullptr);
+    for (int k = 0; k < 3; ++k) d[4 + k] = c[k];
+    for (int k = 0; k < 9; ++k) d[7 + k] = Sp[k];
+    d[16] = 0.0;
+    double* r = tab + t * 10;
+    for (int k = 0; k < 9; ++k) r[k] = m[3 + k];
+    r[9] = m[12];
+  }
+  __syncthreads();
+  sum_bins(tab, B, 10, red);
+  if (t == 0) {
+    double Tm[9], lam[3];
+    const double Nt = red[9] + eps;
+    for (int k = 0; k < 9; ++k) Tm[k] = red[k] / Nt;
+    eigvalsh3_desc(Tm, lam);
+    P.map_misc[0] = fmax(lam[2], 0.0) / fmax(lam[0], eps);
+    P.map_misc[1] = red[9];
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_map_derive(PipeDev P) {
+  __shared__ double red[16];
+  __shared__ double tab[64 * 10];
+  map_derive_wg(P, red, tab);
+}
+
+// process_noise_state_to_Q_jax (inverse_wishart_jax.py:35-68)
+GC_DEV void iw_Q_wg(const PipeDev& P, double* Qs, double* Qp, double* Sx, double* red) {
+  const int t = threadIdx.x, n = kDZ;
+  for (int idx = t; idx < NN; idx += kWG) Qs[idx] = 0.0;
+  __syncthreads();
+  if (t == 0) {
+    for (int b = 0; b < 7; ++b) {
+      const double den = softplus(50.0 * (P.nu_proc[b] - kBlockDim[b] - 1.0)) / 50.0 + 1e-12;
+      const int s0 = kBlockStart[b];
+      const int e0 = (s0 + 6 < n) ? s0 + 6 : n;
+      for (int i = 0; i < e0 - s0; ++i)
+        for (int j = 0; j < e0 - s0; ++j) {
+          const double m = (i < kBlockDim[b] && j < kBlockDim[b]) ? 1.0 : 0.0;
+          Qs[(s0 + i) * n + (s0 + j)] = P.Psi_proc[b * 36 + i * 6 + j] / den * m;
+        }
+    }
+  }
+  __syncthreads();
+  wg_psd_project(Qs, Qp, P.eps_psd, n, Sx, red, nullptr);
+  for (int idx = t; idx < NN; idx += kWG) P.Q[idx] = Qp[idx];
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(256) k_iw_Q(PipeDev P) {
+  extern __shared__ double sm[];
+  iw_Q_wg(P, sm, sm + NN, sm + 2 * NN, sm + 4 * NN + 4 * kDZ);
+}
+
+GC_DEV double nu_project(double nu_raw, double dim, double nu_max) {
+  const double nmin = dim + 1.0 + 0.5;
+  const double nf = nmin + softplus(nu_raw - nmin);
+  return nu_max - softplus(nu_max - nf);
+}
+
+// ================================================= a16 combine + a15 IW apply + map update
+__global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
+  extern __shared__ double sm[];
+  double* Lr = sm;
+  double* Lc = Lr + NN;
+  double* Sx = Lc + NN;  // 2NN + 88
+  double* red = Sx + 2 * NN + 4 * kDZ;
+  double* c6 = red + 16;
+  double* blk = c6 + 8;   // 36
+  double* blkp = blk + 36;
+  double* tab = blkp + 36;  // 64 x 10
+  double* Qs = tab + 640;   // NN
+  double* Qp = Qs + NN;     // NN
+  const int t = threadIdx.x, n = kDZ;
+  const int PLn = partial_len(P.B);
+  // fixed rank-order reduction of the gathered partial records
+  for (int e = t; e < PLn; e += kWG) {
+    double s = 0.0;
+    for (int g = 0; g < P.G; ++g) s += P.gather[(int64_t)g * PLn + e];
+    P.send[e] = s;  // reuse send as the reduced record
+  }
+  __syncthreads();
+  const double* R = P.send;
+  for (int i = t; i < NN; i += kWG) Lr[i] = R[kPL + i];
+  __syncthreads();
+  wg_psd_project(Lr, Lc, P.eps_psd, n, Sx, red, c6);
+  double* cb = P.comb;
+  for (int i = t; i < NN; i += kWG) cb[i] = Lc[i];
+  if (t < n) { cb[NN + t] = R[kPH + t]; cb[NN + n + t] = R[kPZ + t]; }
+  if (t < 6) cb[NN + 2 * n + t] = R[kPX0 + t];
+  // weight-only certificate terms (hypothesis.py:183-205), replicated on every rank
+  double l2 = 0.0, lc = 0.0, la = 0.0, lw = 0.0;
+  for (int k = t; k < P.H; k += kWG) lw += fmax(P.weights[k], P.weight_floor);
+  const double wsum = wg_sum(lw, red);
+  for (int k = t; k < P.H; k += kWG) {
+    const double wf = fmax(P.weights[k], P.weight_floor), wn = wf / wsum;
+    l2 += wn * wn; lc += (wn > P.weight_floor) ? 1.0 : 0.0; la += fabs(wf - P.weights[k]);
+  }
+  const double s2 = wg_sum(l2, red), scnt = wg_sum(lc, red), sadj = wg_sum(la, red);
+  if (t == 0) {
+    double* cc = cb + NN + 2 * n + 6;
+    cc[0] = R[kPSTAMP0];
+    cc[1] = c6[0]; cc[2] = c6[2]; cc[3] = c6[3]; cc[4] = c6[4]; cc[5] = c6[5];
+    cc[6] = 1.0 / s2; cc[7] = scnt / P.H; cc[8] = sadj / P.H; cc[9] = sadj;
+    double mm = 0.0;
+    for (int i = 0; i < n; ++i) mm += R[kPMU + i] * R[kPMU + i];
+    cc[10] = R[kPMU2] - mm;  // spread proxy Σ w‖μ_j‖² − ‖Σ w μ_j‖²
+  }
+  __syncthreads();
+  // ---- process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
+  double pd_acc = 0.0, nu_acc = 0.0;
+  for (int b = 0; b < 7; ++b) {
+    if (t < 36) {
+      const int i = t / 6, j = t % 6;
+      const double m = (i < kBlockDim[b] && j < kBlockDim[b]) ? 1.0 : 0.0;
+      blk[t] = (kRhoProc[b] * P.Psi_proc[b * 36 + t] + S.w_process * R[kPDPSIP + b * 36 + t]) * m;
+    }
+    __syncthreads();
+    wg_psd_project(blk, blkp, P.eps_psd, 6, Sx, red, c6);
+    if (t < 36) P.Psi_proc[b * 36 + t] = blkp[t];
+    if (t == 0) {
+      pd_acc += c6[0];
+      const double nr = kRhoProc[b] * P.nu_proc[b] + S.w_process * R[kPDNUP + b];
+      const double nn = nu_project(nr, kBlockDim[b], P.nu_max);
+      nu_acc += fabs(nn - nr);
+      P.nu_proc[b] = nn;
+    }
+    __syncthreads();
+  }
+  // ---- measurement-noise IW apply (measurement_noise_iw_jax.py:59-100)
+  if (t < 3) {
+    double Mr[9], Mp[9], cc[6];
+    for (int k = 0; k < 9; ++k) Mr[k] = kRhoMeas[t] * P.Psi_meas[t * 9 + k] + R[kPDPSIM + t * 9 + k];
+    double Ms[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Ms[3 * i + j] = 0.5 * (Mr[3 * i + j] + Mr[3 * j + i]);
+    psd_project3(Ms, P.eps_psd, Mp, cc);
+    for (int k = 0; k < 9; ++k) P.Psi_meas[t * 9 + k] = Mp[k];
+    const double nr = kRhoMeas[t] * P.nu_meas[t] + R[kPDNUM + t];
+    const double nn = nu_project(nr, 3.0, P.nu_max);
+    P.nu_meas[t] = nn;
+    tab[t] = cc[0];
+    tab[3 + t] = fabs(nn - nr);
+  }
+  __syncthreads();
+  if (t == 0) {
+    P.iw_cert[0] = pd_acc; P.iw_cert[1] = nu_acc;
+    P.iw_cert[2] = tab[0] + tab[1] + tab[2]; P.iw_cert[3] = tab[3] + tab[4] + tab[5];
+  }
+  __syncthreads();
+  iw_Q_wg(P, Qs, Qp, Sx, red);
+  // ---- map update: γ·map + increments of hypothesis 0 (bin_atlas.py:137-163, :232-257)
+  for (int e = t; e < P.B * kMapRec; e += kWG) P.map[e] = P.forgetting * P.map[e] + R[kPMAP + e];
+  __syncthreads();
+  map_derive_wg(P, red, tab);
+}
+
+// ------------------------------------------------------------------------------ launchers
+static size_t lds_evidence() { return sizeof(double) * (7 * NN + 2 * NN + 4 * kDZ + 10 * kDZ + 8 + 64 * 16 + 32 + 128 + 6); }
+static size_t lds_final() { return sizeof(double) * (2 * NN + 2 * NN + 4 * kDZ + 16 + 8 + 72 + 640 + 2 * NN); }
+
+}  // namespace gc
+
+namespace gc {
+static void allow_big_lds(const void* fn, size_t bytes) {
+  if (bytes > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+}
+hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
+  allow_big_lds((const void*)k_evidence, lds_evidence());
+  hipLaunchKernelGGL(k_evidence, dim3(P.Hl), dim3(256), lds_evidence(), st, P, S);
+  return hipGetLastError();
+}
+hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
+  hipLaunchKernelGGL(k_combine_local, dim3(1), dim3(256), 0, st, P);
+  return hipGetLastError();
+}
+hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
+  allow_big_lds((const void*)k_combine_final, lds_final());
+  hipLaunchKernelGGL(k_combine_final, dim3(1), dim3(256), lds_final(), st, P, S);
+  return hipGetLastError();
+}
+hipError_t launch_map_derive(const PipeDev& P, hipStream_t st) {
+  hipLaunchKernelGGL(k_map_derive, dim3(1), dim3(256), 0, st, P);
+  return hipGetLastError();
+}
+hipError_t launch_iw_Q(const PipeDev& P, hipStream_t st) {
+  hipLaunchKernelGGL(k_iw_Q, dim3(1), dim3(256), sizeof(double) * (4 * NN + 4 * kDZ + 16), st, P);
+  return hipGetLastError();
+}
+}  // namespace gc

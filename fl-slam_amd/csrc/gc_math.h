@@ -28,6 +28,13 @@ GC_DEV double sigmoid(double x) {
   return e / (1.0 + e);
 }
 
+// smooth_window_weights (imu_preintegration.py:19-43)
+GC_DEV double window_weight(double t, double t0, double t1, double sigma) {
+  const double sig = fmax(sigma, 1e-6);
+  const double wr = sigmoid((t - t0) / sig) * sigmoid((t1 - t) / sig);
+  return wr * (1.0 - 1e-12) + 1e-12;
+}
+
 // jax.nn.softplus = log1p(exp(-|x|)) + max(x, 0)
 GC_DEV double softplus(double x) { return log1p(exp(-fabs(x))) + fmax(x, 0.0); }
 

@@ -1,0 +1,67 @@
+// gc_pipe.h — device-resident state of the batched per-scan pipeline (one rank's shard of
+// hypotheses) and the launch interface shared by gc_belief.hip and gc_pipeline.cpp.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace gc {
+
+constexpr int kMapRec = 26;   // [S_dir 3, S_dir_scatter 9, N_dir, N_pos, sum_p 3, sum_ppT 9]
+constexpr int kMapDer = 17;   // [mu_dir 3, kappa, centroid 3, Sigma_c 9, pad]
+constexpr int kPredCert = 8;  // [lift, psd_delta, eig_min, eig_max, cond, nnc, trace_cov, trigger]
+constexpr int kImuOut = 8;    // [ess_scan, sigma_warp, dt_imu, omega_avg 3, pad 2]
+constexpr int kIoCert = 10;   // [ess odom/imu/gyro, sf odom/imu/gyro, exc_dt, exc_ex, nll, trigger]
+constexpr int kHypDiag = 40;  // see include/gcslam.h GC_HYP_DIAG layout
+constexpr int kCombCert = 16;
+
+// Partial-sum record exchanged between ranks once per scan (doubles).
+constexpr int kPL = 0, kPH = 484, kPZ = 506, kPMU = 528, kPMU2 = 550, kPDPSIP = 551, kPDNUP = 803,
+              kPDPSIM = 810, kPDNUM = 837, kPX0 = 841, kPSTAMP0 = 847, kPMAP = 848;
+__host__ __device__ inline int partial_len(int B) { return kPMAP + B * kMapRec; }
+
+struct PipeDev {
+  int Hl;        // local hypotheses
+  int H;         // total hypotheses
+  int h_begin;   // global index of local hypothesis 0
+  int B;         // bins
+  int M;         // IMU slots (<= 512)
+  int64_t n_in, n_cap;
+  double tau, o0, o1, o2;
+  double eps_psd, eps_lift, eps_mass, lambda_ou, c_frob, forgetting, weight_floor;
+  double power_beta_min, power_beta_exc_c, power_beta_z_c, alpha_min, alpha_max, c0_cond;
+  double nu_max;
+  // per local hypothesis
+  double *X, *z, *L, *h, *stamp;           // belief (in/out)
+  double *Lpred, *hpred, *pred_cert, *pose_pred, *xi, *imu_out, *dPsiM;
+  double *stats, *bincert;                 // (Hl, B, 38), (Hl, 8)
+  double *io_L, *io_h, *io_cert;           // synthetic IMU/odom-branch evidence
+  double *dPsiP, *mu_fin, *diag;
+  // shared
+  double *weights;                         // (H)
+  double *Q;                               // (22, 22)
+  double *bins;                            // (B, 3)
+  double *map, *map_der, *map_misc;        // (B, 26), (B, 17), [z_scale, N_dir_total, ...]
+  double *map_inc;                         // (B, 26) written by hypothesis 0's owner
+  double *nu_proc, *Psi_proc, *nu_meas, *Psi_meas;  // (7), (7,36), (3), (3,9)
+  double *budget;                          // 8 budget scalars
+  double *send, *gather;                   // (P), (G, P)
+  int G;                                   // ranks
+  double *comb;                            // combined belief: L 484, h 22, z 22, X 6, stamp, cert 16
+  double *iw_cert;                         // [proc psd, proc nu, meas psd, meas nu]
+};
+
+struct ScanArgs {
+  const double *imu_t, *imu_g, *imu_a;     // (M), (M,3), (M,3)
+  double t0, t1, t_last, t_scan, dt;
+  double w_process;                        // min(1, scan_count)
+};
+
+// launchers (gc_belief.hip)
+hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st);
+hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st);
+hipError_t launch_combine_local(const PipeDev& P, hipStream_t st);
+hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st);
+hipError_t launch_map_derive(const PipeDev& P, hipStream_t st);
+hipError_t launch_iw_Q(const PipeDev& P, hipStream_t st);
+
+}  // namespace gc

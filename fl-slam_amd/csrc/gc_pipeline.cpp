@@ -1,0 +1,276 @@
+// gc_pipeline.cpp — the batched per-scan driver (replaces the hypothesis loop of
+// backend_node.py:2036-2119): one rank's shard of hypotheses lives in HBM; gc_pipeline_run_scan
+// enqueues the whole 14-step scan for all of them plus the combine/IW exchange on one stream.
+#include <hip/hip_runtime.h>
+#include <cstring>
+#include <vector>
+#include "gc_internal.h"
+#include "gc_pipe.h"
+
+struct gc_comm;
+namespace gc {
+int comm_allgather(gc_comm* comm, gc_ctx* ctx, const double* d_send, double* d_recv, int64_t count);
+int comm_size(const gc_comm* comm);
+}
+
+struct gc_pipeline {
+  gc_ctx* ctx = nullptr;
+  gc::PipeDev P{};
+  std::vector<void*> allocs;
+  struct Slot {
+    double *pts = nullptr, *t = nullptr, *w = nullptr, *imu_t = nullptr, *imu_g = nullptr, *imu_a = nullptr;
+    int64_t n_in = 0;
+  } slots[GC_PIPE_MAX_SLOTS];
+  gc_comm* comm = nullptr;
+  double* d_cfg_origin = nullptr;
+};
+
+namespace {
+
+int dalloc(gc_pipeline* p, size_t count, double** out) {
+  void* ptr = nullptr;
+  GC_HIP(p->ctx, hipMalloc(&ptr, (count ? count : 1) * sizeof(double)));
+  GC_HIP(p->ctx, hipMemsetAsync(ptr, 0, (count ? count : 1) * sizeof(double), p->ctx->stream));
+  p->allocs.push_back(ptr);
+  *out = static_cast<double*>(ptr);
+  return GC_OK;
+}
+
+int up(gc_pipeline* p, double* d, const double* h, size_t count) {
+  if (!h || count == 0) return GC_OK;
+  GC_HIP(p->ctx, hipMemcpyAsync(d, h, count * sizeof(double), hipMemcpyHostToDevice, p->ctx->stream));
+  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
+  return GC_OK;
+}
+
+int down(gc_pipeline* p, double* h, const double* d, size_t count) {
+  if (!h || count == 0) return GC_OK;
+  GC_HIP(p->ctx, hipMemcpyAsync(h, d, count * sizeof(double), hipMemcpyDeviceToHost, p->ctx->stream));
+  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
+  return GC_OK;
+}
+
+#define GC_TRY(expr)             \
+  do {                           \
+    int _rc = (expr);            \
+    if (_rc != GC_OK) return _rc; \
+  } while (0)
+
+}  // namespace
+
+extern "C" {
+
+int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const double* cfg, gc_pipeline** out) {
+  GC_CHECK_ARG(nullptr, ctx && dims && cfg && out, "NULL argument");
+  GC_CHECK_ARG(ctx, dims->H_total > 0 && dims->h_count > 0 && dims->h_begin >= 0 &&
+                        dims->h_begin + dims->h_count <= dims->H_total, "bad hypothesis shard");
+  GC_CHECK_ARG(ctx, dims->h_count <= 1024, "at most 1024 hypotheses per rank");
+  GC_CHECK_ARG(ctx, dims->B >= 1 && dims->B <= 64, "B must be in [1, 64]");
+  GC_CHECK_ARG(ctx, dims->M >= 2 && dims->M <= 512, "IMU slots M must be in [2, 512]");
+  GC_CHECK_ARG(ctx, dims->n_in_max > 0 && dims->n_cap > 0, "point counts must be positive");
+  GC_CHECK_ARG(ctx, dims->world_size >= 1 && dims->rank >= 0 && dims->rank < dims->world_size, "bad rank");
+  GC_HIP(ctx, hipSetDevice(ctx->device));
+  gc_pipeline* p = new gc_pipeline();
+  p->ctx = ctx;
+  gc::PipeDev& P = p->P;
+  P.Hl = dims->h_count; P.H = dims->H_total; P.h_begin = dims->h_begin; P.B = dims->B; P.M = dims->M;
+  P.n_in = dims->n_in_max; P.n_cap = dims->n_cap; P.G = dims->world_size;
+  P.tau = cfg[GC_PCFG_TAU]; P.o0 = cfg[GC_PCFG_ORIGIN]; P.o1 = cfg[GC_PCFG_ORIGIN + 1]; P.o2 = cfg[GC_PCFG_ORIGIN + 2];
+  P.eps_psd = cfg[GC_PCFG_EPS_PSD]; P.eps_lift = cfg[GC_PCFG_EPS_LIFT]; P.eps_mass = cfg[GC_PCFG_EPS_MASS];
+  P.lambda_ou = cfg[GC_PCFG_LAMBDA_OU]; P.c_frob = cfg[GC_PCFG_C_FROB]; P.forgetting = cfg[GC_PCFG_FORGETTING];
+  P.weight_floor = cfg[GC_PCFG_WEIGHT_FLOOR]; P.power_beta_min = cfg[GC_PCFG_POWER_BETA_MIN];
+  P.power_beta_exc_c = cfg[GC_PCFG_POWER_BETA_EXC_C]; P.power_beta_z_c = cfg[GC_PCFG_POWER_BETA_Z_C];
+  P.alpha_min = cfg[GC_PCFG_ALPHA_MIN]; P.alpha_max = cfg[GC_PCFG_ALPHA_MAX]; P.c0_cond = cfg[GC_PCFG_C0_COND];
+  P.nu_max = cfg[GC_PCFG_NU_MAX];
+  const int Hl = P.Hl, B = P.B, NN = 484;
+  const int PL = gc::partial_len(B);
+  int rc = GC_OK;
+  double** fields[] = {&P.X, &P.z, &P.L, &P.h, &P.stamp, &P.Lpred, &P.hpred, &P.pred_cert, &P.pose_pred, &P.xi,
+                       &P.imu_out, &P.dPsiM, &P.stats, &P.bincert, &P.io_L, &P.io_h, &P.io_cert, &P.dPsiP,
+                       &P.mu_fin, &P.diag};
+  const size_t sizes[] = {(size_t)Hl * 6, (size_t)Hl * 22, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl,
+                          (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kPredCert, (size_t)Hl * 6,
+                          (size_t)Hl * 6, (size_t)Hl * gc::kImuOut, (size_t)Hl * 27, (size_t)Hl * B * 38,
+                          (size_t)Hl * 8, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kIoCert,
+                          (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag};
+  for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
+  double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
+                       &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert};
+  const size_t ssz[] = {(size_t)P.H, (size_t)NN, (size_t)B * 3, (size_t)B * gc::kMapRec, (size_t)B * gc::kMapDer, 8,
+                        (size_t)B * gc::kMapRec, 7, 7 * 36, 3, 27, 8, (size_t)PL, (size_t)PL * P.G,
+                        GC_COMB_LEN, 4};
+  for (size_t i = 0; i < sizeof(ssz) / sizeof(ssz[0]) && rc == GC_OK; ++i) rc = dalloc(p, ssz[i], shared[i]);
+  if (rc != GC_OK) {
+    gc_pipeline_destroy(p);
+    return rc;
+  }
+  if (P.G == 1) {  // single rank: the combine reads its own partial record in place
+    P.gather = P.send;
+  }
+  *out = p;
+  return GC_OK;
+}
+
+int32_t gc_pipeline_destroy(gc_pipeline* p) {
+  if (!p) return GC_OK;
+  (void)hipStreamSynchronize(p->ctx->stream);
+  for (void* a : p->allocs) (void)hipFree(a);
+  for (auto& s : p->slots) {
+    for (double* d : {s.pts, s.t, s.w, s.imu_t, s.imu_g, s.imu_a})
+      if (d) (void)hipFree(d);
+  }
+  delete p;
+  return GC_OK;
+}
+
+int32_t gc_pipeline_set_bins(gc_pipeline* p, const double* h_bins) {
+  GC_CHECK_ARG(nullptr, p && h_bins, "NULL argument");
+  return up(p, p->P.bins, h_bins, (size_t)p->P.B * 3);
+}
+
+int32_t gc_pipeline_set_beliefs(gc_pipeline* p, const double* h_X, const double* h_z, const double* h_L,
+                                const double* h_h, const double* h_stamp) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const size_t Hl = p->P.Hl;
+  GC_TRY(up(p, p->P.X, h_X, Hl * 6));
+  GC_TRY(up(p, p->P.z, h_z, Hl * 22));
+  GC_TRY(up(p, p->P.L, h_L, Hl * 484));
+  GC_TRY(up(p, p->P.h, h_h, Hl * 22));
+  return up(p, p->P.stamp, h_stamp, Hl);
+}
+
+int32_t gc_pipeline_get_beliefs(gc_pipeline* p, double* h_X, double* h_z, double* h_L, double* h_h,
+                                double* h_stamp) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const size_t Hl = p->P.Hl;
+  GC_TRY(down(p, h_X, p->P.X, Hl * 6));
+  GC_TRY(down(p, h_z, p->P.z, Hl * 22));
+  GC_TRY(down(p, h_L, p->P.L, Hl * 484));
+  GC_TRY(down(p, h_h, p->P.h, Hl * 22));
+  return down(p, h_stamp, p->P.stamp, Hl);
+}
+
+int32_t gc_pipeline_set_weights(gc_pipeline* p, const double* h_w) {
+  GC_CHECK_ARG(nullptr, p && h_w, "NULL argument");
+  return up(p, p->P.weights, h_w, p->P.H);
+}
+
+int32_t gc_pipeline_set_io_evidence(gc_pipeline* p, const double* h_L, const double* h_h, const double* h_cert) {
+  GC_CHECK_ARG(nullptr, p && h_L && h_h && h_cert, "NULL argument");
+  const size_t Hl = p->P.Hl;
+  GC_TRY(up(p, p->P.io_L, h_L, Hl * 484));
+  GC_TRY(up(p, p->P.io_h, h_h, Hl * 22));
+  return up(p, p->P.io_cert, h_cert, Hl * gc::kIoCert);
+}
+
+int32_t gc_pipeline_set_iw(gc_pipeline* p, const double* nu_proc, const double* Psi_proc, const double* nu_meas,
+                           const double* Psi_meas) {
+  GC_CHECK_ARG(nullptr, p && nu_proc && Psi_proc && nu_meas && Psi_meas, "NULL argument");
+  GC_TRY(up(p, p->P.nu_proc, nu_proc, 7));
+  GC_TRY(up(p, p->P.Psi_proc, Psi_proc, 252));
+  GC_TRY(up(p, p->P.nu_meas, nu_meas, 3));
+  GC_TRY(up(p, p->P.Psi_meas, Psi_meas, 27));
+  GC_HIP(p->ctx, gc::launch_iw_Q(p->P, p->ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_pipeline_get_iw(gc_pipeline* p, double* nu_proc, double* Psi_proc, double* nu_meas, double* Psi_meas,
+                           double* Q, double* cert4) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_TRY(down(p, nu_proc, p->P.nu_proc, 7));
+  GC_TRY(down(p, Psi_proc, p->P.Psi_proc, 252));
+  GC_TRY(down(p, nu_meas, p->P.nu_meas, 3));
+  GC_TRY(down(p, Psi_meas, p->P.Psi_meas, 27));
+  GC_TRY(down(p, Q, p->P.Q, 484));
+  return down(p, cert4, p->P.iw_cert, 4);
+}
+
+int32_t gc_pipeline_set_map(gc_pipeline* p, const double* h_map) {
+  GC_CHECK_ARG(nullptr, p && h_map, "NULL argument");
+  GC_TRY(up(p, p->P.map, h_map, (size_t)p->P.B * gc::kMapRec));
+  GC_HIP(p->ctx, gc::launch_map_derive(p->P, p->ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_pipeline_get_map(gc_pipeline* p, double* h_map, double* h_map_der, double* h_misc2) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_TRY(down(p, h_map, p->P.map, (size_t)p->P.B * gc::kMapRec));
+  GC_TRY(down(p, h_map_der, p->P.map_der, (size_t)p->P.B * gc::kMapDer));
+  return down(p, h_misc2, p->P.map_misc, 2);
+}
+
+int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_pts, const double* h_t,
+                               const double* h_w, int64_t n_in, const double* h_imu_t, const double* h_imu_g,
+                               const double* h_imu_a) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS, "slot out of range");
+  GC_CHECK_ARG(p->ctx, n_in > 0 && n_in <= p->P.n_in, "n_in must be in [1, n_in_max]");
+  GC_CHECK_ARG(p->ctx, h_pts && h_t && h_w && h_imu_t && h_imu_g && h_imu_a, "NULL scan array");
+  auto& s = p->slots[slot];
+  if (!s.pts) {
+    const size_t n = (size_t)p->P.n_in, M = (size_t)p->P.M;
+    double** bufs[] = {&s.pts, &s.t, &s.w, &s.imu_t, &s.imu_g, &s.imu_a};
+    const size_t cnt[] = {3 * n, n, n, M, 3 * M, 3 * M};
+    for (int i = 0; i < 6; ++i) GC_HIP(p->ctx, hipMalloc((void**)bufs[i], cnt[i] * sizeof(double)));
+  }
+  s.n_in = n_in;
+  GC_TRY(up(p, s.pts, h_pts, 3 * (size_t)n_in));
+  GC_TRY(up(p, s.t, h_t, (size_t)n_in));
+  GC_TRY(up(p, s.w, h_w, (size_t)n_in));
+  GC_TRY(up(p, s.imu_t, h_imu_t, (size_t)p->P.M));
+  GC_TRY(up(p, s.imu_g, h_imu_g, 3 * (size_t)p->P.M));
+  return up(p, s.imu_a, h_imu_a, 3 * (size_t)p->P.M);
+}
+
+int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, comm == nullptr || gc::comm_size(comm) == p->P.G, "communicator size != world_size");
+  p->comm = comm;
+  return GC_OK;
+}
+
+int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
+                             double t_scan, double dt_sec, int64_t scan_count) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS && p->slots[slot].pts, "scan slot not staged");
+  GC_CHECK_ARG(p->ctx, p->P.G == 1 || p->comm, "world_size > 1 needs gc_pipeline_attach_comm");
+  gc_ctx* ctx = p->ctx;
+  const auto& s = p->slots[slot];
+  gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
+                 scan_count >= 1 ? 1.0 : 0.0};
+  gc::PipeDev& P = p->P;
+  // a1 budget scalars (the fused kernel reads the selection / mass scale from them)
+  GC_TRY(gc_budget_stats(ctx, s.w, s.n_in, P.n_cap, P.budget));
+  // a2 + a3
+  GC_HIP(ctx, gc::launch_predict_imu(P, S, ctx->stream));
+  // a1 -> a4 -> a5 -> a6 fused over all local hypotheses
+  const double origin[3] = {P.o0, P.o1, P.o2};
+  GC_TRY(gc_scan_bins_fused(ctx, P.Hl, s.n_in, P.n_cap, P.B, s.pts, s.t, s.w, P.budget, scan_start, scan_end,
+                            P.xi, P.bins, P.tau, origin, P.eps_psd, P.eps_mass, P.stats, P.bincert));
+  // a7 .. a15
+  GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
+  // a16: partial sums, exchange, fixed-order reduction + IW apply + map update
+  GC_HIP(ctx, gc::launch_combine_local(P, ctx->stream));
+  if (P.G > 1) GC_TRY(gc::comm_allgather(p->comm, ctx, P.send, P.gather, gc::partial_len(P.B)));
+  GC_HIP(ctx, gc::launch_combine_final(P, S, ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out) {
+  GC_CHECK_ARG(nullptr, p && h_out, "NULL argument");
+  return down(p, h_out, p->P.comb, GC_COMB_LEN);
+}
+
+int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag) {
+  GC_CHECK_ARG(nullptr, p && h_diag, "NULL argument");
+  return down(p, h_diag, p->P.diag, (size_t)p->P.Hl * gc::kHypDiag);
+}
+
+int32_t gc_pipeline_get_bin_stats(gc_pipeline* p, double* h_stats, double* h_cert, double* h_xi) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_TRY(down(p, h_stats, p->P.stats, (size_t)p->P.Hl * p->P.B * 38));
+  GC_TRY(down(p, h_cert, p->P.bincert, (size_t)p->P.Hl * 8));
+  return down(p, h_xi, p->P.xi, (size_t)p->P.Hl * 6);
+}
+
+}  // extern "C"

@@ -79,13 +79,6 @@ GC_DEV void deskew_point(const double* p, double alpha, const double* xi, double
   mat3_tvec(R, q, out);
 }
 
-// smooth_window_weights (imu_preintegration.py:19-43)
-GC_DEV double window_weight(double t, double t0, double t1, double sigma) {
-  const double sig = fmax(sigma, 1e-6);
-  const double wr = sigmoid((t - t0) / sig) * sigmoid((t1 - t) / sig);
-  return wr * (1.0 - 1e-12) + 1e-12;
-}
-
 // Features g (pre-multiplied by w) for the moment sums of binning.py:160-173.
 GC_DEV void point_features(const double* p, const double* d, double w, double* f) {
   f[0] = w;

@@ -50,7 +50,43 @@ SIGNATURES = {
                            _f64, _f64, _vp, _vp],
     "gc_kappa_from_resultant_batch": [_vp, _i64, _vp, _f64, _f64, _f64, _f64, _vp],
     "gc_domain_projection_psd_batch": [_vp, _i32, _i32, _vp, _f64, _vp, _vp],
+    "gc_pipeline_create": [_vp, _vp, _vp, C.POINTER(_vp)],
+    "gc_pipeline_destroy": [_vp],
+    "gc_pipeline_set_bins": [_vp, _vp],
+    "gc_pipeline_set_beliefs": [_vp, _vp, _vp, _vp, _vp, _vp],
+    "gc_pipeline_get_beliefs": [_vp, _vp, _vp, _vp, _vp, _vp],
+    "gc_pipeline_set_weights": [_vp, _vp],
+    "gc_pipeline_set_io_evidence": [_vp, _vp, _vp, _vp],
+    "gc_pipeline_set_iw": [_vp, _vp, _vp, _vp, _vp],
+    "gc_pipeline_get_iw": [_vp, _vp, _vp, _vp, _vp, _vp, _vp],
+    "gc_pipeline_set_map": [_vp, _vp],
+    "gc_pipeline_get_map": [_vp, _vp, _vp, _vp],
+    "gc_pipeline_stage_scan": [_vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
+    "gc_pipeline_run_scan": [_vp, _i32, _f64, _f64, _f64, _f64, _f64, _i64],
+    "gc_pipeline_get_combined": [_vp, _vp],
+    "gc_pipeline_get_hyp_diag": [_vp, _vp],
+    "gc_pipeline_get_bin_stats": [_vp, _vp, _vp, _vp],
+    "gc_pipeline_attach_comm": [_vp, _vp],
+    "gc_comm_unique_id": [_vp],
+    "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],
+    "gc_comm_destroy": [_vp],
+    "gc_comm_allgather_f64": [_vp, _vp, _vp, _vp, _i64],
 }
+
+GC_PCFG_LEN = 18
+GC_PIPE_MAX_SLOTS = 8
+GC_MAP_REC = 26
+GC_MAP_DER = 17
+GC_IO_CERT = 10
+GC_HYP_DIAG = 40
+GC_COMB_LEN = 484 + 22 + 22 + 6 + 16
+GC_COMM_ID_BYTES = 128
+
+
+class PipelineDims(C.Structure):
+    _fields_ = [("H_total", C.c_int32), ("h_begin", C.c_int32), ("h_count", C.c_int32), ("B", C.c_int32),
+                ("M", C.c_int32), ("world_size", C.c_int32), ("rank", C.c_int32), ("pad_", C.c_int32),
+                ("n_in_max", C.c_int64), ("n_cap", C.c_int64)]
 
 _lib = None
 _lock = threading.Lock()

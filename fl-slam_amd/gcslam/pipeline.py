@@ -1,0 +1,218 @@
+"""Batched per-scan driver: the reference's per-hypothesis loop, hypothesis combine and IW
+apply (backend_node.py:2036-2119, pipeline.py:316-1621) as one device-resident pipeline over
+this rank's shard of hypotheses (C-ABI gc_pipeline_*, include/gcslam.h).
+
+Host code only stages inputs, launches ``run_scan`` and reads results back; every arithmetic
+step runs in libgcslam on the GPU. With ``world_size > 1`` the per-scan exchange is one RCCL
+all-gather of a fixed-layout partial record followed by a rank-ordered reduction, so every
+rank ends the scan with a bit-identical combined belief, IW state and map.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+from . import _abi
+from .constants import (FORGETTING_FACTOR, GC_ALPHA_MAX, GC_ALPHA_MIN, GC_B_BINS, GC_C0_COND, GC_C_FROB,
+                        GC_EPS_LIFT, GC_EPS_MASS, GC_EPS_PSD, GC_MAX_IMU_PREINT_LEN, GC_OU_DAMPING_LAMBDA,
+                        GC_TAU_SOFT_ASSIGN, POWER_BETA_EXC_C, POWER_BETA_MIN, POWER_BETA_Z_C, T_BASE_LIDAR)
+from .ops.binning import create_fibonacci_atlas
+
+
+def shard(H_total: int, rank: int, world: int):
+    """Contiguous hypothesis shard [h0, h1) of one rank."""
+    return (H_total * rank) // world, (H_total * (rank + 1)) // world
+
+
+@dataclass
+class PipelineConfig:
+    n_points_cap: int = 65536
+    n_bins: int = GC_B_BINS
+    imu_len: int = GC_MAX_IMU_PREINT_LEN
+    tau: float = GC_TAU_SOFT_ASSIGN
+    lidar_origin: tuple = tuple(T_BASE_LIDAR[:3])
+    eps_psd: float = GC_EPS_PSD
+    eps_lift: float = GC_EPS_LIFT
+    eps_mass: float = GC_EPS_MASS
+    lambda_ou: float = GC_OU_DAMPING_LAMBDA
+    c_frob: float = GC_C_FROB
+    forgetting_factor: float = FORGETTING_FACTOR
+    weight_floor: Optional[float] = None  # default 0.01 / H (docs/GC_SLAM.md:122)
+    power_beta_min: float = POWER_BETA_MIN
+    power_beta_exc_c: float = POWER_BETA_EXC_C
+    power_beta_z_c: float = POWER_BETA_Z_C
+    alpha_min: float = GC_ALPHA_MIN
+    alpha_max: float = GC_ALPHA_MAX
+    c0_cond: float = GC_C0_COND
+    nu_max: float = 1000.0
+
+    def as_array(self, H_total: int) -> np.ndarray:
+        floor = 0.01 / H_total if self.weight_floor is None else self.weight_floor
+        return np.array([self.tau, *self.lidar_origin, self.eps_psd, self.eps_lift, self.eps_mass,
+                         self.lambda_ou, self.c_frob, self.forgetting_factor, floor, self.power_beta_min,
+                         self.power_beta_exc_c, self.power_beta_z_c, self.alpha_min, self.alpha_max,
+                         self.c0_cond, self.nu_max], dtype=np.float64)
+
+
+def _p(a):
+    return a.ctypes.data if a is not None else None
+
+
+def _f(a, shape=None):
+    a = np.ascontiguousarray(a, dtype=np.float64)
+    if shape is not None and a.shape != tuple(shape):
+        a = a.reshape(shape)
+    return a
+
+
+class BatchedScanPipeline:
+    """One rank's device-resident hypothesis shard."""
+
+    def __init__(self, H_total: int, n_in_max: int, cfg: PipelineConfig = None, rank: int = 0,
+                 world_size: int = 1, ctx: _abi.Context = None):
+        self.cfg = cfg or PipelineConfig()
+        self.ctx = ctx or _abi.default_context()
+        self.H = H_total
+        self.h0, self.h1 = shard(H_total, rank, world_size)
+        self.Hl = self.h1 - self.h0
+        self.B = self.cfg.n_bins
+        self.M = self.cfg.imu_len
+        self.rank, self.world = rank, world_size
+        d = _abi.PipelineDims(H_total, self.h0, self.Hl, self.B, self.M, world_size, rank, 0,
+                              int(n_in_max), int(self.cfg.n_points_cap))
+        cfgv = self.cfg.as_array(H_total)
+        h = C.c_void_p()
+        _abi.call("gc_pipeline_create", self.ctx.handle, C.addressof(d), cfgv.ctypes.data, C.byref(h), ctx=self.ctx)
+        self.handle = h.value
+        self._comm = None
+        self.set_bins(create_fibonacci_atlas(self.B).dirs)
+        self.set_weights(np.full(H_total, 1.0 / H_total))
+
+    # ---------------------------------------------------------------- state in / out
+    def _call(self, name, *args):
+        _abi.call(name, self.handle, *args, ctx=self.ctx)
+
+    def set_bins(self, bins):
+        self._call("gc_pipeline_set_bins", _p(_f(bins, (self.B, 3))))
+
+    def set_weights(self, w):
+        self._call("gc_pipeline_set_weights", _p(_f(w, (self.H,))))
+
+    def set_beliefs(self, X, z, L, h, stamp=None):
+        """Local shard arrays: X (Hl,6), z (Hl,22), L (Hl,22,22), h (Hl,22), stamp (Hl,)."""
+        stamp = np.zeros(self.Hl) if stamp is None else stamp
+        self._call("gc_pipeline_set_beliefs", _p(_f(X, (self.Hl, 6))), _p(_f(z, (self.Hl, 22))),
+                   _p(_f(L, (self.Hl, 22, 22))), _p(_f(h, (self.Hl, 22))), _p(_f(stamp, (self.Hl,))))
+
+    def get_beliefs(self):
+        X, z, L, h, st = (np.empty(s) for s in ((self.Hl, 6), (self.Hl, 22), (self.Hl, 22, 22), (self.Hl, 22),
+                                                 (self.Hl,)))
+        self._call("gc_pipeline_get_beliefs", _p(X), _p(z), _p(L), _p(h), _p(st))
+        return dict(X_anchor=X, z_lin=z, L=L, h=h, stamp=st)
+
+    def set_io_evidence(self, L, h, cert):
+        self._call("gc_pipeline_set_io_evidence", _p(_f(L, (self.Hl, 22, 22))), _p(_f(h, (self.Hl, 22))),
+                   _p(_f(cert, (self.Hl, _abi.GC_IO_CERT))))
+
+    def set_iw(self, nu_proc, Psi_proc, nu_meas, Psi_meas):
+        self._call("gc_pipeline_set_iw", _p(_f(nu_proc, (7,))), _p(_f(Psi_proc, (7, 6, 6))),
+                   _p(_f(nu_meas, (3,))), _p(_f(Psi_meas, (3, 3, 3))))
+
+    def get_iw(self):
+        out = [np.empty(s) for s in ((7,), (7, 6, 6), (3,), (3, 3, 3), (22, 22), (4,))]
+        self._call("gc_pipeline_get_iw", *[_p(o) for o in out])
+        return dict(nu_proc=out[0], Psi_proc=out[1], nu_meas=out[2], Psi_meas=out[3], Q=out[4], cert=out[5])
+
+    def set_map(self, map_rec):
+        self._call("gc_pipeline_set_map", _p(_f(map_rec, (self.B, _abi.GC_MAP_REC))))
+
+    def get_map(self):
+        m, d, x = np.empty((self.B, _abi.GC_MAP_REC)), np.empty((self.B, _abi.GC_MAP_DER)), np.empty(2)
+        self._call("gc_pipeline_get_map", _p(m), _p(d), _p(x))
+        return dict(map=m, derived=d, z_scale=x[0], N_dir_total=x[1])
+
+    # ---------------------------------------------------------------- scans
+    def stage_scan(self, slot: int, scan: dict):
+        P = _f(scan["points"])
+        n = P.shape[0]
+        self._call("gc_pipeline_stage_scan", int(slot), _p(P), _p(_f(scan["timestamps"], (n,))),
+                   _p(_f(scan["weights"], (n,))), n, _p(_f(scan["imu_stamps"], (self.M,))),
+                   _p(_f(scan["imu_gyro"], (self.M, 3))), _p(_f(scan["imu_accel"], (self.M, 3))))
+
+    def run_scan(self, slot: int, scan: dict, scan_count: int):
+        self._call("gc_pipeline_run_scan", int(slot), float(scan["scan_start"]), float(scan["scan_end"]),
+                   float(scan["t_last"]), float(scan["t_scan"]), float(scan["dt_sec"]), int(scan_count))
+
+    def combined(self):
+        o = np.empty(_abi.GC_COMB_LEN)
+        self._call("gc_pipeline_get_combined", _p(o))
+        c = o[528 + 6:]
+        return dict(L=o[:484].reshape(22, 22), h=o[484:506], z_lin=o[506:528], X_anchor=o[528:534],
+                    stamp=c[0], psd_delta=c[1], eig_min=c[2], eig_max=c[3], cond=c[4], near_null=c[5],
+                    ess=c[6], support_frac=c[7], mass_eps_ratio=c[8], floor_adjustment=c[9], spread=c[10])
+
+    def hyp_diag(self):
+        o = np.empty((self.Hl, _abi.GC_HYP_DIAG))
+        self._call("gc_pipeline_get_hyp_diag", _p(o))
+        return o
+
+    def bin_stats(self):
+        s, c, x = np.empty((self.Hl, self.B, 38)), np.empty((self.Hl, 8)), np.empty((self.Hl, 6))
+        self._call("gc_pipeline_get_bin_stats", _p(s), _p(c), _p(x))
+        return s, c, x
+
+    # ---------------------------------------------------------------- multi-GPU
+    @staticmethod
+    def comm_unique_id() -> bytes:
+        buf = (C.c_uint8 * _abi.GC_COMM_ID_BYTES)()
+        _abi.check(_abi.lib().gc_comm_unique_id(C.addressof(buf)))
+        return bytes(buf)
+
+    def attach_comm(self, uid: bytes):
+        buf = (C.c_uint8 * _abi.GC_COMM_ID_BYTES).from_buffer_copy(uid)
+        h = C.c_void_p()
+        _abi.call("gc_comm_init", self.ctx.handle, self.world, self.rank, C.addressof(buf), C.byref(h), ctx=self.ctx)
+        self._comm = h.value
+        self._call("gc_pipeline_attach_comm", self._comm)
+
+    def close(self):
+        if getattr(self, "handle", None):
+            _abi.lib().gc_pipeline_destroy(self.handle)
+            self.handle = None
+        if self._comm:
+            _abi.lib().gc_comm_destroy(self._comm)
+            self._comm = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def map_record(S_dir, S_dir_scatter, N_dir, N_pos, sum_p, sum_ppT) -> np.ndarray:
+    """MapBinStats (archive/bin_atlas.py:79-98) -> (B, 26) device record layout."""
+    B = np.asarray(N_dir).shape[0]
+    return np.concatenate([np.asarray(S_dir).reshape(B, 3), np.asarray(S_dir_scatter).reshape(B, 9),
+                           np.asarray(N_dir).reshape(B, 1), np.asarray(N_pos).reshape(B, 1),
+                           np.asarray(sum_p).reshape(B, 3), np.asarray(sum_ppT).reshape(B, 9)], axis=1)
+
+
+def iw_process_prior():
+    """create_datasheet_process_noise_state (structures/inverse_wishart_jax.py:43-80):
+    ν = p + 1.5, Ψ = Σ_prior · 0.5 on each padded 6x6 block (init-time constants)."""
+    dims = np.array([3, 3, 3, 3, 3, 1, 6])
+    diag = np.array([1e-4, 8.7e-7, 9.5e-5, 1e-8, 1e-6, 1e-6, 1e-8])
+    Psi = np.zeros((7, 6, 6))
+    for i in range(7):
+        Psi[i, :dims[i], :dims[i]] = np.eye(dims[i]) * diag[i] * 0.5
+    return dims + 1.5, Psi
+
+
+def iw_meas_prior(lidar_sigma: float = 0.01):
+    """create_datasheet_measurement_noise_state (structures/measurement_noise_iw_jax.py:37-68)."""
+    return np.full(3, 4.5), np.stack([8.7e-7 * np.eye(3), 9.5e-5 * np.eye(3), lidar_sigma * np.eye(3)]) * 0.5

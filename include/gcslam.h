@@ -134,6 +134,97 @@ int32_t gc_kappa_from_resultant_batch(gc_ctx* ctx, int64_t n, const double* d_R,
 int32_t gc_domain_projection_psd_batch(gc_ctx* ctx, int32_t batch, int32_t d, const double* d_M,
                                        double eps_psd, double* d_M_out, double* d_cert_out);
 
+/* ------------------------------------------------------------------ batched scan pipeline
+ * Replaces the per-hypothesis loop + combine + IW apply of backend_node.py:2036-2119 (and
+ * process_scan_single_hypothesis, pipeline.py:316-1591, with the legacy bin path a4-a8 of
+ * SURVEY §3.2) by one device-resident driver over this rank's shard of hypotheses. */
+typedef struct gc_pipeline gc_pipeline;
+typedef struct gc_comm gc_comm;
+
+typedef struct {
+  int32_t H_total;   /* hypotheses per scan (all ranks) */
+  int32_t h_begin;   /* first global hypothesis of this rank */
+  int32_t h_count;   /* hypotheses on this rank (<= 1024) */
+  int32_t B;         /* bins (<= 64) */
+  int32_t M;         /* IMU slots (GC_MAX_IMU_PREINT_LEN = 512) */
+  int32_t world_size;
+  int32_t rank;
+  int32_t pad_;
+  int64_t n_in_max;  /* raw points per scan (max) */
+  int64_t n_cap;     /* N_POINTS_CAP */
+} gc_pipeline_dims;
+
+/* configuration doubles (PipelineConfig, pipeline.py:96-160; constants.py) */
+#define GC_PCFG_TAU 0
+#define GC_PCFG_ORIGIN 1 /* 3: lidar origin in the base frame */
+#define GC_PCFG_EPS_PSD 4
+#define GC_PCFG_EPS_LIFT 5
+#define GC_PCFG_EPS_MASS 6
+#define GC_PCFG_LAMBDA_OU 7
+#define GC_PCFG_C_FROB 8
+#define GC_PCFG_FORGETTING 9
+#define GC_PCFG_WEIGHT_FLOOR 10
+#define GC_PCFG_POWER_BETA_MIN 11
+#define GC_PCFG_POWER_BETA_EXC_C 12
+#define GC_PCFG_POWER_BETA_Z_C 13
+#define GC_PCFG_ALPHA_MIN 14
+#define GC_PCFG_ALPHA_MAX 15
+#define GC_PCFG_C0_COND 16
+#define GC_PCFG_NU_MAX 17
+#define GC_PCFG_LEN 18
+
+#define GC_PIPE_MAX_SLOTS 8
+/* map bin record (B x 26): [S_dir 3, S_dir_scatter 9, N_dir, N_pos, sum_p 3, sum_ppT 9] */
+#define GC_MAP_REC 26
+/* map-derived record (B x 17): [mu_dir 3, kappa, centroid 3, Sigma_c 9, pad] */
+#define GC_MAP_DER 17
+/* IMU/odom-branch cert row (10): ess odom/imu/gyro, support odom/imu/gyro, exc_dt, exc_ex,
+ * nll_per_ess sum, trigger-magnitude sum */
+#define GC_IO_CERT 10
+/* per-hypothesis diagnostics (40): [0:6] world pose of the final belief, 6 T, 7 beta, 8 alpha,
+ * 9 s_dt, 10 s_ex, 11 anchor rho, 12 frobenius strength, 13 cond_pose6, 14 ess_total,
+ * 15 dt_asymmetry, 16 z_to_xy, 17 nll_per_ess, 18 MF trigger, 19 planar trigger,
+ * 20 fusion psd delta, [21:24] t_wls, [24:27] log R_mf, [27:30] MF singular values,
+ * [30:36] xi_body, 36 support_frac, 37 excitation_total */
+#define GC_HYP_DIAG 40
+/* combined output (GC_COMB_LEN): L 484, h 22, z_lin 22, X_anchor(hyp 0) 6, then
+ * [stamp, psd_delta, eig_min, eig_max, cond, nnc, ess, support_frac, mass_eps_ratio,
+ *  floor_adjustment, spread_proxy, 5 pad] */
+#define GC_COMB_LEN (484 + 22 + 22 + 6 + 16)
+
+int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const double* h_cfg, gc_pipeline** out);
+int32_t gc_pipeline_destroy(gc_pipeline* p);
+int32_t gc_pipeline_set_bins(gc_pipeline* p, const double* h_bins);
+int32_t gc_pipeline_set_beliefs(gc_pipeline* p, const double* h_X, const double* h_z, const double* h_L,
+                                const double* h_h, const double* h_stamp);
+int32_t gc_pipeline_get_beliefs(gc_pipeline* p, double* h_X, double* h_z, double* h_L, double* h_h,
+                                double* h_stamp);
+int32_t gc_pipeline_set_weights(gc_pipeline* p, const double* h_weights);
+int32_t gc_pipeline_set_io_evidence(gc_pipeline* p, const double* h_L, const double* h_h, const double* h_cert);
+int32_t gc_pipeline_set_iw(gc_pipeline* p, const double* h_nu_proc7, const double* h_Psi_proc7x36,
+                           const double* h_nu_meas3, const double* h_Psi_meas3x9);
+int32_t gc_pipeline_get_iw(gc_pipeline* p, double* h_nu_proc7, double* h_Psi_proc7x36, double* h_nu_meas3,
+                           double* h_Psi_meas3x9, double* h_Q22x22, double* h_cert4);
+int32_t gc_pipeline_set_map(gc_pipeline* p, const double* h_map);
+int32_t gc_pipeline_get_map(gc_pipeline* p, double* h_map, double* h_map_der, double* h_misc2);
+int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_points, const double* h_t,
+                               const double* h_w, int64_t n_in, const double* h_imu_t, const double* h_imu_gyro,
+                               const double* h_imu_accel);
+/* Enqueue one scan (all local hypotheses, exchange, combine, IW apply, map update). */
+int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
+                             double t_scan, double dt_sec, int64_t scan_count);
+int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out);
+int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag);
+int32_t gc_pipeline_get_bin_stats(gc_pipeline* p, double* h_stats, double* h_cert, double* h_xi);
+int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm);
+
+/* ------------------------------------------------------------------ RCCL communicator */
+#define GC_COMM_ID_BYTES 128
+int32_t gc_comm_unique_id(uint8_t* h_id_out);
+int32_t gc_comm_init(gc_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* h_id, gc_comm** out);
+int32_t gc_comm_destroy(gc_comm* comm);
+int32_t gc_comm_allgather_f64(gc_ctx* ctx, gc_comm* comm, const double* d_send, double* d_recv, int64_t count);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,51 @@
+"""TEST INFRASTRUCTURE — builds identical inputs for the oracle and the GPU pipeline
+(synthetic scans, hypotheses, IMU/odom evidence, IW priors, warm-up map)."""
+
+from __future__ import annotations
+
+import numpy as np
+
+from . import gc_oracle as O
+
+SCAN_KEYS = ["points", "timestamps", "weights", "ring", "tag", "imu_stamps", "imu_gyro", "imu_accel",
+             "scan_start", "scan_end", "t_last", "t_scan", "dt_sec"]
+
+
+def scan_input(s):
+    return O.ScanInput(**{k: s[k] for k in SCAN_KEYS})
+
+
+def warmup_map(scan, cap, origin, bins):
+    """MapBinStats of one warm-up scan placed at the identity pose (no deskew, zero pose cov)."""
+    bud = O.point_budget_resample(scan["points"], scan["timestamps"], scan["weights"], None, None, cap)
+    sa = O.bin_soft_assign(O.point_directions(bud["points"], origin), bins)
+    mm = O.scan_bin_moment_match(bud["points"], None, bud["weights"], sa["resp"], None, origin)
+    return O.pose_cov_inflation_pushforward(mm, np.eye(3), np.zeros(3), np.zeros((6, 6)))
+
+
+def map_to_record(m: O.MapStats):
+    B = m.N_dir.shape[0]
+    return np.concatenate([m.S_dir, m.S_dir_scatter.reshape(B, 9), m.N_dir[:, None], m.N_pos[:, None],
+                           m.sum_p, m.sum_ppT.reshape(B, 9)], axis=1)
+
+
+def build(H=4, n_az=256, n_scans=3, seed_scan0=0):
+    import sys, os
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fl-slam_amd"))
+    from gcslam import synth
+    scans = [synth.make_scan(seed_scan0 + k, n_az=n_az) for k in range(n_scans + 1)]
+    n = scans[0]["points"].shape[0]
+    cfg = O.PipeConfig(n_points_cap=n)
+    bins = O.fibonacci_atlas(48)
+    hy = synth.make_hypotheses(H)
+    Lio, hio, cert = synth.make_io_evidence(H)
+    m0 = warmup_map(scans[0], n, cfg.lidar_origin, bins)
+    nuP, PsiP = O.iw_process_init()
+    nuM, PsiM = O.iw_meas_init()
+    beliefs = [O.Belief(hy["X_anchor"][i].copy(), hy["z_lin"][i].copy(), hy["L"][i].copy(), hy["h"][i].copy())
+               for i in range(H)]
+    ios = [O.IOEvidence(Lio[i], hio[i], cert[i, 0:3], cert[i, 3:6], cert[i, 6], cert[i, 7], cert[i, 8], cert[i, 9])
+           for i in range(H)]
+    state = O.ScanState(beliefs, hy["weights"].copy(), nuP, PsiP, nuM, PsiM, m0, 0)
+    return dict(scans=scans[1:], n=n, cfg=cfg, bins=bins, hyp=hy, io=(Lio, hio, cert), ios=ios, state=state,
+                map_record=map_to_record(m0), iw=(nuP, PsiP, nuM, PsiM))

@@ -1,0 +1,75 @@
+"""End-to-end parity of the batched scan pipeline (a1-a16 + combine + IW + map) against the
+oracle's restatement of the reference pipeline, over several consecutive scans.
+
+Tolerances (written per assertion): the north-star bar is pose within 1e-6 abs; beliefs and
+IW state are also compared relatively. Differences come only from ulps (ocml vs libm sin/cos/exp,
+Jacobi vs LAPACK eigh, parallel-scan vs sequential preintegration, summation order)."""
+
+import numpy as np
+import pytest
+
+from oracle import gc_oracle as O
+from oracle import cases
+
+pytestmark = pytest.mark.gpu
+
+
+def _gpu_pipeline(case, ctx):
+    from gcslam.pipeline import BatchedScanPipeline, PipelineConfig
+    H = len(case["state"].beliefs)
+    pipe = BatchedScanPipeline(H, case["n"], PipelineConfig(n_points_cap=case["n"]), ctx=ctx)
+    hy = case["hyp"]
+    pipe.set_beliefs(hy["X_anchor"], hy["z_lin"], hy["L"], hy["h"], hy["stamp"])
+    pipe.set_weights(hy["weights"])
+    pipe.set_io_evidence(*case["io"])
+    pipe.set_iw(*case["iw"])
+    pipe.set_map(case["map_record"])
+    return pipe
+
+
+def _close(a, b, rel, abs_=0.0, what=""):
+    a, b = np.asarray(a), np.asarray(b)
+    err = np.max(np.abs(a - b))
+    scale = max(np.max(np.abs(b)), 1e-300)
+    assert err <= rel * scale + abs_, f"{what}: max|diff| {err:.3e} vs scale {scale:.3e}"
+
+
+@pytest.mark.parametrize("H", [4, 5])
+def test_pipeline_matches_oracle_over_scans(ctx, H):
+    case = cases.build(H=H, n_az=256, n_scans=3)
+    pipe = _gpu_pipeline(case, ctx)
+    st = case["state"]
+    for k, s in enumerate(case["scans"]):
+        pipe.stage_scan(0, s)
+        pipe.run_scan(0, s, st.scan_count)
+        st, comb, res = O.process_scan(st, cases.scan_input(s), case["ios"], case["bins"], case["cfg"])
+        ctx.sync()
+        diag = pipe.hyp_diag()
+        stats, bcert, xi = pipe.bin_stats()
+        bel = pipe.get_beliefs()
+        for i in range(H):
+            r = res[i]
+            _close(xi[i], r["xi_body"], 1e-9, 1e-12, f"scan{k} hyp{i} xi_body")
+            _close(stats[i, :, 0], r["moments"]["N"], 1e-10, 0, f"scan{k} hyp{i} bin N")
+            _close(stats[i, :, 16:25].reshape(-1, 3, 3), r["moments"]["Sigma_p"], 1e-7, 1e-12, f"Sigma_p {k}/{i}")
+            _close(diag[i, 24:27], O.so3_log(r["mf"]["R_mf"]), 1e-7, 1e-10, f"scan{k} hyp{i} R_mf")
+            _close(diag[i, 21:24], r["planar"]["t_wls"], 1e-7, 1e-10, f"scan{k} hyp{i} t_wls")
+            assert abs(diag[i, 6] - r["T"]) <= 1e-8 * abs(r["T"]) + 1e-10, (k, i, diag[i, 6], r["T"])
+            assert abs(diag[i, 7] - r["beta"]) < 1e-10 and abs(diag[i, 8] - r["alpha"]) < 1e-12
+            assert abs(diag[i, 11] - r["rho"]) < 1e-8
+            b = r["belief"]
+            _close(diag[i, 0:6], r["pose"], 0.0, 1e-6, f"scan{k} hyp{i} world pose")       # north-star bar
+            _close(bel["X_anchor"][i], b.X_anchor, 0.0, 1e-6, f"scan{k} hyp{i} X_anchor")
+            _close(bel["L"][i], b.L, 1e-8, 0.0, f"scan{k} hyp{i} L")
+            _close(bel["z_lin"][i], b.z_lin, 1e-6, 1e-9, f"scan{k} hyp{i} z_lin")
+        c = pipe.combined()
+        _close(c["L"], comb["L"], 1e-8, 0.0, f"scan{k} combined L")
+        _close(c["h"], comb["h"], 1e-6, 1e-9, f"scan{k} combined h")
+        _close(c["z_lin"], comb["z_lin"], 1e-6, 1e-9, f"scan{k} combined z_lin")
+        iw = pipe.get_iw()
+        _close(iw["nu_proc"], st.nu_proc, 1e-12, 0, "nu_proc")
+        _close(iw["Psi_proc"], st.Psi_proc, 1e-7, 1e-18, "Psi_proc")
+        _close(iw["Psi_meas"], st.Psi_meas, 1e-7, 1e-18, "Psi_meas")
+        _close(iw["Q"], O.iw_process_Q(st.nu_proc, st.Psi_proc), 1e-7, 1e-18, "Q")
+        mp = pipe.get_map()
+        _close(mp["map"], cases.map_to_record(st.map), 1e-8, 1e-12, f"scan{k} map")
