@@ -80,54 +80,77 @@ def bytes_moment_match(n, B):
     return n * (24 + 72 + 8 + 8 + B * 8) + 24 + B * (1 + 3 + 9 + 3 + 9 + 1) * 8
 
 
+def warmup_map_record(ctx, _abi, scan, n, B, bins, origin):
+    """Initial MapBinStats from one warm-up scan at the identity pose (zero pose covariance):
+    the GPU bin statistics of the un-deskewed scan, pushed forward with R = I, t = 0."""
+    from gcslam.constants import GC_TAU_SOFT_ASSIGN
+    d = {k: _abi.DeviceArray.from_host(ctx, scan[k]) for k in ("points", "timestamps", "weights")}
+    scal = _abi.DeviceArray(ctx, 8)
+    _abi.call("gc_budget_stats", ctx.handle, d["weights"].ptr, n, n, scal.ptr, ctx=ctx)
+    xi = _abi.DeviceArray.from_host(ctx, np.zeros((1, 6)))
+    db = _abi.DeviceArray.from_host(ctx, bins)
+    st, ce = _abi.DeviceArray(ctx, (1, B, 38)), _abi.DeviceArray(ctx, (1, 8))
+    oa, op = _abi.f64p(origin)
+    # a wide deskew window (t0 - 1000 s .. t1 + 1000 s) weights every point by the same ~0.987
+    _abi.call("gc_scan_bins_fused", ctx.handle, 1, n, n, B, d["points"].ptr, d["timestamps"].ptr, d["weights"].ptr,
+              scal.ptr, scan["scan_start"] - 1e3, scan["scan_end"] + 1e3, xi.ptr, db.ptr, GC_TAU_SOFT_ASSIGN, op,
+              1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
+    s = st.download()[0]
+    N, pb, Sp = s[:, 0], s[:, 13:16], s[:, 16:25].reshape(B, 3, 3)
+    from gcslam.pipeline import map_record
+    return map_record(s[:, 1:4], s[:, 4:13], N, N, N[:, None] * pb,
+                      N[:, None, None] * (Sp + np.einsum("bi,bj->bij", pb, pb)))
+
+
 def main():
     args = parse()
     dist = Dist(args.gpus)
     from gcslam import _abi
-    from gcslam.constants import GC_B_BINS, GC_TAU_SOFT_ASSIGN, T_BASE_LIDAR
+    from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
     from gcslam.ops.binning import create_fibonacci_atlas
-    from gcslam.synth import make_scan
+    from gcslam.pipeline import BatchedScanPipeline, PipelineConfig, iw_meas_prior, iw_process_prior
+    from gcslam.synth import make_hypotheses, make_io_evidence, make_scan
 
     ctx = _abi.Context(dist.local_rank)
     H_total = args.hyps
-    h0 = (H_total * dist.rank) // dist.world
-    h1 = (H_total * (dist.rank + 1)) // dist.world
-    H = h1 - h0
     B = GC_B_BINS
     origin = np.asarray(T_BASE_LIDAR[:3])
     bins = create_fibonacci_atlas(B).dirs
-    scans = [make_scan(k, n_az=args.n_az) for k in range(args.scans)]
+    scans = [make_scan(k + 1, n_az=args.n_az) for k in range(args.scans)]
     n = scans[0]["points"].shape[0]
-    rng = np.random.default_rng(20261015 + 99)
-    xi_all = np.zeros((H_total, 6))
-    xi_all[:, 0] = 0.1 + rng.normal(0, 0.005, H_total)
-    xi_all[:, 5] = 0.03 + rng.normal(0, 0.002, H_total)
-    xi = xi_all[h0:h1]
+    pipe = BatchedScanPipeline(H_total, n, PipelineConfig(n_points_cap=n), rank=dist.rank,
+                               world_size=dist.world, ctx=ctx)
+    h0, h1 = pipe.h0, pipe.h1
+    H = h1 - h0
+    hy = make_hypotheses(H_total)
+    Lio, hio, cio = make_io_evidence(H_total)
+    pipe.set_beliefs(hy["X_anchor"][h0:h1], hy["z_lin"][h0:h1], hy["L"][h0:h1], hy["h"][h0:h1], hy["stamp"][h0:h1])
+    pipe.set_weights(hy["weights"])
+    pipe.set_io_evidence(Lio[h0:h1], hio[h0:h1], cio[h0:h1])
+    pipe.set_iw(*iw_process_prior(), *iw_meas_prior())
+    pipe.set_map(warmup_map_record(ctx, _abi, make_scan(0, n_az=args.n_az), n, B, bins, origin))
+    if dist.world > 1:
+        uid = [pipe.comm_unique_id() if dist.rank == 0 else None]
+        dist.td.broadcast_object_list(uid, src=0)
+        pipe.attach_comm(uid[0])
+    for k, s in enumerate(scans):
+        pipe.stage_scan(k, s)
 
-    # resident inputs
-    dscan = [{k: _abi.DeviceArray.from_host(ctx, s[k]) for k in ("points", "timestamps", "weights")} for s in scans]
-    dxi = _abi.DeviceArray.from_host(ctx, xi)
-    dbins = _abi.DeviceArray.from_host(ctx, bins)
-    dscal = _abi.DeviceArray(ctx, 8)
-    dstats = _abi.DeviceArray(ctx, (H, B, 38))
-    dcert = _abi.DeviceArray(ctx, (H, 8))
-    oa, op = _abi.f64p(origin)
+    count = [0]
 
-    def step(k):
-        s, d = scans[k % len(scans)], dscan[k % len(scans)]
-        _abi.call("gc_budget_stats", ctx.handle, d["weights"].ptr, n, n, dscal.ptr, ctx=ctx)
-        _abi.call("gc_scan_bins_fused", ctx.handle, H, n, n, B, d["points"].ptr, d["timestamps"].ptr,
-                  d["weights"].ptr, dscal.ptr, s["scan_start"], s["scan_end"], dxi.ptr, dbins.ptr,
-                  GC_TAU_SOFT_ASSIGN, op, 1e-12, 1e-12, dstats.ptr, dcert.ptr, ctx=ctx)
+    def step():
+        k = count[0] % len(scans)
+        pipe.run_scan(k, scans[k], count[0])
+        count[0] += 1
 
-    for k in range(args.warmup):
-        step(k)
+    for _ in range(args.warmup):
+        step()
     ctx.sync()
     dist.barrier()
     ctx.sync()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
+    for _ in range(args.steps):
+        step()
     ctx.sync()
     dist.barrier()
     t1 = time.perf_counter()
@@ -146,16 +169,23 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (VLP-16-like 16x%d ray-cast box room, SURVEY §8d)" % args.n_az,
-        "config": {"workload": "C3 front half: budget + per-hypothesis deskew + soft-assign + moment-match "
-                               "(fused) over all hypotheses; per-hypothesis twists synthetic",
+        "data": "synthetic (VLP-16-like 16x%d ray-cast box room + 200 Hz IMU, SURVEY §8d; "
+                "IMU/odom-branch evidence synthetic)" % args.n_az,
+        "config": {"workload": "C3: one 64k-point scan x %d hypotheses through the full batched pipeline "
+                               "(a1-a16: budget, predict, IMU preint, deskew, soft-assign, moment-match, "
+                               "Matrix-Fisher, planar, tempering, fusion, recompose, IW, map, anchor drift, "
+                               "barycenter combine)" % H_total,
                    "points": n, "hypotheses": H_total, "bins": B, "parallelism": "hypotheses/%d" % dist.world},
     }
 
     if dist.rank == 0 and not args.no_roofline:
-        out["roofline"] = roofline_leg(ctx, _abi, scans[0], dscan[0], xi, dbins, B, n, H, origin)
+        rng = np.random.default_rng(5)
+        xi = np.zeros((H, 6)); xi[:, 0] = 0.1 + rng.normal(0, 0.005, H); xi[:, 5] = 0.03 + rng.normal(0, 0.002, H)
+        d0 = {k: _abi.DeviceArray.from_host(ctx, scans[0][k]) for k in ("points", "timestamps", "weights")}
+        dbins = _abi.DeviceArray.from_host(ctx, bins)
+        out["roofline"] = roofline_leg(ctx, _abi, scans[0], d0, xi, dbins, B, n, H, origin)
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
-        out["cpu_baseline"] = cpu_leg(scans[0], xi_all, bins, origin, n, H_total, args.cpu_budget_s)
+        out["cpu_baseline"] = cpu_leg(args.n_az, H_total, args.cpu_budget_s)
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
 
@@ -200,28 +230,30 @@ def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=3):
             "hypotheses": H}
 
 
-def cpu_leg(s, xi_all, bins, origin, n, H_total, budget_s):
-    """Oracle front half on whole hypotheses until the time budget is spent; extrapolated."""
+def cpu_leg(n_az, H_total, budget_s):
+    """The CPU oracle (NumPy restatement of the reference pipeline) on whole hypotheses of the
+    same workload until the time budget is spent; per-scan time extrapolated to H hypotheses."""
     sys.path.insert(0, ROOT)
     from threadpoolctl import threadpool_limits
-    from oracle import gc_oracle as O
+    from oracle import cases, gc_oracle as O
+    case = cases.build(H=H_total, n_az=n_az, n_scans=1)
+    st, s = case["state"], case["scans"][0]
+    Q = O.iw_process_Q(st.nu_proc, st.Psi_proc)
+    md = O.map_derived(st.map)
+    scan = cases.scan_input(s)
     with threadpool_limits(limits=1):
         t0 = time.perf_counter()
         done = 0
         while done < H_total:
-            bud = O.point_budget_resample(s["points"], s["timestamps"], s["weights"], None, None, n)
-            p0, wd, _ = O.deskew_constant_twist(bud["points"], bud["timestamps"], bud["weights"],
-                                                s["scan_start"], s["scan_end"], xi_all[done])
-            sa = O.bin_soft_assign(O.point_directions(p0, origin), bins)
-            O.scan_bin_moment_match(p0, None, wd, sa["resp"], None, origin)
+            O.scan_hypothesis(st.beliefs[done], scan, Q, case["ios"][done], st.map, md, case["bins"], case["cfg"])
             done += 1
             if time.perf_counter() - t0 > budget_s:
                 break
         dt = time.perf_counter() - t0
     per_hyp = dt / done
     return {"value": 1.0 / (per_hyp * H_total), "unit": "scans/s", "cores": 1, "kind": "port",
-            "sample": "%d of %d hypotheses of one %d-point scan through the oracle front half (NumPy, 1 thread), "
-                      "extrapolated; %s" % (done, H_total, n, os.environ.get("HOSTNAME", "")),
+            "sample": "%d of %d hypotheses of one %d-point scan through the oracle pipeline (a1-a14 per "
+                      "hypothesis, NumPy, 1 BLAS thread), extrapolated to the full scan" % (done, H_total, case["n"]),
             "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
 
 

@@ -87,11 +87,11 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   const double dc = (1.0 - ef) / (2.0 * P.lambda_ou + kF64Eps);
   for (int i = t; i < N2; i += kWG) W2[i] = ef * W2[i] + dc * P.Q[i];
   __syncthreads();
-  wg_psd_project(W2, W3, P.eps_psd, n, Sx, red, c1);  // cov_psd -> W3
+  wg_psd_project_fast(W2, W3, P.eps_psd, n, Sx, red, c1);  // cov_psd -> W3
   double trl = (t < n) ? W3[t * n + t] : 0.0;
   const double trace_cov = wg_sum(trl, red);
   wg_inverse_lifted(W3, W2, P.eps_lift, n, W4, W1);   // L_pred raw -> W2
-  wg_psd_project(W2, W1, P.eps_psd, n, Sx, red, c2);  // L_pred -> W1
+  wg_psd_project_fast(W2, W1, P.eps_psd, n, Sx, red, c2);  // L_pred -> W1
   wg_matvec(W1, mu_prev, hpred, n);                   // h_pred = L_pred mu_prev
   for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
   if (t < n) P.hpred[(int64_t)h * n + t] = hpred[t];

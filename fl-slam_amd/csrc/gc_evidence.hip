@@ -259,7 +259,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   for (int i = t; i < NN; i += kWG) W2[i] = Lps[i] + alpha * Lev[i];
   if (t < n) hpo[t] = hps[t] + alpha * hev[t];
   __syncthreads();
-  wg_psd_project(W2, Lpo, P.eps_psd, n, Sx, red, c6);
+  wg_psd_project_fast(W2, Lpo, P.eps_psd, n, Sx, red, c6);
   // a12 recompose: T from every operator's trigger magnitude (pipeline.py:1211)
   if (t == 0) {
     const double* bc = P.bincert + (int64_t)hl * 8;
@@ -414,51 +414,49 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
 }
 
 // ==================================================================== a16 partial sums (local)
+// grid: ceil(P_len / 64) blocks x 256 threads; block covers 64 record entries, its 4 waves sum
+// interleaved hypothesis subsets, combined in fixed order (deterministic).
 __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
-  __shared__ double wn_s[1024];
+  __shared__ double part[4][64];
   __shared__ double red[8];
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, lane = t & 63, g = t >> 6;
+  const int n = kDZ, Hl = P.Hl;
   // floored / renormalised weights over ALL hypotheses (hypothesis.py:77-82), replicated
   double loc = 0.0;
   for (int k = t; k < P.H; k += kWG) loc += fmax(P.weights[k], P.weight_floor);
   const double wsum = wg_sum(loc, red);
-  double* out = P.send;
-  const int Hl = P.Hl, n = kDZ;
-  for (int k = t; k < Hl && k < 1024; k += kWG) wn_s[k] = fmax(P.weights[P.h_begin + k], P.weight_floor) / wsum;
-  __syncthreads();
-  for (int e = t; e < kPMAP; e += kWG) {
-    double s = 0.0;
-    if (e < kPH) {
-      for (int k = 0; k < Hl; ++k) s += wn_s[k] * P.L[(int64_t)k * NN + e];
-    } else if (e < kPZ) {
-      for (int k = 0; k < Hl; ++k) s += wn_s[k] * P.h[(int64_t)k * n + (e - kPH)];
-    } else if (e < kPMU) {
-      for (int k = 0; k < Hl; ++k) s += wn_s[k] * P.z[(int64_t)k * n + (e - kPZ)];
-    } else if (e < kPMU2) {
-      for (int k = 0; k < Hl; ++k) s += wn_s[k] * P.mu_fin[(int64_t)k * n + (e - kPMU)];
-    } else if (e == kPMU2) {
-      for (int k = 0; k < Hl; ++k) {
+  const int e = blockIdx.x * 64 + lane;
+  const int PLn = partial_len(P.B);
+  double s = 0.0;
+  if (e < kPMAP) {
+    for (int k = g; k < Hl; k += 4) {
+      const double wr = P.weights[P.h_begin + k];
+      const double wn = fmax(wr, P.weight_floor) / wsum;
+      double v = 0.0;
+      if (e < kPH) v = wn * P.L[(int64_t)k * NN + e];
+      else if (e < kPZ) v = wn * P.h[(int64_t)k * n + (e - kPH)];
+      else if (e < kPMU) v = wn * P.z[(int64_t)k * n + (e - kPZ)];
+      else if (e < kPMU2) v = wn * P.mu_fin[(int64_t)k * n + (e - kPMU)];
+      else if (e == kPMU2) {
         double q = 0.0;
         for (int i = 0; i < n; ++i) q += P.mu_fin[(int64_t)k * n + i] * P.mu_fin[(int64_t)k * n + i];
-        s += wn_s[k] * q;
-      }
-    } else if (e < kPDNUP) {
-      for (int k = 0; k < Hl; ++k) s += P.weights[P.h_begin + k] * P.dPsiP[(int64_t)k * 252 + (e - kPDPSIP)];
-    } else if (e < kPDPSIM) {
-      for (int k = 0; k < Hl; ++k) s += P.weights[P.h_begin + k] * 1.0;
-    } else if (e < kPDNUM) {
-      for (int k = 0; k < Hl; ++k) s += P.weights[P.h_begin + k] * P.dPsiM[(int64_t)k * 27 + (e - kPDPSIM)];
-    } else if (e < kPDNUM + 3) {
-      const double dn = (e - kPDNUM < 2) ? 1.0 : 0.0;
-      for (int k = 0; k < Hl; ++k) s += P.weights[P.h_begin + k] * dn;
-    } else if (e >= kPX0 && e < kPX0 + 6) {
-      s = (P.h_begin == 0) ? P.X[e - kPX0] : 0.0;
-    } else if (e == kPSTAMP0) {
-      s = (P.h_begin == 0) ? P.stamp[0] : 0.0;
+        v = wn * q;
+      } else if (e < kPDNUP) v = wr * P.dPsiP[(int64_t)k * 252 + (e - kPDPSIP)];
+      else if (e < kPDPSIM) v = wr;
+      else if (e < kPDNUM) v = wr * P.dPsiM[(int64_t)k * 27 + (e - kPDPSIM)];
+      else if (e < kPDNUM + 3) v = (e - kPDNUM < 2) ? wr : 0.0;
+      s += v;
     }
-    out[e] = s;
   }
-  for (int e = t; e < P.B * kMapRec; e += kWG) out[kPMAP + e] = (P.h_begin == 0) ? P.map_inc[e] : 0.0;
+  part[g][lane] = s;
+  __syncthreads();
+  if (g == 0 && e < PLn) {
+    double r = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    if (e >= kPX0 && e < kPX0 + 6) r = (P.h_begin == 0) ? P.X[e - kPX0] : 0.0;
+    else if (e == kPSTAMP0) r = (P.h_begin == 0) ? P.stamp[0] : 0.0;
+    else if (e >= kPMAP) r = (P.h_begin == 0) ? P.map_inc[e - kPMAP] : 0.0;
+    P.send[e] = r;
+  }
 }
 
 // Map-derived statistics for the evidence of the next scan (bin_atlas.py:166-207) and the
@@ -505,25 +503,58 @@ __global__ void __launch_bounds__(256) k_map_derive(PipeDev P) {
   map_derive_wg(P, red, tab);
 }
 
-// process_noise_state_to_Q_jax (inverse_wishart_jax.py:35-68)
+// Projection of one padded 6x6 IW block whose active part is the leading d x d (d in {1,3}):
+// the padded block is [A, 0; 0, 0], so its PSD projection is [PSD(A), 0; 0, eps I] and the
+// projection delta picks up (6-d) eps^2 (the reference projects the padded 6x6 as a whole).
+GC_DEV double psd_padded_small(const double* A6, int d, double eps, double* out6) {
+  for (int k = 0; k < 36; ++k) out6[k] = 0.0;
+  double d2 = (6 - d) * eps * eps;
+  if (d == 1) {
+    const double a = A6[0], p = fmax(a, eps);
+    out6[0] = p;
+    d2 += (p - a) * (p - a);
+  } else {
+    double A[9], Pp[9], c[6];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) A[3 * i + j] = A6[6 * i + j];
+    psd_project3(A, eps, Pp, c);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) out6[6 * i + j] = Pp[3 * i + j];
+    d2 += c[0] * c[0];
+  }
+  for (int k = d; k < 6; ++k) out6[7 * k] = eps;
+  return sqrt(d2);
+}
+
+// process_noise_state_to_Q_jax (inverse_wishart_jax.py:35-68). Q is block diagonal (the masked
+// 6x6 patches overwrite each other's zero padding), so its PSD projection is the direct sum of
+// the active blocks' projections: 3x3 blocks in registers, the 6x6 extrinsic block on the WG.
 GC_DEV void iw_Q_wg(const PipeDev& P, double* Qs, double* Qp, double* Sx, double* red) {
   const int t = threadIdx.x, n = kDZ;
-  for (int idx = t; idx < NN; idx += kWG) Qs[idx] = 0.0;
+  for (int idx = t; idx < NN; idx += kWG) Qp[idx] = 0.0;
   __syncthreads();
-  if (t == 0) {
-    for (int b = 0; b < 7; ++b) {
-      const double den = softplus(50.0 * (P.nu_proc[b] - kBlockDim[b] - 1.0)) / 50.0 + 1e-12;
-      const int s0 = kBlockStart[b];
-      const int e0 = (s0 + 6 < n) ? s0 + 6 : n;
-      for (int i = 0; i < e0 - s0; ++i)
-        for (int j = 0; j < e0 - s0; ++j) {
-          const double m = (i < kBlockDim[b] && j < kBlockDim[b]) ? 1.0 : 0.0;
-          Qs[(s0 + i) * n + (s0 + j)] = P.Psi_proc[b * 36 + i * 6 + j] / den * m;
-        }
+  auto den = [&](int b) { return softplus(50.0 * (P.nu_proc[b] - kBlockDim[b] - 1.0)) / 50.0 + 1e-12; };
+  if (t < 6) {
+    const int b = t, d = kBlockDim[b], s0 = kBlockStart[b];
+    const double dn = den(b);
+    if (d == 1) {
+      Qp[s0 * n + s0] = fmax(P.Psi_proc[b * 36] / dn, P.eps_psd);
+    } else {
+      double A[9], Pp[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A[3 * i + j] = P.Psi_proc[b * 36 + 6 * i + j] / dn;
+      psd_project3(A, P.eps_psd, Pp, nullptr);
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Qp[(s0 + i) * n + (s0 + j)] = Pp[3 * i + j];
     }
   }
+  const double d6 = den(6);
+  for (int idx = t; idx < 36; idx += kWG) Qs[idx] = P.Psi_proc[6 * 36 + idx] / d6;
   __syncthreads();
-  wg_psd_project(Qs, Qp, P.eps_psd, n, Sx, red, nullptr);
+  double* Q6 = Qs + 36;
+  wg_psd_project_fast(Qs, Q6, P.eps_psd, 6, Sx, red, nullptr);
+  for (int idx = t; idx < 36; idx += kWG) Qp[(16 + idx / 6) * n + (16 + idx % 6)] = Q6[idx];
+  __syncthreads();
   for (int idx = t; idx < NN; idx += kWG) P.Q[idx] = Qp[idx];
   __syncthreads();
 }
@@ -564,7 +595,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
   const double* R = P.send;
   for (int i = t; i < NN; i += kWG) Lr[i] = R[kPL + i];
   __syncthreads();
-  wg_psd_project(Lr, Lc, P.eps_psd, n, Sx, red, c6);
+  wg_psd_project_fast(Lr, Lc, P.eps_psd, n, Sx, red, c6);
   double* cb = P.comb;
   for (int i = t; i < NN; i += kWG) cb[i] = Lc[i];
   if (t < n) { cb[NN + t] = R[kPH + t]; cb[NN + n + t] = R[kPZ + t]; }
@@ -589,25 +620,36 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
   }
   __syncthreads();
   // ---- process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
-  double pd_acc = 0.0, nu_acc = 0.0;
-  for (int b = 0; b < 7; ++b) {
-    if (t < 36) {
-      const int i = t / 6, j = t % 6;
-      const double m = (i < kBlockDim[b] && j < kBlockDim[b]) ? 1.0 : 0.0;
-      blk[t] = (kRhoProc[b] * P.Psi_proc[b * 36 + t] + S.w_process * R[kPDPSIP + b * 36 + t]) * m;
-    }
-    __syncthreads();
-    wg_psd_project(blk, blkp, P.eps_psd, 6, Sx, red, c6);
-    if (t < 36) P.Psi_proc[b * 36 + t] = blkp[t];
-    if (t == 0) {
-      pd_acc += c6[0];
-      const double nr = kRhoProc[b] * P.nu_proc[b] + S.w_process * R[kPDNUP + b];
-      const double nn = nu_project(nr, kBlockDim[b], P.nu_max);
-      nu_acc += fabs(nn - nr);
-      P.nu_proc[b] = nn;
-    }
-    __syncthreads();
+  if (t < 7) {  // ν update (smooth projection) for every block
+    const double nr = kRhoProc[t] * P.nu_proc[t] + S.w_process * R[kPDNUP + t];
+    const double nn = nu_project(nr, kBlockDim[t], P.nu_max);
+    tab[16 + t] = fabs(nn - nr);
+    tab[24 + t] = nn;
   }
+  if (t < 6) {  // 3x3 and 1x1 blocks in registers
+    double A6[36], O6[36];
+    for (int k = 0; k < 36; ++k) {
+      const int i = k / 6, j = k % 6;
+      const double m = (i < kBlockDim[t] && j < kBlockDim[t]) ? 1.0 : 0.0;
+      A6[k] = (kRhoProc[t] * P.Psi_proc[t * 36 + k] + S.w_process * R[kPDPSIP + t * 36 + k]) * m;
+    }
+    tab[8 + t] = psd_padded_small(A6, kBlockDim[t], P.eps_psd, O6);
+    for (int k = 0; k < 36; ++k) Qs[t * 36 + k] = O6[k];
+  }
+  if (t < 36) blk[t] = kRhoProc[6] * P.Psi_proc[6 * 36 + t] + S.w_process * R[kPDPSIP + 6 * 36 + t];
+  __syncthreads();
+  wg_psd_project_fast(blk, blkp, P.eps_psd, 6, Sx, red, c6);
+  for (int k = t; k < 6 * 36; k += kWG) P.Psi_proc[k] = Qs[k];
+  if (t < 36) P.Psi_proc[6 * 36 + t] = blkp[t];
+  if (t < 7) P.nu_proc[t] = tab[24 + t];
+  __syncthreads();
+  double pd_acc = 0.0, nu_acc = 0.0;
+  if (t == 0) {
+    for (int b = 0; b < 6; ++b) pd_acc += tab[8 + b];
+    pd_acc += c6[0];
+    for (int b = 0; b < 7; ++b) nu_acc += tab[16 + b];
+  }
+  __syncthreads();
   // ---- measurement-noise IW apply (measurement_noise_iw_jax.py:59-100)
   if (t < 3) {
     double Mr[9], Mp[9], cc[6];
@@ -652,7 +694,7 @@ hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) 
   return hipGetLastError();
 }
 hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
-  hipLaunchKernelGGL(k_combine_local, dim3(1), dim3(256), 0, st, P);
+  hipLaunchKernelGGL(k_combine_local, dim3((partial_len(P.B) + 63) / 64), dim3(256), 0, st, P);
   return hipGetLastError();
 }
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {

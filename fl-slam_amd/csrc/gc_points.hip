@@ -37,6 +37,34 @@ GC_DEV double group16_max(double v) {
   return v;
 }
 
+// exp(x) for the softmax arguments x <= ~0 (x = (s - 1)/τ, |s| <= 1): 64-entry 2^(j/64) table
+// in LDS, Cody-Waite reduction r = x - k ln2/64 (|r| <= ln2/128), degree-5 Taylor (error
+// < 4e-17 relative), ldexp. ~10 f64 ops instead of ocml's general-range exp.
+constexpr double kLn2Over64Hi = 0.010830424695086549;  // ln2/64 with 20 trailing zero bits
+constexpr double kLn2Over64Lo = 1.162596423439437e-12;  // ln2/64 - hi (exact digits)
+GC_DEV void exp_table_init(double* T) {
+  if (threadIdx.x < 64) T[threadIdx.x] = exp2((double)threadIdx.x / 64.0);
+}
+GC_DEV double exp_neg(double x, const double* T) {
+  const double kf = rint(x * 92.33248261689366);  // 64 / ln2
+  const int k = (int)kf;
+  const double r = fma(-kf, kLn2Over64Lo, fma(-kf, kLn2Over64Hi, x));
+  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
+  p = fma(p, r, 1.0 / 6.0);
+  p = fma(p, r, 0.5);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return ldexp(T[k & 63] * p, k >> 6);
+}
+// 1/z for z > 0 in a normal range: hardware reciprocal + two Newton steps (<= 1 ulp).
+GC_DEV double recip(double z) {
+  double r = __builtin_amdgcn_rcp(z);
+  double e = fma(-z, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-z, r, 1.0);
+  return fma(r, e, r);
+}
+
 GC_DEV void lds_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -97,35 +125,45 @@ GC_DEV void direction(const double* p, const double* o, double eps, double* d) {
 }
 
 // =============================================================================== a1 budget
-__global__ void __launch_bounds__(256) k_budget_stats(const double* __restrict__ w, int64_t n_in,
-                                                      int64_t n_cap, int64_t stride, double* out) {
+// Two-level deterministic reduction: 64 workgroups write [Σw_in, Σw_sel, Σw_sel²] partials, one
+// workgroup finishes. ess = 1 / Σ_cap (ŵ² + ε) is evaluated as (scale/(m_in+ε))² Σw_sel² + cap·ε
+// (algebraically the reference's sum, point_budget.py:100-101).
+constexpr int kBudgetBlocks = 64;
+__global__ void __launch_bounds__(256) k_budget_partials(const double* __restrict__ w, int64_t n_in,
+                                                         int64_t stride, double* part) {
   __shared__ double red[4];
   const int64_t n_sel = (n_in + stride - 1) / stride;
-  double loc_in = 0.0, loc_sel = 0.0;
-  for (int64_t i = threadIdx.x; i < n_in; i += kWG) loc_in += w[i];
-  for (int64_t j = threadIdx.x; j < n_sel; j += kWG) loc_sel += w[j * stride];
-  const double mass_in = wg_sum(loc_in, red);
-  const double mass_sel = wg_sum(loc_sel, red);
-  const double scale = mass_in / (mass_sel + 1e-12);
-  double loc_ess = 0.0, loc_out = 0.0;
-  for (int64_t j = threadIdx.x; j < n_cap; j += kWG) {
-    const double wo = (j < n_sel) ? w[j * stride] * scale : 0.0;
-    const double wn = wo / (mass_in + 1e-12);
-    loc_ess += wn * wn + 1e-12;
-    loc_out += wo;
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n_in; i += (int64_t)gridDim.x * kWG) a += w[i];
+  for (int64_t j = (int64_t)blockIdx.x * kWG + threadIdx.x; j < n_sel; j += (int64_t)gridDim.x * kWG) {
+    const double v = w[j * stride];
+    b += v;
+    c += v * v;
   }
-  const double s_ess = wg_sum(loc_ess, red);
-  const double s_out = wg_sum(loc_out, red);
+  a = wg_sum(a, red);
+  b = wg_sum(b, red);
+  c = wg_sum(c, red);
   if (threadIdx.x == 0) {
-    out[0] = mass_in;
-    out[1] = mass_sel;
-    out[2] = scale;
-    out[3] = 1.0 / s_ess;
-    out[4] = s_out;
-    out[5] = (double)n_sel;
-    out[6] = (double)stride;
-    out[7] = fmin(1.0, (double)n_cap / ((double)n_in + 1e-12));
+    part[3 * blockIdx.x] = a; part[3 * blockIdx.x + 1] = b; part[3 * blockIdx.x + 2] = c;
   }
+}
+
+__global__ void k_budget_final(const double* __restrict__ part, int blocks, int64_t n_in, int64_t n_cap,
+                               int64_t stride, double* out) {
+  if (threadIdx.x != 0) return;
+  double a = 0.0, b = 0.0, c = 0.0;
+  for (int k = 0; k < blocks; ++k) { a += part[3 * k]; b += part[3 * k + 1]; c += part[3 * k + 2]; }
+  const int64_t n_sel = (n_in + stride - 1) / stride;
+  const double scale = a / (b + 1e-12);
+  const double f = scale / (a + 1e-12);
+  out[0] = a;
+  out[1] = b;
+  out[2] = scale;
+  out[3] = 1.0 / (f * f * c + (double)n_cap * 1e-12);
+  out[4] = scale * b;
+  out[5] = (double)n_sel;
+  out[6] = (double)stride;
+  out[7] = fmin(1.0, (double)n_cap / ((double)n_in + 1e-12));
 }
 
 __global__ void k_budget_gather(const double* __restrict__ pts, const double* __restrict__ t,
@@ -204,6 +242,9 @@ __global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, const dou
                                                      const double* __restrict__ bins, double inv_tau,
                                                      double* resp, int32_t* bin_idx, double* partial) {
   __shared__ double red[8];
+  __shared__ double Tx[64];
+  exp_table_init(Tx);
+  __syncthreads();
   const int h = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, bl = lane & 15;
@@ -244,13 +285,13 @@ __global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, const dou
 #pragma unroll
     for (int j = 0; j < BPL; ++j) {
       const double x = S[j] * inv_tau - m;
-      e[j] = bv[j] ? exp(x) : 0.0;
+      e[j] = bv[j] ? exp_neg(x, Tx) : 0.0;
       zl += e[j];
       sl += e[j] * x;
     }
     const double Z = group16_sum(zl);
     const double Sx = group16_sum(sl);
-    const double rZ = 1.0 / Z;
+    const double rZ = recip(Z);
 #pragma unroll
     for (int j = 0; j < BPL; ++j) {
       const double r = e[j] * rZ;
@@ -422,7 +463,7 @@ __global__ void __launch_bounds__(256) k_moment_partials(int64_t n, int B, int i
 // grid (chunks, H). Budget selection + deskew + directions in phase A (lane = point), soft
 // assignment + moment accumulation in phase B (resp stays in registers).
 template <int BPL>
-__global__ void __launch_bounds__(256) k_bins_fused(int64_t n_cap, int B, int iters,
+__global__ void __launch_bounds__(256, 2) k_bins_fused(int64_t n_cap, int B, int iters,
                                                     const double* __restrict__ pts_raw,
                                                     const double* __restrict__ t_raw,
                                                     const double* __restrict__ w_raw,
@@ -447,16 +488,17 @@ __global__ void __launch_bounds__(256) k_bins_fused(int64_t n_cap, int B, int it
   const int64_t stride = (int64_t)bscal[6];
   const double denom = fmax(t1 - t0, 1e-12);
   const double sig = 0.1 * denom;
-  double bx[BPL], by[BPL], bz[BPL];
-  bool bv[BPL];
-#pragma unroll
-  for (int j = 0; j < BPL; ++j) {
-    const int b = bl + 16 * j;
-    bv[j] = b < B;
-    bx[j] = bv[j] ? bins[3 * b] : 0.0;
-    by[j] = bv[j] ? bins[3 * b + 1] : 0.0;
-    bz[j] = bv[j] ? bins[3 * b + 2] : 0.0;
+  // bin directions live in LDS (3 x 64 doubles after the 4 wave slabs), not in VGPRs
+  double* Lb = lds + 4 * 64 * NS;  // bins pre-scaled by 1/τ, then the exp table
+  double* Tx = Lb + 192;
+  if (threadIdx.x < 64) {
+    const int b = threadIdx.x;
+    Lb[b] = b < B ? bins[3 * b] * inv_tau : 0.0;
+    Lb[64 + b] = b < B ? bins[3 * b + 1] * inv_tau : 0.0;
+    Lb[128 + b] = b < B ? bins[3 * b + 2] * inv_tau : 0.0;
   }
+  exp_table_init(Tx);
+  __syncthreads();
   double acc[BPL][NF];
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
@@ -498,24 +540,26 @@ __global__ void __launch_bounds__(256) k_bins_fused(int64_t n_cap, int B, int it
       const int pl = s * 4 + g;
       const double d0 = F[(NF + 0) * 64 + pl], d1 = F[(NF + 1) * 64 + pl], d2 = F[(NF + 2) * 64 + pl];
       const bool valid = F[(NF + 3) * 64 + pl] != 0.0;
-      double e[BPL], zl = 0.0, sl = 0.0;
+      double e[BPL], zl = 0.0, sl = 0.0, em = 0.0;
 #pragma unroll
       for (int j = 0; j < BPL; ++j) {
-        const double x = (d0 * bx[j] + d1 * by[j] + d2 * bz[j]) * inv_tau - xmax;
-        e[j] = bv[j] ? exp(x) : 0.0;
+        const int b = bl + 16 * j;
+        const double x = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -xmax)));
+        e[j] = (b < B) ? exp_neg(x, Tx) : 0.0;
         zl += e[j];
-        sl += e[j] * x;
+        sl = fma(e[j], x, sl);
+        em = fmax(em, e[j]);
       }
       const double Z = group16_sum(zl);
       const double Sx = group16_sum(sl);
-      const double rZ = 1.0 / Z;
-      if (valid) entq += Sx * rZ;
+      const double rZ = recip(Z);
+      if (valid) {
+        entq = fma(Sx, rZ, entq);
+        mxr = fmax(mxr, em * rZ);
+      }
       if (bl == s) zst = valid ? Z : 1.0;
 #pragma unroll
-      for (int j = 0; j < BPL; ++j) {
-        e[j] *= rZ;
-        if (valid) mxr = fmax(mxr, e[j]);
-      }
+      for (int j = 0; j < BPL; ++j) e[j] *= rZ;
 #pragma unroll
       for (int k = 0; k < NF; ++k) {
         const double fk = F[k * 64 + pl];
@@ -658,7 +702,13 @@ int32_t gc_budget_stats(gc_ctx* ctx, const double* d_w, int64_t n_in, int64_t n_
   GC_CHECK_ARG(ctx, n_in > 0 && n_cap > 0, "n_in and n_cap must be positive");
   GC_CHECK_ARG(ctx, d_w && d_out, "NULL buffer");
   const int64_t stride = std::max<int64_t>(1, (n_in + n_cap - 1) / n_cap);
-  hipLaunchKernelGGL(k_budget_stats, dim3(1), dim3(256), 0, ctx->stream, d_w, n_in, n_cap, stride, d_out);
+  void* scr;
+  if (int rc = gc::scratch(ctx, sizeof(double) * 3 * kBudgetBlocks, &scr)) return rc;
+  hipLaunchKernelGGL(k_budget_partials, dim3(kBudgetBlocks), dim3(256), 0, ctx->stream, d_w, n_in, stride,
+                     (double*)scr);
+  GC_LAUNCH_CHECK(ctx);
+  hipLaunchKernelGGL(k_budget_final, dim3(1), dim3(64), 0, ctx->stream, (const double*)scr, kBudgetBlocks, n_in,
+                     n_cap, stride, d_out);
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
 }
@@ -792,7 +842,7 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const int RL = B * NF + REC_EXTRA;
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
-  const size_t sh = sizeof(double) * std::max<size_t>(4 * 64 * (NF + 4), 4 * (size_t)B * NF + 12);
+  const size_t sh = sizeof(double) * (std::max<size_t>(4 * 64 * (NF + 4), 4 * (size_t)B * NF + 12) + 4 * 64);
   dim3 grid((unsigned)chunks, H);
   const double inv_tau = 1.0 / tau;
 #define GC_FUSED(BP)                                                                                     \

@@ -87,6 +87,41 @@ GC_DEV void wg_chol(double* A, int n) {
   __syncthreads();
 }
 
+// In-place lower Cholesky that reports failure (a pivot <= 0 or NaN): returns true on success
+// on every thread. flag: one LDS double.
+GC_DEV bool wg_chol_checked(double* A, int n, double* flag) {
+  if (threadIdx.x == 0) flag[0] = 0.0;
+  __syncthreads();
+  for (int k = 0; k < n; ++k) {
+    if (threadIdx.x == 0) {
+      double d = A[k * n + k];
+      if (!(d > 0.0)) { flag[0] = 1.0; d = 1.0; }
+      A[k * n + k] = sqrt(d);
+    }
+    __syncthreads();
+    const double dk = A[k * n + k];
+    const int m = n - k - 1;
+    if ((int)threadIdx.x < m) {
+      const int i = k + 1 + threadIdx.x;
+      A[i * n + k] = A[i * n + k] / dk;
+    }
+    __syncthreads();
+    const int tri = m * (m + 1) / 2;
+    for (int idx = threadIdx.x; idx < tri; idx += kWG) {
+      int i = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
+      while ((i + 1) * (i + 2) / 2 <= idx) ++i;
+      while (i * (i + 1) / 2 > idx) --i;
+      const int j = idx - i * (i + 1) / 2;
+      const int gi = k + 1 + i, gj = k + 1 + j;
+      A[gi * n + gj] -= A[gi * n + k] * A[gj * n + k];
+    }
+    __syncthreads();
+  }
+  const bool ok = flag[0] == 0.0;
+  __syncthreads();
+  return ok;
+}
+
 // x = (C Cᵀ)^{-1} b for lower-triangular C (thread 0; result visible to all on return).
 GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
   if (threadIdx.x == 0) {
@@ -178,7 +213,8 @@ GC_DEV void wg_jacobi_eigh(double* A, double* V, double* w, int n, double* cs, d
     if (idx / n != idx % n) offloc += A[idx] * A[idx];
   const double fro2 = wg_sum(dloc + offloc, red);
   double off = wg_sum(offloc, red);
-  for (int sweep = 0; sweep < 20 && off > 1e-34 * fro2 && off > 1e-300; ++sweep) {
+  // stop once the off-diagonal mass is at rounding level (||offdiag||_F <= 1e-15 ||A||_F)
+  for (int sweep = 0; sweep < 20 && off > 1e-30 * fro2 && off > 1e-300; ++sweep) {
     for (int r = 0; r < n - 1; ++r) {
       if ((int)threadIdx.x < half) {
         int p, q;
@@ -282,6 +318,38 @@ GC_DEV void wg_psd_project(const double* M, double* Mp, double eps, int n, doubl
     cert6[4] = mx / mn; cert6[5] = nn;
   }
   __syncthreads();
+}
+
+// domain_projection_psd_core with a certified shortcut, for the batched pipeline: if
+// Cholesky of (M_sym - eps I) succeeds, every eigenvalue exceeds eps, the clamp is inactive and
+// the projection is M_sym itself (the reference's V diag(λ) Vᵀ reconstructs M_sym up to
+// rounding, ~1e-15 ||M||). projection_delta is then 0 and the eigen fields of cert6 are NaN
+// (not computed). Otherwise the full Jacobi projection runs. scratch: 2n*n + 4n doubles.
+GC_DEV void wg_psd_project_fast(const double* M, double* Mp, double eps, int n, double* scratch,
+                                double* red, double* cert6) {
+  double symloc = 0.0;
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    const double sv = 0.5 * (M[i * n + j] + M[j * n + i]);
+    const double d = sv - M[idx];
+    symloc += d * d;
+    scratch[idx] = sv - ((i == j) ? eps : 0.0);
+  }
+  const double symd = wg_sum(symloc, red);
+  const bool spd = wg_chol_checked(scratch, n, red + 4);
+  if (spd) {
+    for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+      const int i = idx / n, j = idx % n;
+      Mp[idx] = 0.5 * (M[i * n + j] + M[j * n + i]);
+    }
+    if (cert6 && threadIdx.x == 0) {
+      const double nan = __builtin_nan("");
+      cert6[0] = 0.0; cert6[1] = sqrt(symd); cert6[2] = nan; cert6[3] = nan; cert6[4] = nan; cert6[5] = nan;
+    }
+    __syncthreads();
+    return;
+  }
+  wg_psd_project(M, Mp, eps, n, scratch, red, cert6);
 }
 
 // eigvalsh (ascending not required) of the symmetrised n x n M -> w. scratch: n*n + 3n.
