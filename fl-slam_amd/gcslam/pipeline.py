@@ -216,3 +216,12 @@ def iw_process_prior():
 def iw_meas_prior(lidar_sigma: float = 0.01):
     """create_datasheet_measurement_noise_state (structures/measurement_noise_iw_jax.py:37-68)."""
     return np.full(3, 4.5), np.stack([8.7e-7 * np.eye(3), 9.5e-5 * np.eye(3), lidar_sigma * np.eye(3)]) * 0.5
+
+
+# Layout of the per-rank partial record exchanged once per scan (csrc/gc_pipe.h kP*).
+RECORD = dict(L=(0, 484), h=(484, 506), z=(506, 528), mu=(528, 550), mu2=(550, 551), dPsiP=(551, 803),
+              dnuP=(803, 810), dPsiM=(810, 837), dnuM=(837, 840), X0=(841, 847), stamp0=(847, 848))
+
+
+def partial_len(B: int) -> int:
+    return 848 + 26 * B
