@@ -13,6 +13,8 @@
 // result is bit-reproducible run to run (no float atomics anywhere).
 #include <hip/hip_runtime.h>
 #include <algorithm>
+#include <cstdint>
+#include <type_traits>
 #include "gc_internal.h"
 #include "gc_wgla.h"
 
@@ -22,19 +24,47 @@ constexpr int NF_BASE = 19;   // [1, d(3), dd(6: 00 01 02 11 12 22), p(3), pp(6)
 constexpr int NF_COV = 9;     // full 3x3 point covariance x w
 constexpr int REC_EXTRA = 4;  // [entropy_sum, max_resp, sum_w, n_points]
 
+// 16-lane (DPP row) butterflies: quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror,
+// row_mirror. Every step pairs each lane with a distinct partner holding a disjoint partial, so
+// all 16 lanes end with the bit-identical total; no LDS round trip (ds_bpermute) on the path.
+template <int CTRL>
+GC_DEV double dpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <int CTRL>
+GC_DEV int dpp_i32(int v) {
+  return __builtin_amdgcn_mov_dpp(v, CTRL, 0xF, 0xF, false);
+}
+constexpr int kDppXor1 = 0xB1, kDppXor2 = 0x4E, kDppHalfMirror = 0x141, kDppMirror = 0x140;
+
 GC_DEV double group16_sum(double v) {
-  v += __shfl_xor(v, 8, 16);
-  v += __shfl_xor(v, 4, 16);
-  v += __shfl_xor(v, 2, 16);
-  v += __shfl_xor(v, 1, 16);
+  v += dpp_f64<kDppXor1>(v);
+  v += dpp_f64<kDppXor2>(v);
+  v += dpp_f64<kDppHalfMirror>(v);
+  v += dpp_f64<kDppMirror>(v);
   return v;
 }
 GC_DEV double group16_max(double v) {
-  v = fmax(v, __shfl_xor(v, 8, 16));
-  v = fmax(v, __shfl_xor(v, 4, 16));
-  v = fmax(v, __shfl_xor(v, 2, 16));
-  v = fmax(v, __shfl_xor(v, 1, 16));
+  v = fmax(v, dpp_f64<kDppXor1>(v));
+  v = fmax(v, dpp_f64<kDppXor2>(v));
+  v = fmax(v, dpp_f64<kDppHalfMirror>(v));
+  v = fmax(v, dpp_f64<kDppMirror>(v));
   return v;
+}
+template <int CTRL>
+GC_DEV void argmax_step(double& best, int& bidx) {
+  const double ob = dpp_f64<CTRL>(best);
+  const int oi = dpp_i32<CTRL>(bidx);
+  if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
+}
+// (max, lowest index on ties) over the 16 lanes of a row
+GC_DEV void group16_argmax(double& best, int& bidx) {
+  argmax_step<kDppXor1>(best, bidx);
+  argmax_step<kDppXor2>(best, bidx);
+  argmax_step<kDppHalfMirror>(best, bidx);
+  argmax_step<kDppMirror>(best, bidx);
 }
 
 // exp(x) for the softmax arguments x <= ~0 (x = (s - 1)/τ, |s| <= 1): 64-entry 2^(j/64) table
@@ -235,14 +265,19 @@ __global__ void k_point_dirs(int64_t rows, const double* __restrict__ pts, doubl
 }
 
 // ============================================================================ a5 soft assign
-// grid (ceil(n/256), H); each wave: 16 steps x 4 points. Writes resp rows coalesced
-// (16 bin-lanes x 8 B = 128 B per point and bin-slot).
+// grid (chunks, H), chunk = iters*256 points; each wave owns 64 points per iteration and walks
+// them 4 per step (lanes = 4 point-groups x 16 bin-lanes, lane l owns bins {l, l+16, ..}).
+// Directions arrive lane-per-point (coalesced, prefetched one iteration ahead) and are handed
+// out through a wave-private LDS slab. Softmax sums and the argmax are 16-lane DPP butterflies.
+// Per-point scalars are stashed on lane (g, l) for step l (point 4l+g): one log Z and one
+// coalesced bin-index store per lane per iteration.
 template <int BPL>
-__global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, const double* __restrict__ dirs,
+__global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
                                                      const double* __restrict__ bins, double inv_tau,
                                                      double* resp, int32_t* bin_idx, double* partial) {
   __shared__ double red[8];
   __shared__ double Tx[64];
+  __shared__ double Dl[4][3 * 64];
   exp_table_init(Tx);
   __syncthreads();
   const int h = blockIdx.y;
@@ -259,53 +294,80 @@ __global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, const dou
     bz[j] = bv[j] ? bins[3 * b + 2] : 0.0;
   }
   const double Beps = (double)B * 1e-12;
-  double ent = 0.0, mxr = 0.0;
-  const int64_t base = (int64_t)blockIdx.x * 256 + wv * 64;
-  for (int s = 0; s < 16; ++s) {
-    const int64_t pt = base + s * 4 + g;
-    const bool valid = pt < n;
-    const int64_t row = (int64_t)h * n + (valid ? pt : 0);
-    const double d0 = dirs[3 * row], d1 = dirs[3 * row + 1], d2 = dirs[3 * row + 2];
-    double S[BPL];
-    double best = -1e308;
-    int bidx = 0x7fffffff;
-#pragma unroll
-    for (int j = 0; j < BPL; ++j) {
-      S[j] = sim_nofma(d0, d1, d2, bx[j], by[j], bz[j]);
-      if (bv[j] && S[j] > best) { best = S[j]; bidx = bl + 16 * j; }
+  double* Rh = resp + (int64_t)h * n * B;
+  const double* Dh = dirs + (int64_t)h * n * 3;
+  double* D = Dl[wv];
+  double logacc = 0.0, entq = 0.0, mxr = 0.0;
+  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
+  double nd0, nd1, nd2;
+  {
+    const int64_t p = chunk0 + wv * 64 + lane;
+    const int64_t pc = p < n ? p : n - 1;
+    nd0 = Dh[3 * pc]; nd1 = Dh[3 * pc + 1]; nd2 = Dh[3 * pc + 2];
+  }
+  for (int it = 0; it < iters; ++it) {
+    const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
+    if (wbase >= n) break;  // wave-uniform
+    D[lane] = nd0; D[64 + lane] = nd1; D[128 + lane] = nd2;
+    {
+      const int64_t p = wbase + 256 + lane;
+      const int64_t pc = p < n ? p : n - 1;
+      nd0 = Dh[3 * pc]; nd1 = Dh[3 * pc + 1]; nd2 = Dh[3 * pc + 2];
     }
-    // argmax across the 16 bin-lanes (lowest index on ties)
-    for (int off = 8; off >= 1; off >>= 1) {
-      const double ob = __shfl_xor(best, off, 16);
-      const int oi = __shfl_xor(bidx, off, 16);
-      if (ob > best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
-    }
-    const double m = best * inv_tau;
-    double e[BPL], zl = 0.0, sl = 0.0;
+    lds_wave_sync();
+    double zst = 1.0;
+    int ist = 0;
+#pragma unroll 2
+    for (int s = 0; s < 16; ++s) {
+      const int pl = s * 4 + g;
+      const int64_t pt = wbase + pl;
+      const bool valid = pt < n;
+      const double d0 = D[pl], d1 = D[64 + pl], d2 = D[128 + pl];
+      double S[BPL];
+      double best = -1e308;
+      int bidx = 0x7fffffff;
 #pragma unroll
-    for (int j = 0; j < BPL; ++j) {
-      const double x = S[j] * inv_tau - m;
-      e[j] = bv[j] ? exp_neg(x, Tx) : 0.0;
-      zl += e[j];
-      sl += e[j] * x;
-    }
-    const double Z = group16_sum(zl);
-    const double Sx = group16_sum(sl);
-    const double rZ = recip(Z);
+      for (int j = 0; j < BPL; ++j) {
+        S[j] = sim_nofma(d0, d1, d2, bx[j], by[j], bz[j]);
+        if (bv[j] && S[j] > best) { best = S[j]; bidx = bl + 16 * j; }
+      }
+      group16_argmax(best, bidx);  // lowest index on ties
+      const double m = best * inv_tau;
+      double zl = 0.0, sl = 0.0;
 #pragma unroll
-    for (int j = 0; j < BPL; ++j) {
-      const double r = e[j] * rZ;
-      if (valid && bv[j]) {
-        resp[row * B + bl + 16 * j] = r;
-        mxr = fmax(mxr, r);
+      for (int j = 0; j < BPL; ++j) {
+        const double x = S[j] * inv_tau - m;
+        S[j] = bv[j] ? exp_neg(x, Tx) : 0.0;
+        zl += S[j];
+        sl = fma(S[j], x, sl);
+      }
+      const double Z = group16_sum(zl);
+      const double Sx = group16_sum(sl);
+      const double rZ = recip(Z);
+      if (valid) {
+        double* dst = Rh + pt * B + bl;
+#pragma unroll
+        for (int j = 0; j < BPL; ++j) {
+          const double r = S[j] * rZ;
+          if (bv[j]) {
+            dst[16 * j] = r;
+            mxr = fmax(mxr, r);
+          }
+        }
+        if (bl == 0) entq += Sx * rZ + Beps;
+      }
+      if (bl == s) {
+        zst = valid ? Z : 1.0;
+        ist = bidx;
       }
     }
-    if (valid && bl == 0) {
-      ent += (log(Z) - Sx * rZ) - Beps;  // -Σ R log(R+ε) up to ≤ B·ε
-      if (bin_idx) bin_idx[row] = bidx;
-    }
+    logacc += log(zst);
+    const int64_t pi = wbase + 4 * bl + g;  // the point whose scalars this lane stashed
+    if (bin_idx && pi < n) bin_idx[(int64_t)h * n + pi] = ist;
+    lds_wave_sync();
   }
-  const double es = wg_sum(ent, red);
+  // entropy over the chunk's points: Σ (log Z - S/Z - B ε)   (-Σ R log(R+ε) up to ≤ B·ε)
+  const double es = wg_sum(logacc - entq, red);
   const double ms = wg_max(mxr, red);
   if (threadIdx.x == 0) {
     partial[((int64_t)h * gridDim.x + blockIdx.x) * 2] = es;
@@ -371,92 +433,166 @@ GC_DEV void write_partial_record(double (&acc)[BPL][NF], double ent, double mxr,
   }
 }
 
-// Contract variant: responsibilities streamed from HBM. grid (chunks, H), chunk = ITERS*256 pts.
-template <int BPL, bool COV>
-__global__ void __launch_bounds__(256) k_moment_partials(int64_t n, int B, int iters,
-                                                         const double* __restrict__ pts,
-                                                         const double* __restrict__ covs,
-                                                         const double* __restrict__ w,
-                                                         const double* __restrict__ resp,
-                                                         const double* __restrict__ lam, double o0,
-                                                         double o1, double o2, double* partials) {
+// Contract variant: responsibilities streamed from HBM. One wave per workgroup, grid (chunks, H),
+// chunk = iters*32 points. Lanes = 4 feature-quarters x 16 bin-lanes and one point per step:
+// lane (q, l) owns bins {l, l+16, ..} x features [q*NQ, (q+1)*NQ), so every (bin, feature) sum
+// has exactly one owner (no cross-lane reduction) and the accumulators stay small (BPL*NQ
+// doubles). Responsibilities move in 8-point blocks (8B contiguous doubles): each lane loads
+// its 16-byte pieces of block k+2 into registers while block k is consumed from an LDS double
+// buffer (register-staged ring, ~6 KiB in flight per wave). Features are staged per 32 points
+// in LDS (row stride 33: the 4 quarter reads of a step land on distinct banks); the raw
+// inputs of the next 32 points are prefetched into registers one sub-chunk ahead.
+template <int BPL, bool COV, int VW>
+__global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int iters,
+                                                        const double* __restrict__ pts,
+                                                        const double* __restrict__ covs,
+                                                        const double* __restrict__ w,
+                                                        const double* __restrict__ resp,
+                                                        const double* __restrict__ lam, double o0,
+                                                        double o1, double o2, double* partials) {
   constexpr int NF = COV ? NF_BASE + NF_COV : NF_BASE;
-  extern __shared__ double lds[];  // max(4 * 64 * NF, 4*B*NF + 12)
+  constexpr int NQ = (NF + 3) / 4;
+  constexpr int FS = 33;
+  constexpr int BMAX = 16 * BPL;          // padded bins per row in the LDS block image
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
+  using V = typename std::conditional<VW == 2, dvec2, double>::type;  // 16-byte pieces when B is even
+  constexpr int PL = (8 * BMAX / VW + 63) / 64;  // pieces per lane per block
+  __shared__ double F[4 * NQ * FS];
+  __shared__ double RB[2][8 * BMAX];
   const int h = blockIdx.y;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int g = lane >> 4, bl = lane & 15;
-  double* F = lds + wv * (NF * 64);
+  const int lane = threadIdx.x, fq = lane >> 4, bl = lane & 15;
   const double o[3] = {o0, o1, o2};
-  double acc[BPL][NF];
+  const double* Rh = resp + (int64_t)h * n * B;
+  const double* Fq = F + fq * NQ * FS;
+  const int64_t nB = n * (int64_t)B;  // doubles of this hypothesis' rows
+  bool bv[BPL];
+  int jo[BPL];
+#pragma unroll
+  for (int j = 0; j < BPL; ++j) {
+    bv[j] = bl + 16 * j < B;
+    jo[j] = min(bl + 16 * j, B - 1);
+  }
+  double acc[BPL][NQ];
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
 #pragma unroll
-    for (int k = 0; k < NF; ++k) acc[j][k] = 0.0;
-  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
-  for (int it = 0; it < iters; ++it) {
-    const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
-    {  // phase A: lane = point
-      const int64_t pt = wbase + lane;
-      double f[NF];
-      if (pt < n) {
-        const int64_t row = (int64_t)h * n + pt;
-        const double p[3] = {pts[3 * row], pts[3 * row + 1], pts[3 * row + 2]};
-        double d[3];
-        direction(p, o, 1e-12, d);
-        const double we = w[row] * (lam ? lam[row] : 1.0);
-        point_features(p, d, we, f);
-        if constexpr (COV) {
+    for (int q = 0; q < NQ; ++q) acc[j][q] = 0.0;
+  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 32;
+  int64_t cend = chunk0 + (int64_t)iters * 32;
+  cend = cend < n ? cend : n;
+  const int nsub = (int)((cend - chunk0 + 31) / 32);  // >= 1 (grid sized to n)
+
+  // block k covers points [chunk0 + 8k, +8): doubles [(chunk0 + 8k) * B, +8B), clamped in range
+  // (blocks past the end re-read valid rows; their points have zero features). LDS image: row i
+  // (point) at i*BMAX, so lane (., l) reads bin l + 16 j at a fixed stride.
+  int soff[PL];  // this lane's LDS offsets in a block image (-1: no piece)
 #pragma unroll
-          for (int k = 0; k < 9; ++k) f[NF_BASE + k] = we * covs[9 * row + k];
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < NF; ++k) f[k] = 0.0;
-      }
-#pragma unroll
-      for (int k = 0; k < NF; ++k) F[k * 64 + lane] = f[k];
-    }
-    lds_wave_sync();
-    // phase B: 16 steps x 4 points, lanes = 4 groups x 16 bin-lanes
-    double rn[BPL];
-    {
-      const int64_t pt = wbase + g;
-      const int64_t row = (int64_t)h * n + (pt < n ? pt : 0);
-#pragma unroll
-      for (int j = 0; j < BPL; ++j) {
-        const int b = bl + 16 * j;
-        rn[j] = (pt < n && b < B) ? resp[row * B + b] : 0.0;
-      }
-    }
-#pragma unroll 1
-    for (int s = 0; s < 16; ++s) {
-      double r[BPL];
-#pragma unroll
-      for (int j = 0; j < BPL; ++j) r[j] = rn[j];
-      if (s < 15) {  // prefetch next step
-        const int64_t pt = wbase + (s + 1) * 4 + g;
-        const int64_t row = (int64_t)h * n + (pt < n ? pt : 0);
-#pragma unroll
-        for (int j = 0; j < BPL; ++j) {
-          const int b = bl + 16 * j;
-          rn[j] = (pt < n && b < B) ? resp[row * B + b] : 0.0;
-        }
-      }
-      const int pl = s * 4 + g;
-#pragma unroll
-      for (int k = 0; k < NF; ++k) {
-        const double fk = F[k * 64 + pl];
-#pragma unroll
-        for (int j = 0; j < BPL; ++j) acc[j][k] += r[j] * fk;
-      }
-    }
-    lds_wave_sync();
+  for (int m = 0; m < PL; ++m) {
+    const int e = VW * (lane + 64 * m);
+    const int i = e / B, b = e - i * B;  // VW == 2 only for even B: a pair stays in one row
+    soff[m] = e < 8 * B ? i * BMAX + b : -1;
   }
-  int64_t npts = n - chunk0;
-  npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
+#define GC_LOAD_BLK(R, K)                                                  \
+  {                                                                        \
+    const int64_t e0_ = (chunk0 + 8 * (int64_t)(K)) * B;                   \
+    _Pragma("unroll") for (int m = 0; m < PL; ++m) {                       \
+      int64_t e_ = e0_ + VW * (int64_t)(lane + 64 * m);                    \
+      e_ = e_ < nB - VW ? e_ : nB - VW;                                    \
+      R[m] = *reinterpret_cast<const V*>(Rh + e_);                         \
+    }                                                                      \
+  }
+#define GC_STORE_BLK(R, SLOT)                                              \
+  {                                                                        \
+    _Pragma("unroll") for (int m = 0; m < PL; ++m) if (soff[m] >= 0)       \
+        *reinterpret_cast<V*>(&RB[SLOT][soff[m]]) = R[m];                  \
+  }
+  // raw inputs of one 32-point sub-chunk (point = lane & 31), loaded by every lane, unconditionally
+  double rp[3], rc[9], rw;
+#define GC_LOAD_RAW(BASE)                                                  \
+  {                                                                        \
+    const int64_t pt_ = (BASE) + (lane & 31);                              \
+    const bool ok_ = pt_ < n;                                              \
+    const int64_t row_ = (int64_t)h * n + (ok_ ? pt_ : 0);                 \
+    rw = w[row_] * (lam ? lam[row_] : 1.0);                                \
+    rw = ok_ ? rw : 0.0;                                                   \
+    rp[0] = pts[3 * row_]; rp[1] = pts[3 * row_ + 1]; rp[2] = pts[3 * row_ + 2]; \
+    if constexpr (COV) {                                                   \
+      _Pragma("unroll") for (int k_ = 0; k_ < 9; ++k_) rc[k_] = covs[9 * row_ + k_]; \
+    }                                                                      \
+  }
+#define GC_CONSUME(SLOT, S0)                                               \
+  {                                                                        \
+    const double* rs_ = RB[SLOT];                                          \
+    _Pragma("unroll 2") for (int i = 0; i < 8; ++i) {                      \
+      double r_[BPL];                                                      \
+      _Pragma("unroll") for (int j = 0; j < BPL; ++j) r_[j] = rs_[i * BMAX + jo[j]]; \
+      _Pragma("unroll") for (int q = 0; q < NQ; ++q) {                     \
+        const double fk_ = Fq[q * FS + (S0) + i];                          \
+        _Pragma("unroll") for (int j = 0; j < BPL; ++j) acc[j][q] = fma(r_[j], fk_, acc[j][q]); \
+      }                                                                    \
+    }                                                                      \
+  }
+  // register-staged ring: block k lives in set (k & 1) until stored to LDS slot (k & 1)
+  V ra[PL], rb[PL];
+  GC_LOAD_RAW(chunk0)
+  GC_LOAD_BLK(ra, 0)
+  GC_LOAD_BLK(rb, 1)
+  GC_STORE_BLK(ra, 0)
+  for (int c = 0; c < nsub; ++c) {
+    lds_wave_sync();  // previous sub-chunk's feature reads are done
+    if (lane < 32) {
+      double d[3], f[NF_BASE];
+      direction(rp, o, 1e-12, d);
+      point_features(rp, d, rw, f);
+#pragma unroll
+      for (int kk = 0; kk < NF_BASE; ++kk) F[kk * FS + lane] = f[kk];
+    } else {
+      const int pl = lane - 32;
+      if constexpr (COV) {
+#pragma unroll
+        for (int kk = 0; kk < NF_COV; ++kk) F[(NF_BASE + kk) * FS + pl] = rw * rc[kk];
+      }
+#pragma unroll
+      for (int kk = NF; kk < 4 * NQ; ++kk) F[kk * FS + pl] = 0.0;
+    }
+    GC_LOAD_RAW(chunk0 + 32 * (int64_t)(c + 1))
+    const int k0 = 4 * c;
+    GC_LOAD_BLK(ra, k0 + 2)
+    lds_wave_sync();
+    GC_CONSUME(0, 0)
+    lds_wave_sync();
+    GC_STORE_BLK(rb, 1)
+    GC_LOAD_BLK(rb, k0 + 3)
+    lds_wave_sync();
+    GC_CONSUME(1, 8)
+    lds_wave_sync();
+    GC_STORE_BLK(ra, 0)
+    GC_LOAD_BLK(ra, k0 + 4)
+    lds_wave_sync();
+    GC_CONSUME(0, 16)
+    lds_wave_sync();
+    GC_STORE_BLK(rb, 1)
+    GC_LOAD_BLK(rb, k0 + 5)
+    lds_wave_sync();
+    GC_CONSUME(1, 24)
+    lds_wave_sync();
+    GC_STORE_BLK(ra, 0)
+  }
+#undef GC_LOAD_BLK
+#undef GC_STORE_BLK
+#undef GC_CONSUME
+#undef GC_LOAD_RAW
+  const int64_t npts = cend - chunk0;
   const int RL = B * NF + REC_EXTRA;
-  write_partial_record<BPL, NF>(acc, 0.0, 0.0, 0.0, (double)npts, B, lds,
-                                partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
+  double* rec = partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL;
+#pragma unroll
+  for (int j = 0; j < BPL; ++j)
+#pragma unroll
+    for (int q = 0; q < NQ; ++q) {
+      const int k = fq * NQ + q;
+      if (bv[j] && k < NF) rec[(bl + 16 * j) * NF + k] = acc[j][q];
+    }
+  if (lane < REC_EXTRA) rec[B * NF + lane] = lane == 3 ? (double)npts : 0.0;
 }
 
 // =========================================================== fused a1 -> a4 -> a5 -> a6
@@ -764,17 +900,18 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
   GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
   GC_CHECK_ARG(ctx, tau > 0.0, "tau must be positive");
   GC_CHECK_ARG(ctx, d_dirs && d_bins && d_resp_out && d_cert_out, "NULL buffer");
-  const int64_t blocks = (n + 255) / 256;
+  int iters = 4;
+  while (iters > 1 && ((n + iters * 256 - 1) / (iters * 256)) * (int64_t)H < 4096) iters >>= 1;
+  const int64_t blocks = (n + iters * 256 - 1) / (iters * 256);
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * 2 * blocks * H, &scr)) return rc;
   const double inv_tau = 1.0 / tau;
   dim3 grid((unsigned)blocks, H);
-  switch (bpl_for(B)) {
-    case 1: hipLaunchKernelGGL(k_soft_assign<1>, grid, dim3(256), 0, ctx->stream, n, B, d_dirs, d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr); break;
-    case 2: hipLaunchKernelGGL(k_soft_assign<2>, grid, dim3(256), 0, ctx->stream, n, B, d_dirs, d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr); break;
-    case 3: hipLaunchKernelGGL(k_soft_assign<3>, grid, dim3(256), 0, ctx->stream, n, B, d_dirs, d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr); break;
-    default: hipLaunchKernelGGL(k_soft_assign<4>, grid, dim3(256), 0, ctx->stream, n, B, d_dirs, d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr); break;
-  }
+#define GC_SA(BP)                                                                                     \
+  hipLaunchKernelGGL((k_soft_assign<BP>), grid, dim3(256), 0, ctx->stream, n, B, iters, d_dirs, d_bins, inv_tau, \
+                     d_resp_out, d_bin_index_out, (double*)scr)
+  switch (bpl_for(B)) { case 1: GC_SA(1); break; case 2: GC_SA(2); break; case 3: GC_SA(3); break; default: GC_SA(4); }
+#undef GC_SA
   GC_LAUNCH_CHECK(ctx);
   hipLaunchKernelGGL(k_soft_assign_finalize, dim3((H + 63) / 64), dim3(64), 0, ctx->stream, (const double*)scr,
                      blocks, H, n, d_cert_out);
@@ -801,19 +938,26 @@ int32_t gc_scan_bin_moment_match(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, c
   GC_CHECK_ARG(ctx, d_points && d_w && d_resp && d_stats_out && d_cert_out, "NULL buffer");
   double o[3] = {0.0, 0.0, 0.0};
   if (h_origin3) { o[0] = h_origin3[0]; o[1] = h_origin3[1]; o[2] = h_origin3[2]; }
-  const int iters = pick_iters(n, H);
-  const int64_t chunks = (n + iters * 256 - 1) / (iters * 256);
+  int iters = 32;  // chunk = iters * 32 points, one wave per chunk
+  while (iters > 1 && ((n + iters * 32 - 1) / (iters * 32)) * (int64_t)H < 16384) iters >>= 1;
+  const int64_t chunks = (n + iters * 32 - 1) / (iters * 32);
   const bool cov = d_covs != nullptr;
   const int NF = cov ? NF_BASE + NF_COV : NF_BASE;
   const int RL = B * NF + REC_EXTRA;
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
-  const size_t sh = sizeof(double) * std::max<size_t>(4 * 64 * NF, 4 * (size_t)B * NF + 12);
   dim3 grid((unsigned)chunks, H);
   const int bpl = bpl_for(B);
-#define GC_MOM(BP, CV)                                                                                   \
-  hipLaunchKernelGGL((k_moment_partials<BP, CV>), grid, dim3(256), sh, ctx->stream, n, B, iters, d_points, \
-                     d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr)
+  const int vw = ((B & 1) == 0 && ((uintptr_t)d_resp & 15) == 0) ? 2 : 1;
+#define GC_MOM(BP, CV)                                                                                        \
+  do {                                                                                                        \
+    if (vw == 2)                                                                                              \
+      hipLaunchKernelGGL((k_moment_partials<BP, CV, 2>), grid, dim3(64), 0, ctx->stream, n, B, iters, d_points, \
+                         d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr);                      \
+    else                                                                                                      \
+      hipLaunchKernelGGL((k_moment_partials<BP, CV, 1>), grid, dim3(64), 0, ctx->stream, n, B, iters, d_points, \
+                         d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr);                      \
+  } while (0)
   if (cov) {
     switch (bpl) { case 1: GC_MOM(1, true); break; case 2: GC_MOM(2, true); break; case 3: GC_MOM(3, true); break; default: GC_MOM(4, true); }
   } else {
