@@ -20,6 +20,8 @@
 
 namespace gc {
 
+typedef double v4d __attribute__((ext_vector_type(4)));  // f64 MFMA accumulator (4 per lane)
+
 constexpr int NF_BASE = 19;   // [1, d(3), dd(6: 00 01 02 11 12 22), p(3), pp(6)] x w
 constexpr int NF_COV = 9;     // full 3x3 point covariance x w
 constexpr int REC_EXTRA = 4;  // [entropy_sum, max_resp, sum_w, n_points]
@@ -67,24 +69,25 @@ GC_DEV void group16_argmax(double& best, int& bidx) {
   argmax_step<kDppMirror>(best, bidx);
 }
 
-// exp(x) for the softmax arguments x <= ~0 (x = (s - 1)/τ, |s| <= 1): 64-entry 2^(j/64) table
-// in LDS, Cody-Waite reduction r = x - k ln2/64 (|r| <= ln2/128), degree-5 Taylor (error
-// < 4e-17 relative), ldexp. ~10 f64 ops instead of ocml's general-range exp.
-constexpr double kLn2Over64Hi = 0.010830424695086549;  // ln2/64 with 20 trailing zero bits
-constexpr double kLn2Over64Lo = 1.162596423439437e-12;  // ln2/64 - hi (exact digits)
-GC_DEV void exp_table_init(double* T) {
-  if (threadIdx.x < 64) T[threadIdx.x] = exp2((double)threadIdx.x / 64.0);
+// exp(x) for the softmax arguments x <= ~0 (x = (s - 1)/τ, |s| <= 1): 256-entry 2^(j/256)
+// table in LDS, Cody-Waite reduction r = x - k ln2/256 (|r| <= ln2/512), degree-4 Taylor
+// (truncation < 4e-17 relative), ldexp. ~12 f64 ops instead of ocml's general-range exp.
+constexpr int kExpTab = 256;
+constexpr double kLn2OverTabHi = 0x1.62e42ffp-9;               // ln2/256, 24 trailing zero bits
+constexpr double kLn2OverTabLo = -1.6409824502660487e-13;      // ln2/256 - hi
+constexpr double kTabOverLn2 = 369.3299304675746;              // 256 / ln2
+GC_DEV void exp_table_init(double* T) {  // needs blockDim.x >= 256
+  if (threadIdx.x < kExpTab) T[threadIdx.x] = exp2((double)threadIdx.x / kExpTab);
 }
 GC_DEV double exp_neg(double x, const double* T) {
-  const double kf = rint(x * 92.33248261689366);  // 64 / ln2
+  const double kf = rint(x * kTabOverLn2);
   const int k = (int)kf;
-  const double r = fma(-kf, kLn2Over64Lo, fma(-kf, kLn2Over64Hi, x));
-  double p = fma(r, 1.0 / 120.0, 1.0 / 24.0);
-  p = fma(p, r, 1.0 / 6.0);
+  const double r = fma(-kf, kLn2OverTabLo, fma(-kf, kLn2OverTabHi, x));
+  double p = fma(r, 1.0 / 24.0, 1.0 / 6.0);
   p = fma(p, r, 0.5);
   p = fma(p, r, 1.0);
   p = fma(p, r, 1.0);
-  return ldexp(T[k & 63] * p, k >> 6);
+  return ldexp(T[k & (kExpTab - 1)] * p, k >> 8);
 }
 // 1/z for z > 0 in a normal range: hardware reciprocal + two Newton steps (<= 1 ulp).
 GC_DEV double recip(double z) {
@@ -276,7 +279,7 @@ __global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, int iters
                                                      const double* __restrict__ bins, double inv_tau,
                                                      double* resp, int32_t* bin_idx, double* partial) {
   __shared__ double red[8];
-  __shared__ double Tx[64];
+  __shared__ double Tx[kExpTab];
   __shared__ double Dl[4][3 * 64];
   exp_table_init(Tx);
   __syncthreads();
@@ -342,7 +345,6 @@ __global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, int iters
         sl = fma(S[j], x, sl);
       }
       const double Z = group16_sum(zl);
-      const double Sx = group16_sum(sl);
       const double rZ = recip(Z);
       if (valid) {
         double* dst = Rh + pt * B + bl;
@@ -354,7 +356,8 @@ __global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, int iters
             mxr = fmax(mxr, r);
           }
         }
-        if (bl == 0) entq += Sx * rZ + Beps;
+        entq = fma(sl, rZ, entq);  // Σ_lanes sl / Z = S/Z of the point (lane partials, summed at the end)
+        if (bl == 0) entq += Beps;
       }
       if (bl == s) {
         zst = valid ? Z : 1.0;
@@ -434,14 +437,15 @@ GC_DEV void write_partial_record(double (&acc)[BPL][NF], double ent, double mxr,
 }
 
 // Contract variant: responsibilities streamed from HBM. One wave per workgroup, grid (chunks, H),
-// chunk = iters*32 points. Lanes = 4 feature-quarters x 16 bin-lanes and one point per step:
-// lane (q, l) owns bins {l, l+16, ..} x features [q*NQ, (q+1)*NQ), so every (bin, feature) sum
-// has exactly one owner (no cross-lane reduction) and the accumulators stay small (BPL*NQ
-// doubles). Responsibilities move in 8-point blocks (8B contiguous doubles): each lane loads
-// its 16-byte pieces of block k+2 into registers while block k is consumed from an LDS double
-// buffer (register-staged ring, ~6 KiB in flight per wave). Features are staged per 32 points
-// in LDS (row stride 33: the 4 quarter reads of a step land on distinct banks); the raw
-// inputs of the next 32 points are prefetched into registers one sub-chunk ahead.
+// chunk = iters*32 points. The moment sums Mom[b][k] = Σ_p R[p][b] F[p][k] run on the matrix
+// core: per 4-point step, bin tile j (16 bins) x feature tile t (16 features) is one
+// v_mfma_f64_16x16x4_f64 with A[bin][point] = R (lane (g, l): point g, bin 16j + l) and
+// B[point][feature] = F (lane (g, l): point g, feature 16t + l). Every (bin, feature) sum has
+// one owner lane, so the chunk record is written without a reduction. Responsibilities move
+// in 8-point blocks (8B contiguous doubles): each lane loads its 16-byte pieces of block k+2
+// into registers while block k is consumed from an LDS double buffer (register-staged ring,
+// ~6 KiB in flight per wave). Features are staged per 32 points in LDS; the raw inputs of the
+// next 32 points are prefetched into registers one sub-chunk ahead.
 template <int BPL, bool COV, int VW>
 __global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int iters,
                                                         const double* __restrict__ pts,
@@ -451,32 +455,24 @@ __global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int it
                                                         const double* __restrict__ lam, double o0,
                                                         double o1, double o2, double* partials) {
   constexpr int NF = COV ? NF_BASE + NF_COV : NF_BASE;
-  constexpr int NQ = (NF + 3) / 4;
+  constexpr int NT = (NF + 15) / 16;      // feature tiles (zero-padded to 16 NT)
   constexpr int FS = 33;
   constexpr int BMAX = 16 * BPL;          // padded bins per row in the LDS block image
   typedef double dvec2 __attribute__((ext_vector_type(2)));
   using V = typename std::conditional<VW == 2, dvec2, double>::type;  // 16-byte pieces when B is even
   constexpr int PL = (8 * BMAX / VW + 63) / 64;  // pieces per lane per block
-  __shared__ double F[4 * NQ * FS];
+  __shared__ double F[16 * NT * FS];
   __shared__ double RB[2][8 * BMAX];
   const int h = blockIdx.y;
-  const int lane = threadIdx.x, fq = lane >> 4, bl = lane & 15;
+  const int lane = threadIdx.x, g = lane >> 4, bl = lane & 15;
   const double o[3] = {o0, o1, o2};
   const double* Rh = resp + (int64_t)h * n * B;
-  const double* Fq = F + fq * NQ * FS;
   const int64_t nB = n * (int64_t)B;  // doubles of this hypothesis' rows
-  bool bv[BPL];
-  int jo[BPL];
-#pragma unroll
-  for (int j = 0; j < BPL; ++j) {
-    bv[j] = bl + 16 * j < B;
-    jo[j] = min(bl + 16 * j, B - 1);
-  }
-  double acc[BPL][NQ];
+  v4d acc[BPL][NT];
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) acc[j][q] = 0.0;
+    for (int t = 0; t < NT; ++t) acc[j][t] = v4d{0.0, 0.0, 0.0, 0.0};
   const int64_t chunk0 = (int64_t)blockIdx.x * iters * 32;
   int64_t cend = chunk0 + (int64_t)iters * 32;
   cend = cend < n ? cend : n;
@@ -522,13 +518,15 @@ __global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int it
   }
 #define GC_CONSUME(SLOT, S0)                                               \
   {                                                                        \
-    const double* rs_ = RB[SLOT];                                          \
-    _Pragma("unroll 2") for (int i = 0; i < 8; ++i) {                      \
-      double r_[BPL];                                                      \
-      _Pragma("unroll") for (int j = 0; j < BPL; ++j) r_[j] = rs_[i * BMAX + jo[j]]; \
-      _Pragma("unroll") for (int q = 0; q < NQ; ++q) {                     \
-        const double fk_ = Fq[q * FS + (S0) + i];                          \
-        _Pragma("unroll") for (int j = 0; j < BPL; ++j) acc[j][q] = fma(r_[j], fk_, acc[j][q]); \
+    _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2) {                     \
+      const double* rs_ = RB[SLOT] + (4 * s2 + g) * BMAX + bl;             \
+      const int pl_ = (S0) + 4 * s2 + g;                                   \
+      double fb_[NT];                                                      \
+      _Pragma("unroll") for (int t = 0; t < NT; ++t) fb_[t] = F[(16 * t + bl) * FS + pl_]; \
+      _Pragma("unroll") for (int j = 0; j < BPL; ++j) {                    \
+        const double ra_ = rs_[16 * j];                                    \
+        _Pragma("unroll") for (int t = 0; t < NT; ++t)                     \
+          acc[j][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ra_, fb_[t], acc[j][t], 0, 0, 0); \
       }                                                                    \
     }                                                                      \
   }
@@ -553,7 +551,7 @@ __global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int it
         for (int kk = 0; kk < NF_COV; ++kk) F[(NF_BASE + kk) * FS + pl] = rw * rc[kk];
       }
 #pragma unroll
-      for (int kk = NF; kk < 4 * NQ; ++kk) F[kk * FS + pl] = 0.0;
+      for (int kk = NF; kk < 16 * NT; ++kk) F[kk * FS + pl] = 0.0;
     }
     GC_LOAD_RAW(chunk0 + 32 * (int64_t)(c + 1))
     const int k0 = 4 * c;
@@ -588,18 +586,74 @@ __global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int it
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
 #pragma unroll
-    for (int q = 0; q < NQ; ++q) {
-      const int k = fq * NQ + q;
-      if (bv[j] && k < NF) rec[(bl + 16 * j) * NF + k] = acc[j][q];
-    }
+    for (int t = 0; t < NT; ++t)
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int b = 16 * j + g + 4 * r, k = 16 * t + bl;  // D[row g + 4r][col l]
+        if (b < B && k < NF) rec[b * NF + k] = acc[j][t][r];
+      }
   if (lane < REC_EXTRA) rec[B * NF + lane] = lane == 3 ? (double)npts : 0.0;
 }
 
+// MFMA epilogue: reduce per-lane tiles over the 4 waves (LDS, fixed order) into one partial
+// record. Lane (g, l) holds D_j[row g + 4r][col l] = Σ R[·][16j + g + 4r] F[·][l] for the 16
+// MFMA features, and per-group partial sums accx[j][t] (bin 16j + l, feature 16 + t).
+template <int BPL, int NX>
+GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL][NX], double ent, double mxr,
+                                      double sumw, double npts, int B, double* lds, double* rec) {
+  constexpr int NF = 16 + NX;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, bl = lane & 15;
+#pragma unroll
+  for (int j = 0; j < BPL; ++j)
+#pragma unroll
+    for (int t = 0; t < NX; ++t) {
+      double v = accx[j][t];
+      v += __shfl_xor(v, 16, 64);
+      v += __shfl_xor(v, 32, 64);
+      accx[j][t] = v;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < BPL; ++j) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const int b = 16 * j + g + 4 * r;
+      if (b < B) lds[(wv * B + b) * NF + bl] = acc4[j][r];
+    }
+    const int b = 16 * j + bl;
+    if (g == 0 && b < B)
+#pragma unroll
+      for (int t = 0; t < NX; ++t) lds[(wv * B + b) * NF + 16 + t] = accx[j][t];
+  }
+  double e = wave_sum(ent), m = wave_max(mxr), s = wave_sum(sumw);
+  if (lane == 0) {
+    lds[4 * B * NF + wv * 3 + 0] = e;
+    lds[4 * B * NF + wv * 3 + 1] = m;
+    lds[4 * B * NF + wv * 3 + 2] = s;
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < B * NF; i += kWG)
+    rec[i] = (lds[i] + lds[B * NF + i]) + (lds[2 * B * NF + i] + lds[3 * B * NF + i]);
+  if (threadIdx.x == 0) {
+    const double* ex = lds + 4 * B * NF;
+    rec[B * NF + 0] = (ex[0] + ex[3]) + (ex[6] + ex[9]);
+    rec[B * NF + 1] = fmax(fmax(ex[1], ex[4]), fmax(ex[7], ex[10]));
+    rec[B * NF + 2] = (ex[2] + ex[5]) + (ex[8] + ex[11]);
+    rec[B * NF + 3] = npts;
+  }
+}
+
 // =========================================================== fused a1 -> a4 -> a5 -> a6
-// grid (chunks, H). Budget selection + deskew + directions in phase A (lane = point), soft
-// assignment + moment accumulation in phase B (resp stays in registers).
+// grid (chunks, H). Budget selection + deskew + directions + features in phase A (lane =
+// point), soft assignment in phase B (lanes = 4 point-groups x 16 bin-lanes, 4 points per
+// step). The moment sums are a GEMM, Mom[b][k] = Σ_p R[p][b] F[p][k]: the step's (16 bins x 4
+// points) responsibility tile of bin block j is exactly the A operand of
+// v_mfma_f64_16x16x4_f64 as the lanes already hold it, and F[p][k] for 4 points x 16 features
+// is one LDS read per lane (B operand). The matrix core accumulates features 0..15 while the
+// VALU does the exp/softmax; features 16..18 stay on the VALU. Responsibilities never leave
+// registers.
 template <int BPL>
-__global__ void __launch_bounds__(256, 2) k_bins_fused(int64_t n_cap, int B, int iters,
+__global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int iters,
                                                     const double* __restrict__ pts_raw,
                                                     const double* __restrict__ t_raw,
                                                     const double* __restrict__ w_raw,
@@ -609,7 +663,8 @@ __global__ void __launch_bounds__(256, 2) k_bins_fused(int64_t n_cap, int B, int
                                                     double o0, double o1, double o2,
                                                     double* partials) {
   constexpr int NF = NF_BASE;
-  constexpr int NS = NF + 4;  // + d(3) + valid flag
+  constexpr int NX = NF - 16;  // features on the VALU
+  constexpr int NS = NF + 4;   // + d(3) + valid flag
   extern __shared__ double lds[];
   const int h = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -624,22 +679,24 @@ __global__ void __launch_bounds__(256, 2) k_bins_fused(int64_t n_cap, int B, int
   const int64_t stride = (int64_t)bscal[6];
   const double denom = fmax(t1 - t0, 1e-12);
   const double sig = 0.1 * denom;
-  // bin directions live in LDS (3 x 64 doubles after the 4 wave slabs), not in VGPRs
-  double* Lb = lds + 4 * 64 * NS;  // bins pre-scaled by 1/τ, then the exp table
-  double* Tx = Lb + 192;
+  double* Tx = lds + 4 * 64 * NS;
+  double* Lb = Tx + kExpTab;  // bin directions pre-scaled by 1/τ (x, y, z rows of 64)
+  exp_table_init(Tx);
   if (threadIdx.x < 64) {
     const int b = threadIdx.x;
     Lb[b] = b < B ? bins[3 * b] * inv_tau : 0.0;
     Lb[64 + b] = b < B ? bins[3 * b + 1] * inv_tau : 0.0;
     Lb[128 + b] = b < B ? bins[3 * b + 2] * inv_tau : 0.0;
   }
-  exp_table_init(Tx);
   __syncthreads();
-  double acc[BPL][NF];
+  v4d acc4[BPL];
+  double accx[BPL][NX];
 #pragma unroll
-  for (int j = 0; j < BPL; ++j)
+  for (int j = 0; j < BPL; ++j) {
+    acc4[j] = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-    for (int k = 0; k < NF; ++k) acc[j][k] = 0.0;
+    for (int t = 0; t < NX; ++t) accx[j][t] = 0.0;
+  }
   double sumw = 0.0, logacc = 0.0, entq = 0.0, mxr = 0.0;
   const double xmax = inv_tau;  // S <= 1 for unit vectors: exp never overflows
   const double Beps = (double)B * 1e-12;
@@ -676,44 +733,48 @@ __global__ void __launch_bounds__(256, 2) k_bins_fused(int64_t n_cap, int B, int
       const int pl = s * 4 + g;
       const double d0 = F[(NF + 0) * 64 + pl], d1 = F[(NF + 1) * 64 + pl], d2 = F[(NF + 2) * 64 + pl];
       const bool valid = F[(NF + 3) * 64 + pl] != 0.0;
+      const double fb = F[bl * 64 + pl];  // MFMA B operand: feature bl of point 4s + g
       double e[BPL], zl = 0.0, sl = 0.0, em = 0.0;
 #pragma unroll
       for (int j = 0; j < BPL; ++j) {
-        const int b = bl + 16 * j;
+        const int b = bl + 16 * j;  // Lb is zero past B: x = -1/τ stays finite, then masked
         const double x = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -xmax)));
-        e[j] = (b < B) ? exp_neg(x, Tx) : 0.0;
+        const double ex = exp_neg(x, Tx);
+        e[j] = (b < B) ? ex : 0.0;
         zl += e[j];
         sl = fma(e[j], x, sl);
         em = fmax(em, e[j]);
       }
       const double Z = group16_sum(zl);
-      const double Sx = group16_sum(sl);
       const double rZ = recip(Z);
       if (valid) {
-        entq = fma(Sx, rZ, entq);
+        entq = fma(sl, rZ, entq);  // lane partials of S/Z, summed over lanes at the end
         mxr = fmax(mxr, em * rZ);
       }
       if (bl == s) zst = valid ? Z : 1.0;
 #pragma unroll
-      for (int j = 0; j < BPL; ++j) e[j] *= rZ;
+      for (int j = 0; j < BPL; ++j) {
+        const double r = e[j] * rZ;
+        acc4[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r, fb, acc4[j], 0, 0, 0);
+      }
 #pragma unroll
-      for (int k = 0; k < NF; ++k) {
-        const double fk = F[k * 64 + pl];
+      for (int t = 0; t < NX; ++t) {
+        const double fk = F[(16 + t) * 64 + pl];
 #pragma unroll
-        for (int j = 0; j < BPL; ++j) acc[j][k] += e[j] * fk;
+        for (int j = 0; j < BPL; ++j) accx[j][t] = fma(e[j] * rZ, fk, accx[j][t]);
       }
     }
     // each lane stashed the Z of one point per 16 steps: one log per lane per iteration
     logacc += log(zst);
     lds_wave_sync();
   }
-  // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε  (entq is group-uniform)
+  // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
   int64_t npts = n_cap - chunk0;
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
-  const double ent = logacc - (bl == 0 ? entq : 0.0) - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
+  const double ent = logacc - entq - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
   const int RL = B * NF + REC_EXTRA;
-  write_partial_record<BPL, NF>(acc, ent, mxr, (lane == 0 ? 0.0 : 0.0) + sumw, (double)npts, B, lds,
-                                partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
+  write_partial_record_mfma<BPL, NX>(acc4, accx, ent, mxr, sumw, (double)npts, B, lds,
+                                     partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
 }
 
 // ================================================================ finalize (a6 + certs)
@@ -986,7 +1047,7 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const int RL = B * NF + REC_EXTRA;
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
-  const size_t sh = sizeof(double) * (std::max<size_t>(4 * 64 * (NF + 4), 4 * (size_t)B * NF + 12) + 4 * 64);
+  const size_t sh = sizeof(double) * std::max<size_t>(4 * 64 * (NF + 4) + kExpTab + 192, 4 * (size_t)B * NF + 12);
   dim3 grid((unsigned)chunks, H);
   const double inv_tau = 1.0 / tau;
 #define GC_FUSED(BP)                                                                                     \
