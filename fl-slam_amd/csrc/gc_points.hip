@@ -89,6 +89,26 @@ GC_DEV double exp_neg(double x, const double* T) {
   p = fma(p, r, 1.0);
   return ldexp(T[k & (kExpTab - 1)] * p, k >> 8);
 }
+// exp_neg over N independent arguments, phased so the N table reads are in flight together
+// (one LDS round trip per step instead of one per bin).
+template <int N>
+GC_DEV void exp_neg_n(const double (&x)[N], const double* T, double (&out)[N]) {
+  double kf[N], tv[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    kf[j] = rint(x[j] * kTabOverLn2);
+    tv[j] = T[(int)kf[j] & (kExpTab - 1)];
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double r = fma(-kf[j], kLn2OverTabLo, fma(-kf[j], kLn2OverTabHi, x[j]));
+    double p = fma(r, 1.0 / 24.0, 1.0 / 6.0);
+    p = fma(p, r, 0.5);
+    p = fma(p, r, 1.0);
+    p = fma(p, r, 1.0);
+    out[j] = ldexp(tv[j] * p, (int)kf[j] >> 8);
+  }
+}
 // 1/z for z > 0 in a normal range: hardware reciprocal + two Newton steps (<= 1 ulp).
 GC_DEV double recip(double z) {
   double r = __builtin_amdgcn_rcp(z);
@@ -334,15 +354,18 @@ __global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, int iters
         S[j] = sim_nofma(d0, d1, d2, bx[j], by[j], bz[j]);
         if (bv[j] && S[j] > best) { best = S[j]; bidx = bl + 16 * j; }
       }
-      group16_argmax(best, bidx);  // lowest index on ties
-      const double m = best * inv_tau;
-      double zl = 0.0, sl = 0.0;
+      group16_argmax(best, bidx);  // lowest index on ties (integer contract only)
+      // softmax shift: the bound S <= 1 (unit directions) instead of the row max, so the exp
+      // chain does not wait on the argmax butterfly; R is the same ratio
+      double zl = 0.0, sl = 0.0, x[BPL], ex[BPL];
+#pragma unroll
+      for (int j = 0; j < BPL; ++j) x[j] = fma(S[j], inv_tau, -inv_tau);
+      exp_neg_n<BPL>(x, Tx, ex);  // unconditional: no branch around the table reads
 #pragma unroll
       for (int j = 0; j < BPL; ++j) {
-        const double x = S[j] * inv_tau - m;
-        S[j] = bv[j] ? exp_neg(x, Tx) : 0.0;
+        S[j] = bv[j] ? ex[j] : 0.0;
         zl += S[j];
-        sl = fma(S[j], x, sl);
+        sl = fma(S[j], x[j], sl);
       }
       const double Z = group16_sum(zl);
       const double rZ = recip(Z);
@@ -530,12 +553,14 @@ __global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int it
       }                                                                    \
     }                                                                      \
   }
-  // register-staged ring: block k lives in set (k & 1) until stored to LDS slot (k & 1)
-  V ra[PL], rb[PL];
+  // register-staged ring: block k is loaded into register set (k & 3) three blocks ahead and
+  // stored to LDS slot (k & 1) one block ahead of its consumption (~9 KiB in flight per wave)
+  V r0[PL], r1[PL], r2[PL], r3[PL];
   GC_LOAD_RAW(chunk0)
-  GC_LOAD_BLK(ra, 0)
-  GC_LOAD_BLK(rb, 1)
-  GC_STORE_BLK(ra, 0)
+  GC_LOAD_BLK(r0, 0)
+  GC_LOAD_BLK(r1, 1)
+  GC_LOAD_BLK(r2, 2)
+  GC_STORE_BLK(r0, 0)
   for (int c = 0; c < nsub; ++c) {
     lds_wave_sync();  // previous sub-chunk's feature reads are done
     if (lane < 32) {
@@ -555,26 +580,17 @@ __global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int it
     }
     GC_LOAD_RAW(chunk0 + 32 * (int64_t)(c + 1))
     const int k0 = 4 * c;
-    GC_LOAD_BLK(ra, k0 + 2)
-    lds_wave_sync();
-    GC_CONSUME(0, 0)
-    lds_wave_sync();
-    GC_STORE_BLK(rb, 1)
-    GC_LOAD_BLK(rb, k0 + 3)
-    lds_wave_sync();
-    GC_CONSUME(1, 8)
-    lds_wave_sync();
-    GC_STORE_BLK(ra, 0)
-    GC_LOAD_BLK(ra, k0 + 4)
-    lds_wave_sync();
-    GC_CONSUME(0, 16)
-    lds_wave_sync();
-    GC_STORE_BLK(rb, 1)
-    GC_LOAD_BLK(rb, k0 + 5)
-    lds_wave_sync();
-    GC_CONSUME(1, 24)
-    lds_wave_sync();
-    GC_STORE_BLK(ra, 0)
+#define GC_RING_STEP(RNEXT3, RNEXT1, KB)                                   \
+    GC_LOAD_BLK(RNEXT3, k0 + (KB) + 3)                                     \
+    lds_wave_sync();                                                       \
+    GC_CONSUME((KB) & 1, 8 * (KB))                                         \
+    lds_wave_sync();                                                       \
+    GC_STORE_BLK(RNEXT1, ((KB) + 1) & 1)
+    GC_RING_STEP(r3, r1, 0)
+    GC_RING_STEP(r0, r2, 1)
+    GC_RING_STEP(r1, r3, 2)
+    GC_RING_STEP(r2, r0, 3)
+#undef GC_RING_STEP
   }
 #undef GC_LOAD_BLK
 #undef GC_STORE_BLK
@@ -734,15 +750,18 @@ __global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int
       const double d0 = F[(NF + 0) * 64 + pl], d1 = F[(NF + 1) * 64 + pl], d2 = F[(NF + 2) * 64 + pl];
       const bool valid = F[(NF + 3) * 64 + pl] != 0.0;
       const double fb = F[bl * 64 + pl];  // MFMA B operand: feature bl of point 4s + g
-      double e[BPL], zl = 0.0, sl = 0.0, em = 0.0;
+      double e[BPL], x[BPL], ex[BPL], zl = 0.0, sl = 0.0, em = 0.0;
 #pragma unroll
       for (int j = 0; j < BPL; ++j) {
         const int b = bl + 16 * j;  // Lb is zero past B: x = -1/τ stays finite, then masked
-        const double x = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -xmax)));
-        const double ex = exp_neg(x, Tx);
-        e[j] = (b < B) ? ex : 0.0;
+        x[j] = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -xmax)));
+      }
+      exp_neg_n<BPL>(x, Tx, ex);
+#pragma unroll
+      for (int j = 0; j < BPL; ++j) {
+        e[j] = (bl + 16 * j < B) ? ex[j] : 0.0;
         zl += e[j];
-        sl = fma(e[j], x, sl);
+        sl = fma(e[j], x[j], sl);
         em = fmax(em, e[j]);
       }
       const double Z = group16_sum(zl);
