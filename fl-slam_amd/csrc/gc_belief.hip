@@ -18,6 +18,7 @@
 #include "gc_internal.h"
 #include "gc_pipe.h"
 #include "gc_wgla.h"
+#include "gc_opsdev.h"
 
 namespace gc {
 
@@ -78,30 +79,12 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   for (int i = t; i < N2; i += kWG) Lp[i] = P.L[(int64_t)h * N2 + i];
   if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
   __syncthreads();
-  // --- mu_prev and cov_prev from one lifted Cholesky (predict.py:66-67)
-  wg_solve_lifted(Lp, hprev, mu_prev, P.eps_lift, n, W1);
-  wg_chol_inverse(W1, W2, W3, n);
+  // --- a2 predict (predict.py:43-98): L_pred -> W1, h_pred, mu_prev, cert
+  wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,
+             P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2);
   if (t == 0) compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);  // pose0 = world pose of belief_prev
-  // --- OU propagation (predict.py:69-72)
-  const double ef = exp(-2.0 * P.lambda_ou * S.dt);
-  const double dc = (1.0 - ef) / (2.0 * P.lambda_ou + kF64Eps);
-  for (int i = t; i < N2; i += kWG) W2[i] = ef * W2[i] + dc * P.Q[i];
-  __syncthreads();
-  wg_psd_project_fast(W2, W3, P.eps_psd, n, Sx, red, c1);  // cov_psd -> W3
-  double trl = (t < n) ? W3[t * n + t] : 0.0;
-  const double trace_cov = wg_sum(trl, red);
-  wg_inverse_lifted(W3, W2, P.eps_lift, n, W4, W1);   // L_pred raw -> W2
-  wg_psd_project_fast(W2, W1, P.eps_psd, n, Sx, red, c2);  // L_pred -> W1
-  wg_matvec(W1, mu_prev, hpred, n);                   // h_pred = L_pred mu_prev
   for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
   if (t < n) P.hpred[(int64_t)h * n + t] = hpred[t];
-  if (t == 0) {
-    double* pc = P.pred_cert + (int64_t)h * kPredCert;
-    const double lift = 2.0 * P.eps_lift * n;
-    pc[0] = lift; pc[1] = c1[0] + c2[0]; pc[2] = c2[2]; pc[3] = c2[3]; pc[4] = c2[4]; pc[5] = c2[5];
-    pc[6] = trace_cov;
-    pc[7] = lift + (c1[0] + c2[0]) + fabs(1.0 - S.dt);  // dt_scale = dt (predict.py:185-189)
-  }
   // --- predicted moments: Σ_pred[15,15] and mu_inc (pipeline.py:436-453) from chol(L_pred+εI)
   for (int i = t; i < N2; i += kWG) W4[i] = W1[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
   __syncthreads();
@@ -136,85 +119,24 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   const int ia = 2 * t, ib = 2 * t + 1;
   auto stamp = [&](int i) { return i < M ? S.imu_t[i] : 0.0; };
   const double ta = stamp(ia), tb = stamp(ib);
-  // dt_i = max(t_{i+1} - t_i, 0), last slot 0 (imu_preintegration.py:84-85)
-  const double dta = (ib < M) ? fmax(tb - ta, 0.0) : 0.0;
-  const double dtb = ib < M ? ((ib + 1 < M) ? fmax(stamp(ib + 1) - tb, 0.0) : 0.0) : 0.0;
   const double wa = ia < M ? window_weight(ta, S.t0, S.t1, sigma_warp) : 0.0;
   const double wb = ib < M ? window_weight(tb, S.t0, S.t1, sigma_warp) : 0.0;
-  const double dea = wa * dta, deb = wb * dtb;
+  const double* R0 = misc + 16;
+  double* pre = misc + 32;  // kPreint
+  wg_preintegrate(M, S.imu_t, S.imu_g, S.imu_a, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, red, pre);
+  const double ess_scan = wg_sum(wa + wb, red);
+  if (t == 0) {
+    double dR[9], dpose[6], xi[6];
+    mat3_mul_tn(R0, pre, dR);
+    mat3_tvec(R0, pre + 9, dpose);
+    so3_log(dR, dpose + 3);
+    se3_log(dpose, xi);
+    for (int k = 0; k < 6; ++k) P.xi[(int64_t)h * 6 + k] = xi[k];
+  }
   double ga[3] = {0, 0, 0}, gb[3] = {0, 0, 0}, aa[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
   for (int k = 0; k < 3; ++k) {
     if (ia < M) { ga[k] = S.imu_g[3 * ia + k]; aa[k] = S.imu_a[3 * ia + k]; }
     if (ib < M) { gb[k] = S.imu_g[3 * ib + k]; ab[k] = S.imu_a[3 * ib + k]; }
-  }
-  double dRa[9], dRb[9], Pl[9];
-  {
-    double wv[3] = {(ga[0] - bg[0]) * dea, (ga[1] - bg[1]) * dea, (ga[2] - bg[2]) * dea};
-    so3_exp(wv, dRa);
-    double wv2[3] = {(gb[0] - bg[0]) * deb, (gb[1] - bg[1]) * deb, (gb[2] - bg[2]) * deb};
-    so3_exp(wv2, dRb);
-    mat3_mul(dRa, dRb, Pl);
-  }
-  for (int k = 0; k < 9; ++k) A[t * 9 + k] = Pl[k];
-  __syncthreads();
-  // inclusive Hillis-Steele scan of 3x3 products: X_t = Pl_0 ... Pl_t
-  double* src = A;
-  double* dst = Bm;
-  for (int off = 1; off < kWG; off <<= 1) {
-    double Xn[9];
-    if (t >= off) {
-      mat3_mul(src + (t - off) * 9, src + t * 9, Xn);
-    } else {
-      for (int k = 0; k < 9; ++k) Xn[k] = src[t * 9 + k];
-    }
-    for (int k = 0; k < 9; ++k) dst[t * 9 + k] = Xn[k];
-    __syncthreads();
-    double* tmp = src; src = dst; dst = tmp;
-  }
-  const double* R0 = misc + 16;
-  double Ea[9], Rb[9];
-  if (t == 0) {
-    for (int k = 0; k < 9; ++k) Ea[k] = R0[k];
-  } else {
-    mat3_mul(R0, src + (t - 1) * 9, Ea);
-  }
-  mat3_mul(Ea, dRa, Rb);
-  double awa[3], awb[3], tmp3[3];
-  const double aba[3] = {aa[0] - ba[0], aa[1] - ba[1], aa[2] - ba[2]};
-  const double abb[3] = {ab[0] - ba[0], ab[1] - ba[1], ab[2] - ba[2]};
-  mat3_vec(Ea, aba, tmp3);
-  for (int k = 0; k < 3; ++k) awa[k] = tmp3[k] + kG[k];
-  mat3_vec(Rb, abb, tmp3);
-  for (int k = 0; k < 3; ++k) awb[k] = tmp3[k] + kG[k];
-  // exclusive prefix sum of velocity increments
-  for (int k = 0; k < 3; ++k) V1[t * 3 + k] = awa[k] * dea + awb[k] * deb;
-  __syncthreads();
-  double* vs = V1;
-  double* vd = V2;
-  for (int off = 1; off < kWG; off <<= 1) {
-    double v[3];
-    for (int k = 0; k < 3; ++k) v[k] = vs[t * 3 + k] + ((t >= off) ? vs[(t - off) * 3 + k] : 0.0);
-    for (int k = 0; k < 3; ++k) vd[t * 3 + k] = v[k];
-    __syncthreads();
-    double* tp = vs; vs = vd; vd = tp;
-  }
-  double va[3], pc[3];
-  for (int k = 0; k < 3; ++k) {
-    va[k] = (t > 0) ? vs[(t - 1) * 3 + k] : 0.0;
-    const double vb = va[k] + awa[k] * dea;
-    pc[k] = va[k] * dea + 0.5 * awa[k] * (dea * dea) + vb * deb + 0.5 * awb[k] * (deb * deb);
-  }
-  const double pe0 = wg_sum(pc[0], red), pe1 = wg_sum(pc[1], red), pe2 = wg_sum(pc[2], red);
-  const double ess_scan = wg_sum(wa + wb, red);
-  if (t == 0) {
-    double Rend[9], dR[9], dpose[6], xi[6];
-    mat3_mul(R0, src + (kWG - 1) * 9, Rend);
-    mat3_mul_tn(R0, Rend, dR);
-    const double pe[3] = {pe0, pe1, pe2};
-    mat3_tvec(R0, pe, dpose);
-    so3_log(dR, dpose + 3);
-    se3_log(dpose, xi);
-    for (int k = 0; k < 6; ++k) P.xi[(int64_t)h * 6 + k] = xi[k];
   }
   // --- scan-to-scan window: omega_avg and measurement-noise IW statistics
   //     (pipeline.py:537-566, measurement_noise_iw_jax.py:130-218)

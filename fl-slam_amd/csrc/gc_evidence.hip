@@ -5,6 +5,7 @@
 #include "gc_internal.h"
 #include "gc_pipe.h"
 #include "gc_wgla.h"
+#include "gc_opsdev.h"
 
 namespace gc {
 
@@ -47,6 +48,8 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   double* acc = tab + 64 * 16;          // 32
   double* sc = acc + 32;                // 128 scalars
   double* c6 = sc + 128;                // 6
+  double* mf = c6 + 6;                  // kMF  Matrix-Fisher record
+  double* pt = mf + kMF;                // kPT  planar record
   const int hl = blockIdx.x;
   const int t = threadIdx.x;
   const int n = kDZ, B = P.B;
@@ -75,51 +78,14 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   if (t < B) {
     const double* s = st + t * 38;
     const double* m = P.map + t * kMapRec;
-    const double sN = s[0], mN = m[12];
-    const double wb = sqrt(sN * mN + eps);
-    const double sn = sqrt(s[1] * s[1] + s[2] * s[2] + s[3] * s[3]);
-    const double mn = sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
-    double us[3], um[3];
-    for (int k = 0; k < 3; ++k) { us[k] = s[1 + k] / (sn + eps); um[k] = m[k] / (mn + eps); }
-    const double conf = (sn * (1.0 / (sN + eps))) * (mn * (1.0 / (mN + eps)));
-    const double wf = wb * conf;
-    double* r = tab + t * 10;
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) r[3 * i + j] = wf * um[i] * us[j];
-    r[9] = wf;
+    mf_bin_row(s[0], s + 1, m[12], m, eps, tab + t * 10);
   }
   __syncthreads();
   sum_bins(tab, B, 10, acc);
   if (t == 0) {
-    double U[9], s3[3], V[9];
-    svd3(acc, U, s3, V);
-    double UVt[9];
-    mat3_mul_nt(U, V, UVt);
-    const double dsg = det3(UVt);
-    const double sgn = (dsg > 0.0) ? 1.0 : ((dsg < 0.0) ? -1.0 : 0.0);
-    for (int k = 0; k < 3; ++k) U[3 * k + 2] *= sgn;
-    double Rmf[9];
-    mat3_mul_nt(U, V, Rmf);
-    const double ld[3] = {s3[1] + s3[2], s3[0] + s3[2], s3[0] + s3[1]};
-    double Lr[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j)
-        Lr[3 * i + j] = V[3 * i] * ld[0] * V[3 * j] + V[3 * i + 1] * ld[1] * V[3 * j + 1] +
-                        V[3 * i + 2] * ld[2] * V[3 * j + 2];
-    double Rp[9], Rerr[9], dl[3], Lrot[9], cc[6];
+    double Rp[9];
     so3_exp(P.pose_pred + (int64_t)hl * 6 + 3, Rp);
-    mat3_mul_tn(Rp, Rmf, Rerr);
-    so3_log(Rerr, dl);
-    psd_project3(Lr, P.eps_psd, Lrot, cc);
-    double hr[3];
-    mat3_vec(Lrot, dl, hr);
-    const double Neff = acc[9];
-    const double nll = 0.5 * (dl[0] * hr[0] + dl[1] * hr[1] + dl[2] * hr[2]);
-    for (int k = 0; k < 9; ++k) { sc[k] = Rmf[k]; sc[9 + k] = Lrot[k]; }
-    for (int k = 0; k < 3; ++k) sc[18 + k] = hr[k];
-    sc[21] = nll / (Neff + eps);               // MF nll_per_ess
-    sc[22] = cc[0] + eps / (Neff + eps);       // MF trigger
-    sc[23] = s3[0]; sc[24] = s3[1]; sc[25] = s3[2];
+    mf_finalize(acc, Rp, eps, P.eps_psd, mf);
   }
   __syncthreads();
   // ---------------------------------------------- a8 planar translation WLS (R_hat = R_mf)
@@ -127,54 +93,19 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     const double* s = st + t * 38;
     const double* m = P.map + t * kMapRec;
     const double* md = P.map_der + t * kMapDer;
-    const double* R = sc;
-    double RS[9], RSR[9], Sc[9], Si[9], rp[3], tb[3];
-    mat3_mul(R, s + 16, RS);
-    mat3_mul_nt(RS, R, RSR);
-    for (int k = 0; k < 9; ++k) Sc[k] = md[7 + k] + RSR[k] + ((k % 4 == 0) ? eps : 0.0);
-    inv3(Sc, Si);
-    const double wb = sqrt(s[0] * m[13] + eps);
-    mat3_vec(R, s + 13, rp);
-    for (int k = 0; k < 3; ++k) tb[k] = md[4 + k] - rp[k];
-    double* r = tab + t * 13;
-    for (int k = 0; k < 9; ++k) r[k] = wb * Si[k];
-    double hb[3];
-    mat3_vec(r, tb, hb);
-    r[9] = hb[0]; r[10] = hb[1]; r[11] = hb[2];
-    r[12] = wb;
+    planar_bin_row(mf, s[0], s + 13, s + 16, m[13], md + 4, md + 7, eps, tab + t * 13);
   }
   __syncthreads();
   sum_bins(tab, B, 13, acc);
-  if (t == 0) {
-    double Lr[9];
-    for (int k = 0; k < 9; ++k) Lr[k] = acc[k] + ((k % 4 == 0) ? eps : 0.0);
-    double tw[3];
-    solve3(Lr, acc + 9, tw);
-    const double zsc = P.map_misc[0];
-    const double msk[3] = {1.0, 1.0, zsc};
-    double Lm[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) Lm[3 * i + j] = acc[3 * i + j] * msk[i] * msk[j];
-    const double* tp = P.pose_pred + (int64_t)hl * 6;
-    const double dl[3] = {tw[0] - tp[0], tw[1] - tp[1], tw[2] - tp[2]};
-    double Lt[9], cc[6], ht[3];
-    psd_project3(Lm, P.eps_psd, Lt, cc);
-    mat3_vec(Lt, dl, ht);
-    const double Neff = acc[12];
-    const double nll = 0.5 * (dl[0] * ht[0] + dl[1] * ht[1] + dl[2] * ht[2]);
-    for (int k = 0; k < 9; ++k) sc[30 + k] = Lt[k];
-    for (int k = 0; k < 3; ++k) { sc[39 + k] = ht[k]; sc[42 + k] = tw[k]; }
-    sc[45] = nll / (Neff + eps);
-    sc[46] = cc[0] + eps / (Neff + eps);
-  }
+  if (t == 0) planar_finalize(acc, P.map_misc[0], P.pose_pred + (int64_t)hl * 6, eps, P.eps_psd, pt);
   __syncthreads();
   // ---------------------------------------------- a9 evidence sum: L_raw = L_io + L_lidar
   if (t < 9) {
     const int i = t / 3, j = t % 3;
-    Lev[i * n + j] += sc[30 + t];                 // translation block [0:3, 0:3]
-    Lev[(3 + i) * n + (3 + j)] += sc[9 + t];      // rotation block [3:6, 3:6]
+    Lev[i * n + j] += pt[3 + t];                  // translation block [0:3, 0:3]
+    Lev[(3 + i) * n + (3 + j)] += mf[9 + t];      // rotation block [3:6, 3:6]
   }
-  if (t < 3) { hev[t] += sc[39 + t]; hev[3 + t] += sc[18 + t]; }
+  if (t < 3) { hev[t] += pt[12 + t]; hev[3 + t] += mf[18 + t]; }
   __syncthreads();
   if (t == 0) {
     // aggregate_certificates([deskew, assign, moments, MF, planar]) then [ev, odom, imu, gyro]
@@ -187,7 +118,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     const double ess_tot = (ess_ev + io[0] + io[1] + io[2]) / 4.0;
     const double sf_tot = (sf_ev + io[3] + io[4] + io[5]) / 4.0;
     const double exc = fmax(0.0, io[6]) + fmax(0.0, io[7]);
-    const double nll = sc[21] + sc[45] + io[8];
+    const double nll = mf[28] + pt[20] + io[8];
     // tempering β from raw-evidence sentinels (pipeline.py:1070-1111)
     double dp = 0.0, dp2 = 0.0, dv = 0.0, dv2 = 0.0;
     for (int k = 0; k < 6; ++k) { dp += Lev[15 * n + k] * Lev[15 * n + k]; dp2 += Lev[k * n + 15] * Lev[k * n + 15]; }
@@ -265,7 +196,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     const double* bc = P.bincert + (int64_t)hl * 8;
     const double trig_budget = 1e-12 / (P.budget[0] + 1e-12);
     double T = trig_budget + P.pred_cert[(int64_t)hl * kPredCert + 7] + P.io_cert[(int64_t)hl * kIoCert + 9];
-    T += 0.0 + bc[7] + sc[22] + sc[46];                // deskew, assign (exact), moments, MF, planar
+    T += 0.0 + bc[7] + mf[30] + pt[22];                // deskew, assign (exact), moments, MF, planar
     T += fabs(1.0 - sc[50]);                           // PowerTempering
     T += fabs(1.0 - (1.0 - s_dt)) + fabs(1.0 - (1.0 - s_ex));  // ExcitationPriorScaling
     T += fabs(1.0 - alpha);                            // FusionScale
@@ -278,21 +209,8 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   wg_chol(Wc, n);
   wg_chol_solve(Wc, hpo, dz, n);
   if (t == 0) {
-    const double T = sc[61];
-    const double s = T / (T + P.c_frob);
-    const double* x1 = zl;  // z_lin pose slice
-    double c1[3], c2[3], c3[3];
-    cross3(x1 + 3, dz, c1);
-    cross3(x1, dz + 3, c2);
-    cross3(x1 + 3, dz + 3, c3);
-    double dpc[6];
-    for (int k = 0; k < 3; ++k) {
-      dpc[k] = dz[k] + s * (0.5 * (c1[k] + c2[k]));
-      dpc[3 + k] = dz[3 + k] + s * (0.5 * c3[k]);
-    }
-    compose_exp2(P.X + (int64_t)hl * 6, dpc, sc + 64);  // X_new
-    for (int k = 0; k < 6; ++k) sc[70 + k] = dpc[k];
-    sc[63] = s;
+    double bch[6];
+    sc[63] = recompose_pose(P.X + (int64_t)hl * 6, zl, dz, sc[61], P.c_frob, sc + 64, sc + 70, bch);  // X_new, δ'
   }
   __syncthreads();
   if (t < n) {
@@ -310,16 +228,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   wg_chol(W3, n);
   wg_chol_solve(W3, hps, mups, n);
   wg_chol_inverse(Wc, W2, Sx, n);  // Σ_post -> W2
-  for (int idx = t; idx < 7 * 36; idx += kWG) {
-    const int b = idx / 36, i = (idx % 36) / 6, j = idx % 6;
-    const int d = kBlockDim[b], s0 = kBlockStart[b];
-    double v = 0.0;
-    if (i < d && j < d) {
-      const double r_i = mupo[s0 + i] - mups[s0 + i], r_j = mupo[s0 + j] - mups[s0 + j];
-      v = r_i * r_j + W2[(s0 + i) * n + (s0 + j)];
-    }
-    P.dPsiP[(int64_t)hl * 252 + idx] = v;
-  }
+  for (int idx = t; idx < 7 * 36; idx += kWG) P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
   // a13 map increment from hypothesis 0 only (backend_node.py:2081-2083), build-defined pushforward
   if (P.h_begin + hl == 0) {
     if (t == 0) {
@@ -330,51 +239,11 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
       sc[89] = zt[0]; sc[90] = zt[1]; sc[91] = 0.0;  // planar map: t[2] = 0 (CHANGELOG.md:575-578)
     }
     __syncthreads();
-    if (t < B) {
-      const double* s = st + t * 38;
-      const double* R = sc + 80;
-      const double* tt = sc + 89;
-      double* o = P.map_inc + t * kMapRec;
-      const double N = s[0];
-      double v3[3], M3[9], M4[9];
-      mat3_vec(R, s + 1, v3);
-      for (int k = 0; k < 3; ++k) o[k] = v3[k];
-      mat3_mul(R, s + 4, M3);
-      mat3_mul_nt(M3, R, M4);
-      for (int k = 0; k < 9; ++k) o[3 + k] = M4[k];
-      o[12] = N; o[13] = N;
-      double pw[3];
-      mat3_vec(R, s + 13, pw);
-      for (int k = 0; k < 3; ++k) pw[k] += tt[k];
-      // Σ_w = R Σ_p Rᵀ + J Σ_pose Jᵀ, J = [R | -R [p̄]×]
-      mat3_mul(R, s + 16, M3);
-      mat3_mul_nt(M3, R, M4);
-      const double* pb = s + 13;
-      const double K[9] = {0.0, -pb[2], pb[1], pb[2], 0.0, -pb[0], -pb[1], pb[0], 0.0};
-      double RK[9], J[18];
-      mat3_mul(R, K, RK);
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) { J[i * 6 + j] = R[3 * i + j]; J[i * 6 + 3 + j] = -RK[3 * i + j]; }
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) {
-          double v = 0.0;
-          for (int a = 0; a < 6; ++a) {
-            double ja = 0.0;
-            for (int c = 0; c < 6; ++c) ja += W2[a * n + c] * J[j * 6 + c];
-            v += J[i * 6 + a] * ja;
-          }
-          M4[3 * i + j] += v;
-        }
-      for (int k = 0; k < 3; ++k) o[14 + k] = N * pw[k];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) o[17 + 3 * i + j] = N * (M4[3 * i + j] + pw[i] * pw[j]);
-    }
+    if (t < B) pushforward_bin(st + t * 38, sc + 80, sc + 89, W2, n, P.map_inc + t * kMapRec);
   }
   // a14 anchor drift (anchor_drift.py:93-191): δz = μ_post of the recomposed belief
   if (t == 0) {
-    const double dm = sqrt(mupo[0] * mupo[0] + mupo[1] * mupo[1] + mupo[2] * mupo[2]);
-    const double dr = sqrt(mupo[3] * mupo[3] + mupo[4] * mupo[4] + mupo[5] * mupo[5]);
-    const double rho = clampd(fmax(dm / 0.5, dr / 0.2), 0.0, 1.0);
+    const double rho = drift_rho(mupo, nullptr, nullptr);
     double d6[6];
     for (int k = 0; k < 6; ++k) d6[k] = rho * mupo[k];
     compose_exp2(sc + 64, d6, sc + 92);  // X_fin
@@ -402,12 +271,12 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     for (int k = 0; k < 6; ++k) dg[k] = pose[k];
     dg[6] = sc[61]; dg[7] = sc[50]; dg[8] = alpha; dg[9] = s_dt; dg[10] = s_ex; dg[11] = rho;
     dg[12] = sc[63]; dg[13] = sc[60]; dg[14] = sc[53]; dg[15] = sc[51]; dg[16] = sc[52]; dg[17] = sc[56];
-    dg[18] = sc[22]; dg[19] = sc[46]; dg[20] = sc[62];
-    for (int k = 0; k < 3; ++k) dg[21 + k] = sc[42 + k];  // t_wls
+    dg[18] = mf[30]; dg[19] = pt[22]; dg[20] = sc[62];
+    for (int k = 0; k < 3; ++k) dg[21 + k] = pt[k];       // t_wls
     double wmf[3];
-    so3_log(sc, wmf);
+    so3_log(mf, wmf);
     for (int k = 0; k < 3; ++k) dg[24 + k] = wmf[k];      // log R_mf
-    for (int k = 0; k < 3; ++k) dg[27 + k] = sc[23 + k];  // MF singular values
+    for (int k = 0; k < 3; ++k) dg[27 + k] = mf[24 + k];  // MF singular values
     for (int k = 0; k < 6; ++k) dg[30 + k] = P.xi[(int64_t)hl * 6 + k];
     dg[36] = sc[54]; dg[37] = sc[55]; dg[38] = 0.0; dg[39] = 0.0;
   }
@@ -679,7 +548,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
 }
 
 // ------------------------------------------------------------------------------ launchers
-static size_t lds_evidence() { return sizeof(double) * (7 * NN + 2 * NN + 4 * kDZ + 10 * kDZ + 8 + 64 * 16 + 32 + 128 + 6); }
+static size_t lds_evidence() { return sizeof(double) * (7 * NN + 2 * NN + 4 * kDZ + 10 * kDZ + 8 + 64 * 16 + 32 + 128 + 6 + kMF + kPT); }
 static size_t lds_final() { return sizeof(double) * (2 * NN + 2 * NN + 4 * kDZ + 16 + 8 + 72 + 640 + 2 * NN); }
 
 }  // namespace gc

@@ -1,0 +1,348 @@
+// gc_opsdev.h — device building blocks of the per-hypothesis operators, shared by the batched
+// scan pipeline kernels (gc_belief.hip, gc_evidence.hip) and the per-operator batched entries
+// (gc_ops.hip), so both paths run the same arithmetic.
+//
+//  thread-level: Matrix-Fisher / planar per-bin rows and finalisation (a7, a8), Frobenius
+//  recompose (a12), anchor drift ρ (a14), pose-covariance pushforward of one bin (a13).
+//  workgroup-level: lifted mean/world pose of a belief, OU predict (a2), process-noise IW
+//  block statistics (a15).
+#pragma once
+#include "gc_math.h"
+#include "gc_wgla.h"
+
+namespace gc {
+
+constexpr int kNN = kDZ * kDZ;
+
+// ------------------------------------------------------------------------------------ a7
+// Output record of matrix_fisher_rotation_evidence (matrix_fisher_evidence.py:155-394).
+constexpr int kMF = 32;  // [R_mf 9, L_rot 9, h_rot 3, delta 3, svd 3, N_eff, nll/ess, psd Δ, trig, nll]
+// Per-bin cross-covariance row (thread b): r = w_b u_map u_scanᵀ (9) and w_b (1), with
+// w_b = √(N_s N_m + ε) · R̄_s R̄_m (matrix_fisher_evidence.py:180-205).
+GC_DEV void mf_bin_row(double sN, const double* s_dir, double mN, const double* m_dir, double eps, double* r) {
+  const double wb = sqrt(sN * mN + eps);
+  const double sn = sqrt(s_dir[0] * s_dir[0] + s_dir[1] * s_dir[1] + s_dir[2] * s_dir[2]);
+  const double mn = sqrt(m_dir[0] * m_dir[0] + m_dir[1] * m_dir[1] + m_dir[2] * m_dir[2]);
+  double us[3], um[3];
+  for (int k = 0; k < 3; ++k) { us[k] = s_dir[k] / (sn + eps); um[k] = m_dir[k] / (mn + eps); }
+  const double conf = (sn * (1.0 / (sN + eps))) * (mn * (1.0 / (mN + eps)));
+  const double wf = wb * conf;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) r[3 * i + j] = wf * um[i] * us[j];
+  r[9] = wf;
+}
+// SVD, det-sign fix, R_mf = U Vᵀ, L = V diag(s1+s2, s0+s2, s0+s1) Vᵀ, δ = log(R_predᵀ R_mf),
+// PSD(L), h = L δ (matrix_fisher_evidence.py:206-262).
+GC_DEV void mf_finalize(const double* acc, const double* Rp, double eps, double eps_psd, double* out) {
+  double U[9], s3[3], V[9];
+  svd3(acc, U, s3, V);
+  double UVt[9];
+  mat3_mul_nt(U, V, UVt);
+  const double dsg = det3(UVt);
+  const double sgn = (dsg > 0.0) ? 1.0 : ((dsg < 0.0) ? -1.0 : 0.0);
+  for (int k = 0; k < 3; ++k) U[3 * k + 2] *= sgn;
+  double Rmf[9];
+  mat3_mul_nt(U, V, Rmf);
+  const double ld[3] = {s3[1] + s3[2], s3[0] + s3[2], s3[0] + s3[1]};
+  double Lr[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      Lr[3 * i + j] = V[3 * i] * ld[0] * V[3 * j] + V[3 * i + 1] * ld[1] * V[3 * j + 1] +
+                      V[3 * i + 2] * ld[2] * V[3 * j + 2];
+  double Rerr[9], dl[3], Lrot[9], cc[6];
+  mat3_mul_tn(Rp, Rmf, Rerr);
+  so3_log(Rerr, dl);
+  psd_project3(Lr, eps_psd, Lrot, cc);
+  double hr[3];
+  mat3_vec(Lrot, dl, hr);
+  const double Neff = acc[9];
+  const double nll = 0.5 * (dl[0] * hr[0] + dl[1] * hr[1] + dl[2] * hr[2]);
+  for (int k = 0; k < 9; ++k) { out[k] = Rmf[k]; out[9 + k] = Lrot[k]; }
+  for (int k = 0; k < 3; ++k) { out[18 + k] = hr[k]; out[21 + k] = dl[k]; out[24 + k] = s3[k]; }
+  out[27] = Neff;
+  out[28] = nll / (Neff + eps);
+  out[29] = cc[0];
+  out[30] = cc[0] + eps / (Neff + eps);  // trigger: psd Δ + mass-ε ratio
+  out[31] = nll;
+}
+
+// ------------------------------------------------------------------------------------ a8
+// Output record of planar_translation_evidence (matrix_fisher_evidence.py:413-671).
+constexpr int kPT = 26;  // [t_wls 3, L_t 9, h_t 3, delta 3, z_scale, N_eff, nll/ess, psd Δ, trig, xy, z, nll]
+// Per-bin WLS row (thread b): W_b = √(N_s N_pos + ε) (Σ_map + R Σ_p Rᵀ + εI)⁻¹ (9), W_b t_b (3),
+// √(·) (1), with t_b = c_map − R p̄.
+GC_DEV void planar_bin_row(const double* R, double sN, const double* s_pbar, const double* s_Sig, double mNpos,
+                           const double* m_c, const double* m_Sig, double eps, double* r) {
+  double RS[9], RSR[9], Sc[9], Si[9], rp[3], tb[3];
+  mat3_mul(R, s_Sig, RS);
+  mat3_mul_nt(RS, R, RSR);
+  for (int k = 0; k < 9; ++k) Sc[k] = m_Sig[k] + RSR[k] + ((k % 4 == 0) ? eps : 0.0);
+  inv3(Sc, Si);
+  const double wb = sqrt(sN * mNpos + eps);
+  mat3_vec(R, s_pbar, rp);
+  for (int k = 0; k < 3; ++k) tb[k] = m_c[k] - rp[k];
+  for (int k = 0; k < 9; ++k) r[k] = wb * Si[k];
+  double hb[3];
+  mat3_vec(r, tb, hb);
+  r[9] = hb[0]; r[10] = hb[1]; r[11] = hb[2];
+  r[12] = wb;
+}
+// t_wls = (L + εI)⁻¹ h; L ⊙ m mᵀ with m = [1, 1, z_scale]; δ = t_wls − t_pred; PSD; h = L δ.
+GC_DEV void planar_finalize(const double* acc, double zsc, const double* tp, double eps, double eps_psd,
+                            double* out) {
+  double Lr[9];
+  for (int k = 0; k < 9; ++k) Lr[k] = acc[k] + ((k % 4 == 0) ? eps : 0.0);
+  double tw[3];
+  solve3(Lr, acc + 9, tw);
+  const double msk[3] = {1.0, 1.0, zsc};
+  double Lm[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Lm[3 * i + j] = acc[3 * i + j] * msk[i] * msk[j];
+  const double dl[3] = {tw[0] - tp[0], tw[1] - tp[1], tw[2] - tp[2]};
+  double Lt[9], cc[6], ht[3];
+  psd_project3(Lm, eps_psd, Lt, cc);
+  mat3_vec(Lt, dl, ht);
+  const double Neff = acc[12];
+  const double nll = 0.5 * (dl[0] * ht[0] + dl[1] * ht[1] + dl[2] * ht[2]);
+  for (int k = 0; k < 3; ++k) { out[k] = tw[k]; out[12 + k] = ht[k]; out[15 + k] = dl[k]; }
+  for (int k = 0; k < 9; ++k) out[3 + k] = Lt[k];
+  out[18] = zsc;
+  out[19] = Neff;
+  out[20] = nll / (Neff + eps);
+  out[21] = cc[0];
+  out[22] = cc[0] + eps / (Neff + eps);
+  out[23] = 0.5 * (Lt[0] + Lt[4]);
+  out[24] = Lt[8];
+  out[25] = nll;
+}
+// Vertical observability of the map: λ3/λ1 of Σ_b S_dir_scatter / (Σ_b N_dir + ε)
+// (matrix_fisher_evidence.py:572-589), from the summed scatter (9) and N_dir total.
+GC_DEV double planar_z_scale(const double* Ssum, double Ntot, double eps) {
+  double T[9];
+  for (int k = 0; k < 9; ++k) T[k] = Ssum[k] / (Ntot + eps);
+  double ev[3];
+  eigvalsh3_desc(T, ev);
+  return fmax(ev[2], 0.0) / fmax(ev[0], eps);
+}
+
+// ------------------------------------------------------------------------------------ a12
+// Frobenius recompose given δz = (L + εI)⁻¹h (recompose.py:50-205): s = T/(T + c_frob),
+// δ' = δ + s·½[z_lin, δ] (BCH3 on the pose slice), X_new = X ∘ Exp(δ'). Writes X_new (6),
+// δ' (6) and the bch term (6); returns s.
+GC_DEV double recompose_pose(const double* X, const double* zl, const double* dz, double T, double c_frob,
+                             double* X_new, double* dpc, double* bch) {
+  const double s = T / (T + c_frob);
+  double c1[3], c2[3], c3[3];
+  cross3(zl + 3, dz, c1);
+  cross3(zl, dz + 3, c2);
+  cross3(zl + 3, dz + 3, c3);
+  for (int k = 0; k < 3; ++k) {
+    bch[k] = 0.5 * (c1[k] + c2[k]);
+    bch[3 + k] = 0.5 * c3[k];
+    dpc[k] = dz[k] + s * bch[k];
+    dpc[3 + k] = dz[3 + k] + s * bch[3 + k];
+  }
+  double e[6];
+  se3_exp(dpc, e);
+  se3_compose(X, e, X_new);
+  return s;
+}
+
+// ------------------------------------------------------------------------------------ a14
+// ρ = clip(max(‖δt‖/0.5, ‖δθ‖/0.2), 0, 1) (anchor_drift.py:64-91); also returns the drifts.
+GC_DEV double drift_rho(const double* mu, double* drift_m, double* drift_r) {
+  const double dm = sqrt(mu[0] * mu[0] + mu[1] * mu[1] + mu[2] * mu[2]);
+  const double dr = sqrt(mu[3] * mu[3] + mu[4] * mu[4] + mu[5] * mu[5]);
+  if (drift_m) *drift_m = dm;
+  if (drift_r) *drift_r = dr;
+  return clampd(fmax(dm / 0.5, dr / 0.2), 0.0, 1.0);
+}
+
+// ------------------------------------------------------------------------------------ a13
+// Push one scan bin into the world frame (build-defined PoseCovInflationPushforward):
+// s_dir → R s, S → R S Rᵀ, N_dir = N_pos = N, sum_p = N p_w, sum_ppT = N (Σ_w + p_w p_wᵀ) with
+// Σ_w = R Σ_p Rᵀ + J Σ_pose Jᵀ, J = [R | −R[p̄]×], p_w = R p̄ + t. Σ_pose: 6x6 (row stride ld).
+// s: bin stats record (GC_BIN_STATS layout); o: map record (kMapRec).
+GC_DEV void pushforward_bin(const double* s, const double* R, const double* tt, const double* Sp, int ld,
+                            double* o) {
+  const double N = s[0];
+  double v3[3], M3[9], M4[9];
+  mat3_vec(R, s + 1, v3);
+  for (int k = 0; k < 3; ++k) o[k] = v3[k];
+  mat3_mul(R, s + 4, M3);
+  mat3_mul_nt(M3, R, M4);
+  for (int k = 0; k < 9; ++k) o[3 + k] = M4[k];
+  o[12] = N; o[13] = N;
+  double pw[3];
+  mat3_vec(R, s + 13, pw);
+  for (int k = 0; k < 3; ++k) pw[k] += tt[k];
+  mat3_mul(R, s + 16, M3);
+  mat3_mul_nt(M3, R, M4);
+  const double* pb = s + 13;
+  const double K[9] = {0.0, -pb[2], pb[1], pb[2], 0.0, -pb[0], -pb[1], pb[0], 0.0};
+  double RK[9], J[18];
+  mat3_mul(R, K, RK);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) { J[i * 6 + j] = R[3 * i + j]; J[i * 6 + 3 + j] = -RK[3 * i + j]; }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double v = 0.0;
+      for (int a = 0; a < 6; ++a) {
+        double ja = 0.0;
+        for (int c = 0; c < 6; ++c) ja += Sp[a * ld + c] * J[j * 6 + c];
+        v += J[i * 6 + a] * ja;
+      }
+      M4[3 * i + j] += v;
+    }
+  for (int k = 0; k < 3; ++k) o[14 + k] = N * pw[k];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) o[17 + 3 * i + j] = N * (M4[3 * i + j] + pw[i] * pw[j]);
+}
+
+// ------------------------------------------------------------------------------------ a15
+constexpr int kIwBlockStart[7] = {0, 3, 6, 9, 12, 15, 16};
+constexpr int kIwBlockDim[7] = {3, 3, 3, 3, 3, 1, 6};
+// Process-noise IW statistics entry idx of (7, 6, 6) (inverse_wishart_jax.py:71-123):
+// dΨ_b = (r rᵀ + Σ_post)[block b] with r = μ_post − μ_pred, zero outside the d_b x d_b block.
+GC_DEV double iw_proc_stat(int idx, const double* mupo, const double* mups, const double* Spost) {
+  const int b = idx / 36, i = (idx % 36) / 6, j = idx % 6;
+  const int d = kIwBlockDim[b], s0 = kIwBlockStart[b];
+  if (i >= d || j >= d) return 0.0;
+  const double r_i = mupo[s0 + i] - mups[s0 + i], r_j = mupo[s0 + j] - mups[s0 + j];
+  return r_i * r_j + Spost[(s0 + i) * kDZ + (s0 + j)];
+}
+
+// ------------------------------------------------------------------------------------ a2
+constexpr int kPredCertLen = 8;  // [lift, psd Δ, eig_min, eig_max, cond, nnc, trace Σ', trigger]
+// predict_diffusion core (predict.py:43-98), one workgroup: μ = (L+εI)⁻¹h, Σ = (L+εI)⁻¹,
+// Σ' = e^{-2λdt}Σ + (1−e^{-2λdt})/(2λ) Q, PSD, L' = (Σ'+εI)⁻¹, PSD, h' = L' μ.
+// Lp (in, n x n, LDS) and hprev (in) are preserved; outputs Lout/hout/mu (LDS), cert (thread 0).
+// Scratch: W1..W3 (n x n each), Sx (2 n² + 4 n), red (>= 8), c1/c2 (6 each).
+GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, double dt, double eps_psd,
+                       double eps_lift, double lambda_ou, double* Lout, double* hout, double* mu, double* cert,
+                       double* W1, double* W2, double* W3, double* Sx, double* red, double* c1, double* c2) {
+  const int t = threadIdx.x, n = kDZ;
+  wg_solve_lifted(Lp, hprev, mu, eps_lift, n, W1);  // W1 = chol(L + εI)
+  wg_chol_inverse(W1, W2, W3, n);                    // W2 = Σ
+  const double ef = exp(-2.0 * lambda_ou * dt);
+  const double dc = (1.0 - ef) / (2.0 * lambda_ou + kF64Eps);
+  for (int i = t; i < kNN; i += kWG) W2[i] = ef * W2[i] + dc * Q[i];
+  __syncthreads();
+  wg_psd_project_fast(W2, W3, eps_psd, n, Sx, red, c1);  // Σ'_psd -> W3
+  double trl = (t < n) ? W3[t * n + t] : 0.0;
+  const double trace_cov = wg_sum(trl, red);
+  wg_inverse_lifted(W3, W2, eps_lift, n, W1, Lout);      // L' raw -> W2 (Lout as work)
+  wg_psd_project_fast(W2, Lout, eps_psd, n, Sx, red, c2);
+  wg_matvec(Lout, mu, hout, n);
+  if (t == 0 && cert) {
+    const double lift = 2.0 * eps_lift * n;
+    cert[0] = lift; cert[1] = c1[0] + c2[0]; cert[2] = c2[2]; cert[3] = c2[3]; cert[4] = c2[4]; cert[5] = c2[5];
+    cert[6] = trace_cov;
+    cert[7] = lift + (c1[0] + c2[0]) + fabs(1.0 - dt);  // trigger; dt_scale = dt (predict.py:185-189)
+  }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------ a3
+// Weighted IMU preintegration (imu_preintegration.py:46-147) over M <= 512 samples, two per
+// thread (a = 2t, b = 2t+1): rotation by an inclusive Hillis-Steele scan of the 3x3 factors
+// Exp((ω−b_g) w dt), velocity by a prefix sum, position by the closed-form sum
+// p = Σ v_i de_i + ½ a_i de_i². wa/wb are the two samples' weights, R0 the start rotation.
+// Thread 0 writes out[kPreint] = [R_end 9, p_end 3, v_end 3, Σde, Σa_body de 3,
+// Σa_world_nog de 3, Σa_world de 3]. Scratch A, Bm: 256 x 9; V1, V2: 256 x 3.
+constexpr int kPreint = 25;
+GC_DEV void wg_preintegrate(int M, const double* stamps, const double* gyro, const double* accel, double wa,
+                            double wb, const double* R0, const double* bg, const double* ba, const double* g,
+                            double* A, double* Bm, double* V1, double* V2, double* red, double* out) {
+  const int t = threadIdx.x;
+  const int ia = 2 * t, ib = 2 * t + 1;
+  auto stamp = [&](int i) { return i < M ? stamps[i] : 0.0; };
+  const double ta = stamp(ia), tb = stamp(ib);
+  // dt_i = max(t_{i+1} - t_i, 0), last slot 0 (imu_preintegration.py:84-85)
+  const double dta = (ib < M) ? fmax(tb - ta, 0.0) : 0.0;
+  const double dtb = ib < M ? ((ib + 1 < M) ? fmax(stamp(ib + 1) - tb, 0.0) : 0.0) : 0.0;
+  const double dea = (ia < M ? wa : 0.0) * dta, deb = (ib < M ? wb : 0.0) * dtb;
+  double ga[3] = {0, 0, 0}, gb[3] = {0, 0, 0}, aa[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
+  for (int k = 0; k < 3; ++k) {
+    if (ia < M) { ga[k] = gyro[3 * ia + k]; aa[k] = accel[3 * ia + k]; }
+    if (ib < M) { gb[k] = gyro[3 * ib + k]; ab[k] = accel[3 * ib + k]; }
+  }
+  double dRa[9], dRb[9], Pl[9];
+  {
+    double wv[3] = {(ga[0] - bg[0]) * dea, (ga[1] - bg[1]) * dea, (ga[2] - bg[2]) * dea};
+    so3_exp(wv, dRa);
+    double wv2[3] = {(gb[0] - bg[0]) * deb, (gb[1] - bg[1]) * deb, (gb[2] - bg[2]) * deb};
+    so3_exp(wv2, dRb);
+    mat3_mul(dRa, dRb, Pl);
+  }
+  for (int k = 0; k < 9; ++k) A[t * 9 + k] = Pl[k];
+  __syncthreads();
+  // inclusive Hillis-Steele scan of 3x3 products: X_t = Pl_0 ... Pl_t
+  double* src = A;
+  double* dst = Bm;
+  for (int off = 1; off < kWG; off <<= 1) {
+    double Xn[9];
+    if (t >= off) {
+      mat3_mul(src + (t - off) * 9, src + t * 9, Xn);
+    } else {
+      for (int k = 0; k < 9; ++k) Xn[k] = src[t * 9 + k];
+    }
+    for (int k = 0; k < 9; ++k) dst[t * 9 + k] = Xn[k];
+    __syncthreads();
+    double* tmp = src; src = dst; dst = tmp;
+  }
+  double Ea[9], Rb[9];
+  if (t == 0) {
+    for (int k = 0; k < 9; ++k) Ea[k] = R0[k];
+  } else {
+    mat3_mul(R0, src + (t - 1) * 9, Ea);
+  }
+  mat3_mul(Ea, dRa, Rb);
+  double nga[3], ngb[3], awa[3], awb[3];
+  const double aba[3] = {aa[0] - ba[0], aa[1] - ba[1], aa[2] - ba[2]};
+  const double abb[3] = {ab[0] - ba[0], ab[1] - ba[1], ab[2] - ba[2]};
+  mat3_vec(Ea, aba, nga);
+  mat3_vec(Rb, abb, ngb);
+  for (int k = 0; k < 3; ++k) { awa[k] = nga[k] + g[k]; awb[k] = ngb[k] + g[k]; }
+  // exclusive prefix sum of velocity increments
+  for (int k = 0; k < 3; ++k) V1[t * 3 + k] = awa[k] * dea + awb[k] * deb;
+  __syncthreads();
+  double* vs = V1;
+  double* vd = V2;
+  for (int off = 1; off < kWG; off <<= 1) {
+    double v[3];
+    for (int k = 0; k < 3; ++k) v[k] = vs[t * 3 + k] + ((t >= off) ? vs[(t - off) * 3 + k] : 0.0);
+    for (int k = 0; k < 3; ++k) vd[t * 3 + k] = v[k];
+    __syncthreads();
+    double* tp = vs; vs = vd; vd = tp;
+  }
+  double pc[3];
+  for (int k = 0; k < 3; ++k) {
+    const double va = (t > 0) ? vs[(t - 1) * 3 + k] : 0.0;
+    const double vb = va + awa[k] * dea;
+    pc[k] = va * dea + 0.5 * awa[k] * (dea * dea) + vb * deb + 0.5 * awb[k] * (deb * deb);
+  }
+  double sums[13];
+  for (int k = 0; k < 3; ++k) {
+    sums[k] = pc[k];
+    sums[3 + k] = aba[k] * dea + abb[k] * deb;
+    sums[6 + k] = nga[k] * dea + ngb[k] * deb;
+    sums[9 + k] = awa[k] * dea + awb[k] * deb;
+  }
+  sums[12] = dea + deb;
+  for (int q = 0; q < 13; ++q) sums[q] = wg_sum(sums[q], red);
+  if (t == 0) {
+    mat3_mul(R0, src + (kWG - 1) * 9, out);  // R_end
+    for (int k = 0; k < 3; ++k) {
+      out[9 + k] = sums[k];                  // p_end (world)
+      out[12 + k] = vs[(kWG - 1) * 3 + k];   // v_end (world)
+      out[16 + k] = sums[3 + k];
+      out[19 + k] = sums[6 + k];
+      out[22 + k] = sums[9 + k];
+    }
+    out[15] = sums[12];
+  }
+  __syncthreads();
+}
+
+}  // namespace gc
