@@ -10,10 +10,6 @@
 namespace gc {
 
 constexpr int NN = kDZ * kDZ;
-constexpr int kBlockStart[7] = {0, 3, 6, 9, 12, 15, 16};
-constexpr int kBlockDim[7] = {3, 3, 3, 3, 3, 1, 6};
-constexpr double kRhoProc[7] = {0.99, 0.995, 0.95, 0.999, 0.999, 0.9999, 0.9999};
-constexpr double kRhoMeas[3] = {0.995, 0.995, 0.99};
 
 GC_DEV void compose_exp2(const double* X, const double* d6, double* out) {
   double e[6];
@@ -372,71 +368,13 @@ __global__ void __launch_bounds__(256) k_map_derive(PipeDev P) {
   map_derive_wg(P, red, tab);
 }
 
-// Projection of one padded 6x6 IW block whose active part is the leading d x d (d in {1,3}):
-// the padded block is [A, 0; 0, 0], so its PSD projection is [PSD(A), 0; 0, eps I] and the
-// projection delta picks up (6-d) eps^2 (the reference projects the padded 6x6 as a whole).
-GC_DEV double psd_padded_small(const double* A6, int d, double eps, double* out6) {
-  for (int k = 0; k < 36; ++k) out6[k] = 0.0;
-  double d2 = (6 - d) * eps * eps;
-  if (d == 1) {
-    const double a = A6[0], p = fmax(a, eps);
-    out6[0] = p;
-    d2 += (p - a) * (p - a);
-  } else {
-    double A[9], Pp[9], c[6];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) A[3 * i + j] = A6[6 * i + j];
-    psd_project3(A, eps, Pp, c);
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) out6[6 * i + j] = Pp[3 * i + j];
-    d2 += c[0] * c[0];
-  }
-  for (int k = d; k < 6; ++k) out6[7 * k] = eps;
-  return sqrt(d2);
-}
-
-// process_noise_state_to_Q_jax (inverse_wishart_jax.py:35-68). Q is block diagonal (the masked
-// 6x6 patches overwrite each other's zero padding), so its PSD projection is the direct sum of
-// the active blocks' projections: 3x3 blocks in registers, the 6x6 extrinsic block on the WG.
 GC_DEV void iw_Q_wg(const PipeDev& P, double* Qs, double* Qp, double* Sx, double* red) {
-  const int t = threadIdx.x, n = kDZ;
-  for (int idx = t; idx < NN; idx += kWG) Qp[idx] = 0.0;
-  __syncthreads();
-  auto den = [&](int b) { return softplus(50.0 * (P.nu_proc[b] - kBlockDim[b] - 1.0)) / 50.0 + 1e-12; };
-  if (t < 6) {
-    const int b = t, d = kBlockDim[b], s0 = kBlockStart[b];
-    const double dn = den(b);
-    if (d == 1) {
-      Qp[s0 * n + s0] = fmax(P.Psi_proc[b * 36] / dn, P.eps_psd);
-    } else {
-      double A[9], Pp[9];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) A[3 * i + j] = P.Psi_proc[b * 36 + 6 * i + j] / dn;
-      psd_project3(A, P.eps_psd, Pp, nullptr);
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) Qp[(s0 + i) * n + (s0 + j)] = Pp[3 * i + j];
-    }
-  }
-  const double d6 = den(6);
-  for (int idx = t; idx < 36; idx += kWG) Qs[idx] = P.Psi_proc[6 * 36 + idx] / d6;
-  __syncthreads();
-  double* Q6 = Qs + 36;
-  wg_psd_project_fast(Qs, Q6, P.eps_psd, 6, Sx, red, nullptr);
-  for (int idx = t; idx < 36; idx += kWG) Qp[(16 + idx / 6) * n + (16 + idx % 6)] = Q6[idx];
-  __syncthreads();
-  for (int idx = t; idx < NN; idx += kWG) P.Q[idx] = Qp[idx];
-  __syncthreads();
+  wg_iw_Q(P.nu_proc, P.Psi_proc, P.eps_psd, P.Q, Qs, Qp, Sx, red);
 }
 
 __global__ void __launch_bounds__(256) k_iw_Q(PipeDev P) {
   extern __shared__ double sm[];
   iw_Q_wg(P, sm, sm + NN, sm + 2 * NN, sm + 4 * NN + 4 * kDZ);
-}
-
-GC_DEV double nu_project(double nu_raw, double dim, double nu_max) {
-  const double nmin = dim + 1.0 + 0.5;
-  const double nf = nmin + softplus(nu_raw - nmin);
-  return nu_max - softplus(nu_max - nf);
 }
 
 // ================================================= a16 combine + a15 IW apply + map update
@@ -489,57 +427,11 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
   }
   __syncthreads();
   // ---- process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
-  if (t < 7) {  // ν update (smooth projection) for every block
-    const double nr = kRhoProc[t] * P.nu_proc[t] + S.w_process * R[kPDNUP + t];
-    const double nn = nu_project(nr, kBlockDim[t], P.nu_max);
-    tab[16 + t] = fabs(nn - nr);
-    tab[24 + t] = nn;
-  }
-  if (t < 6) {  // 3x3 and 1x1 blocks in registers
-    double A6[36], O6[36];
-    for (int k = 0; k < 36; ++k) {
-      const int i = k / 6, j = k % 6;
-      const double m = (i < kBlockDim[t] && j < kBlockDim[t]) ? 1.0 : 0.0;
-      A6[k] = (kRhoProc[t] * P.Psi_proc[t * 36 + k] + S.w_process * R[kPDPSIP + t * 36 + k]) * m;
-    }
-    tab[8 + t] = psd_padded_small(A6, kBlockDim[t], P.eps_psd, O6);
-    for (int k = 0; k < 36; ++k) Qs[t * 36 + k] = O6[k];
-  }
-  if (t < 36) blk[t] = kRhoProc[6] * P.Psi_proc[6 * 36 + t] + S.w_process * R[kPDPSIP + 6 * 36 + t];
-  __syncthreads();
-  wg_psd_project_fast(blk, blkp, P.eps_psd, 6, Sx, red, c6);
-  for (int k = t; k < 6 * 36; k += kWG) P.Psi_proc[k] = Qs[k];
-  if (t < 36) P.Psi_proc[6 * 36 + t] = blkp[t];
-  if (t < 7) P.nu_proc[t] = tab[24 + t];
-  __syncthreads();
-  double pd_acc = 0.0, nu_acc = 0.0;
-  if (t == 0) {
-    for (int b = 0; b < 6; ++b) pd_acc += tab[8 + b];
-    pd_acc += c6[0];
-    for (int b = 0; b < 7; ++b) nu_acc += tab[16 + b];
-  }
-  __syncthreads();
+  wg_iw_proc_apply(P.nu_proc, P.Psi_proc, R + kPDPSIP, R + kPDNUP, S.w_process, P.eps_psd, P.nu_max, P.nu_proc,
+                   P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab);
   // ---- measurement-noise IW apply (measurement_noise_iw_jax.py:59-100)
-  if (t < 3) {
-    double Mr[9], Mp[9], cc[6];
-    for (int k = 0; k < 9; ++k) Mr[k] = kRhoMeas[t] * P.Psi_meas[t * 9 + k] + R[kPDPSIM + t * 9 + k];
-    double Ms[9];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) Ms[3 * i + j] = 0.5 * (Mr[3 * i + j] + Mr[3 * j + i]);
-    psd_project3(Ms, P.eps_psd, Mp, cc);
-    for (int k = 0; k < 9; ++k) P.Psi_meas[t * 9 + k] = Mp[k];
-    const double nr = kRhoMeas[t] * P.nu_meas[t] + R[kPDNUM + t];
-    const double nn = nu_project(nr, 3.0, P.nu_max);
-    P.nu_meas[t] = nn;
-    tab[t] = cc[0];
-    tab[3 + t] = fabs(nn - nr);
-  }
-  __syncthreads();
-  if (t == 0) {
-    P.iw_cert[0] = pd_acc; P.iw_cert[1] = nu_acc;
-    P.iw_cert[2] = tab[0] + tab[1] + tab[2]; P.iw_cert[3] = tab[3] + tab[4] + tab[5];
-  }
-  __syncthreads();
+  wg_iw_meas_apply(P.nu_meas, P.Psi_meas, R + kPDPSIM, R + kPDNUM, P.eps_psd, P.nu_max, P.nu_meas, P.Psi_meas,
+                   P.iw_cert + 2, tab);
   iw_Q_wg(P, Qs, Qp, Sx, red);
   // ---- map update: γ·map + increments of hypothesis 0 (bin_atlas.py:137-163, :232-257)
   for (int e = t; e < P.B * kMapRec; e += kWG) P.map[e] = P.forgetting * P.map[e] + R[kPMAP + e];

@@ -218,9 +218,12 @@ constexpr int kPredCertLen = 8;  // [lift, psd Δ, eig_min, eig_max, cond, nnc, 
 // Σ' = e^{-2λdt}Σ + (1−e^{-2λdt})/(2λ) Q, PSD, L' = (Σ'+εI)⁻¹, PSD, h' = L' μ.
 // Lp (in, n x n, LDS) and hprev (in) are preserved; outputs Lout/hout/mu (LDS), cert (thread 0).
 // Scratch: W1..W3 (n x n each), Sx (2 n² + 4 n), red (>= 8), c1/c2 (6 each).
+// full_cert: exact eigen certificate (per-operator entry); otherwise the Cholesky-certified
+// fast projection (pipeline: only the projection delta is consumed, eigen fields NaN).
 GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, double dt, double eps_psd,
                        double eps_lift, double lambda_ou, double* Lout, double* hout, double* mu, double* cert,
-                       double* W1, double* W2, double* W3, double* Sx, double* red, double* c1, double* c2) {
+                       double* W1, double* W2, double* W3, double* Sx, double* red, double* c1, double* c2,
+                       bool full_cert = false) {
   const int t = threadIdx.x, n = kDZ;
   wg_solve_lifted(Lp, hprev, mu, eps_lift, n, W1);  // W1 = chol(L + εI)
   wg_chol_inverse(W1, W2, W3, n);                    // W2 = Σ
@@ -228,11 +231,13 @@ GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, d
   const double dc = (1.0 - ef) / (2.0 * lambda_ou + kF64Eps);
   for (int i = t; i < kNN; i += kWG) W2[i] = ef * W2[i] + dc * Q[i];
   __syncthreads();
-  wg_psd_project_fast(W2, W3, eps_psd, n, Sx, red, c1);  // Σ'_psd -> W3
+  if (full_cert) wg_psd_project(W2, W3, eps_psd, n, Sx, red, c1);  // Σ'_psd -> W3
+  else wg_psd_project_fast(W2, W3, eps_psd, n, Sx, red, c1);
   double trl = (t < n) ? W3[t * n + t] : 0.0;
   const double trace_cov = wg_sum(trl, red);
   wg_inverse_lifted(W3, W2, eps_lift, n, W1, Lout);      // L' raw -> W2 (Lout as work)
-  wg_psd_project_fast(W2, Lout, eps_psd, n, Sx, red, c2);
+  if (full_cert) wg_psd_project(W2, Lout, eps_psd, n, Sx, red, c2);
+  else wg_psd_project_fast(W2, Lout, eps_psd, n, Sx, red, c2);
   wg_matvec(Lout, mu, hout, n);
   if (t == 0 && cert) {
     const double lift = 2.0 * eps_lift * n;
@@ -342,6 +347,145 @@ GC_DEV void wg_preintegrate(int M, const double* stamps, const double* gyro, con
     }
     out[15] = sums[12];
   }
+  __syncthreads();
+}
+
+// ------------------------------------------------------------------------------------ a15
+constexpr double kIwRhoProc[7] = {0.99, 0.995, 0.95, 0.999, 0.999, 0.9999, 0.9999};  // constants.py:265-281
+constexpr double kIwRhoMeas[3] = {0.995, 0.995, 0.99};
+
+// ν projection: ν_min + softplus(ν − ν_min), then soft cap at ν_max (inverse_wishart_jax.py:160-170).
+GC_DEV double nu_project(double nu_raw, double dim, double nu_max) {
+  const double nmin = dim + 1.0 + 0.5;
+  const double nf = nmin + softplus(nu_raw - nmin);
+  return nu_max - softplus(nu_max - nf);
+}
+
+// Projection of one padded 6x6 IW block whose active part is the leading d x d (d in {1,3}):
+// the padded block is [A, 0; 0, 0], so its PSD projection is [PSD(A), 0; 0, eps I] and the
+// projection delta picks up (6-d) eps^2 (the reference projects the padded 6x6 as a whole).
+GC_DEV double psd_padded_small(const double* A6, int d, double eps, double* out6) {
+  for (int k = 0; k < 36; ++k) out6[k] = 0.0;
+  double d2 = (6 - d) * eps * eps;
+  if (d == 1) {
+    const double a = A6[0], p = fmax(a, eps);
+    out6[0] = p;
+    d2 += (p - a) * (p - a);
+  } else {
+    double A[9], Pp[9], c[6];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) A[3 * i + j] = A6[6 * i + j];
+    psd_project3(A, eps, Pp, c);
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) out6[6 * i + j] = Pp[3 * i + j];
+    d2 += c[0] * c[0];
+  }
+  for (int k = d; k < 6; ++k) out6[7 * k] = eps;
+  return sqrt(d2);
+}
+
+// Process-noise IW apply (inverse_wishart_jax.py:126-185), one workgroup:
+// Ψ_b' = PSD((ρ_b Ψ_b + w dΨ_b) ⊙ mask_b), ν_b' = proj(ρ_b ν_b + w dν_b).
+// Outputs may alias the inputs (all reads precede the writes). cert (thread 0) =
+// [Σ_b psd Δ_b, Σ_b |ν_b' − ν_b,raw|]. Scratch: Qs 216, blk 36, blkp 36, Sx 2*36+24, red 16,
+// c6 8, tab 32.
+GC_DEV void wg_iw_proc_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double w,
+                             double eps_psd, double nu_max, double* nu_out, double* Psi_out, double* cert,
+                             double* Qs, double* blk, double* blkp, double* Sx, double* red, double* c6,
+                             double* tab) {
+  const int t = threadIdx.x;
+  if (t < 7) {
+    const double nr = kIwRhoProc[t] * nu[t] + w * dnu[t];
+    const double nn = nu_project(nr, kIwBlockDim[t], nu_max);
+    tab[16 + t] = fabs(nn - nr);
+    tab[24 + t] = nn;
+  }
+  if (t < 6) {  // 3x3 and 1x1 blocks in registers
+    double A6[36], O6[36];
+    for (int k = 0; k < 36; ++k) {
+      const int i = k / 6, j = k % 6;
+      const double m = (i < kIwBlockDim[t] && j < kIwBlockDim[t]) ? 1.0 : 0.0;
+      A6[k] = (kIwRhoProc[t] * Psi[t * 36 + k] + w * dPsi[t * 36 + k]) * m;
+    }
+    tab[8 + t] = psd_padded_small(A6, kIwBlockDim[t], eps_psd, O6);
+    for (int k = 0; k < 36; ++k) Qs[t * 36 + k] = O6[k];
+  }
+  if (t < 36) blk[t] = kIwRhoProc[6] * Psi[6 * 36 + t] + w * dPsi[6 * 36 + t];
+  __syncthreads();
+  wg_psd_project_fast(blk, blkp, eps_psd, 6, Sx, red, c6);
+  for (int k = t; k < 6 * 36; k += kWG) Psi_out[k] = Qs[k];
+  if (t < 36) Psi_out[6 * 36 + t] = blkp[t];
+  if (t < 7) nu_out[t] = tab[24 + t];
+  __syncthreads();
+  if (t == 0 && cert) {
+    double pd = c6[0], na = 0.0;
+    for (int b = 0; b < 6; ++b) pd += tab[8 + b];
+    for (int b = 0; b < 7; ++b) na += tab[16 + b];
+    cert[0] = pd;
+    cert[1] = na;
+  }
+  __syncthreads();
+}
+
+// Measurement-noise IW apply (measurement_noise_iw_jax.py:59-100), threads 0..2 (one block each):
+// Ψ' = PSD(sym(ρ Ψ + dΨ)), ν' = proj(ρ ν + dν). tab: 6 doubles; cert (thread 0) = [Σ psd Δ, Σ |Δν|].
+GC_DEV void wg_iw_meas_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu,
+                             double eps_psd, double nu_max, double* nu_out, double* Psi_out, double* cert,
+                             double* tab) {
+  const int t = threadIdx.x;
+  if (t < 3) {
+    double Mr[9], Mp[9], cc[6], Ms[9];
+    for (int k = 0; k < 9; ++k) Mr[k] = kIwRhoMeas[t] * Psi[t * 9 + k] + dPsi[t * 9 + k];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) Ms[3 * i + j] = 0.5 * (Mr[3 * i + j] + Mr[3 * j + i]);
+    psd_project3(Ms, eps_psd, Mp, cc);
+    const double nr = kIwRhoMeas[t] * nu[t] + dnu[t];
+    const double nn = nu_project(nr, 3.0, nu_max);
+    tab[t] = cc[0];
+    tab[3 + t] = fabs(nn - nr);
+    for (int k = 0; k < 9; ++k) Psi_out[t * 9 + k] = Mp[k];
+    nu_out[t] = nn;
+  }
+  __syncthreads();
+  if (t == 0 && cert) {
+    cert[0] = tab[0] + tab[1] + tab[2];
+    cert[1] = tab[3] + tab[4] + tab[5];
+  }
+  __syncthreads();
+}
+
+// process_noise_state_to_Q_jax (inverse_wishart_jax.py:35-68). Q is block diagonal (the masked
+// 6x6 patches overwrite each other's zero padding), so its PSD projection is the direct sum of
+// the active blocks' projections: 3x3 blocks in registers, the 6x6 extrinsic block on the WG.
+// Q_out: global 22x22. Scratch: Qs (72), Qp (n²), Sx (2*36+24), red (16).
+GC_DEV void wg_iw_Q(const double* nu, const double* Psi, double eps_psd, double* Q_out, double* Qs, double* Qp,
+                    double* Sx, double* red) {
+  const int t = threadIdx.x, n = kDZ;
+  for (int idx = t; idx < kNN; idx += kWG) Qp[idx] = 0.0;
+  __syncthreads();
+  auto den = [&](int b) { return softplus(50.0 * (nu[b] - kIwBlockDim[b] - 1.0)) / 50.0 + 1e-12; };
+  if (t < 6) {
+    const int b = t, d = kIwBlockDim[b], s0 = kIwBlockStart[b];
+    const double dn = den(b);
+    if (d == 1) {
+      Qp[s0 * n + s0] = fmax(Psi[b * 36] / dn, eps_psd);
+    } else {
+      double A[9], Pp[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A[3 * i + j] = Psi[b * 36 + 6 * i + j] / dn;
+      psd_project3(A, eps_psd, Pp, nullptr);
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) Qp[(s0 + i) * n + (s0 + j)] = Pp[3 * i + j];
+    }
+  }
+  const double d6 = den(6);
+  for (int idx = t; idx < 36; idx += kWG) Qs[idx] = Psi[6 * 36 + idx] / d6;
+  __syncthreads();
+  double* Q6 = Qs + 36;
+  wg_psd_project_fast(Qs, Q6, eps_psd, 6, Sx, red, nullptr);
+  for (int idx = t; idx < 36; idx += kWG) Qp[(16 + idx / 6) * n + (16 + idx % 6)] = Q6[idx];
+  __syncthreads();
+  for (int idx = t; idx < kNN; idx += kWG) Q_out[idx] = Qp[idx];
   __syncthreads();
 }
 

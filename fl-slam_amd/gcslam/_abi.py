@@ -71,6 +71,24 @@ SIGNATURES = {
     "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],
     "gc_comm_destroy": [_vp],
     "gc_comm_allgather_f64": [_vp, _vp, _vp, _vp, _i64],
+    "gc_belief_world_pose_batch": [_vp, _i32, _vp, _vp, _vp, _f64, _vp, _vp],
+    "gc_predict_diffusion_batch": [_vp, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _f64, _vp, _vp, _vp],
+    "gc_smooth_window_weights": [_vp, _i32, _vp, _f64, _f64, _f64, _vp],
+    "gc_preintegrate_imu_batch": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _dptr, _vp],
+    "gc_imu_meas_iw_suffstats_batch": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _vp],
+    "gc_matrix_fisher_batch": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _f64, _vp],
+    "gc_planar_translation_batch": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _f64, _f64,
+                                    _vp],
+    "gc_excitation_scaling_batch": [_vp, _i32, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
+    "gc_fusion_scale_batch": [_vp, _i32, _vp, _f64, _f64, _f64, _f64, _vp],
+    "gc_info_fusion_additive_batch": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp],
+    "gc_recompose_batch": [_vp, _i32, _vp, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp, _vp],
+    "gc_anchor_drift_batch": [_vp, _i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp, _vp, _vp],
+    "gc_iw_process_suffstats_batch": [_vp, _i32, _vp, _vp, _vp, _vp, _f64, _vp, _vp],
+    "gc_iw_process_apply": [_vp, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp],
+    "gc_iw_process_Q": [_vp, _vp, _vp, _f64, _vp],
+    "gc_iw_meas_apply": [_vp, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp],
+    "gc_hypothesis_barycenter": [_vp, _i32, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp],
 }
 
 GC_PCFG_LEN = 18
@@ -81,6 +99,15 @@ GC_IO_CERT = 10
 GC_HYP_DIAG = 40
 GC_COMB_LEN = 484 + 22 + 22 + 6 + 16
 GC_COMM_ID_BYTES = 128
+GC_PRED_CERT = 8
+GC_PREINT_OUT = 32
+GC_MF_OUT = 66
+GC_PT_OUT = 26
+GC_RECOMPOSE_OUT = 19
+GC_DRIFT_OUT = 3
+GC_FUSION_ROW = 8
+GC_FUSION_OUT = 4
+GC_BARY_CERT = 16
 
 
 class PipelineDims(C.Structure):

@@ -8,10 +8,34 @@ from .binning import (BinAtlas, BinSoftAssignResult, ScanBinStats, bin_soft_assi
                       create_fibonacci_atlas, scan_bin_moment_match)
 from .kappa import kappa_from_resultant_batch
 from .primitives import domain_projection_psd, domain_projection_psd_batch
+from .predict import predict_diffusion
+from .imu_preintegration import (imu_accel_meas_iw_suffstats_from_gravity_dir_jax,
+                                 imu_gyro_meas_iw_suffstats_from_avg_rate_jax,
+                                 preintegrate_imu_relative_pose_jax, smooth_window_weights)
+from .matrix_fisher_evidence import (MatrixFisherResult, PlanarTranslationResult, ScatterMetrics,
+                                     matrix_fisher_rotation_evidence, planar_translation_evidence)
+from .excitation import apply_excitation_prior_scaling_jax, compute_excitation_scales_jax
+from .fusion import FusionScaleResult, fusion_scale_from_certificates, info_fusion_additive
+from .recompose import (AnchorDriftResult, RecomposeResult, anchor_drift_update,
+                        pose_update_frobenius_recompose)
+from .inverse_wishart import (MeasurementNoiseIWState, ProcessNoiseIWState,
+                              measurement_noise_apply_suffstats_jax,
+                              process_noise_iw_apply_suffstats_jax,
+                              process_noise_iw_suffstats_from_info_jax, process_noise_state_to_Q_jax)
+from .hypothesis import HypothesisProjectionResult, hypothesis_barycenter_projection
 
 __all__ = [
     "PointBudgetResult", "point_budget_resample", "DeskewConstantTwistResult",
     "deskew_constant_twist", "BinAtlas", "BinSoftAssignResult", "ScanBinStats",
     "bin_soft_assign", "create_fibonacci_atlas", "scan_bin_moment_match",
     "kappa_from_resultant_batch", "domain_projection_psd", "domain_projection_psd_batch",
+    "predict_diffusion", "smooth_window_weights", "preintegrate_imu_relative_pose_jax",
+    "imu_gyro_meas_iw_suffstats_from_avg_rate_jax", "imu_accel_meas_iw_suffstats_from_gravity_dir_jax",
+    "MatrixFisherResult", "PlanarTranslationResult", "ScatterMetrics", "matrix_fisher_rotation_evidence",
+    "planar_translation_evidence", "compute_excitation_scales_jax", "apply_excitation_prior_scaling_jax",
+    "FusionScaleResult", "fusion_scale_from_certificates", "info_fusion_additive", "RecomposeResult",
+    "AnchorDriftResult", "pose_update_frobenius_recompose", "anchor_drift_update", "ProcessNoiseIWState",
+    "MeasurementNoiseIWState", "process_noise_iw_suffstats_from_info_jax", "process_noise_iw_apply_suffstats_jax",
+    "process_noise_state_to_Q_jax", "measurement_noise_apply_suffstats_jax", "HypothesisProjectionResult",
+    "hypothesis_barycenter_projection",
 ]

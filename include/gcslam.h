@@ -225,6 +225,105 @@ int32_t gc_comm_init(gc_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* h
 int32_t gc_comm_destroy(gc_comm* comm);
 int32_t gc_comm_allgather_f64(gc_ctx* ctx, gc_comm* comm, const double* d_send, double* d_recv, int64_t count);
 
+/* ------------------------------------------------------------------------------------------
+ * Per-operator entries: each reference operator of the hot path as one launch over H
+ * independent items (the gcslam.ops mirror calls them with H = 1 at the reference's
+ * per-hypothesis call sites). Matrices are row-major f64; "belief" arrays are
+ * X_anchor (H,6), z_lin (H,22), L (H,22,22), h (H,22). The same device code runs inside the
+ * batched pipeline above.
+ * ------------------------------------------------------------------------------------------ */
+#define GC_PRED_CERT 8      /* [lift, psd_delta, eig_min, eig_max, cond, nnc, trace_cov, trigger] */
+#define GC_PREINT_OUT 32    /* [delta_pose 6, delta_R 9, p_body 3, v_body 3, ess, a_body_mean 3,
+                               a_world_nog_mean 3, a_world_mean 3, dt_eff_sum] */
+#define GC_MF_OUT 66        /* [R_mf 9, L_rot 9, h_rot 3, delta_rot 3, svd 3, N_eff, nll_per_ess, psd_delta,
+                               trigger, nll, map scatter 17, scan scatter 17]; scatter = [eigenvalues 3
+                               (descending), eigenvectors 9 (row-major, columns = vectors), linearity,
+                               planarity, sphericity, anisotropy, effective_rank] */
+#define GC_PT_OUT 26        /* [t_wls 3, L_trans 9, h_trans 3, delta_trans 3, z_scale, N_eff, nll_per_ess,
+                               psd_delta, trigger, xy_info_scale, z_info_scale, nll] */
+#define GC_RECOMPOSE_OUT 19 /* [delta_pose 6, X_new 6, frobenius_strength, bch_correction 6] */
+#define GC_DRIFT_OUT 3      /* [rho, drift_m, drift_r] */
+#define GC_FUSION_ROW 8     /* in: [cond, ess_total, support_frac, excitation_total, dt_asymmetry,
+                               z_to_xy_ratio, power_beta, nll_per_ess] */
+#define GC_FUSION_OUT 4     /* [alpha, excitation_total, ess_to_excitation, cond_to_support] */
+#define GC_BARY_CERT 16     /* [floor_adjustment, spread, ess, support_frac, mass_eps, psd cert 6, pad 5] */
+
+/* BeliefGaussianInfo.mean_increment + world pose X ∘ Exp(δz) (common/belief.py:373-425). */
+int32_t gc_belief_world_pose_batch(gc_ctx* ctx, int32_t H, const double* d_X, const double* d_L, const double* d_h,
+                                   double eps_lift, double* d_pose_out, double* d_mean_out);
+/* predict_diffusion (backend/operators/predict.py:106-214 -> core :43-98); Q (22,22) shared. */
+int32_t gc_predict_diffusion_batch(gc_ctx* ctx, int32_t H, const double* d_L, const double* d_h, const double* d_Q,
+                                   double dt_sec, double eps_psd, double eps_lift, double lambda_ou, double* d_L_out,
+                                   double* d_h_out, double* d_cert_out);
+/* smooth_window_weights (backend/operators/imu_preintegration.py:20-43). */
+int32_t gc_smooth_window_weights(gc_ctx* ctx, int32_t M, const double* d_stamps, double t0, double t1, double sigma,
+                                 double* d_w_out);
+/* preintegrate_imu_relative_pose_jax (imu_preintegration.py:47-147); M <= 512 samples shared by
+   the H items; weights (H, weights_stride) or shared (stride 0); rotvec0/biases (H,3);
+   h_gravity3 NULL = (0, 0, -9.81). out (H, GC_PREINT_OUT). */
+int32_t gc_preintegrate_imu_batch(gc_ctx* ctx, int32_t H, int32_t M, const double* d_stamps, const double* d_gyro,
+                                  const double* d_accel, const double* d_weights, int64_t weights_stride,
+                                  const double* d_rotvec0, const double* d_gyro_bias, const double* d_accel_bias,
+                                  const double* h_gravity3, double* d_out);
+/* imu_gyro_meas_iw_suffstats_from_avg_rate_jax + imu_accel_meas_iw_suffstats_from_gravity_dir_jax
+   (measurement_noise_iw_jax.py:131-218); out (H, 18) = [dPsi_gyro 9, dPsi_accel 9]. */
+int32_t gc_imu_meas_iw_suffstats_batch(gc_ctx* ctx, int32_t H, int32_t M, const double* d_gyro, const double* d_accel,
+                                       const double* d_weights, const double* d_gyro_bias, const double* d_accel_bias,
+                                       const double* d_omega_avg, const double* d_rotvec0, double dt_imu,
+                                       double eps_mass, double eps_psd, double* d_out);
+/* matrix_fisher_rotation_evidence (archive/legacy_operators/matrix_fisher_evidence.py:264-394):
+   pose_pred (H,6) = world pose of belief_pred; scan (H,B,*), map (B,*); scatter inputs may be
+   NULL (metrics then use zero scatter). out (H, GC_MF_OUT). */
+int32_t gc_matrix_fisher_batch(gc_ctx* ctx, int32_t H, int32_t B, const double* d_pose_pred, const double* d_scan_s_dir,
+                               const double* d_scan_N, const double* d_scan_S_dir_scatter, const double* d_map_S_dir,
+                               const double* d_map_N_dir, const double* d_map_S_dir_scatter, double eps_psd,
+                               double eps_mass, double* d_out);
+/* planar_translation_evidence (matrix_fisher_evidence.py:502-671); R_hat (H,9); out (H, GC_PT_OUT). */
+int32_t gc_planar_translation_batch(gc_ctx* ctx, int32_t H, int32_t B, const double* d_pose_pred, const double* d_R_hat,
+                                    const double* d_scan_p_bar, const double* d_scan_Sigma_p, const double* d_scan_N,
+                                    const double* d_map_centroid, const double* d_map_Sigma_c,
+                                    const double* d_map_N_pos, const double* d_map_S_dir_scatter,
+                                    const double* d_map_N_dir, double eps_psd, double eps_mass, double* d_out);
+/* compute_excitation_scales_jax + apply_excitation_prior_scaling_jax (backend/operators/excitation.py:15-64);
+   s_out (H,2) = [s_dt, s_ex]. With d_L_ev == NULL, s_out is an input and only the scaling is applied. */
+int32_t gc_excitation_scaling_batch(gc_ctx* ctx, int32_t H, const double* d_L_ev, const double* d_L_prior,
+                                    const double* d_h_prior, double eps, double* d_s_out, double* d_L_out,
+                                    double* d_h_out);
+/* fusion_scale_from_certificates (backend/operators/fusion.py:46-142) over H certificate rows. */
+int32_t gc_fusion_scale_batch(gc_ctx* ctx, int32_t H, const double* d_rows, double alpha_min, double alpha_max,
+                              double c0_cond, double eps_mass, double* d_out);
+/* info_fusion_additive (backend/operators/fusion.py:150-230); alpha (H); cert (H,6) PSD cert. */
+int32_t gc_info_fusion_additive_batch(gc_ctx* ctx, int32_t H, const double* d_L_pred, const double* d_h_pred,
+                                      const double* d_L_ev, const double* d_h_ev, const double* d_alpha,
+                                      double eps_psd, double* d_L_out, double* d_h_out, double* d_cert_out);
+/* pose_update_frobenius_recompose (backend/operators/recompose.py:94-205); T (H). */
+int32_t gc_recompose_batch(gc_ctx* ctx, int32_t H, const double* d_X, const double* d_z, const double* d_L,
+                           const double* d_h, const double* d_T, double c_frob, double eps_lift, double* d_X_out,
+                           double* d_z_out, double* d_h_out, double* d_res_out);
+/* anchor_drift_update (backend/operators/anchor_drift.py:93-191). */
+int32_t gc_anchor_drift_batch(gc_ctx* ctx, int32_t H, const double* d_X, const double* d_z, const double* d_L,
+                              const double* d_h, double eps_lift, double* d_X_out, double* d_z_out, double* d_h_out,
+                              double* d_res_out);
+/* process_noise_iw_suffstats_from_info_jax (inverse_wishart_jax.py:72-123): dPsi (H,7,6,6), dnu (H,7). */
+int32_t gc_iw_process_suffstats_batch(gc_ctx* ctx, int32_t H, const double* d_L_pred, const double* d_h_pred,
+                                      const double* d_L_post, const double* d_h_post, double eps_lift,
+                                      double* d_dPsi_out, double* d_dnu_out);
+/* process_noise_iw_apply_suffstats_jax (inverse_wishart_jax.py:127-185): nu (7), Psi (7,6,6);
+   cert (2) = [psd_delta sum, nu projection sum]. Outputs may alias the inputs. */
+int32_t gc_iw_process_apply(gc_ctx* ctx, const double* d_nu, const double* d_Psi, const double* d_dPsi,
+                            const double* d_dnu, double eps_psd, double nu_max, double* d_nu_out, double* d_Psi_out,
+                            double* d_cert_out);
+/* process_noise_state_to_Q_jax (inverse_wishart_jax.py:36-68): Q (22,22). */
+int32_t gc_iw_process_Q(gc_ctx* ctx, const double* d_nu, const double* d_Psi, double eps_psd, double* d_Q_out);
+/* measurement_noise_apply_suffstats_jax (measurement_noise_iw_jax.py:60-100): nu (3), Psi (3,3,3). */
+int32_t gc_iw_meas_apply(gc_ctx* ctx, const double* d_nu, const double* d_Psi, const double* d_dPsi,
+                         const double* d_dnu, double eps_psd, double nu_max, double* d_nu_out, double* d_Psi_out,
+                         double* d_cert_out);
+/* hypothesis_barycenter_projection (backend/operators/hypothesis.py:125-236 -> core :52-122). */
+int32_t gc_hypothesis_barycenter(gc_ctx* ctx, int32_t H, const double* d_L, const double* d_h, const double* d_z,
+                                 const double* d_weights, double weight_floor, double eps_psd, double eps_lift,
+                                 double* d_L_out, double* d_h_out, double* d_z_out, double* d_cert_out);
+
 #ifdef __cplusplus
 }
 #endif

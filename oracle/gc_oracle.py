@@ -295,19 +295,24 @@ def preintegrate(stamps, gyro, accel, w, rotvec0, bg, ba, g=GRAVITY_W):
     R0 = R.copy()
     v = np.zeros(3); p = np.zeros(3)
     swdt = 0.0
+    s_body, s_nog, s_w = np.zeros(3), np.zeros(3), np.zeros(3)
     for i in range(stamps.shape[0]):
         de = w[i] * dt[i]
         dR = so3_exp((gyro[i] - bg) * de)
-        a_nog = R @ (accel[i] - ba)
+        a_b = accel[i] - ba
+        a_nog = R @ a_b
         a_w = a_nog + g
         swdt += de
+        s_body += a_b * de; s_nog += a_nog * de; s_w += a_w * de
         p = p + v * de + 0.5 * a_w * (de * de)
         v = v + a_w * de
         R = R @ dR
     dRel = R0.T @ R
     p_b = R0.T @ p
+    den = max(swdt, 1e-12)
     return dict(delta_pose=np.concatenate([p_b, so3_log(dRel)]), ess=float(np.sum(w)),
-                delta_R=dRel, delta_p=p_b, delta_v=R0.T @ v, dt_eff_sum=swdt)
+                delta_R=dRel, delta_p=p_b, delta_v=R0.T @ v, dt_eff_sum=swdt,
+                a_body_mean=s_body / den, a_world_nog_mean=s_nog / den, a_world_mean=s_w / den)
 
 
 def imu_dt_mean(stamps):
@@ -538,7 +543,8 @@ def scatter_metrics(S, N_total, eps=EPS_MASS):
     tot = lam.sum() + eps
     p = lam / tot
     ent = -np.sum(p * np.log(p + eps))
-    return dict(eigenvalues=lam, linearity=(lam[0] - lam[1]) * il, planarity=(lam[1] - lam[2]) * il,
+    return dict(eigenvalues=lam, eigenvectors=V[:, idx], linearity=(lam[0] - lam[1]) * il,
+                planarity=(lam[1] - lam[2]) * il,
                 sphericity=lam[2] * il, anisotropy=1.0 - lam[2] * il, effective_rank=math.exp(ent))
 
 
