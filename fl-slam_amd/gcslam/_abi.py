@@ -89,6 +89,7 @@ SIGNATURES = {
     "gc_iw_process_Q": [_vp, _vp, _vp, _f64, _vp],
     "gc_iw_meas_apply": [_vp, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp],
     "gc_hypothesis_barycenter": [_vp, _i32, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp],
+    "gc_primitive_map_fuse": [_vp, _vp, _vp, _vp, _f64, _f64, _f64, _i64, _vp],
 }
 
 GC_PCFG_LEN = 18

@@ -324,6 +324,52 @@ int32_t gc_hypothesis_barycenter(gc_ctx* ctx, int32_t H, const double* d_L, cons
                                  const double* d_weights, double weight_floor, double eps_psd, double eps_lift,
                                  double* d_L_out, double* d_h_out, double* d_z_out, double* d_cert_out);
 
+/* ------------------------------------------------------------------------------------------
+ * C5 map update (a13 C5 analogue): transform_gaussian_to_world (backend/pipeline.py:1248-1256)
+ * fused into primitive_map_fuse (backend/structures/primitive_map.py:992-1163). The map is one
+ * flat tile of m_slots slots in device memory (SoA, row-major per slot); tile t / local slot j of
+ * the reference map to slot t * m_tile + j. Colour fields are all NULL (no camera colour
+ * tracking) or all set. All pointers inside the structs are device pointers.
+ * ------------------------------------------------------------------------------------------ */
+typedef struct gc_primitive_map {
+  int64_t m_slots;
+  int32_t n_lobes;          /* GC_VMF_N_LOBES (3) */
+  int32_t pad_;
+  double* Lambdas;          /* (M, 3, 3) */
+  double* thetas;           /* (M, 3) */
+  double* etas;             /* (M, n_lobes, 3) */
+  double* weights;          /* (M) */
+  double* timestamps;       /* (M) */
+  int64_t* last_supported_scan_seq;  /* (M) */
+  int64_t* last_update_scan_seq;     /* (M) */
+  double* cam_mass;         /* (M) or NULL */
+  double* lidar_mass;       /* (M) or NULL */
+  double* rgb_cam_accum;    /* (M, 3) or NULL */
+  double* rgb_cam_denom;    /* (M) or NULL */
+  double* rgb;              /* (M, 3) or NULL */
+  double* colors;           /* (M, 3) or NULL */
+} gc_primitive_map;
+
+typedef struct gc_fuse_batch {
+  int64_t K;
+  const int32_t* target_slots;      /* (K) slot per row; out-of-range rows are dropped */
+  const double* Lambdas;            /* (K, 3, 3) body (or world) frame */
+  const double* thetas;             /* (K, 3) */
+  const double* etas;               /* (K, n_lobes, 3) */
+  const double* weights;            /* (K) */
+  const double* responsibilities;   /* (K) */
+  const uint8_t* valid_mask;        /* (K) or NULL = all valid */
+  const double* colors;             /* (K, 3) or NULL */
+  const int32_t* sources;           /* (K) 0 = camera, 1 = lidar, or NULL */
+} gc_fuse_batch;
+
+/* Fuse K rows into the map in place. h_pose6 (host, [t, rotvec]) = world pose z_t of the
+   pushforward, or NULL when the rows are already in the world frame. n_fused_out (host, may be
+   NULL) = number of distinct in-range slots touched; it synchronises the stream. */
+int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc_fuse_batch* meas,
+                              const double* h_pose6, double eps_lift, double eps_mass, double timestamp,
+                              int64_t scan_seq, int64_t* n_fused_out);
+
 #ifdef __cplusplus
 }
 #endif

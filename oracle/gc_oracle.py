@@ -961,3 +961,61 @@ def process_scan(state: ScanState, scan: ScanInput, ios, bins, cfg: PipeConfig, 
     new_map = map_forget_and_add(state.map, res[0]["map_inc"])
     st = ScanState(new_beliefs, state.weights.copy(), nu_p, Psi_p, nu_m, Psi_m, new_map, state.scan_count + 1)
     return st, comb, res
+
+
+# ---------------------------------------------------------------------------------------
+# a13 C5 analogue: transform_gaussian_to_world (pipeline.py:1248-1256) + primitive_map_fuse
+# (structures/primitive_map.py:992-1163), sequential scatter-add semantics (np.add.at, row order)
+# ---------------------------------------------------------------------------------------
+def transform_gaussian_to_world(Lb, tb, eb, pose, eps_lift=EPS_LIFT):
+    """Rows (K,3,3), (K,3), (K,L,3) -> world frame for z_t = pose = [t, rotvec]."""
+    R = so3_exp(pose[3:6])
+    t = pose[0:3]
+    Lw = np.einsum("ij,kjl,ml->kim", R, Lb, R)
+    mu_b = np.linalg.solve(Lb + eps_lift * np.eye(3)[None], tb[..., None])[..., 0]
+    mu_w = mu_b @ R.T + t[None]
+    tw = np.einsum("kij,kj->ki", Lw, mu_w)
+    ew = np.einsum("ij,klj->kli", R, eb)
+    return Lw, tw, ew
+
+
+def primitive_map_fuse(tile: dict, slots, Lambdas, thetas, etas, weights, resp, timestamp, scan_seq, valid=None,
+                       colors=None, sources=None, eps_mass=EPS_MASS):
+    """Returns a new tile dict (fields as create_empty_tile) after the fuse; out-of-range slots dropped."""
+    M = tile["weights"].shape[0]
+    slots = np.asarray(slots, np.int64)
+    keep = (slots >= 0) & (slots < M)
+    r = np.asarray(resp, np.float64) * (1.0 if valid is None else np.asarray(valid, np.float64))
+    idx, rk = slots[keep], r[keep]
+    out = {k: v.copy() for k, v in tile.items()}
+    dL = np.zeros_like(tile["Lambdas"]); np.add.at(dL, idx, rk[:, None, None] * np.asarray(Lambdas)[keep])
+    dt = np.zeros_like(tile["thetas"]); np.add.at(dt, idx, rk[:, None] * np.asarray(thetas)[keep])
+    de = np.zeros_like(tile["etas"]); np.add.at(de, idx, rk[:, None, None] * np.asarray(etas)[keep])
+    w = np.asarray(weights)[keep]
+    dw = np.zeros(M); np.add.at(dw, idx, rk * w)
+    dr = np.zeros(M); np.add.at(dr, idx, rk)
+    out["Lambdas"] = tile["Lambdas"] + dL
+    out["thetas"] = tile["thetas"] + dt
+    out["etas"] = tile["etas"] + de
+    out["weights"] = tile["weights"] + dw
+    out["timestamps"][np.unique(idx)] = timestamp
+    upd = dr > 0.0
+    out["last_supported_scan_seq"] = np.where(upd, scan_seq, tile["last_supported_scan_seq"])
+    out["last_update_scan_seq"] = np.where(upd, scan_seq, tile["last_update_scan_seq"])
+    if "cam_mass" in tile and sources is not None:
+        src = np.asarray(sources)[keep]
+        wc = rk * w * (src == 0); wl = rk * w * (src == 1)
+        dc = np.zeros(M); np.add.at(dc, idx, wc)
+        dl = np.zeros(M); np.add.at(dl, idx, wl)
+        out["cam_mass"] = tile["cam_mass"] + dc
+        out["lidar_mass"] = tile["lidar_mass"] + dl
+        if colors is not None:
+            da = np.zeros((M, 3)); np.add.at(da, idx, np.clip(np.asarray(colors)[keep], 0.0, 1.0) * wc[:, None])
+            out["rgb_cam_accum"] = tile["rgb_cam_accum"] + da
+            dd = np.zeros(M); np.add.at(dd, idx, wc)
+            out["rgb_cam_denom"] = tile["rgb_cam_denom"] + dd
+    if "cam_mass" in tile:
+        est = np.clip(out["rgb_cam_accum"] / np.maximum(out["rgb_cam_denom"][:, None], eps_mass), 0.0, 1.0)
+        out["rgb"] = np.where((out["cam_mass"] > 0.0)[:, None], est, 0.5)
+        out["colors"] = out["rgb"].copy()
+    return out, int(np.unique(idx).shape[0])
