@@ -42,6 +42,7 @@ def parse():
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--no-map", action="store_true", help="skip the C5 PrimitiveMap fuse leg")
     return ap.parse_args()
 
 
@@ -184,6 +185,8 @@ def main():
         d0 = {k: _abi.DeviceArray.from_host(ctx, scans[0][k]) for k in ("points", "timestamps", "weights")}
         dbins = _abi.DeviceArray.from_host(ctx, bins)
         out["roofline"] = roofline_leg(ctx, _abi, scans[0], d0, xi, dbins, B, n, H, origin)
+    if dist.rank == 0 and not args.no_map:
+        out["c5_map_fuse"] = map_fuse_leg(ctx, _abi)
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args.n_az, H_total, args.cpu_budget_s)
     if dist.rank == 0:
@@ -228,6 +231,42 @@ def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=3):
             "per_kernel": {"soft_assign": {"ms": ms_sa, "bytes": b_sa, "GB/s": b_sa / (ms_sa * 1e-3) / 1e9},
                            "moment_match": {"ms": ms_mm, "bytes": b_mm, "GB/s": b_mm / (ms_mm * 1e-3) / 1e9}},
             "hypotheses": H}
+
+
+def map_fuse_leg(ctx, _abi, m_slots=1 << 20, rows=1 << 17, reps=5):
+    """C5 map update: 1,048,576-slot PrimitiveMap (random SPD Λ with eigenvalues
+    10..1e4, θ, 3-lobe η, w in (0, 1]) and 131,072 measurement rows pushed to the world frame and
+    fused (transform_gaussian_to_world + primitive_map_fuse, colour tracking on)."""
+    from gcslam.primitive_map import DeviceFuseBatch, DevicePrimitiveMap, fuse_device
+    rng = np.random.default_rng(20261015)
+    M, K, Lb = m_slots, rows, 3
+
+    def spd(n):
+        Q, _ = np.linalg.qr(rng.normal(size=(n, 3, 3)))
+        return np.einsum("nij,nj,nkj->nik", Q, 10.0 ** rng.uniform(1, 4, (n, 3)), Q)
+
+    dm = DevicePrimitiveMap(1, M, ctx=ctx)
+    dm.upload(Lambdas=spd(M), thetas=rng.normal(size=(M, 3)), etas=rng.normal(size=(M, Lb, 3)),
+              weights=rng.uniform(1e-3, 1.0, M))
+    slots = rng.integers(0, M, K)
+    batch = DeviceFuseBatch(ctx, slots, spd(K), rng.normal(size=(K, 3)), rng.normal(size=(K, Lb, 3)),
+                            rng.uniform(0, 1, K), rng.uniform(0, 1, K), rng.uniform(0, 1, K) > 0.05,
+                            rng.uniform(0, 1, (K, 3)), np.ones(K, np.int32))
+    pose = np.array([1.0, -2.0, 0.0, 0.01, -0.02, 0.7])
+    n_unique = fuse_device(dm, batch, 0.0, 0, pose)  # warm (and the touched-slot count)
+    ev = [_abi.Event(ctx) for _ in range(2)]
+    ev[0].record()
+    for r in range(reps):
+        fuse_device(dm, batch, float(r + 1), r + 1, pose, count=False)
+    ev[1].record()
+    ctx.sync()
+    ms = ev[0].elapsed_ms(ev[1]) / reps
+    row_b = 4 + 72 + 24 + 72 + 8 + 8 + 1 + 24 + 4
+    slot_rmw = 2 * (72 + 24 + 72 + 8 + 8 + 24 + 8 + 24 + 8)   # core 176 B + stamps/seqs + cam/lidar/accum/denom
+    colour_pass = M * (8 + 8 + 24 + 24 + 24)                   # rgb/colors recomputed for every slot
+    b = K * row_b + n_unique * slot_rmw + colour_pass
+    return {"slots": M, "rows": K, "distinct_slots": n_unique, "ms": ms, "bytes": b,
+            "GB/s": b / (ms * 1e-3) / 1e9, "kernel": "k_fuse_keys + radix sort + k_fuse_segments + k_fuse_colors"}
 
 
 def cpu_leg(n_az, H_total, budget_s):
