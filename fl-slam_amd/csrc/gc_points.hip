@@ -288,39 +288,34 @@ __global__ void k_point_dirs(int64_t rows, const double* __restrict__ pts, doubl
 }
 
 // ============================================================================ a5 soft assign
-// grid (chunks, H), chunk = iters*256 points; each wave owns 64 points per iteration and walks
-// them 4 per step (lanes = 4 point-groups x 16 bin-lanes, lane l owns bins {l, l+16, ..}).
-// Directions arrive lane-per-point (coalesced, prefetched one iteration ahead) and are handed
-// out through a wave-private LDS slab. Softmax sums and the argmax are 16-lane DPP butterflies.
-// Per-point scalars are stashed on lane (g, l) for step l (point 4l+g): one log Z and one
-// coalesced bin-index store per lane per iteration.
-template <int BPL>
-__global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
+// grid (chunks, H), chunk = iters*256 points; each wave owns 64 points per iteration with
+// lane = point: the 16*BPL similarities, exps and the softmax sum of a point stay in one lane
+// (no cross-lane reductions), the bin directions are wave-uniform (scalar loads), and the
+// argmax is a running compare in bin order (lowest index on ties). The lane's normalised row
+// is transposed through a wave-private LDS slab one 16-bin block at a time (row stride 18
+// doubles: the 8 lanes of a ds_write_b128 group hit disjoint banks) and leaves as contiguous
+// 128-B row segments, 16 B per lane (FULL: B == 16*BPL) or 8 B per lane (ragged B).
+template <int BPL, bool FULL>
+__global__ void __launch_bounds__(256, 3) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
                                                      const double* __restrict__ bins, double inv_tau,
                                                      double* resp, int32_t* bin_idx, double* partial) {
+  constexpr int NB = 16 * BPL;
+  constexpr int RS = 18;
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
   __shared__ double red[8];
   __shared__ double Tx[kExpTab];
-  __shared__ double Dl[4][3 * 64];
+  __shared__ __attribute__((aligned(16))) double Sl[4][64 * RS];
   exp_table_init(Tx);
   __syncthreads();
   const int h = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int g = lane >> 4, bl = lane & 15;
-  double bx[BPL], by[BPL], bz[BPL];
-  bool bv[BPL];
-#pragma unroll
-  for (int j = 0; j < BPL; ++j) {
-    const int b = bl + 16 * j;
-    bv[j] = b < B;
-    bx[j] = bv[j] ? bins[3 * b] : 0.0;
-    by[j] = bv[j] ? bins[3 * b + 1] : 0.0;
-    bz[j] = bv[j] ? bins[3 * b + 2] : 0.0;
-  }
-  const double Beps = (double)B * 1e-12;
   double* Rh = resp + (int64_t)h * n * B;
   const double* Dh = dirs + (int64_t)h * n * 3;
-  double* D = Dl[wv];
-  double logacc = 0.0, entq = 0.0, mxr = 0.0;
+  double* S = Sl[wv];
+  const double Beps = (double)B * 1e-12;
+  // Σ log Z is kept as a product of mantissas and a sum of exponents (frexp), one log at the end
+  double zm = 1.0, entq = 0.0, mxr = 0.0;
+  int ze = 0;
   const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
   double nd0, nd1, nd2;
   {
@@ -331,68 +326,94 @@ __global__ void __launch_bounds__(256) k_soft_assign(int64_t n, int B, int iters
   for (int it = 0; it < iters; ++it) {
     const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
     if (wbase >= n) break;  // wave-uniform
-    D[lane] = nd0; D[64 + lane] = nd1; D[128 + lane] = nd2;
+    const double d0 = nd0, d1 = nd1, d2 = nd2;
     {
       const int64_t p = wbase + 256 + lane;
       const int64_t pc = p < n ? p : n - 1;
       nd0 = Dh[3 * pc]; nd1 = Dh[3 * pc + 1]; nd2 = Dh[3 * pc + 2];
     }
-    lds_wave_sync();
-    double zst = 1.0;
-    int ist = 0;
-#pragma unroll 2
-    for (int s = 0; s < 16; ++s) {
-      const int pl = s * 4 + g;
-      const int64_t pt = wbase + pl;
-      const bool valid = pt < n;
-      const double d0 = D[pl], d1 = D[64 + pl], d2 = D[128 + pl];
-      double S[BPL];
-      double best = -1e308;
-      int bidx = 0x7fffffff;
+    const int64_t pt = wbase + lane;
+    const bool valid = pt < n;
+    // bin directions: wave-uniform scalar loads (constant address space), re-issued every
+    // iteration rather than hoisted into 288 registers
+    const __attribute__((address_space(4))) double* bp = (const __attribute__((address_space(4))) double*)bins;
+    asm volatile("" : "+s"(bp));
+    double ex[NB];
+    double best = -1e308, Z = 0.0, sl = 0.0;
+    int bidx = 0;
 #pragma unroll
-      for (int j = 0; j < BPL; ++j) {
-        S[j] = sim_nofma(d0, d1, d2, bx[j], by[j], bz[j]);
-        if (bv[j] && S[j] > best) { best = S[j]; bidx = bl + 16 * j; }
-      }
-      group16_argmax(best, bidx);  // lowest index on ties (integer contract only)
-      // softmax shift: the bound S <= 1 (unit directions) instead of the row max, so the exp
-      // chain does not wait on the argmax butterfly; R is the same ratio
-      double zl = 0.0, sl = 0.0, x[BPL], ex[BPL];
+    for (int j0 = 0; j0 < NB; j0 += 8) {
+      asm volatile("" : "+s"(bp));  // this group's scalar loads are issued here, not all up front
+      double x[8];
 #pragma unroll
-      for (int j = 0; j < BPL; ++j) x[j] = fma(S[j], inv_tau, -inv_tau);
-      exp_neg_n<BPL>(x, Tx, ex);  // unconditional: no branch around the table reads
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = j0 + jj;
+        const bool ok = FULL || j < B;  // wave-uniform
+        const double s = ok ? sim_nofma(d0, d1, d2, bp[3 * j], bp[3 * j + 1], bp[3 * j + 2]) : -4.0;
+        if (s > best) { best = s; bidx = j; }
+        x[jj] = fma(s, inv_tau, -inv_tau);
+      }
+      asm volatile("" : "+v"(best), "+v"(bidx));  // keep the argmax chain per group (no 48 live S)
+      double e8[8];
+      exp_neg_n<8>(x, Tx, e8);
 #pragma unroll
-      for (int j = 0; j < BPL; ++j) {
-        S[j] = bv[j] ? ex[j] : 0.0;
-        zl += S[j];
-        sl = fma(S[j], x[j], sl);
+      for (int jj = 0; jj < 8; ++jj) {
+        const int j = j0 + jj;
+        ex[j] = (FULL || j < B) ? e8[jj] : 0.0;
+        Z += ex[j];
+        sl = fma(ex[j], x[jj], sl);
       }
-      const double Z = group16_sum(zl);
-      const double rZ = recip(Z);
-      if (valid) {
-        double* dst = Rh + pt * B + bl;
-#pragma unroll
-        for (int j = 0; j < BPL; ++j) {
-          const double r = S[j] * rZ;
-          if (bv[j]) {
-            dst[16 * j] = r;
-            mxr = fmax(mxr, r);
-          }
-        }
-        entq = fma(sl, rZ, entq);  // Σ_lanes sl / Z = S/Z of the point (lane partials, summed at the end)
-        if (bl == 0) entq += Beps;
-      }
-      if (bl == s) {
-        zst = valid ? Z : 1.0;
-        ist = bidx;
-      }
+      asm volatile("" : "+v"(Z), "+v"(sl));  // accumulate now: the x of a group die here
     }
-    logacc += log(zst);
-    const int64_t pi = wbase + 4 * bl + g;  // the point whose scalars this lane stashed
-    if (bin_idx && pi < n) bin_idx[(int64_t)h * n + pi] = ist;
-    lds_wave_sync();
+    const double rZ = recip(Z);
+    double eb;
+    {
+      const double xb[1] = {fma(best, inv_tau, -inv_tau)};
+      double o1[1];
+      exp_neg_n<1>(xb, Tx, o1);  // = ex[bidx] bit for bit (same argument, same evaluation)
+      eb = o1[0];
+    }
+    if (valid) {
+      // entropy of the point: log Z - S/Z - B ε   (-Σ R log(R+ε) up to ≤ B·ε)
+      int e;
+      zm *= frexp(Z, &e);
+      ze += e;
+      entq += fma(sl, rZ, Beps);
+      mxr = fmax(mxr, eb * rZ);
+      if (bin_idx) bin_idx[(int64_t)h * n + pt] = bidx;
+    }
+#pragma unroll
+    for (int blk = 0; blk < BPL; ++blk) {
+#pragma unroll
+      for (int q = 0; q < 8; ++q)
+        *reinterpret_cast<dvec2*>(&S[lane * RS + 2 * q]) =
+            dvec2{ex[16 * blk + 2 * q] * rZ, ex[16 * blk + 2 * q + 1] * rZ};
+      lds_wave_sync();
+      if constexpr (FULL) {
+        // lane writes pieces (point 8m + lane/8, bins 16 blk + 2 (lane%8) +{0,1}); B == NB
+        const int i0 = lane >> 3, q = lane & 7;
+        double* rowp = Rh + (wbase + i0) * NB + 16 * blk + 2 * q;
+        const int64_t lim = n - wbase - i0;
+#pragma unroll
+        for (int m = 0; m < 8; ++m) {
+          const dvec2 v = *reinterpret_cast<const dvec2*>(&S[(i0 + 8 * m) * RS + 2 * q]);
+          if (8 * m < lim) *reinterpret_cast<dvec2*>(rowp + 8 * m * NB) = v;
+        }
+      } else {
+#pragma unroll
+        for (int m = 0; m < 16; ++m) {
+          const int e = lane + 64 * m, i = e >> 4, k = e & 15;
+          const double v = S[i * RS + k];
+          if (wbase + i < n && 16 * blk + k < B) Rh[(wbase + i) * B + 16 * blk + k] = v;
+        }
+      }
+      lds_wave_sync();
+    }
+    int e;
+    zm = frexp(zm, &e);  // renormalise once per 64 points: |log2 zm| stays below ~64
+    ze += e;
   }
-  // entropy over the chunk's points: Σ (log Z - S/Z - B ε)   (-Σ R log(R+ε) up to ≤ B·ε)
+  const double logacc = log(zm) + (double)ze * 0.69314718055994530942;
   const double es = wg_sum(logacc - entq, red);
   const double ms = wg_max(mxr, red);
   if (threadIdx.x == 0) {
@@ -987,9 +1008,16 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
   if (int rc = gc::scratch(ctx, sizeof(double) * 2 * blocks * H, &scr)) return rc;
   const double inv_tau = 1.0 / tau;
   dim3 grid((unsigned)blocks, H);
-#define GC_SA(BP)                                                                                     \
-  hipLaunchKernelGGL((k_soft_assign<BP>), grid, dim3(256), 0, ctx->stream, n, B, iters, d_dirs, d_bins, inv_tau, \
-                     d_resp_out, d_bin_index_out, (double*)scr)
+  const bool full = (B % 16) == 0 && ((uintptr_t)d_resp_out & 15) == 0;
+#define GC_SA(BP)                                                                                        \
+  do {                                                                                                   \
+    if (full)                                                                                            \
+      hipLaunchKernelGGL((k_soft_assign<BP, true>), grid, dim3(256), 0, ctx->stream, n, B, iters, d_dirs, d_bins, \
+                         inv_tau, d_resp_out, d_bin_index_out, (double*)scr);                            \
+    else                                                                                                 \
+      hipLaunchKernelGGL((k_soft_assign<BP, false>), grid, dim3(256), 0, ctx->stream, n, B, iters, d_dirs, d_bins, \
+                         inv_tau, d_resp_out, d_bin_index_out, (double*)scr);                            \
+  } while (0)
   switch (bpl_for(B)) { case 1: GC_SA(1); break; case 2: GC_SA(2); break; case 3: GC_SA(3); break; default: GC_SA(4); }
 #undef GC_SA
   GC_LAUNCH_CHECK(ctx);
