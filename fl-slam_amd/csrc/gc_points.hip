@@ -436,190 +436,146 @@ __global__ void k_soft_assign_finalize(const double* __restrict__ partial, int64
 }
 
 // ===================================================================== a6 moment partials
-// Shared epilogue: reduce BPL x NF accumulators over the 4 point-groups (xor 16/32) and the
-// 4 waves (LDS, fixed order), append the extras and write one partial record.
-template <int BPL, int NF>
-GC_DEV void write_partial_record(double (&acc)[BPL][NF], double ent, double mxr, double sumw,
-                                 double npts, int B, double* lds, double* rec) {
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, bl = lane & 15;
-#pragma unroll
-  for (int j = 0; j < BPL; ++j)
-#pragma unroll
-    for (int k = 0; k < NF; ++k) {
-      double v = acc[j][k];
-      v += __shfl_xor(v, 16, 64);
-      v += __shfl_xor(v, 32, 64);
-      acc[j][k] = v;
-    }
-  __syncthreads();
-  if (lane < 16) {
-#pragma unroll
-    for (int j = 0; j < BPL; ++j) {
-      const int b = bl + 16 * j;
-      if (b < B)
-#pragma unroll
-        for (int k = 0; k < NF; ++k) lds[(wv * B + b) * NF + k] = acc[j][k];
-    }
-  }
-  // extras
-  double e = wave_sum(ent), m = wave_max(mxr), s = wave_sum(sumw);
-  if (lane == 0) {
-    lds[4 * B * NF + wv * 3 + 0] = e;
-    lds[4 * B * NF + wv * 3 + 1] = m;
-    lds[4 * B * NF + wv * 3 + 2] = s;
-  }
-  __syncthreads();
-  for (int i = threadIdx.x; i < B * NF; i += kWG)
-    rec[i] = (lds[i] + lds[B * NF + i]) + (lds[2 * B * NF + i] + lds[3 * B * NF + i]);
-  if (threadIdx.x == 0) {
-    const double* ex = lds + 4 * B * NF;
-    rec[B * NF + 0] = (ex[0] + ex[3]) + (ex[6] + ex[9]);
-    rec[B * NF + 1] = fmax(fmax(ex[1], ex[4]), fmax(ex[7], ex[10]));
-    rec[B * NF + 2] = (ex[2] + ex[5]) + (ex[8] + ex[11]);
-    rec[B * NF + 3] = npts;
-  }
-}
-
-// Contract variant: responsibilities streamed from HBM. One wave per workgroup, grid (chunks, H),
-// chunk = iters*32 points. The moment sums Mom[b][k] = Σ_p R[p][b] F[p][k] run on the matrix
-// core: per 4-point step, bin tile j (16 bins) x feature tile t (16 features) is one
-// v_mfma_f64_16x16x4_f64 with A[bin][point] = R (lane (g, l): point g, bin 16j + l) and
-// B[point][feature] = F (lane (g, l): point g, feature 16t + l). Every (bin, feature) sum has
-// one owner lane, so the chunk record is written without a reduction. Responsibilities move
-// in 8-point blocks (8B contiguous doubles): each lane loads its 16-byte pieces of block k+2
-// into registers while block k is consumed from an LDS double buffer (register-staged ring,
-// ~6 KiB in flight per wave). Features are staged per 32 points in LDS; the raw inputs of the
-// next 32 points are prefetched into registers one sub-chunk ahead.
-template <int BPL, bool COV, int VW>
-__global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int iters,
-                                                        const double* __restrict__ pts,
-                                                        const double* __restrict__ covs,
-                                                        const double* __restrict__ w,
-                                                        const double* __restrict__ resp,
-                                                        const double* __restrict__ lam, double o0,
-                                                        double o1, double o2, double* partials) {
+// Contract variant: responsibilities streamed from HBM. grid (chunks, H), 4 waves per workgroup,
+// each wave owns `groups` consecutive 32-point groups of the chunk. The moment sums
+// Mom[b][k] = Σ_p R[p][b] F[p][k] run on the matrix core: per 4-point step s, bin tile j
+// (16 bins) x feature tile t (16 features) is one v_mfma_f64_16x16x4_f64 with
+// A[bin][point] = R (lane (g, l): point 4s + g, bin 16j + l) and B[point][feature] = F
+// (lane (g, l): point 4s + g, feature 16t + l). The A operand is loaded from HBM straight into
+// its lane (8 B per lane: four full 128-B row segments per load), a whole 32-point group ahead
+// of its use (register double buffer, ~12 KiB of responsibilities in flight per wave); no LDS
+// round trip. Features are computed lane = point for the next group and handed over through a
+// wave-private LDS slab (feature-major, stride 34: the B-operand reads are bank-conflict free).
+// NACC = 2: even and odd steps accumulate into separate tiles (2*BPL*NT independent MFMA chains)
+// added in the epilogue. The 4 waves are reduced in a fixed order into one record per chunk.
+constexpr int kMomFS = 34;
+template <int BPL, bool COV, bool LAM, int NACC>
+__global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, int groups,
+                                                           const double* __restrict__ pts,
+                                                           const double* __restrict__ covs,
+                                                           const double* __restrict__ w,
+                                                           const double* __restrict__ resp,
+                                                           const double* __restrict__ lam, double o0,
+                                                           double o1, double o2, double* partials) {
   constexpr int NF = COV ? NF_BASE + NF_COV : NF_BASE;
-  constexpr int NT = (NF + 15) / 16;      // feature tiles (zero-padded to 16 NT)
-  constexpr int FS = 33;
-  constexpr int BMAX = 16 * BPL;          // padded bins per row in the LDS block image
-  typedef double dvec2 __attribute__((ext_vector_type(2)));
-  using V = typename std::conditional<VW == 2, dvec2, double>::type;  // 16-byte pieces when B is even
-  constexpr int PL = (8 * BMAX / VW + 63) / 64;  // pieces per lane per block
-  __shared__ double F[16 * NT * FS];
-  __shared__ double RB[2][8 * BMAX];
+  constexpr int NT = (NF + 15) / 16;  // feature tiles (zero-padded to 16 NT)
+  extern __shared__ double lds[];
   const int h = blockIdx.y;
-  const int lane = threadIdx.x, g = lane >> 4, bl = lane & 15;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, bl = lane & 15;
+  double* F = lds + wv * (16 * NT * kMomFS);
   const double o[3] = {o0, o1, o2};
   const double* Rh = resp + (int64_t)h * n * B;
-  const int64_t nB = n * (int64_t)B;  // doubles of this hypothesis' rows
-  v4d acc[BPL][NT];
+  const int64_t wbeg = ((int64_t)blockIdx.x * 4 + wv) * groups * 32;
+  int64_t wend = wbeg + (int64_t)groups * 32;
+  wend = wend < n ? wend : n;
+  const int ng = wbeg < n ? (int)((wend - wbeg + 31) / 32) : 0;
+  v4d acc[NACC][BPL][NT];
 #pragma unroll
-  for (int j = 0; j < BPL; ++j)
+  for (int e = 0; e < NACC; ++e)
 #pragma unroll
-    for (int t = 0; t < NT; ++t) acc[j][t] = v4d{0.0, 0.0, 0.0, 0.0};
-  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 32;
-  int64_t cend = chunk0 + (int64_t)iters * 32;
-  cend = cend < n ? cend : n;
-  const int nsub = (int)((cend - chunk0 + 31) / 32);  // >= 1 (grid sized to n)
-
-  // block k covers points [chunk0 + 8k, +8): doubles [(chunk0 + 8k) * B, +8B), clamped in range
-  // (blocks past the end re-read valid rows; their points have zero features). LDS image: row i
-  // (point) at i*BMAX, so lane (., l) reads bin l + 16 j at a fixed stride.
-  int soff[PL];  // this lane's LDS offsets in a block image (-1: no piece)
+    for (int j = 0; j < BPL; ++j)
 #pragma unroll
-  for (int m = 0; m < PL; ++m) {
-    const int e = VW * (lane + 64 * m);
-    const int i = e / B, b = e - i * B;  // VW == 2 only for even B: a pair stays in one row
-    soff[m] = e < 8 * B ? i * BMAX + b : -1;
+      for (int t = 0; t < NT; ++t) acc[e][j][t] = v4d{0.0, 0.0, 0.0, 0.0};
+  // this lane's responsibility column offsets (bins 16 j + l), clamped into the row
+  int cb[BPL];
+  bool cv[BPL];
+#pragma unroll
+  for (int j = 0; j < BPL; ++j) {
+    cv[j] = bl + 16 * j < B;
+    cb[j] = cv[j] ? bl + 16 * j : 0;
   }
-#define GC_LOAD_BLK(R, K)                                                  \
-  {                                                                        \
-    const int64_t e0_ = (chunk0 + 8 * (int64_t)(K)) * B;                   \
-    _Pragma("unroll") for (int m = 0; m < PL; ++m) {                       \
-      int64_t e_ = e0_ + VW * (int64_t)(lane + 64 * m);                    \
-      e_ = e_ < nB - VW ? e_ : nB - VW;                                    \
-      R[m] = *reinterpret_cast<const V*>(Rh + e_);                         \
-    }                                                                      \
+  double Ra[8][BPL], Rb[8][BPL];  // group c (A operands of its 8 steps) and group c + 1
+#define GC_LOAD_R(RR, BASE)                                                     \
+  {                                                                             \
+    _Pragma("unroll") for (int s_ = 0; s_ < 8; ++s_) {                          \
+      int64_t p_ = (BASE) + 4 * s_ + g;                                         \
+      p_ = p_ < n ? p_ : n - 1;                                                 \
+      const double* row_ = Rh + p_ * B;                                         \
+      _Pragma("unroll") for (int j_ = 0; j_ < BPL; ++j_) RR[s_][j_] = row_[cb[j_]]; \
+    }                                                                           \
   }
-#define GC_STORE_BLK(R, SLOT)                                              \
-  {                                                                        \
-    _Pragma("unroll") for (int m = 0; m < PL; ++m) if (soff[m] >= 0)       \
-        *reinterpret_cast<V*>(&RB[SLOT][soff[m]]) = R[m];                  \
-  }
-  // raw inputs of one 32-point sub-chunk (point = lane & 31), loaded by every lane, unconditionally
-  double rp[3], rc[9], rw;
-#define GC_LOAD_RAW(BASE)                                                  \
-  {                                                                        \
-    const int64_t pt_ = (BASE) + (lane & 31);                              \
-    const bool ok_ = pt_ < n;                                              \
-    const int64_t row_ = (int64_t)h * n + (ok_ ? pt_ : 0);                 \
-    rw = w[row_] * (lam ? lam[row_] : 1.0);                                \
-    rw = ok_ ? rw : 0.0;                                                   \
+  // raw inputs of one 32-point group (point = lane & 31), loaded by every lane into registers and
+  // consumed branch-free a group later (no load is sunk into a lane-conditional block)
+  double rp[3], rc[9], rw, rl;
+  bool rok;
+#define GC_LOAD_RAW(BASE)                                                       \
+  {                                                                             \
+    const int64_t pt_ = (BASE) + (lane & 31);                                   \
+    rok = pt_ < wend;                                                           \
+    const int64_t row_ = (int64_t)h * n + (pt_ < n ? pt_ : n - 1);              \
+    rw = w[row_];                                                               \
+    if constexpr (LAM) rl = lam[row_];                                          \
     rp[0] = pts[3 * row_]; rp[1] = pts[3 * row_ + 1]; rp[2] = pts[3 * row_ + 2]; \
-    if constexpr (COV) {                                                   \
+    if constexpr (COV) {                                                        \
       _Pragma("unroll") for (int k_ = 0; k_ < 9; ++k_) rc[k_] = covs[9 * row_ + k_]; \
-    }                                                                      \
+    }                                                                           \
   }
-#define GC_CONSUME(SLOT, S0)                                               \
-  {                                                                        \
-    _Pragma("unroll") for (int s2 = 0; s2 < 2; ++s2) {                     \
-      const double* rs_ = RB[SLOT] + (4 * s2 + g) * BMAX + bl;             \
-      const int pl_ = (S0) + 4 * s2 + g;                                   \
-      double fb_[NT];                                                      \
-      _Pragma("unroll") for (int t = 0; t < NT; ++t) fb_[t] = F[(16 * t + bl) * FS + pl_]; \
-      _Pragma("unroll") for (int j = 0; j < BPL; ++j) {                    \
-        const double ra_ = rs_[16 * j];                                    \
-        _Pragma("unroll") for (int t = 0; t < NT; ++t)                     \
-          acc[j][t] = __builtin_amdgcn_mfma_f64_16x16x4f64(ra_, fb_[t], acc[j][t], 0, 0, 0); \
-      }                                                                    \
-    }                                                                      \
+  // lanes 0..31 write features 0..15 of their point, lanes 32..63 features 16..31
+  // (pp[11 12 22], cov x w, zero padding)
+#define GC_FEATURES()                                                           \
+  {                                                                             \
+    lds_wave_sync(); /* the previous group's B-operand reads are done */        \
+    double wl_ = LAM ? rw * rl : rw;                                            \
+    wl_ = rok ? wl_ : 0.0;                                                      \
+    double d_[3], f_[NF_BASE];                                                  \
+    direction(rp, o, 1e-12, d_);                                                \
+    point_features(rp, d_, wl_, f_);                                            \
+    const bool lo_ = lane < 32;                                                 \
+    double* Fl_ = F + (lo_ ? 0 : 16 * kMomFS) + (lane & 31);                    \
+    _Pragma("unroll") for (int k_ = 0; k_ < 16; ++k_) {                         \
+      const int kk_ = 16 + k_;                                                  \
+      double hi_ = 0.0;                                                         \
+      if (kk_ < NF_BASE) hi_ = f_[kk_ < NF_BASE ? kk_ : 0];                      \
+      else if (COV && kk_ < NF) hi_ = wl_ * rc[kk_ - NF_BASE < 9 ? kk_ - NF_BASE : 0]; \
+      Fl_[k_ * kMomFS] = lo_ ? f_[k_] : hi_;                                    \
+    }                                                                           \
+    lds_wave_sync();                                                            \
   }
-  // register-staged ring: block k is loaded into register set (k & 3) three blocks ahead and
-  // stored to LDS slot (k & 1) one block ahead of its consumption (~9 KiB in flight per wave)
-  V r0[PL], r1[PL], r2[PL], r3[PL];
-  GC_LOAD_RAW(chunk0)
-  GC_LOAD_BLK(r0, 0)
-  GC_LOAD_BLK(r1, 1)
-  GC_LOAD_BLK(r2, 2)
-  GC_STORE_BLK(r0, 0)
-  for (int c = 0; c < nsub; ++c) {
-    lds_wave_sync();  // previous sub-chunk's feature reads are done
-    if (lane < 32) {
-      double d[3], f[NF_BASE];
-      direction(rp, o, 1e-12, d);
-      point_features(rp, d, rw, f);
-#pragma unroll
-      for (int kk = 0; kk < NF_BASE; ++kk) F[kk * FS + lane] = f[kk];
-    } else {
-      const int pl = lane - 32;
-      if constexpr (COV) {
-#pragma unroll
-        for (int kk = 0; kk < NF_COV; ++kk) F[(NF_BASE + kk) * FS + pl] = rw * rc[kk];
-      }
-#pragma unroll
-      for (int kk = NF; kk < 16 * NT; ++kk) F[kk * FS + pl] = 0.0;
+#define GC_CONSUME(RR)                                                          \
+  {                                                                             \
+    _Pragma("unroll") for (int s_ = 0; s_ < 8; ++s_) {                          \
+      double fb_[NT];                                                           \
+      _Pragma("unroll") for (int t_ = 0; t_ < NT; ++t_) fb_[t_] = F[(16 * t_ + bl) * kMomFS + 4 * s_ + g]; \
+      _Pragma("unroll") for (int j_ = 0; j_ < BPL; ++j_) {                      \
+        const double ra_ = cv[j_] ? RR[s_][j_] : 0.0;                           \
+        _Pragma("unroll") for (int t_ = 0; t_ < NT; ++t_)                       \
+          acc[s_ % NACC][j_][t_] = __builtin_amdgcn_mfma_f64_16x16x4f64(ra_, fb_[t_], acc[s_ % NACC][j_][t_], 0, 0, 0); \
+      }                                                                         \
+    }                                                                           \
+  }
+  if (ng > 0) {
+    // loads past the wave's range are issued unconditionally (clamped rows, zero weights) so the
+    // body is straight-line and every wait is a counted vmcnt, not a drain
+    GC_LOAD_RAW(wbeg)
+    __builtin_amdgcn_sched_barrier(0);
+    GC_LOAD_R(Ra, wbeg)
+    __builtin_amdgcn_sched_barrier(0);
+    for (int c = 0; c < ng; c += 2) {
+      GC_FEATURES()
+      const int64_t b1 = wbeg + 32 * (int64_t)(c + 1);
+      GC_LOAD_RAW(b1)  // raw first: the next features wait for these, not for the R stream
+      __builtin_amdgcn_sched_barrier(0);
+      GC_LOAD_R(Rb, b1)
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch ahead of the consumption
+      GC_CONSUME(Ra)
+      __builtin_amdgcn_sched_barrier(0);
+      GC_FEATURES()
+      const int64_t b2 = wbeg + 32 * (int64_t)(c + 2);
+      GC_LOAD_RAW(b2)
+      __builtin_amdgcn_sched_barrier(0);
+      GC_LOAD_R(Ra, b2)
+      __builtin_amdgcn_sched_barrier(0);
+      GC_CONSUME(Rb)
+      __builtin_amdgcn_sched_barrier(0);
     }
-    GC_LOAD_RAW(chunk0 + 32 * (int64_t)(c + 1))
-    const int k0 = 4 * c;
-#define GC_RING_STEP(RNEXT3, RNEXT1, KB)                                   \
-    GC_LOAD_BLK(RNEXT3, k0 + (KB) + 3)                                     \
-    lds_wave_sync();                                                       \
-    GC_CONSUME((KB) & 1, 8 * (KB))                                         \
-    lds_wave_sync();                                                       \
-    GC_STORE_BLK(RNEXT1, ((KB) + 1) & 1)
-    GC_RING_STEP(r3, r1, 0)
-    GC_RING_STEP(r0, r2, 1)
-    GC_RING_STEP(r1, r3, 2)
-    GC_RING_STEP(r2, r0, 3)
-#undef GC_RING_STEP
   }
-#undef GC_LOAD_BLK
-#undef GC_STORE_BLK
-#undef GC_CONSUME
+#undef GC_LOAD_R
 #undef GC_LOAD_RAW
-  const int64_t npts = cend - chunk0;
-  const int RL = B * NF + REC_EXTRA;
-  double* rec = partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL;
+#undef GC_FEATURES
+#undef GC_CONSUME
+  // epilogue: even + odd tiles, then the 4 waves in a fixed order (LDS reused)
+  __syncthreads();
+  double* red = lds;  // [4][B][NF]
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
 #pragma unroll
@@ -627,9 +583,16 @@ __global__ void __launch_bounds__(64) k_moment_partials(int64_t n, int B, int it
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
         const int b = 16 * j + g + 4 * r, k = 16 * t + bl;  // D[row g + 4r][col l]
-        if (b < B && k < NF) rec[b * NF + k] = acc[j][t][r];
+        if (b < B && k < NF) red[(wv * B + b) * NF + k] = NACC == 2 ? acc[0][j][t][r] + acc[NACC - 1][j][t][r] : acc[0][j][t][r];
       }
-  if (lane < REC_EXTRA) rec[B * NF + lane] = lane == 3 ? (double)npts : 0.0;
+  __syncthreads();
+  int64_t npts = n - (int64_t)blockIdx.x * 4 * groups * 32;
+  npts = npts < 0 ? 0 : (npts > (int64_t)4 * groups * 32 ? (int64_t)4 * groups * 32 : npts);
+  const int RL = B * NF + REC_EXTRA;
+  double* rec = partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL;
+  for (int i = threadIdx.x; i < B * NF; i += kWG)
+    rec[i] = (red[i] + red[B * NF + i]) + (red[2 * B * NF + i] + red[3 * B * NF + i]);
+  if (threadIdx.x < REC_EXTRA) rec[B * NF + threadIdx.x] = threadIdx.x == 3 ? (double)npts : 0.0;
 }
 
 // MFMA epilogue: reduce per-lane tiles over the 4 waves (LDS, fixed order) into one partial
@@ -1046,9 +1009,10 @@ int32_t gc_scan_bin_moment_match(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, c
   GC_CHECK_ARG(ctx, d_points && d_w && d_resp && d_stats_out && d_cert_out, "NULL buffer");
   double o[3] = {0.0, 0.0, 0.0};
   if (h_origin3) { o[0] = h_origin3[0]; o[1] = h_origin3[1]; o[2] = h_origin3[2]; }
-  int iters = 32;  // chunk = iters * 32 points, one wave per chunk
-  while (iters > 1 && ((n + iters * 32 - 1) / (iters * 32)) * (int64_t)H < 16384) iters >>= 1;
-  const int64_t chunks = (n + iters * 32 - 1) / (iters * 32);
+  // chunk = 4 waves x groups x 32 points; aim for >= ~8 workgroups per CU over the grid
+  int groups = 16;
+  while (groups > 1 && ((n + 128 * groups - 1) / (128 * groups)) * (int64_t)H < 4096) groups >>= 1;
+  const int64_t chunks = (n + 128 * groups - 1) / (128 * groups);
   const bool cov = d_covs != nullptr;
   const int NF = cov ? NF_BASE + NF_COV : NF_BASE;
   const int RL = B * NF + REC_EXTRA;
@@ -1056,15 +1020,16 @@ int32_t gc_scan_bin_moment_match(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, c
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
   dim3 grid((unsigned)chunks, H);
   const int bpl = bpl_for(B);
-  const int vw = ((B & 1) == 0 && ((uintptr_t)d_resp & 15) == 0) ? 2 : 1;
-#define GC_MOM(BP, CV)                                                                                        \
-  do {                                                                                                        \
-    if (vw == 2)                                                                                              \
-      hipLaunchKernelGGL((k_moment_partials<BP, CV, 2>), grid, dim3(64), 0, ctx->stream, n, B, iters, d_points, \
-                         d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr);                      \
-    else                                                                                                      \
-      hipLaunchKernelGGL((k_moment_partials<BP, CV, 1>), grid, dim3(64), 0, ctx->stream, n, B, iters, d_points, \
-                         d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr);                      \
+  const int NT = (NF + 15) / 16;
+  const size_t sh = sizeof(double) * std::max<size_t>((size_t)4 * 16 * NT * kMomFS, (size_t)4 * B * NF);
+#define GC_MOM(BP, CV)                                                                                          \
+  do {                                                                                                          \
+    if (d_lambda)                                                                                               \
+      hipLaunchKernelGGL((k_moment_partials<BP, CV, true, 1>), grid, dim3(256), sh, ctx->stream, n, B, groups,  \
+                         d_points, d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr);             \
+    else                                                                                                        \
+      hipLaunchKernelGGL((k_moment_partials<BP, CV, false, 1>), grid, dim3(256), sh, ctx->stream, n, B, groups, \
+                         d_points, d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr);             \
   } while (0)
   if (cov) {
     switch (bpl) { case 1: GC_MOM(1, true); break; case 2: GC_MOM(2, true); break; case 3: GC_MOM(3, true); break; default: GC_MOM(4, true); }
