@@ -34,8 +34,9 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=50,
+                    help="untimed steps first: the clocks ramp over the first ~30 ms of sustained f64 load")
     ap.add_argument("--hyps", type=int, default=256, help="total hypotheses per scan (strong scaling)")
     ap.add_argument("--n-az", type=int, default=4096, help="azimuth steps (x16 rings = points)")
     ap.add_argument("--scans", type=int, default=4, help="distinct resident scans cycled through")
@@ -43,6 +44,9 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--cpu-budget-s", type=float, default=15.0)
     ap.add_argument("--no-map", action="store_true", help="skip the C5 PrimitiveMap fuse leg")
+    ap.add_argument("--roofline-only", action="store_true",
+                    help="run only the contract-pair roofline leg (PMC traffic passes, tools/pmc_traffic.sh)")
+    ap.add_argument("--roofline-reps", type=int, default=10)
     return ap.parse_args()
 
 
@@ -114,6 +118,20 @@ def main():
 
     ctx = _abi.Context(dist.local_rank)
     H_total = args.hyps
+    if args.roofline_only:
+        from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
+        from gcslam.ops.binning import create_fibonacci_atlas
+        from gcslam.synth import make_scan
+        s0 = make_scan(1, n_az=args.n_az)
+        rng = np.random.default_rng(5)
+        xi = np.zeros((H_total, 6)); xi[:, 0] = 0.1 + rng.normal(0, 0.005, H_total)
+        xi[:, 5] = 0.03 + rng.normal(0, 0.002, H_total)
+        d0 = {k: _abi.DeviceArray.from_host(ctx, s0[k]) for k in ("points", "timestamps", "weights")}
+        dbins = _abi.DeviceArray.from_host(ctx, create_fibonacci_atlas(GC_B_BINS).dirs)
+        r = roofline_leg(ctx, _abi, s0, d0, xi, dbins, GC_B_BINS, s0["points"].shape[0], H_total,
+                         np.asarray(T_BASE_LIDAR[:3]), reps=args.roofline_reps, warm=2)
+        print(json.dumps({"roofline": r}), flush=True)
+        return
     B = GC_B_BINS
     origin = np.asarray(T_BASE_LIDAR[:3])
     bins = create_fibonacci_atlas(B).dirs
@@ -184,7 +202,7 @@ def main():
         xi = np.zeros((H, 6)); xi[:, 0] = 0.1 + rng.normal(0, 0.005, H); xi[:, 5] = 0.03 + rng.normal(0, 0.002, H)
         d0 = {k: _abi.DeviceArray.from_host(ctx, scans[0][k]) for k in ("points", "timestamps", "weights")}
         dbins = _abi.DeviceArray.from_host(ctx, bins)
-        out["roofline"] = roofline_leg(ctx, _abi, scans[0], d0, xi, dbins, B, n, H, origin)
+        out["roofline"] = roofline_leg(ctx, _abi, scans[0], d0, xi, dbins, B, n, H, origin, reps=args.roofline_reps)
     if dist.rank == 0 and not args.no_map:
         out["c5_map_fuse"] = map_fuse_leg(ctx, _abi)
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
@@ -193,7 +211,20 @@ def main():
         print(json.dumps(out), flush=True)
 
 
-def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=3):
+def measured_traffic(H, n, B):
+    """HBM bytes per launch of the contract pair from the committed rocprofv3 PMC summary
+    (tools/pmc_traffic.sh; FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE), when it
+    was collected at this exact shape; None otherwise."""
+    f = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
+    if not os.path.exists(f):
+        return None
+    t = json.load(open(f))
+    if (t.get("H"), t.get("n"), t.get("B")) != (H, n, B):
+        return None
+    return t
+
+
+def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=3):
     """BinSoftAssign + ScanBinMomentMatch contract kernels over H hypotheses, HBM-bound."""
     from gcslam.constants import GC_TAU_SOFT_ASSIGN
     dxi = _abi.DeviceArray.from_host(ctx, xi)
@@ -210,7 +241,7 @@ def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=3):
     st = _abi.DeviceArray(ctx, (H, B, 38)); ce = _abi.DeviceArray(ctx, (H, 8))
     ev = [_abi.Event(ctx) for _ in range(3)]
     t_sa, t_mm = [], []
-    for r in range(reps + 1):
+    for r in range(reps + warm):
         ev[0].record()
         _abi.call("gc_bin_soft_assign", ctx.handle, H, n, B, dirs.ptr, dbins.ptr, GC_TAU_SOFT_ASSIGN, resp.ptr,
                   idx.ptr, sac.ptr, ctx=ctx)
@@ -219,18 +250,20 @@ def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=3):
                   1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
         ev[2].record()
         ctx.sync()
-        if r > 0:
+        if r >= warm:
             t_sa.append(ev[0].elapsed_ms(ev[1]))
             t_mm.append(ev[1].elapsed_ms(ev[2]))
     ms_sa, ms_mm = float(np.mean(t_sa)), float(np.mean(t_mm))
     b_sa, b_mm = H * bytes_soft_assign(n, B), H * bytes_moment_match(n, B)
     ach = (b_sa + b_mm) / ((ms_sa + ms_mm) * 1e-3) / 1e9
+    tr = measured_traffic(H, n, B)
     return {"bound": "hbm", "achieved": ach, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": ach / HBM_PEAK_GBS,
-            "traffic": None,
+            "traffic": tr["pair_bytes"] if tr else None,
+            "traffic_source": tr["source"] if tr else None,
             "kernel": "BinSoftAssign+ScanBinMomentMatch (k_soft_assign + k_moment_partials/k_bins_finalize)",
             "per_kernel": {"soft_assign": {"ms": ms_sa, "bytes": b_sa, "GB/s": b_sa / (ms_sa * 1e-3) / 1e9},
                            "moment_match": {"ms": ms_mm, "bytes": b_mm, "GB/s": b_mm / (ms_mm * 1e-3) / 1e9}},
-            "hypotheses": H}
+            "hypotheses": H, "points": n, "bins": B}
 
 
 def map_fuse_leg(ctx, _abi, m_slots=1 << 20, rows=1 << 17, reps=5):

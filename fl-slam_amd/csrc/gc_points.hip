@@ -295,8 +295,11 @@ __global__ void k_point_dirs(int64_t rows, const double* __restrict__ pts, doubl
 // is transposed through a wave-private LDS slab one 16-bin block at a time (row stride 18
 // doubles: the 8 lanes of a ds_write_b128 group hit disjoint banks) and leaves as contiguous
 // 128-B row segments, 16 B per lane (FULL: B == 16*BPL) or 8 B per lane (ragged B).
+#ifndef GC_SA_OCC
+#define GC_SA_OCC 3  // waves per SIMD the register budget is sized for (tuning knob, probes)
+#endif
 template <int BPL, bool FULL>
-__global__ void __launch_bounds__(256, 3) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
+__global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
                                                      const double* __restrict__ bins, double inv_tau,
                                                      double* resp, int32_t* bin_idx, double* partial) {
   constexpr int NB = 16 * BPL;
@@ -317,21 +320,26 @@ __global__ void __launch_bounds__(256, 3) k_soft_assign(int64_t n, int B, int it
   double zm = 1.0, entq = 0.0, mxr = 0.0;
   int ze = 0;
   const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
+  // directions of the wave's next 64 points: 192 contiguous doubles, three fully coalesced 512-B
+  // loads (8 B per lane, any alignment), handed to lane = point through the LDS slab
+  const int64_t nd = 3 * n;
   double nd0, nd1, nd2;
-  {
-    const int64_t p = chunk0 + wv * 64 + lane;
-    const int64_t pc = p < n ? p : n - 1;
-    nd0 = Dh[3 * pc]; nd1 = Dh[3 * pc + 1]; nd2 = Dh[3 * pc + 2];
+#define GC_LOAD_DIRS(WB)                                             \
+  {                                                                  \
+    const int64_t e0_ = 3 * (WB) + lane;                             \
+    nd0 = Dh[e0_ < nd ? e0_ : nd - 1];                               \
+    nd1 = Dh[e0_ + 64 < nd ? e0_ + 64 : nd - 1];                     \
+    nd2 = Dh[e0_ + 128 < nd ? e0_ + 128 : nd - 1];                   \
   }
+  GC_LOAD_DIRS(chunk0 + wv * 64)
   for (int it = 0; it < iters; ++it) {
     const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
     if (wbase >= n) break;  // wave-uniform
-    const double d0 = nd0, d1 = nd1, d2 = nd2;
-    {
-      const int64_t p = wbase + 256 + lane;
-      const int64_t pc = p < n ? p : n - 1;
-      nd0 = Dh[3 * pc]; nd1 = Dh[3 * pc + 1]; nd2 = Dh[3 * pc + 2];
-    }
+    S[lane] = nd0; S[64 + lane] = nd1; S[128 + lane] = nd2;
+    lds_wave_sync();
+    const double d0 = S[3 * lane], d1 = S[3 * lane + 1], d2 = S[3 * lane + 2];
+    lds_wave_sync();
+    GC_LOAD_DIRS(wbase + 256)
     const int64_t pt = wbase + lane;
     const bool valid = pt < n;
     // bin directions: wave-uniform scalar loads (constant address space), re-issued every
@@ -414,6 +422,7 @@ __global__ void __launch_bounds__(256, 3) k_soft_assign(int64_t n, int B, int it
     ze += e;
   }
   const double logacc = log(zm) + (double)ze * 0.69314718055994530942;
+#undef GC_LOAD_DIRS
   const double es = wg_sum(logacc - entq, red);
   const double ms = wg_max(mxr, red);
   if (threadIdx.x == 0) {
@@ -489,7 +498,7 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
   {                                                                             \
     _Pragma("unroll") for (int s_ = 0; s_ < 8; ++s_) {                          \
       int64_t p_ = (BASE) + 4 * s_ + g;                                         \
-      p_ = p_ < n ? p_ : n - 1;                                                 \
+      p_ = p_ < wend ? p_ : wend - 1; /* prefetch past the range re-reads a line */ \
       const double* row_ = Rh + p_ * B;                                         \
       _Pragma("unroll") for (int j_ = 0; j_ < BPL; ++j_) RR[s_][j_] = row_[cb[j_]]; \
     }                                                                           \
@@ -502,7 +511,7 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
   {                                                                             \
     const int64_t pt_ = (BASE) + (lane & 31);                                   \
     rok = pt_ < wend;                                                           \
-    const int64_t row_ = (int64_t)h * n + (pt_ < n ? pt_ : n - 1);              \
+    const int64_t row_ = (int64_t)h * n + (rok ? pt_ : wend - 1);               \
     rw = w[row_];                                                               \
     if constexpr (LAM) rl = lam[row_];                                          \
     rp[0] = pts[3 * row_]; rp[1] = pts[3 * row_ + 1]; rp[2] = pts[3 * row_ + 2]; \
@@ -652,8 +661,17 @@ GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL
 // is one LDS read per lane (B operand). The matrix core accumulates features 0..15 while the
 // VALU does the exp/softmax; features 16..18 stay on the VALU. Responsibilities never leave
 // registers.
+// feature slab row stride: the B-operand read F[l][4s + g] of the 32 lanes of a ds_read_b64
+// group lands on 32 distinct bank pairs (4 l + 2 g + 8 s mod 64)
+constexpr int kFusedFS = 66;
+#ifndef GC_FUSED_OCC
+#define GC_FUSED_OCC 2  // waves per SIMD the register budget is sized for (tuning knob, probes)
+#endif
+#ifndef GC_FUSED_NACC
+#define GC_FUSED_NACC 2  // MFMA accumulator sets (even / odd steps)
+#endif
 template <int BPL>
-__global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int iters,
+__global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap, int B, int iters,
                                                     const double* __restrict__ pts_raw,
                                                     const double* __restrict__ t_raw,
                                                     const double* __restrict__ w_raw,
@@ -669,7 +687,7 @@ __global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int
   const int h = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, bl = lane & 15;
-  double* F = lds + wv * (NS * 64);
+  double* F = lds + wv * (NS * kFusedFS);
   const double o[3] = {o0, o1, o2};
   double xr[6];
 #pragma unroll
@@ -679,7 +697,7 @@ __global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int
   const int64_t stride = (int64_t)bscal[6];
   const double denom = fmax(t1 - t0, 1e-12);
   const double sig = 0.1 * denom;
-  double* Tx = lds + 4 * 64 * NS;
+  double* Tx = lds + 4 * kFusedFS * NS;
   double* Lb = Tx + kExpTab;  // bin directions pre-scaled by 1/τ (x, y, z rows of 64)
   exp_table_init(Tx);
   if (threadIdx.x < 64) {
@@ -689,11 +707,13 @@ __global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int
     Lb[128 + b] = b < B ? bins[3 * b + 2] * inv_tau : 0.0;
   }
   __syncthreads();
-  v4d acc4[BPL];
+  constexpr int NACC = GC_FUSED_NACC;
+  v4d acc4[NACC][BPL];  // NACC = 2: even / odd steps, 2*BPL independent MFMA accumulation chains
   double accx[BPL][NX];
 #pragma unroll
   for (int j = 0; j < BPL; ++j) {
-    acc4[j] = v4d{0.0, 0.0, 0.0, 0.0};
+    acc4[0][j] = v4d{0.0, 0.0, 0.0, 0.0};
+    acc4[NACC - 1][j] = v4d{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int t = 0; t < NX; ++t) accx[j][t] = 0.0;
   }
@@ -720,20 +740,20 @@ __global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int
       point_features(q, d, wd, f);
       sumw += wd;
 #pragma unroll
-      for (int k = 0; k < NF; ++k) F[k * 64 + lane] = f[k];
-      F[(NF + 0) * 64 + lane] = d[0];
-      F[(NF + 1) * 64 + lane] = d[1];
-      F[(NF + 2) * 64 + lane] = d[2];
-      F[(NF + 3) * 64 + lane] = inr ? 1.0 : 0.0;
+      for (int k = 0; k < NF; ++k) F[k * kFusedFS + lane] = f[k];
+      F[(NF + 0) * kFusedFS + lane] = d[0];
+      F[(NF + 1) * kFusedFS + lane] = d[1];
+      F[(NF + 2) * kFusedFS + lane] = d[2];
+      F[(NF + 3) * kFusedFS + lane] = inr ? 1.0 : 0.0;
     }
     lds_wave_sync();
     double zst = 1.0;
-#pragma unroll 1
+#pragma unroll 2
     for (int s = 0; s < 16; ++s) {
       const int pl = s * 4 + g;
-      const double d0 = F[(NF + 0) * 64 + pl], d1 = F[(NF + 1) * 64 + pl], d2 = F[(NF + 2) * 64 + pl];
-      const bool valid = F[(NF + 3) * 64 + pl] != 0.0;
-      const double fb = F[bl * 64 + pl];  // MFMA B operand: feature bl of point 4s + g
+      const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
+      const bool valid = F[(NF + 3) * kFusedFS + pl] != 0.0;
+      const double fb = F[bl * kFusedFS + pl];  // MFMA B operand: feature bl of point 4s + g
       double e[BPL], x[BPL], ex[BPL], zl = 0.0, sl = 0.0, em = 0.0;
 #pragma unroll
       for (int j = 0; j < BPL; ++j) {
@@ -758,11 +778,11 @@ __global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int
 #pragma unroll
       for (int j = 0; j < BPL; ++j) {
         const double r = e[j] * rZ;
-        acc4[j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r, fb, acc4[j], 0, 0, 0);
+        acc4[s % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r, fb, acc4[s % NACC][j], 0, 0, 0);
       }
 #pragma unroll
       for (int t = 0; t < NX; ++t) {
-        const double fk = F[(16 + t) * 64 + pl];
+        const double fk = F[(16 + t) * kFusedFS + pl];
 #pragma unroll
         for (int j = 0; j < BPL; ++j) accx[j][t] = fma(e[j] * rZ, fk, accx[j][t]);
       }
@@ -776,7 +796,10 @@ __global__ void __launch_bounds__(256, 3) k_bins_fused(int64_t n_cap, int B, int
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
   const double ent = logacc - entq - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
   const int RL = B * NF + REC_EXTRA;
-  write_partial_record_mfma<BPL, NX>(acc4, accx, ent, mxr, sumw, (double)npts, B, lds,
+#pragma unroll
+  for (int j = 0; j < BPL; ++j)
+    if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
+  write_partial_record_mfma<BPL, NX>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds,
                                      partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
 }
 
@@ -1059,7 +1082,7 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const int RL = B * NF + REC_EXTRA;
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
-  const size_t sh = sizeof(double) * std::max<size_t>(4 * 64 * (NF + 4) + kExpTab + 192, 4 * (size_t)B * NF + 12);
+  const size_t sh = sizeof(double) * std::max<size_t>(4 * kFusedFS * (NF + 4) + kExpTab + 192, 4 * (size_t)B * NF + 12);
   dim3 grid((unsigned)chunks, H);
   const double inv_tau = 1.0 / tau;
 #define GC_FUSED(BP)                                                                                     \

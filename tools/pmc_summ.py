@@ -13,7 +13,7 @@ for f in glob.glob(os.path.join(root, "**", "*counter_collection.csv"), recursiv
             k = r["Kernel_Name"].split("(")[0][:60]
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for k, cs in sorted(acc.items()):
-    if not any(s in k for s in ("soft_assign", "moment_partials", "bins_fused", "evidence", "predict", "combine", "finalize")):
+    if not any(s in k for s in ("soft_assign", "moment_partials", "bins_fused", "evidence", "predict", "combine", "finalize", "k_read", "k_store")):
         continue
     print(k)
     for c, v in sorted(cs.items()):

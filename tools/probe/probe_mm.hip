@@ -65,5 +65,23 @@ int main(int argc, char** argv) {
     char nm[64]; snprintf(nm, 64, "k_moment_partials groups=%d", groups);
     timeit(nm, [&] { hipLaunchKernelGGL((gc::k_moment_partials<3, true, true, 1>), dim3(chunks, H), dim3(256), sh, 0, n, B, groups, pts, covs, w, resp, lam, 0.1, 0.2, 0.3, part); });
   }
+  if (argc > 2) {  // interleave with the soft-assign contract kernel, as in the bench's roofline leg
+    double *dirs, *bins, *sap; int32_t* idx;
+    hipMalloc(&dirs, sizeof(double) * H * n * 3); hipMalloc(&bins, sizeof(double) * 3 * B);
+    hipMalloc(&sap, sizeof(double) * 2 * 64 * H); hipMalloc(&idx, sizeof(int32_t) * H * n);
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, dirs, (int64_t)H * n * 3, 7, -0.577, 0.577);
+    hipLaunchKernelGGL(k_fill, dim3(1), dim3(256), 0, 0, bins, (int64_t)3 * B, 8, -0.577, 0.577);
+    hipEvent_t ev[3]; for (auto& e : ev) hipEventCreate(&e);
+    const size_t sh = sizeof(double) * std::max<size_t>((size_t)4 * 32 * gc::kMomFS, (size_t)4 * B * 28);
+    for (int r = 0; r < 4; ++r) {
+      hipEventRecord(ev[0]);
+      hipLaunchKernelGGL((gc::k_soft_assign<3, true>), dim3(64, H), dim3(256), 0, 0, n, B, 4, dirs, bins, 10.0, resp, idx, sap);
+      hipEventRecord(ev[1]);
+      hipLaunchKernelGGL((gc::k_moment_partials<3, true, true, 1>), dim3(32, H), dim3(256), sh, 0, n, B, 16, pts, covs, w, resp, lam, 0.1, 0.2, 0.3, part);
+      hipEventRecord(ev[2]); hipEventSynchronize(ev[2]);
+      float a, b; hipEventElapsedTime(&a, ev[0], ev[1]); hipEventElapsedTime(&b, ev[1], ev[2]);
+      printf("interleaved: soft_assign %.3f ms, moment_partials %.3f ms\n", a, b);
+    }
+  }
   return 0;
 }
