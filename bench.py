@@ -114,7 +114,7 @@ def main():
     from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
     from gcslam.ops.binning import create_fibonacci_atlas
     from gcslam.pipeline import BatchedScanPipeline, PipelineConfig, iw_meas_prior, iw_process_prior
-    from gcslam.synth import make_hypotheses, make_io_evidence, make_scan
+    from gcslam.synth import make_hypotheses, make_scan
 
     ctx = _abi.Context(dist.local_rank)
     H_total = args.hyps
@@ -142,10 +142,9 @@ def main():
     h0, h1 = pipe.h0, pipe.h1
     H = h1 - h0
     hy = make_hypotheses(H_total)
-    Lio, hio, cio = make_io_evidence(H_total)
     pipe.set_beliefs(hy["X_anchor"][h0:h1], hy["z_lin"][h0:h1], hy["L"][h0:h1], hy["h"][h0:h1], hy["stamp"][h0:h1])
     pipe.set_weights(hy["weights"])
-    pipe.set_io_evidence(Lio[h0:h1], hio[h0:h1], cio[h0:h1])
+    pipe.set_io_mode(True)  # IMU/odom branch evaluated on the device from each scan's odometry + IMU
     pipe.set_iw(*iw_process_prior(), *iw_meas_prior())
     pipe.set_map(warmup_map_record(ctx, _abi, make_scan(0, n_az=args.n_az), n, B, bins, origin))
     if dist.world > 1:
@@ -188,8 +187,8 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": "synthetic (VLP-16-like 16x%d ray-cast box room + 200 Hz IMU, SURVEY §8d; "
-                "IMU/odom-branch evidence synthetic)" % args.n_az,
+        "data": "synthetic (VLP-16-like 16x%d ray-cast box room + 200 Hz IMU + wheel odometry, SURVEY §8d)"
+                % args.n_az,
         "config": {"workload": "C3: one 64k-point scan x %d hypotheses through the full batched pipeline "
                                "(a1-a16: budget, predict, IMU preint, deskew, soft-assign, moment-match, "
                                "Matrix-Fisher, planar, tempering, fusion, recompose, IW, map, anchor drift, "
@@ -308,24 +307,26 @@ def cpu_leg(n_az, H_total, budget_s):
     sys.path.insert(0, ROOT)
     from threadpoolctl import threadpool_limits
     from oracle import cases, gc_oracle as O
-    case = cases.build(H=H_total, n_az=n_az, n_scans=1)
+    case = cases.build(H=H_total, n_az=n_az, n_scans=1, io="computed")
     st, s = case["state"], case["scans"][0]
     Q = O.iw_process_Q(st.nu_proc, st.Psi_proc)
+    Sga = (O.iw_meas_mode(st.nu_meas, st.Psi_meas, 0), O.iw_meas_mode(st.nu_meas, st.Psi_meas, 1))
     md = O.map_derived(st.map)
     scan = cases.scan_input(s)
     with threadpool_limits(limits=1):
         t0 = time.perf_counter()
         done = 0
         while done < H_total:
-            O.scan_hypothesis(st.beliefs[done], scan, Q, case["ios"][done], st.map, md, case["bins"], case["cfg"])
+            O.scan_hypothesis(st.beliefs[done], scan, Q, None, st.map, md, case["bins"], case["cfg"], Sga)
             done += 1
             if time.perf_counter() - t0 > budget_s:
                 break
         dt = time.perf_counter() - t0
     per_hyp = dt / done
     return {"value": 1.0 / (per_hyp * H_total), "unit": "scans/s", "cores": 1, "kind": "port",
-            "sample": "%d of %d hypotheses of one %d-point scan through the oracle pipeline (a1-a14 per "
-                      "hypothesis, NumPy, 1 BLAS thread), extrapolated to the full scan" % (done, H_total, case["n"]),
+            "sample": "%d of %d hypotheses of one %d-point scan through the oracle pipeline (a1-a14 + IMU/odom "
+                      "branch per hypothesis, NumPy, 1 BLAS thread), extrapolated to the full scan"
+                      % (done, H_total, case["n"]),
             "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
 
 

@@ -23,7 +23,7 @@
 namespace gc {
 
 constexpr int N2 = kDZ * kDZ;
-constexpr double kG[3] = {0.0, 0.0, -9.81};
+
 
 // ------------------------------------------------------------------ small shared helpers
 // X ∘ Exp(δ[0:6]) (belief.py:408-425), thread-local.
@@ -83,6 +83,7 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,
              P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2);
   if (t == 0) compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);  // pose0 = world pose of belief_prev
+  if (t < n) P.mu_aux[(int64_t)h * kMuAux + t] = mu_prev[t];
   for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
   if (t < n) P.hpred[(int64_t)h * n + t] = hpred[t];
   // --- predicted moments: Σ_pred[15,15] and mu_inc (pipeline.py:436-453) from chol(L_pred+εI)
@@ -95,10 +96,12 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
     misc[6] = fmax(sqrt(s1515), 0.01);                  // sigma_warp
     compose_exp(P.X + (int64_t)h * 6, mu_inc, misc + 8);  // pose_pred (for MF / planar)
     for (int k = 0; k < 6; ++k) P.pose_pred[(int64_t)h * 6 + k] = misc[8 + k];
+    for (int k = 0; k < 6; ++k) P.mu_aux[(int64_t)h * kMuAux + 44 + k] = misc[k];
     double R0[9];
     so3_exp(misc + 3, R0);
     for (int k = 0; k < 9; ++k) misc[16 + k] = R0[k];
   }
+  if (t < n) P.mu_aux[(int64_t)h * kMuAux + 22 + t] = mu_inc[t];
   __syncthreads();
   // ------------------------------------------------------------------ IMU (a3)
   const double sigma_warp = misc[6];
@@ -123,6 +126,7 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   const double wb = ib < M ? window_weight(tb, S.t0, S.t1, sigma_warp) : 0.0;
   const double* R0 = misc + 16;
   double* pre = misc + 32;  // kPreint
+  const double kG[3] = {0.0, 0.0, -9.81 * P.gravity_scale};  // GC_GRAVITY_W · imu_gravity_scale
   wg_preintegrate(M, S.imu_t, S.imu_g, S.imu_a, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, red, pre);
   const double ess_scan = wg_sum(wa + wb, red);
   if (t == 0) {

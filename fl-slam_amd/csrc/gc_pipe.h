@@ -11,7 +11,10 @@ constexpr int kMapDer = 17;   // [mu_dir 3, kappa, centroid 3, Sigma_c 9, pad]
 constexpr int kPredCert = 8;  // [lift, psd_delta, eig_min, eig_max, cond, nnc, trace_cov, trigger]
 constexpr int kImuOut = 8;    // [ess_scan, sigma_warp, dt_imu, omega_avg 3, pad 2]
 constexpr int kIoCert = 10;   // [ess odom/imu/gyro, sf odom/imu/gyro, exc_dt, exc_ex, nll, trigger]
-constexpr int kHypDiag = 40;  // see include/gcslam.h GC_HYP_DIAG layout
+constexpr int kHypDiag = 40;
+constexpr int kMuAux = 50;    // [mu_prev 22 (belief_prev increment), mu_inc 22 (belief_pred), pose0 6]
+constexpr int kIoParts = 40;  // GC_IO_PARTS layout (include/gcslam.h)
+constexpr int kOdomLen = 84;  // [pose 6, cov 36, twist 6, twist_cov 36]  // see include/gcslam.h GC_HYP_DIAG layout
 constexpr int kCombCert = 16;
 
 // Partial-sum record exchanged between ranks once per scan (doubles).
@@ -30,11 +33,13 @@ struct PipeDev {
   double eps_psd, eps_lift, eps_mass, lambda_ou, c_frob, forgetting, weight_floor;
   double power_beta_min, power_beta_exc_c, power_beta_z_c, alpha_min, alpha_max, c0_cond;
   double nu_max;
+  double planar_z_ref, planar_z_sigma, planar_vz_sigma, gravity_scale;
   // per local hypothesis
   double *X, *z, *L, *h, *stamp;           // belief (in/out)
   double *Lpred, *hpred, *pred_cert, *pose_pred, *xi, *imu_out, *dPsiM;
   double *stats, *bincert;                 // (Hl, B, 38), (Hl, 8)
-  double *io_L, *io_h, *io_cert;           // synthetic IMU/odom-branch evidence
+  double *io_L, *io_h, *io_cert;           // IMU/odom-branch evidence (computed or given)
+  double *mu_aux, *io_parts;               // (Hl, kMuAux), (Hl, kIoParts)
   double *dPsiP, *mu_fin, *diag;
   // shared
   double *weights;                         // (H)
@@ -58,6 +63,7 @@ struct ScanArgs {
 
 // launchers (gc_belief.hip)
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st);
+hipError_t launch_io_branch(const PipeDev& P, const ScanArgs& S, const double* d_odom, hipStream_t st);
 hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st);
 hipError_t launch_combine_local(const PipeDev& P, hipStream_t st);
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st);

@@ -19,8 +19,10 @@ struct gc_pipeline {
   std::vector<void*> allocs;
   struct Slot {
     double *pts = nullptr, *t = nullptr, *w = nullptr, *imu_t = nullptr, *imu_g = nullptr, *imu_a = nullptr;
+    double* odom = nullptr;  // kOdomLen doubles (device), staged by gc_pipeline_stage_odom
     int64_t n_in = 0;
   } slots[GC_PIPE_MAX_SLOTS];
+  int io_mode = GC_IO_COMPUTED;
   gc_comm* comm = nullptr;
   double* d_cfg_origin = nullptr;
 };
@@ -82,17 +84,20 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   P.power_beta_exc_c = cfg[GC_PCFG_POWER_BETA_EXC_C]; P.power_beta_z_c = cfg[GC_PCFG_POWER_BETA_Z_C];
   P.alpha_min = cfg[GC_PCFG_ALPHA_MIN]; P.alpha_max = cfg[GC_PCFG_ALPHA_MAX]; P.c0_cond = cfg[GC_PCFG_C0_COND];
   P.nu_max = cfg[GC_PCFG_NU_MAX];
+  P.planar_z_ref = cfg[GC_PCFG_PLANAR_Z_REF]; P.planar_z_sigma = cfg[GC_PCFG_PLANAR_Z_SIGMA];
+  P.planar_vz_sigma = cfg[GC_PCFG_PLANAR_VZ_SIGMA]; P.gravity_scale = cfg[GC_PCFG_GRAVITY_SCALE];
   const int Hl = P.Hl, B = P.B, NN = 484;
   const int PL = gc::partial_len(B);
   int rc = GC_OK;
   double** fields[] = {&P.X, &P.z, &P.L, &P.h, &P.stamp, &P.Lpred, &P.hpred, &P.pred_cert, &P.pose_pred, &P.xi,
                        &P.imu_out, &P.dPsiM, &P.stats, &P.bincert, &P.io_L, &P.io_h, &P.io_cert, &P.dPsiP,
-                       &P.mu_fin, &P.diag};
+                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts};
   const size_t sizes[] = {(size_t)Hl * 6, (size_t)Hl * 22, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl,
                           (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kPredCert, (size_t)Hl * 6,
                           (size_t)Hl * 6, (size_t)Hl * gc::kImuOut, (size_t)Hl * 27, (size_t)Hl * B * 38,
                           (size_t)Hl * 8, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kIoCert,
-                          (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag};
+                          (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag, (size_t)Hl * gc::kMuAux,
+                          (size_t)Hl * gc::kIoParts};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert};
@@ -116,7 +121,7 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
   (void)hipStreamSynchronize(p->ctx->stream);
   for (void* a : p->allocs) (void)hipFree(a);
   for (auto& s : p->slots) {
-    for (double* d : {s.pts, s.t, s.w, s.imu_t, s.imu_g, s.imu_a})
+    for (double* d : {s.pts, s.t, s.w, s.imu_t, s.imu_g, s.imu_a, s.odom})
       if (d) (void)hipFree(d);
   }
   delete p;
@@ -160,7 +165,43 @@ int32_t gc_pipeline_set_io_evidence(gc_pipeline* p, const double* h_L, const dou
   const size_t Hl = p->P.Hl;
   GC_TRY(up(p, p->P.io_L, h_L, Hl * 484));
   GC_TRY(up(p, p->P.io_h, h_h, Hl * 22));
+  p->io_mode = GC_IO_GIVEN;
   return up(p, p->P.io_cert, h_cert, Hl * gc::kIoCert);
+}
+
+int32_t gc_pipeline_set_io_mode(gc_pipeline* p, int32_t mode) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, mode == GC_IO_GIVEN || mode == GC_IO_COMPUTED, "io mode must be GC_IO_GIVEN or GC_IO_COMPUTED");
+  p->io_mode = mode;
+  return GC_OK;
+}
+
+int32_t gc_pipeline_stage_odom(gc_pipeline* p, int32_t slot, const double* h_pose6, const double* h_cov36,
+                               const double* h_twist6, const double* h_twist_cov36) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS, "slot out of range");
+  GC_CHECK_ARG(p->ctx, h_pose6 && h_cov36 && h_twist6 && h_twist_cov36, "NULL odometry array");
+  auto& s = p->slots[slot];
+  if (!s.odom) GC_HIP(p->ctx, hipMalloc((void**)&s.odom, gc::kOdomLen * sizeof(double)));
+  double buf[gc::kOdomLen];
+  std::memcpy(buf, h_pose6, 6 * sizeof(double));
+  std::memcpy(buf + 6, h_cov36, 36 * sizeof(double));
+  std::memcpy(buf + 42, h_twist6, 6 * sizeof(double));
+  std::memcpy(buf + 48, h_twist_cov36, 36 * sizeof(double));
+  return up(p, s.odom, buf, gc::kOdomLen);
+}
+
+int32_t gc_pipeline_get_io_parts(gc_pipeline* p, double* h_parts) {
+  GC_CHECK_ARG(nullptr, p && h_parts, "NULL argument");
+  return down(p, h_parts, p->P.io_parts, (size_t)p->P.Hl * gc::kIoParts);
+}
+
+int32_t gc_pipeline_get_io_evidence(gc_pipeline* p, double* h_L, double* h_h, double* h_cert) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const size_t Hl = p->P.Hl;
+  GC_TRY(down(p, h_L, p->P.io_L, Hl * 484));
+  GC_TRY(down(p, h_h, p->P.io_h, Hl * 22));
+  return down(p, h_cert, p->P.io_cert, Hl * gc::kIoCert);
 }
 
 int32_t gc_pipeline_set_iw(gc_pipeline* p, const double* nu_proc, const double* Psi_proc, const double* nu_meas,
@@ -234,6 +275,8 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
   GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS && p->slots[slot].pts, "scan slot not staged");
   GC_CHECK_ARG(p->ctx, p->P.G == 1 || p->comm, "world_size > 1 needs gc_pipeline_attach_comm");
+  GC_CHECK_ARG(p->ctx, p->io_mode == GC_IO_GIVEN || p->slots[slot].odom,
+               "GC_IO_COMPUTED needs the slot's odometry (gc_pipeline_stage_odom)");
   gc_ctx* ctx = p->ctx;
   const auto& s = p->slots[slot];
   gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
@@ -243,6 +286,8 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
   GC_TRY(gc_budget_stats(ctx, s.w, s.n_in, P.n_cap, P.budget));
   // a2 + a3
   GC_HIP(ctx, gc::launch_predict_imu(P, S, ctx->stream));
+  // a9a IMU/odom evidence branch (pipeline.py:595-776)
+  if (p->io_mode == GC_IO_COMPUTED) GC_HIP(ctx, gc::launch_io_branch(P, S, s.odom, ctx->stream));
   // a1 -> a4 -> a5 -> a6 fused over all local hypotheses
   const double origin[3] = {P.o0, P.o1, P.o2};
   GC_TRY(gc_scan_bins_fused(ctx, P.Hl, s.n_in, P.n_cap, P.B, s.pts, s.t, s.w, P.budget, scan_start, scan_end,

@@ -57,6 +57,12 @@ SIGNATURES = {
     "gc_pipeline_get_beliefs": [_vp, _vp, _vp, _vp, _vp, _vp],
     "gc_pipeline_set_weights": [_vp, _vp],
     "gc_pipeline_set_io_evidence": [_vp, _vp, _vp, _vp],
+    "gc_pipeline_set_io_mode": [_vp, _i32],
+    "gc_pipeline_stage_odom": [_vp, _i32, _vp, _vp, _vp, _vp],
+    "gc_pipeline_get_io_parts": [_vp, _vp],
+    "gc_pipeline_get_io_evidence": [_vp, _vp, _vp, _vp],
+    "gc_io_factor_batch": [_vp, _i32, _i32, _vp, _vp],
+    "gc_imu_vmf_gravity_tr_batch": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _vp, _dptr, _f64, _f64, _f64, _vp],
     "gc_pipeline_set_iw": [_vp, _vp, _vp, _vp, _vp],
     "gc_pipeline_get_iw": [_vp, _vp, _vp, _vp, _vp, _vp, _vp],
     "gc_pipeline_set_map": [_vp, _vp],
@@ -92,11 +98,18 @@ SIGNATURES = {
     "gc_primitive_map_fuse": [_vp, _vp, _vp, _vp, _f64, _f64, _f64, _i64, _vp],
 }
 
-GC_PCFG_LEN = 18
+GC_PCFG_LEN = 22
 GC_PIPE_MAX_SLOTS = 8
 GC_MAP_REC = 26
 GC_MAP_DER = 17
 GC_IO_CERT = 10
+GC_IO_PARTS = 40
+GC_IO_GIVEN, GC_IO_COMPUTED = 0, 1
+GC_IOF_IN = 64
+GC_IOF_OUT = 484 + 22 + 16
+(GC_IOF_ODOM_QUADRATIC, GC_IOF_IMU_GYRO_ROTATION, GC_IOF_IMU_PREINT_FACTOR, GC_IOF_PLANAR_Z_PRIOR,
+ GC_IOF_VELOCITY_Z_PRIOR, GC_IOF_ODOM_VELOCITY, GC_IOF_ODOM_YAWRATE, GC_IOF_KINEMATIC, GC_IOF_IMU_DEPENDENCE,
+ GC_IOF_ODOM_DEPENDENCE) = range(10)
 GC_HYP_DIAG = 40
 GC_COMB_LEN = 484 + 22 + 22 + 6 + 16
 GC_COMM_ID_BYTES = 128

@@ -39,6 +39,11 @@ GC_RANGE_WEIGHT_SIGMA = 0.25
 GC_RANGE_WEIGHT_MIN_R = 0.5
 GC_RANGE_WEIGHT_MAX_R = 50.0
 GC_IW_NU_WEAK_ADD = 0.5
+GC_IMU_GYRO_NOISE_DENSITY = 8.7e-7   # constants.py:190
+GC_IMU_ACCEL_NOISE_DENSITY = 9.5e-5  # constants.py:201
+GC_PLANAR_Z_REF = 0.0                # constants.py:294
+GC_PLANAR_Z_SIGMA = 0.1              # constants.py:305
+GC_PLANAR_VZ_SIGMA = 0.01            # constants.py:310
 
 # PipelineConfig defaults (pipeline.py:118-131; gc_unified.yaml:41-57)
 POWER_BETA_MIN = 0.25

@@ -23,6 +23,14 @@ from .inverse_wishart import (MeasurementNoiseIWState, ProcessNoiseIWState,
                               process_noise_iw_apply_suffstats_jax,
                               process_noise_iw_suffstats_from_info_jax, process_noise_state_to_Q_jax)
 from .hypothesis import HypothesisProjectionResult, hypothesis_barycenter_projection
+from .imu_odom_evidence import (ImuDependenceInflationResult, ImuGyroEvidenceResult, ImuPreintegrationFactorResult,
+                                OdomDependenceInflationResult, OdomEvidenceResult, OdomVelocityEvidenceResult,
+                                OdomYawRateEvidenceResult, PlanarPriorResult, PoseTwistConsistencyResult,
+                                TimeResolvedImuResult, VelocityZPriorResult, imu_dependence_inflation,
+                                imu_gyro_rotation_evidence, imu_preintegration_factor,
+                                imu_vmf_gravity_evidence_time_resolved, odom_dependence_inflation,
+                                odom_quadratic_evidence, odom_velocity_evidence, odom_yawrate_evidence,
+                                planar_z_prior, pose_twist_kinematic_consistency, velocity_z_prior)
 
 __all__ = [
     "PointBudgetResult", "point_budget_resample", "DeskewConstantTwistResult",
@@ -37,5 +45,11 @@ __all__ = [
     "AnchorDriftResult", "pose_update_frobenius_recompose", "anchor_drift_update", "ProcessNoiseIWState",
     "MeasurementNoiseIWState", "process_noise_iw_suffstats_from_info_jax", "process_noise_iw_apply_suffstats_jax",
     "process_noise_state_to_Q_jax", "measurement_noise_apply_suffstats_jax", "HypothesisProjectionResult",
-    "hypothesis_barycenter_projection",
+    "hypothesis_barycenter_projection", "OdomEvidenceResult", "odom_quadratic_evidence", "TimeResolvedImuResult",
+    "imu_vmf_gravity_evidence_time_resolved", "ImuDependenceInflationResult", "imu_dependence_inflation",
+    "ImuGyroEvidenceResult", "imu_gyro_rotation_evidence", "ImuPreintegrationFactorResult",
+    "imu_preintegration_factor", "PlanarPriorResult", "planar_z_prior", "VelocityZPriorResult", "velocity_z_prior",
+    "OdomVelocityEvidenceResult", "odom_velocity_evidence", "OdomYawRateEvidenceResult", "odom_yawrate_evidence",
+    "PoseTwistConsistencyResult", "pose_twist_kinematic_consistency", "OdomDependenceInflationResult",
+    "odom_dependence_inflation",
 ]

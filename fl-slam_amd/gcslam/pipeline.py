@@ -19,7 +19,7 @@ import numpy as np
 from . import _abi
 from .constants import (FORGETTING_FACTOR, GC_ALPHA_MAX, GC_ALPHA_MIN, GC_B_BINS, GC_C0_COND, GC_C_FROB,
                         GC_EPS_LIFT, GC_EPS_MASS, GC_EPS_PSD, GC_MAX_IMU_PREINT_LEN, GC_OU_DAMPING_LAMBDA,
-                        GC_TAU_SOFT_ASSIGN, POWER_BETA_EXC_C, POWER_BETA_MIN, POWER_BETA_Z_C, T_BASE_LIDAR)
+                        GC_PLANAR_VZ_SIGMA, GC_PLANAR_Z_REF, GC_PLANAR_Z_SIGMA, GC_TAU_SOFT_ASSIGN, POWER_BETA_EXC_C, POWER_BETA_MIN, POWER_BETA_Z_C, T_BASE_LIDAR)
 from .ops.binning import create_fibonacci_atlas
 
 
@@ -49,13 +49,18 @@ class PipelineConfig:
     alpha_max: float = GC_ALPHA_MAX
     c0_cond: float = GC_C0_COND
     nu_max: float = 1000.0
+    planar_z_ref: float = GC_PLANAR_Z_REF
+    planar_z_sigma: float = GC_PLANAR_Z_SIGMA
+    planar_vz_sigma: float = GC_PLANAR_VZ_SIGMA
+    imu_gravity_scale: float = 1.0
 
     def as_array(self, H_total: int) -> np.ndarray:
         floor = 0.01 / H_total if self.weight_floor is None else self.weight_floor
         return np.array([self.tau, *self.lidar_origin, self.eps_psd, self.eps_lift, self.eps_mass,
                          self.lambda_ou, self.c_frob, self.forgetting_factor, floor, self.power_beta_min,
                          self.power_beta_exc_c, self.power_beta_z_c, self.alpha_min, self.alpha_max,
-                         self.c0_cond, self.nu_max], dtype=np.float64)
+                         self.c0_cond, self.nu_max, self.planar_z_ref, self.planar_z_sigma,
+                         self.planar_vz_sigma, self.imu_gravity_scale], dtype=np.float64)
 
 
 def _p(a):
@@ -115,8 +120,24 @@ class BatchedScanPipeline:
         return dict(X_anchor=X, z_lin=z, L=L, h=h, stamp=st)
 
     def set_io_evidence(self, L, h, cert):
+        """Given (synthetic) IMU/odom-branch evidence; selects GC_IO_GIVEN."""
         self._call("gc_pipeline_set_io_evidence", _p(_f(L, (self.Hl, 22, 22))), _p(_f(h, (self.Hl, 22))),
                    _p(_f(cert, (self.Hl, _abi.GC_IO_CERT))))
+
+    def set_io_mode(self, computed: bool):
+        self._call("gc_pipeline_set_io_mode", _abi.GC_IO_COMPUTED if computed else _abi.GC_IO_GIVEN)
+
+    def io_evidence(self):
+        """(L_io (Hl,22,22), h_io (Hl,22), cert (Hl,10)) of the last scan."""
+        L, h, c = np.empty((self.Hl, 22, 22)), np.empty((self.Hl, 22)), np.empty((self.Hl, _abi.GC_IO_CERT))
+        self._call("gc_pipeline_get_io_evidence", _p(L), _p(h), _p(c))
+        return L, h, c
+
+    def io_parts(self):
+        """(Hl, GC_IO_PARTS) IMU/odom-branch internals of the last scan (include/gcslam.h)."""
+        o = np.empty((self.Hl, _abi.GC_IO_PARTS))
+        self._call("gc_pipeline_get_io_parts", _p(o))
+        return o
 
     def set_iw(self, nu_proc, Psi_proc, nu_meas, Psi_meas):
         self._call("gc_pipeline_set_iw", _p(_f(nu_proc, (7,))), _p(_f(Psi_proc, (7, 6, 6))),
@@ -142,6 +163,10 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_stage_scan", int(slot), _p(P), _p(_f(scan["timestamps"], (n,))),
                    _p(_f(scan["weights"], (n,))), n, _p(_f(scan["imu_stamps"], (self.M,))),
                    _p(_f(scan["imu_gyro"], (self.M, 3))), _p(_f(scan["imu_accel"], (self.M, 3))))
+        if "odom_pose" in scan:  # odometry for the on-device IMU/odom branch (GC_IO_COMPUTED)
+            self._call("gc_pipeline_stage_odom", int(slot), _p(_f(scan["odom_pose"], (6,))),
+                       _p(_f(scan["odom_cov"], (6, 6))), _p(_f(scan["odom_twist"], (6,))),
+                       _p(_f(scan["odom_twist_cov"], (6, 6))))
 
     def run_scan(self, slot: int, scan: dict, scan_count: int):
         self._call("gc_pipeline_run_scan", int(slot), float(scan["scan_start"]), float(scan["scan_end"]),

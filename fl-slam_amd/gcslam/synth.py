@@ -62,9 +62,19 @@ def make_scan(scan_idx: int = 0, n_rings: int = 16, n_az: int = 4096, room=(10.0
     stamps[:n] = st
     gyro[:n] = np.array([0.0, 0.0, omega_z]) + rng.normal(0.0, 1e-3, size=(n, 3))
     accel[:n] = np.array([0.0, 0.0, 9.81]) + rng.normal(0.0, 1e-2, size=(n, 3))
+    # wheel odometry (backend_node.py:1748-1765): planar constant-twist pose at t_scan relative to
+    # the first odom sample, pose cov 1e-2 (trans) / 1e-3 (rot), twist cov 1e-2·I
+    t_rel = t_scan - T0_ABS
+    yaw = omega_z * t_rel
+    odom_pose = np.array([vel_x * np.sin(yaw) / omega_z, vel_x * (1.0 - np.cos(yaw)) / omega_z, 0.0, 0.0, 0.0, yaw])
+    odom_pose[0:2] += rng.normal(0.0, 0.01, size=2)
+    odom_cov = np.diag([1e-2, 1e-2, 1e-2, 1e-3, 1e-3, 1e-3])
+    odom_twist = np.array([vel_x, 0.0, 0.0, 0.0, 0.0, omega_z]) + rng.normal(0.0, 1e-3, size=6)
+    odom_twist_cov = 1e-2 * np.eye(6)
     return dict(points=np.ascontiguousarray(pts), timestamps=ts, weights=w, ring=ring, tag=tag,
                 imu_stamps=stamps, imu_gyro=gyro, imu_accel=accel, scan_start=t_start,
-                scan_end=t_start + SCAN_PERIOD, t_last=t_last, t_scan=t_scan, dt_sec=SCAN_PERIOD)
+                scan_end=t_start + SCAN_PERIOD, t_last=t_last, t_scan=t_scan, dt_sec=SCAN_PERIOD,
+                odom_pose=odom_pose, odom_cov=odom_cov, odom_twist=odom_twist, odom_twist_cov=odom_twist_cov)
 
 
 def make_hypotheses(H: int, seed: int = SEED0, prior_precision: float = 1e-6):

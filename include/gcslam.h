@@ -171,7 +171,11 @@ typedef struct {
 #define GC_PCFG_ALPHA_MAX 15
 #define GC_PCFG_C0_COND 16
 #define GC_PCFG_NU_MAX 17
-#define GC_PCFG_LEN 18
+#define GC_PCFG_PLANAR_Z_REF 18    /* GC_PLANAR_Z_REF (constants.py:294) */
+#define GC_PCFG_PLANAR_Z_SIGMA 19  /* GC_PLANAR_Z_SIGMA (constants.py:305) */
+#define GC_PCFG_PLANAR_VZ_SIGMA 20 /* GC_PLANAR_VZ_SIGMA (constants.py:310) */
+#define GC_PCFG_GRAVITY_SCALE 21   /* PipelineConfig.imu_gravity_scale (pipeline.py:141) */
+#define GC_PCFG_LEN 22
 
 #define GC_PIPE_MAX_SLOTS 8
 /* map bin record (B x 26): [S_dir 3, S_dir_scatter 9, N_dir, N_pos, sum_p 3, sum_ppT 9] */
@@ -201,6 +205,26 @@ int32_t gc_pipeline_get_beliefs(gc_pipeline* p, double* h_X, double* h_z, double
                                 double* h_stamp);
 int32_t gc_pipeline_set_weights(gc_pipeline* p, const double* h_weights);
 int32_t gc_pipeline_set_io_evidence(gc_pipeline* p, const double* h_L, const double* h_h, const double* h_cert);
+/* IMU/odom branch source: GC_IO_GIVEN uses the evidence of gc_pipeline_set_io_evidence (synthetic
+ * input; calling it selects this mode); GC_IO_COMPUTED (default) evaluates _compute_imu_odom_branch (pipeline.py:595-776) on the
+ * device each scan from the slot's odometry (gc_pipeline_stage_odom) and IMU window. */
+#define GC_IO_GIVEN 0
+#define GC_IO_COMPUTED 1
+int32_t gc_pipeline_set_io_mode(gc_pipeline* p, int32_t mode);
+/* Odometry of a scan slot (backend_node.py:1748-1765): relative pose [t, rotvec] (6), pose
+ * covariance (6,6) in [trans, rot] order, body twist [v, ω] (6), twist covariance (6,6). */
+int32_t gc_pipeline_stage_odom(gc_pipeline* p, int32_t slot, const double* h_pose6, const double* h_cov36,
+                               const double* h_twist6, const double* h_twist_cov36);
+/* Per-hypothesis IMU/odom-branch internals of the last scan (GC_IO_COMPUTED), (Hl, GC_IO_PARTS):
+ * [0:6] odom se3 residual, 6 kappa, 7 ess_weighted, 8 ess_raw, 9 mean_reliability,
+ * 10 transport_sigma, 11 Rbar, 12 imu dependence scale, [13:16] gyro r_rot, [16:19] preint r_vel,
+ * [19:22] preint r_pos, 22 planar r_z, 23 v_z, [24:27] odom-velocity r_vel, 27 yaw-rate r_wz,
+ * [28:31] kinematic r_trans, [31:34] kinematic r_rot, 34 odom dependence scale, 35 odom nll,
+ * 36 imu nll, 37 gyro nll, 38 dt_int, 39 trigger-magnitude sum of the 11 certs.
+ * gc_pipeline_get_io_evidence reads back (L_io, h_io, cert row) of the last scan. */
+#define GC_IO_PARTS 40
+int32_t gc_pipeline_get_io_parts(gc_pipeline* p, double* h_parts);
+int32_t gc_pipeline_get_io_evidence(gc_pipeline* p, double* h_L, double* h_h, double* h_cert);
 int32_t gc_pipeline_set_iw(gc_pipeline* p, const double* h_nu_proc7, const double* h_Psi_proc7x36,
                            const double* h_nu_meas3, const double* h_Psi_meas3x9);
 int32_t gc_pipeline_get_iw(gc_pipeline* p, double* h_nu_proc7, double* h_Psi_proc7x36, double* h_nu_meas3,
@@ -247,6 +271,54 @@ int32_t gc_comm_allgather_f64(gc_ctx* ctx, gc_comm* comm, const double* d_send, 
                                z_to_xy_ratio, power_beta, nll_per_ess] */
 #define GC_FUSION_OUT 4     /* [alpha, excitation_total, ess_to_excitation, cond_to_support] */
 #define GC_BARY_CERT 16     /* [floor_adjustment, spread, ess, support_frac, mass_eps, psd cert 6, pad 5] */
+
+/* IMU/odom-branch factors (pipeline.py:595-776), one thread per item.
+ * Item rows: d_in (H, GC_IOF_IN) per kind below; d_out (H, GC_IOF_OUT) = L (22,22) | h (22) |
+ * extras (16). Each kind replaces one reference operator:
+ *  GC_IOF_ODOM_QUADRATIC    odom_quadratic_evidence (odom_evidence.py:87-154)
+ *     in [pose_pred 6, odom_pose 6, cov 36, eps_psd, eps_lift]
+ *     ex [delta_z_pose 6, nll, lift, eig_min, eig_max, cond, nnc]
+ *  GC_IOF_IMU_GYRO_ROTATION imu_gyro_rotation_evidence (imu_gyro_evidence.py:103-163)
+ *     in [rv_start 3, rv_end_pred 3, delta_rotvec 3, Sigma_g 9, dt_int, eps_psd, eps_lift, eps_mass]
+ *     ex [r_rot 3, nll, lift, eig_min, eig_max, nnc]
+ *  GC_IOF_IMU_PREINT_FACTOR imu_preintegration_factor (imu_preintegration_factor.py:46-180)
+ *     in [p_start 3, rv_start 3, v_start 3, p_end_pred 3, v_end_pred 3, delta_v_body 3,
+ *         delta_p_body 3, Sigma_a 9, dt_int, eps_psd, eps_lift, eps_mass]
+ *     ex [r_vel 3, r_pos 3, nll, lift, eig_min, eig_max, cond, nnc]
+ *  GC_IOF_PLANAR_Z_PRIOR    planar_z_prior (planar_prior.py:55-135): in [pose 6, z_ref, sigma_z]; ex [r_z, nll]
+ *  GC_IOF_VELOCITY_Z_PRIOR  velocity_z_prior (planar_prior.py:138-195): in [v_z, sigma_vz]; ex [v_z, nll]
+ *  GC_IOF_ODOM_VELOCITY     odom_velocity_evidence (odom_twist_evidence.py:58-154)
+ *     in [v_pred_world 3, R_world_body 9, v_odom_body 3, Sigma_v 9, eps_psd, eps_lift]
+ *     ex [r_vel 3, nll, lift, eig_min, eig_max, cond, nnc]
+ *  GC_IOF_ODOM_YAWRATE      odom_yawrate_evidence (odom_twist_evidence.py:157-225)
+ *     in [omega_z_pred, omega_z_odom, sigma_wz]; ex [r_wz, nll]
+ *  GC_IOF_KINEMATIC         pose_twist_kinematic_consistency (odom_twist_evidence.py:251-397)
+ *     in [pose_prev 6, pose_curr 6, v_body 3, omega_body 3, dt, Sigma_v 9, Sigma_omega 9, eps_psd, eps_lift]
+ *     ex [r_trans 3, r_rot 3, nll, lift, eig_min, eig_max, cond]
+ *  GC_IOF_IMU_DEPENDENCE    imu_dependence_inflation (imu_evidence.py:562-589): in [transport_sigma, eps_mass]; ex [scale]
+ *  GC_IOF_ODOM_DEPENDENCE   odom_dependence_inflation (odom_twist_evidence.py:400-430):
+ *     in [r_trans 3, r_rot 3, eps_mass]; ex [scale] */
+#define GC_IOF_IN 64
+#define GC_IOF_OUT (484 + 22 + 16)
+#define GC_IOF_ODOM_QUADRATIC 0
+#define GC_IOF_IMU_GYRO_ROTATION 1
+#define GC_IOF_IMU_PREINT_FACTOR 2
+#define GC_IOF_PLANAR_Z_PRIOR 3
+#define GC_IOF_VELOCITY_Z_PRIOR 4
+#define GC_IOF_ODOM_VELOCITY 5
+#define GC_IOF_ODOM_YAWRATE 6
+#define GC_IOF_KINEMATIC 7
+#define GC_IOF_IMU_DEPENDENCE 8
+#define GC_IOF_ODOM_DEPENDENCE 9
+#define GC_IOF_NKINDS 10
+int32_t gc_io_factor_batch(gc_ctx* ctx, int32_t kind, int32_t H, const double* d_in, double* d_out);
+/* imu_vmf_gravity_evidence_time_resolved (imu_evidence.py:402-559), one workgroup per item over
+ * the shared IMU window accel/gyro (M,3); rotvec (H,3), weights (H,M), accel_bias (H,3), g3 host.
+ * d_out (H, GC_IOF_OUT), ex = [kappa, ess_weighted, ess_raw, mean_reliability, transport_sigma,
+ * Rbar, nll, nll_per_ess, psd_delta, eig_min, eig_max, cond, nnc, xbar 3]. */
+int32_t gc_imu_vmf_gravity_tr_batch(gc_ctx* ctx, int32_t H, int32_t M, const double* d_rotvec, const double* d_accel,
+                                    const double* d_gyro, const double* d_w, const double* d_ba, const double* g3,
+                                    double dt_imu, double eps_psd, double eps_mass, double* d_out);
 
 /* BeliefGaussianInfo.mean_increment + world pose X ∘ Exp(δz) (common/belief.py:373-425). */
 int32_t gc_belief_world_pose_batch(gc_ctx* ctx, int32_t H, const double* d_X, const double* d_L, const double* d_h,

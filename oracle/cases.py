@@ -12,7 +12,9 @@ SCAN_KEYS = ["points", "timestamps", "weights", "ring", "tag", "imu_stamps", "im
 
 
 def scan_input(s):
-    return O.ScanInput(**{k: s[k] for k in SCAN_KEYS})
+    odom = (O.OdomInput(s["odom_pose"], s["odom_cov"], s["odom_twist"], s["odom_twist_cov"])
+            if "odom_pose" in s else None)
+    return O.ScanInput(**{k: s[k] for k in SCAN_KEYS}, odom=odom)
 
 
 def warmup_map(scan, cap, origin, bins):
@@ -29,7 +31,9 @@ def map_to_record(m: O.MapStats):
                            m.sum_p, m.sum_ppT.reshape(B, 9)], axis=1)
 
 
-def build(H=4, n_az=256, n_scans=3, seed_scan0=0):
+def build(H=4, n_az=256, n_scans=3, seed_scan0=0, io="synthetic"):
+    """io="synthetic": given IMU/odom-branch evidence (ios list); io="computed": the branch is
+    evaluated from each scan's odometry + IMU window (ios=None)."""
     import sys, os
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fl-slam_amd"))
     from gcslam import synth
@@ -45,7 +49,7 @@ def build(H=4, n_az=256, n_scans=3, seed_scan0=0):
     beliefs = [O.Belief(hy["X_anchor"][i].copy(), hy["z_lin"][i].copy(), hy["L"][i].copy(), hy["h"][i].copy())
                for i in range(H)]
     ios = [O.IOEvidence(Lio[i], hio[i], cert[i, 0:3], cert[i, 3:6], cert[i, 6], cert[i, 7], cert[i, 8], cert[i, 9])
-           for i in range(H)]
+           for i in range(H)] if io == "synthetic" else None
     state = O.ScanState(beliefs, hy["weights"].copy(), nuP, PsiP, nuM, PsiM, m0, 0)
     return dict(scans=scans[1:], n=n, cfg=cfg, bins=bins, hyp=hy, io=(Lio, hio, cert), ios=ios, state=state,
                 map_record=map_to_record(m0), iw=(nuP, PsiP, nuM, PsiM))

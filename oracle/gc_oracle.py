@@ -60,6 +60,7 @@ IW_RHO_MEAS = np.array([0.995, 0.995, 0.99])
 PROC_BLOCK_DIMS = np.array([3, 3, 3, 3, 3, 1, 6])
 PROC_BLOCK_STARTS = np.array([0, 3, 6, 9, 12, 15, 16])
 SMALL_ANGLE = 1e-7
+PLANAR_Z_REF, PLANAR_Z_SIGMA, PLANAR_VZ_SIGMA = 0.0, 0.1, 0.01  # constants.py:294-310
 NEAR_PI = 1e-7
 # Build-declared (never recorded in the reference — parity unpinned):
 B_BINS = 48
@@ -313,6 +314,15 @@ def preintegrate(stamps, gyro, accel, w, rotvec0, bg, ba, g=GRAVITY_W):
     return dict(delta_pose=np.concatenate([p_b, so3_log(dRel)]), ess=float(np.sum(w)),
                 delta_R=dRel, delta_p=p_b, delta_v=R0.T @ v, dt_eff_sum=swdt,
                 a_body_mean=s_body / den, a_world_nog_mean=s_nog / den, a_world_mean=s_w / den)
+
+
+def imu_integration_time(stamps, t_start, t_end):
+    """compute_imu_integration_time (pipeline.py:262-313)."""
+    eps = 1e-9
+    v = np.sort(stamps[(stamps > t_start - eps) & (stamps <= t_end + eps) & (stamps > 0.0)])
+    if v.shape[0] < 2:
+        return 0.0
+    return max(0.0, min(float(np.sum(np.maximum(v[1:] - v[:-1], 0.0))), t_end - t_start))
 
 
 def imu_dt_mean(stamps):
@@ -640,6 +650,250 @@ class IOEvidence:
     trig: float = 0.0
 
 
+# ---------------------------------------------------------------------------------------
+# a9a IMU/odom branch — pipeline.py:595-776 and the 11 operators it calls.
+# Paths: backend/operators/{odom_evidence,imu_evidence,imu_gyro_evidence,
+# imu_preintegration_factor,planar_prior,odom_twist_evidence}.py
+# ---------------------------------------------------------------------------------------
+def se3_inverse(a):
+    """se3_inverse (se3_jax.py:442-453)."""
+    R = so3_exp(a[3:6])
+    return np.concatenate([-(R.T @ a[:3]), so3_log(R.T)])
+
+
+def se3_relative(a, b):
+    """se3_relative (se3_jax.py:457-459): b^{-1} ∘ a."""
+    return se3_compose(se3_inverse(b), a)
+
+
+def _eig_stats(M):
+    ev = np.linalg.eigvalsh(M)
+    return float(ev.min()), float(ev.max()), ev
+
+
+def odom_quadratic_evidence(pose_pred, odom_pose, odom_cov, eps_psd=EPS_PSD, eps_lift=EPS_LIFT):
+    """_odom_quadratic_evidence_core (odom_evidence.py:40-84) + cert (:126-146)."""
+    xi = se3_log(se3_relative(odom_pose, pose_pred))
+    cov_psd = psd_project(odom_cov, eps_psd)[0]
+    Lp, lift = chol_inverse_lifted(cov_psd, eps_lift)
+    L = np.zeros((D_Z, D_Z)); L[0:6, 0:6] = Lp
+    dz = np.zeros(D_Z); dz[0:6] = xi
+    h = L @ dz
+    nll = 0.5 * float(xi @ Lp @ xi)
+    emin, emax, ev = _eig_stats(psd_project(Lp, eps_psd)[0])
+    return dict(L=L, h=h, delta_z=dz, nll=nll, lift=lift, eig_min=emin, eig_max=emax,
+                cond=emax / max(emin, 1e-18), nnc=float(np.sum(ev < 1e-12)), trig=trigger(lift=lift))
+
+
+def transport_consistency(accel_c, gyro, dt, eps_mass=EPS_MASS):
+    """_compute_transport_consistency (imu_evidence.py:277-334)."""
+    df = np.zeros_like(accel_c)
+    df[1:-1] = (accel_c[2:] - accel_c[:-2]) / (2 * dt + eps_mass)
+    df[0] = (accel_c[1] - accel_c[0]) / (dt + eps_mass)
+    df[-1] = (accel_c[-1] - accel_c[-2]) / (dt + eps_mass)
+    return np.linalg.norm(df + np.cross(gyro, accel_c), axis=1)
+
+
+def reliability_weights(e, eps_mass=EPS_MASS):
+    """_compute_reliability_weights (imu_evidence.py:337-368): MAD-based σ."""
+    med = np.median(e)
+    sigma = np.median(np.abs(e - med)) / 0.6745 + eps_mass
+    return np.exp(-0.5 * (e / sigma) ** 2), sigma
+
+
+def imu_vmf_gravity_evidence_time_resolved(rotvec, accel, gyro, w, ba, g, dt_imu, eps_psd=EPS_PSD,
+                                           eps_mass=EPS_MASS):
+    """imu_vmf_gravity_evidence_time_resolved (imu_evidence.py:402-559), incl.
+    _accel_resultant_direction_weighted_jax (:371-399) and kappa_from_resultant_v2 (kappa.py:172-232)."""
+    R0 = so3_exp(rotvec)
+    g_hat = g / (np.linalg.norm(g) + eps_mass)
+    e = transport_consistency(accel - ba[None, :], gyro, dt_imu, eps_mass)
+    rel, sigma = reliability_weights(e, eps_mass)
+    wr = w * rel
+    ess_w, ess_raw = float(np.sum(wr)), float(np.sum(w))
+    a = accel - ba[None, :]
+    x = a / (np.linalg.norm(a, axis=1, keepdims=True) + eps_mass)
+    S = np.sum(wr[:, None] * x, axis=0)
+    Sn = np.linalg.norm(S)
+    xbar = S / (Sn + eps_mass)
+    Rbar = Sn / (ess_w + eps_mass)
+    kappa = kappa_scalar(Rbar)
+    mu0 = R0.T @ (-g_hat)
+    xdm = float(xbar @ mu0)
+    g_rot = -kappa * np.cross(mu0, xbar)
+    H = kappa * (xdm * np.eye(3) - 0.5 * (np.outer(xbar, mu0) + np.outer(mu0, xbar)))
+    H = 0.5 * (H + H.T)
+    Hp, hc = psd_project(H, eps_psd)
+    L = np.zeros((D_Z, D_Z)); L[3:6, 3:6] = Hp
+    h = np.zeros(D_Z); h[3:6] = -g_rot
+    nll = float(-kappa * (mu0 @ xbar))
+    mrel = float(np.mean(rel))
+    mer = ess_w / (ess_raw + eps_mass)
+    return dict(L=L, h=h, kappa=kappa, ess_weighted=ess_w, ess_raw=ess_raw, mean_reliability=mrel,
+                transport_sigma=float(sigma), Rbar=float(Rbar), xbar=xbar, nll=nll,
+                nll_per_ess=nll / (ess_w + eps_mass), psd_delta=float(hc[0]),
+                trig=trigger(psd=float(hc[0]), mass=mer, alpha=mrel))
+
+
+def imu_dependence_inflation(transport_sigma, eps_mass=EPS_MASS):
+    """imu_dependence_inflation (imu_evidence.py:562-589)."""
+    s = max(transport_sigma, 0.0)
+    scale = 1.0 / (1.0 + s * s + eps_mass)
+    return dict(scale=scale, trig=trigger(alpha=scale))
+
+
+def imu_gyro_rotation_evidence(rv_start, rv_end_pred, drv_meas, Sigma_g, dt_int, eps_psd=EPS_PSD,
+                               eps_lift=EPS_LIFT):
+    """_imu_gyro_rotation_evidence_jax (imu_gyro_evidence.py:38-85)."""
+    dtp = max(dt_int, 0.0)
+    R_end_imu = so3_exp(rv_start) @ so3_exp(drv_meas)
+    r = so3_log(so3_exp(rv_end_pred).T @ R_end_imu)
+    dte = dtp + EPS_MASS
+    ms = dtp / dte
+    Sp = psd_project(Sigma_g * dte, eps_psd)[0]
+    Lr, lift = chol_inverse_lifted(Sp, eps_lift)
+    L = np.zeros((D_Z, D_Z)); L[3:6, 3:6] = ms * Lr
+    h = np.zeros(D_Z); h[3:6] = (ms * Lr) @ r
+    nll = 0.5 * float(r @ Lr @ r)
+    emin, emax, ev = _eig_stats(psd_project(Lr, eps_psd)[0])
+    return dict(L=L, h=h, r_rot=r, nll=nll, lift=lift, eig_min=emin, eig_max=emax,
+                nnc=float(np.sum(ev < eps_psd)), trig=trigger(lift=lift))
+
+
+def imu_preintegration_factor(p_start, rv_start, v_start, p_end_pred, v_end_pred, dv_body, dp_body, Sigma_a,
+                              dt_int, eps_psd=EPS_PSD, eps_lift=EPS_LIFT):
+    """imu_preintegration_factor (imu_preintegration_factor.py:46-180)."""
+    R = so3_exp(rv_start)
+    r_vel = (v_start + R @ dv_body) - v_end_pred
+    r_pos = (p_start + v_start * dt_int + R @ dp_body) - p_end_pred
+    dtp = max(dt_int, 0.0)
+    dte = dtp + EPS_MASS
+    ms = dtp / dte
+    Lv, lv = chol_inverse_lifted(psd_project(Sigma_a * dte, eps_psd)[0], eps_lift)
+    Lp, lp = chol_inverse_lifted(psd_project(Sigma_a * dte ** 3, eps_psd)[0], eps_lift)
+    L = np.zeros((D_Z, D_Z)); h = np.zeros(D_Z)
+    L[0:3, 0:3] = ms * Lp; h[0:3] = (ms * Lp) @ r_pos
+    L[6:9, 6:9] = ms * Lv; h[6:9] = (ms * Lv) @ r_vel
+    nll = 0.5 * float(r_vel @ Lv @ r_vel) + 0.5 * float(r_pos @ Lp @ r_pos)
+    return dict(L=L, h=h, r_vel=r_vel, r_pos=r_pos, nll=nll, lift=lv + lp, trig=trigger(lift=lv + lp))
+
+
+def planar_z_prior(pose, z_ref=PLANAR_Z_REF, sigma_z=PLANAR_Z_SIGMA):
+    """planar_z_prior (planar_prior.py:55-135)."""
+    r = float(z_ref - pose[2])
+    prec = 1.0 / sigma_z ** 2
+    L = np.zeros((D_Z, D_Z)); L[2, 2] = prec
+    h = np.zeros(D_Z); h[2] = prec * r
+    return dict(L=L, h=h, r_z=r, nll=0.5 * r * r * prec, trig=trigger())
+
+
+def velocity_z_prior(v_z_pred, sigma_vz=PLANAR_VZ_SIGMA):
+    """velocity_z_prior (planar_prior.py:138-195)."""
+    r = -float(v_z_pred)
+    prec = 1.0 / sigma_vz ** 2
+    L = np.zeros((D_Z, D_Z)); L[8, 8] = prec
+    h = np.zeros(D_Z); h[8] = prec * r
+    return dict(L=L, h=h, v_z=float(v_z_pred), nll=0.5 * r * r * prec, trig=trigger())
+
+
+def odom_velocity_evidence(v_pred_world, R_world_body, v_odom_body, Sigma_v, eps_psd=EPS_PSD, eps_lift=EPS_LIFT):
+    """odom_velocity_evidence (odom_twist_evidence.py:58-154)."""
+    r = v_odom_body - R_world_body.T @ v_pred_world
+    Sp = psd_project(Sigma_v, eps_psd)[0]
+    Lv, lift = chol_inverse_lifted(Sp, eps_lift)
+    L = np.zeros((D_Z, D_Z)); L[6:9, 6:9] = Lv
+    h = np.zeros(D_Z); h[6:9] = Lv @ r
+    emin, emax, ev = _eig_stats(Sp)
+    return dict(L=L, h=h, r_vel=r, nll=0.5 * float(r @ Lv @ r), lift=lift, eig_min=emin, eig_max=emax,
+                trig=trigger(lift=lift))
+
+
+def odom_yawrate_evidence(wz_pred, wz_odom, sigma_wz):
+    """odom_yawrate_evidence (odom_twist_evidence.py:157-225)."""
+    r = float(wz_odom) - float(wz_pred)
+    prec = 1.0 / sigma_wz ** 2
+    L = np.zeros((D_Z, D_Z)); L[5, 5] = prec
+    h = np.zeros(D_Z); h[5] = prec * r
+    return dict(L=L, h=h, r_wz=r, nll=0.5 * r * r * prec, trig=trigger())
+
+
+def pose_twist_kinematic_consistency(pose_prev, pose_curr, v_body, omega_body, dt, Sigma_v, Sigma_omega,
+                                     eps_psd=EPS_PSD, eps_lift=EPS_LIFT):
+    """pose_twist_kinematic_consistency (odom_twist_evidence.py:251-397)."""
+    R_prev, R_curr = so3_exp(pose_prev[3:6]), so3_exp(pose_curr[3:6])
+    r_t = (R_prev @ v_body * dt) - (pose_curr[:3] - pose_prev[:3])
+    r_r = (omega_body * dt) - so3_log(R_prev.T @ R_curr)
+    dt2 = dt * dt + eps_psd
+    St = psd_project(dt2 * Sigma_v, eps_psd)[0]
+    Sr = psd_project(dt2 * Sigma_omega, eps_psd)[0]
+    Lt, lt = chol_inverse_lifted(St, eps_lift)
+    Lr, lr = chol_inverse_lifted(Sr, eps_lift)
+    L = np.zeros((D_Z, D_Z)); h = np.zeros(D_Z)
+    L[0:3, 0:3] = Lt; L[3:6, 3:6] = Lr
+    h[0:3] = Lt @ r_t; h[3:6] = Lr @ r_r
+    nll = 0.5 * float(r_t @ Lt @ r_t) + 0.5 * float(r_r @ Lr @ r_r)
+    return dict(L=L, h=h, r_trans=r_t, r_rot=r_r, nll=nll, lift=lt + lr, trig=trigger(lift=lt + lr))
+
+
+def odom_dependence_inflation(r_trans, r_rot, eps_mass=EPS_MASS):
+    """odom_dependence_inflation (odom_twist_evidence.py:400-430)."""
+    mag = float(np.linalg.norm(r_trans) + np.linalg.norm(r_rot))
+    scale = 1.0 / (1.0 + mag * mag + eps_mass)
+    return dict(scale=scale, trig=trigger(alpha=scale))
+
+
+@dataclass
+class OdomInput:
+    """Per-scan odometry the node hands the pipeline (backend_node.py:1748-1765): relative pose
+    (6), pose covariance (6,6) in [trans, rot] order, twist (6) [v, ω] body, twist cov (6,6)."""
+    pose: np.ndarray
+    cov: np.ndarray
+    twist: np.ndarray
+    twist_cov: np.ndarray
+
+
+def imu_odom_branch(b_prev: Belief, b_pred: Belief, odom: OdomInput, imu_accel, imu_gyro, w_int, ba, pre_int,
+                    dt_int, dt_imu, omega_avg, dt_sec, Sigma_g, Sigma_a, g=GRAVITY_W, z_ref=PLANAR_Z_REF,
+                    sigma_z=PLANAR_Z_SIGMA, sigma_vz=PLANAR_VZ_SIGMA, eps_psd=EPS_PSD, eps_lift=EPS_LIFT,
+                    eps_mass=EPS_MASS):
+    """_compute_imu_odom_branch (pipeline.py:595-776): the 11 factors, their dependence scalings
+    and the summed (L_io, h_io). Returns (IOEvidence, parts). z_lin_pose (:751-755) feeds only the
+    primitive-map branch (visual_pose_evidence), which the bin path does not run."""
+    pose_pred = world_pose(b_pred)
+    pose0 = world_pose(b_prev)
+    rv0 = pose0[3:6]
+    mu_inc = mean_increment(b_pred)
+    od = odom_quadratic_evidence(pose_pred, odom.pose, odom.cov, eps_psd, eps_lift)
+    im = imu_vmf_gravity_evidence_time_resolved(pose_pred[3:6], imu_accel, imu_gyro, w_int, ba, g, dt_imu,
+                                                eps_psd, eps_mass)
+    dep = imu_dependence_inflation(im["transport_sigma"], eps_mass)
+    gy = imu_gyro_rotation_evidence(rv0, pose_pred[3:6], pre_int["delta_pose"][3:6], Sigma_g, dt_int, eps_psd,
+                                    eps_lift)
+    v_start = mean_increment(b_prev)[6:9]
+    pr = imu_preintegration_factor(pose0[0:3], rv0, v_start, pose_pred[0:3], mu_inc[6:9], pre_int["delta_v"],
+                                   pre_int["delta_p"], Sigma_a, dt_int, eps_psd, eps_lift)
+    pl = planar_z_prior(pose_pred, z_ref, sigma_z)
+    vz = velocity_z_prior(mu_inc[8], sigma_vz)
+    ov = odom_velocity_evidence(mu_inc[6:9], so3_exp(pose_pred[3:6]), odom.twist[0:3], odom.twist_cov[0:3, 0:3],
+                                eps_psd, eps_lift)
+    sig_wz = math.sqrt(max(odom.twist_cov[5, 5], 1e-12))
+    wz = odom_yawrate_evidence(omega_avg[2], odom.twist[5], sig_wz)
+    kc = pose_twist_kinematic_consistency(pose0, pose_pred, odom.twist[0:3], odom.twist[3:6], dt_sec,
+                                          odom.twist_cov[0:3, 0:3], odom.twist_cov[3:6, 3:6], eps_psd, eps_lift)
+    odep = odom_dependence_inflation(kc["r_trans"], kc["r_rot"], eps_mass)
+    si, so = dep["scale"], odep["scale"]
+    L = (od["L"] * so + im["L"] * si + gy["L"] * si + pr["L"] + pl["L"] + vz["L"] + ov["L"] * so + wz["L"] * so
+         + kc["L"])
+    h = (od["h"] * so + im["h"] * si + gy["h"] * si + pr["h"] + pl["h"] + vz["h"] + ov["h"] * so + wz["h"] * so
+         + kc["h"])
+    parts = [od, im, dep, gy, pr, pl, vz, ov, wz, kc, odep]
+    io = IOEvidence(L=L, h=h, ess=np.array([0.0, im["ess_weighted"], 0.0]),
+                    support=np.array([1.0, im["mean_reliability"], 1.0]), exc_dt=0.0, exc_ex=0.0,
+                    nll=od["nll"] + im["nll_per_ess"] + gy["nll"], trig=float(sum(p["trig"] for p in parts)))
+    return io, dict(odom=od, imu=im, imu_dep=dep, gyro=gy, preint=pr, planar=pl, vz=vz, odom_vel=ov, odom_wz=wz,
+                    kinematic=kc, odom_dep=odep)
+
+
 def tempering_beta(L_raw, ess_total, exc_total):
     """pipeline.py:1070-1111."""
     eps = EPS_MASS
@@ -845,6 +1099,7 @@ class ScanInput:
     t_last: float
     t_scan: float
     dt_sec: float
+    odom: "OdomInput" = None
 
 
 @dataclass
@@ -856,8 +1111,10 @@ class PipeConfig:
 
 
 def scan_hypothesis(b_prev: Belief, scan: ScanInput, Q, io: IOEvidence, mapst: MapStats, mderived,
-                    bins, cfg: PipeConfig):
-    """One hypothesis through steps a1-a14 (pipeline.py:316-1591 restated for the bin path)."""
+                    bins, cfg: PipeConfig, Sigma_ga=None):
+    """One hypothesis through steps a1-a14 (pipeline.py:316-1591 restated for the bin path).
+    io=None: the IMU/odom branch is computed from scan.odom and the IMU window (a9a), with
+    Sigma_ga = (Σ_g, Σ_a) the measurement-IW modes (backend_node.py:2021-2023)."""
     o = cfg.lidar_origin
     bud = point_budget_resample(scan.points, scan.timestamps, scan.weights, scan.ring, scan.tag, cfg.n_points_cap)
     pts, ts, ws = bud["points"], bud["timestamps"], bud["weights"]
@@ -880,6 +1137,12 @@ def scan_hypothesis(b_prev: Belief, scan: ScanInput, Q, io: IOEvidence, mapst: M
     dPsi_meas[0] = iw_meas_gyro_suffstats(scan.imu_gyro, wv, bg, omega_avg, dt_imu)
     dPsi_meas[1] = iw_meas_accel_suffstats(rv0, scan.imu_accel, wv, ba, dt_imu)
     dnu_meas = np.array([1.0, 1.0, 0.0])
+    io_parts = None
+    if io is None:
+        pre_int = preintegrate(scan.imu_stamps, scan.imu_gyro, scan.imu_accel, w_int, rv0, bg, ba)
+        dt_int = imu_integration_time(scan.imu_stamps, scan.t_last, scan.t_scan)
+        io, io_parts = imu_odom_branch(b_prev, bpred, scan.odom, scan.imu_accel, scan.imu_gyro, w_int, ba, pre_int,
+                                       dt_int, dt_imu, omega_avg, scan.dt_sec, Sigma_ga[0], Sigma_ga[1])
     p0, wd, retained = deskew_constant_twist(pts, ts, ws, scan.scan_start, scan.scan_end, xi)
     dirs = point_directions(p0, o)
     sa = bin_soft_assign(dirs, bins, cfg.tau)
@@ -924,7 +1187,8 @@ def scan_hypothesis(b_prev: Belief, scan: ScanInput, Q, io: IOEvidence, mapst: M
     return dict(belief=b_fin, dPsi_proc=dPsi_p, dnu_proc=dnu_p, dPsi_meas=dPsi_meas, dnu_meas=dnu_meas,
                 map_inc=inc, T=T, beta=beta, alpha=alpha, s_dt=s_dt, s_ex=s_ex, xi_body=xi,
                 moments=mm, assign=sa, mf=mf, planar=tr, rho=dr["rho"], frob=rc["frobenius_strength"],
-                budget=bud, retained=retained, pose=world_pose(b_fin), L_post=L_post, h_post=h_post)
+                budget=bud, retained=retained, pose=world_pose(b_fin), L_post=L_post, h_post=h_post,
+                io=io, io_parts=io_parts)
 
 
 @dataclass
@@ -946,7 +1210,9 @@ def process_scan(state: ScanState, scan: ScanInput, ios, bins, cfg: PipeConfig, 
     H = len(state.beliefs)
     Q = iw_process_Q(state.nu_proc, state.Psi_proc)
     md = map_derived(state.map)
-    res = [scan_hypothesis(state.beliefs[i], scan, Q, ios[i], state.map, md, bins, cfg) for i in range(H)]
+    Sga = (iw_meas_mode(state.nu_meas, state.Psi_meas, 0), iw_meas_mode(state.nu_meas, state.Psi_meas, 1))
+    res = [scan_hypothesis(state.beliefs[i], scan, Q, None if ios is None else ios[i], state.map, md, bins, cfg,
+                           Sga) for i in range(H)]
     aP = np.zeros((7, 6, 6)); an = np.zeros(7); aM = np.zeros((3, 3, 3)); am = np.zeros(3)
     for i, r in enumerate(res):
         w = float(state.weights[i])
