@@ -70,8 +70,10 @@ GC_DEV void group16_argmax(double& best, int& bidx) {
 }
 
 // exp(x) for the softmax arguments x <= ~0 (x = (s - 1)/τ, |s| <= 1): 256-entry 2^(j/256)
-// table in LDS, Cody-Waite reduction r = x - k ln2/256 (|r| <= ln2/512), degree-4 Taylor
+// table in LDS, k = rint(x 256/ln2) by the round-to-integer magic constant (one FMA, k read
+// from the low word), Cody-Waite reduction r = x - k ln2/256 (|r| <= ln2/512), degree-4 Taylor
 // (truncation < 4e-17 relative), ldexp. ~12 f64 ops instead of ocml's general-range exp.
+// Valid for x >= -5.8e6 (k fits in 32 bits; callers clamp).
 constexpr int kExpTab = 256;
 constexpr double kLn2OverTabHi = 0x1.62e42ffp-9;               // ln2/256, 24 trailing zero bits
 constexpr double kLn2OverTabLo = -1.6409824502660487e-13;      // ln2/256 - hi
@@ -79,9 +81,11 @@ constexpr double kTabOverLn2 = 369.3299304675746;              // 256 / ln2
 GC_DEV void exp_table_init(double* T) {  // needs blockDim.x >= 256
   if (threadIdx.x < kExpTab) T[threadIdx.x] = exp2((double)threadIdx.x / kExpTab);
 }
+constexpr double kRoundMagic = 6755399441055744.0;  // 1.5 * 2^52: fma(y, c, M) - M = rint(y c)
 GC_DEV double exp_neg(double x, const double* T) {
-  const double kf = rint(x * kTabOverLn2);
-  const int k = (int)kf;
+  const double ks = fma(x, kTabOverLn2, kRoundMagic);  // k = rint(x 256/ln2) in the low word
+  const double kf = ks - kRoundMagic;
+  const int k = __double2loint(ks);
   const double r = fma(-kf, kLn2OverTabLo, fma(-kf, kLn2OverTabHi, x));
   double p = fma(r, 1.0 / 24.0, 1.0 / 6.0);
   p = fma(p, r, 0.5);
@@ -94,10 +98,13 @@ GC_DEV double exp_neg(double x, const double* T) {
 template <int N>
 GC_DEV void exp_neg_n(const double (&x)[N], const double* T, double (&out)[N]) {
   double kf[N], tv[N];
+  int ki[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    kf[j] = rint(x[j] * kTabOverLn2);
-    tv[j] = T[(int)kf[j] & (kExpTab - 1)];
+    const double ks = fma(x[j], kTabOverLn2, kRoundMagic);
+    kf[j] = ks - kRoundMagic;
+    ki[j] = __double2loint(ks);
+    tv[j] = T[ki[j] & (kExpTab - 1)];
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) {
@@ -106,7 +113,7 @@ GC_DEV void exp_neg_n(const double (&x)[N], const double* T, double (&out)[N]) {
     p = fma(p, r, 0.5);
     p = fma(p, r, 1.0);
     p = fma(p, r, 1.0);
-    out[j] = ldexp(tv[j] * p, (int)kf[j] >> 8);
+    out[j] = ldexp(tv[j] * p, ki[j] >> 8);
   }
 }
 // 1/z for z > 0 in a normal range: hardware reciprocal + two Newton steps (<= 1 ulp).
@@ -158,6 +165,54 @@ GC_DEV void deskew_point(const double* p, double alpha, const double* xi, double
   rodrigues_form(phi, a, b, R);
   q[0] = p[0] - t[0]; q[1] = p[1] - t[1]; q[2] = p[2] - t[2];
   mat3_tvec(R, q, out);
+}
+
+// Fused-kernel variants of the three per-point helpers: reciprocals (hardware rcp + 2 Newton
+// steps, <= 1 ulp) instead of IEEE divisions and the LDS-table exp in the window sigmoid.
+// Results agree with the exact forms to a few ulps; they feed only floating-point moments
+// (the bit-exact bin-index contract runs through direction() / k_point_dirs).
+GC_DEV void deskew_point_fast(const double* p, double alpha, const double* xi, double* out) {
+  const double rho[3] = {alpha * xi[0], alpha * xi[1], alpha * xi[2]};
+  const double phi[3] = {alpha * xi[3], alpha * xi[4], alpha * xi[5]};
+  const double ts = dot3(phi, phi);
+  const double th = sqrt(ts);
+  double Bv, Cv, a, b;
+  if (th < kSmallAngle) {
+    Bv = 0.5 - ts * (1.0 / 24.0);
+    Cv = 1.0 / 6.0 - ts * (1.0 / 120.0);
+    a = 1.0;
+    b = 0.5;
+  } else {
+    double sn, c;
+    sincos(th, &sn, &c);
+    const double its = recip((ts < kSmallAngle * kSmallAngle) ? 1.0 : ts);
+    const double ith = recip(th);
+    Bv = (1.0 - c) * its;
+    Cv = (th - sn) * its * ith;
+    a = sn * ith;
+    b = Bv;
+  }
+  double V[9], R[9], t[3], q[3];
+  rodrigues_form(phi, Bv, Cv, V);
+  mat3_vec(V, rho, t);
+  rodrigues_form(phi, a, b, R);
+  q[0] = p[0] - t[0]; q[1] = p[1] - t[1]; q[2] = p[2] - t[2];
+  mat3_tvec(R, q, out);
+}
+GC_DEV void direction_fast(const double* p, const double* o, double eps, double* d) {
+  const double r0 = p[0] - o[0], r1 = p[1] - o[1], r2 = p[2] - o[2];
+  const double inv = recip(sqrt(r0 * r0 + r1 * r1 + r2 * r2) + eps);
+  d[0] = r0 * inv; d[1] = r1 * inv; d[2] = r2 * inv;
+}
+// σ(x) = 1 / (1 + e^{-x}) from e = exp(-|x|) (table exp; arguments below -745 underflow to 0)
+GC_DEV double sigmoid_fast(double x, const double* T) {
+  const double e = exp_neg(fmax(-fabs(x), -800.0), T);
+  const double r = recip(1.0 + e);
+  return x >= 0.0 ? r : e * r;
+}
+GC_DEV double window_weight_fast(double t, double t0, double t1, double inv_sig, const double* T) {
+  const double wr = sigmoid_fast((t - t0) * inv_sig, T) * sigmoid_fast((t1 - t) * inv_sig, T);
+  return wr * (1.0 - 1e-12) + 1e-12;
 }
 
 // Features g (pre-multiplied by w) for the moment sums of binning.py:160-173.
@@ -670,7 +725,7 @@ constexpr int kFusedFS = 66;
 #ifndef GC_FUSED_NACC
 #define GC_FUSED_NACC 2  // MFMA accumulator sets (even / odd steps)
 #endif
-template <int BPL>
+template <int BPL, bool FULL>
 __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap, int B, int iters,
                                                     const double* __restrict__ pts_raw,
                                                     const double* __restrict__ t_raw,
@@ -696,7 +751,8 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   const int64_t n_sel = (int64_t)bscal[5];
   const int64_t stride = (int64_t)bscal[6];
   const double denom = fmax(t1 - t0, 1e-12);
-  const double sig = 0.1 * denom;
+  const double inv_denom = 1.0 / denom;
+  const double inv_sig = 1.0 / fmax(0.1 * denom, 1e-6);
   double* Tx = lds + 4 * kFusedFS * NS;
   double* Lb = Tx + kExpTab;  // bin directions pre-scaled by 1/τ (x, y, z rows of 64)
   exp_table_init(Tx);
@@ -734,9 +790,9 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
         ww = w_raw[i] * scale;
       }
       double q[3], d[3], f[NF];
-      deskew_point(p, (tt - t0) / denom, xr, q);
-      const double wd = inr ? ww * window_weight(tt, t0, t1, sig) : 0.0;
-      direction(q, o, 1e-12, d);
+      deskew_point_fast(p, (tt - t0) * inv_denom, xr, q);
+      const double wd = inr ? ww * window_weight_fast(tt, t0, t1, inv_sig, Tx) : 0.0;
+      direction_fast(q, o, 1e-12, d);
       point_features(q, d, wd, f);
       sumw += wd;
 #pragma unroll
@@ -763,7 +819,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
       exp_neg_n<BPL>(x, Tx, ex);
 #pragma unroll
       for (int j = 0; j < BPL; ++j) {
-        e[j] = (bl + 16 * j < B) ? ex[j] : 0.0;
+        e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
         zl += e[j];
         sl = fma(e[j], x[j], sl);
         em = fmax(em, e[j]);
@@ -801,6 +857,173 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
     if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
   write_partial_record_mfma<BPL, NX>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds,
                                      partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
+}
+
+// Lane-per-point fused kernel (the product path). Phase A as in k_bins_fused (lane = point:
+// budget gather, deskew, direction, 19 features). Phase B keeps the whole softmax of a point in
+// its lane: the 16*BPL similarities against the 1/τ-prescaled bins (wave-uniform scalar loads),
+// exps (LDS table), Z, the entropy partial and the max responsibility are lane-local, so there
+// is no cross-lane butterfly and one reciprocal per point instead of one per 4-point step. The
+// features are pre-multiplied by 1/Z (Σ_p e_pb (F_pk / Z_p) = Σ_p R_pb F_pk, rounding order
+// only), so the MFMA A operand is the raw e. The point's e row is transposed through a
+// wave-private LDS slab (row stride NB + 2: conflict-free ds_write_b128 rows and ds_read_b64
+// columns) and consumed by 16 steps of BPL v_mfma_f64_16x16x4_f64 (features 0..15) plus VALU
+// FMAs (16..18), 2*BPL independent accumulation chains. f64 MFMA and f64 VALU share the DP
+// pipe on gfx950 (tools/probe/probe_rates.hip), so the kernel is bound by issued DP
+// instructions; this layout issues ~1/3 fewer than k_bins_fused. The e row (2 NB VGPRs) and the
+// full slab (36 KB per wave) size it for one wave per SIMD (up to 512 VGPR+AGPR); the next
+// iteration's point loads are issued before the softmax to cover their latency.
+#ifndef GC_LP_OCC
+#define GC_LP_OCC 1
+#endif
+template <int BPL>
+constexpr int lp_es() { return 16 * BPL + 2; }
+template <int BPL, bool FULL>
+__global__ void __launch_bounds__(256, GC_LP_OCC) k_bins_fused_lp(int64_t n_cap, int B, int iters,
+                                                          const double* __restrict__ pts_raw,
+                                                          const double* __restrict__ t_raw,
+                                                          const double* __restrict__ w_raw,
+                                                          const double* __restrict__ bscal, double t0, double t1,
+                                                          const double* __restrict__ xi,
+                                                          const double* __restrict__ bins_scaled, double inv_tau,
+                                                          double o0, double o1, double o2, double* partials) {
+  constexpr int NF = NF_BASE;
+  constexpr int NX = NF - 16;  // features on the VALU
+  constexpr int NB = 16 * BPL;
+  constexpr int ES = lp_es<BPL>();
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
+  extern __shared__ double lds[];
+  const int h = blockIdx.y;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, bl = lane & 15;
+  double* F = lds + wv * (NF * kFusedFS);                    // [feature][point] x 1/Z
+  double* E = lds + 4 * NF * kFusedFS + wv * (64 * ES);       // [point][bin]
+  double* Tx = lds + 4 * NF * kFusedFS + 4 * 64 * ES;         // exp table
+  const double o[3] = {o0, o1, o2};
+  double xr[6];
+#pragma unroll
+  for (int k = 0; k < 6; ++k) xr[k] = xi[6 * h + k];
+  const double scale = bscal[2];
+  const int64_t n_sel = (int64_t)bscal[5];
+  const int64_t stride = (int64_t)bscal[6];
+  const double denom = fmax(t1 - t0, 1e-12);
+  const double inv_denom = 1.0 / denom;
+  const double inv_sig = 1.0 / fmax(0.1 * denom, 1e-6);
+  exp_table_init(Tx);
+  __syncthreads();
+  v4d acc4[2][BPL];  // even / odd steps
+  double accx[BPL][NX];
+#pragma unroll
+  for (int jt = 0; jt < BPL; ++jt) {
+    acc4[0][jt] = v4d{0.0, 0.0, 0.0, 0.0};
+    acc4[1][jt] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < NX; ++t) accx[jt][t] = 0.0;
+  }
+  double sumw = 0.0, logacc = 0.0, entq = 0.0, mxr = 0.0;
+  const double xmax = inv_tau;  // S <= 1 for unit vectors: exp never overflows
+  const double Beps = (double)B * 1e-12;
+  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
+  // raw point of this lane for iteration `it` (clamped, branch-free; selection applied after)
+  double np0, np1, np2, nt, nw;
+  auto load_raw = [&](int it) {
+    const int64_t j = chunk0 + (int64_t)it * 256 + wv * 64 + lane;
+    const int64_t jj = j < n_sel ? j : (n_sel > 0 ? n_sel - 1 : 0);
+    const int64_t i = jj * stride;
+    np0 = pts_raw[3 * i]; np1 = pts_raw[3 * i + 1]; np2 = pts_raw[3 * i + 2];
+    nt = t_raw[i];
+    nw = w_raw[i];
+  };
+  load_raw(0);
+  for (int it = 0; it < iters; ++it) {
+    const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
+    // ---- phase A: lane = point
+    const int64_t j = wbase + lane;
+    const bool inr = j < n_cap;
+    const bool sel = inr && j < n_sel;
+    double p[3] = {sel ? np0 : 0.0, sel ? np1 : 0.0, sel ? np2 : 0.0};
+    const double tt = sel ? nt : 0.0, ww = sel ? nw * scale : 0.0;
+    if (it + 1 < iters) load_raw(it + 1);  // in flight across this iteration's softmax
+    double q[3], d[3];
+    deskew_point_fast(p, (tt - t0) * inv_denom, xr, q);
+    const double wd = inr ? ww * window_weight_fast(tt, t0, t1, inv_sig, Tx) : 0.0;
+    direction_fast(q, o, 1e-12, d);
+    sumw += wd;
+    lds_wave_sync();  // the previous iteration's operand reads are done
+    {  // features parked in the lane's own slab column until 1/Z is known
+      double f[NF];
+      point_features(q, d, wd, f);
+#pragma unroll
+      for (int k = 0; k < NF; ++k) F[k * kFusedFS + lane] = f[k];
+    }
+    // ---- phase B: the point's softmax, lane-local
+    const __attribute__((address_space(4))) double* bp = (const __attribute__((address_space(4))) double*)bins_scaled;
+    double e[NB];
+    double Z = 0.0, sl = 0.0, em = 0.0;
+#pragma unroll
+    for (int j0 = 0; j0 < NB; j0 += 8) {
+      asm volatile("" : "+s"(bp));  // this group's scalar loads are issued here, not all up front
+      double x[8], e8[8];
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int b = j0 + jj;  // bins past B are zero: x = -1/τ stays finite, then masked
+        x[jj] = fma(d[0], bp[3 * b], fma(d[1], bp[3 * b + 1], fma(d[2], bp[3 * b + 2], -xmax)));
+      }
+      exp_neg_n<8>(x, Tx, e8);
+#pragma unroll
+      for (int jj = 0; jj < 8; ++jj) {
+        const int b = j0 + jj;
+        e[b] = (FULL || b < B) ? e8[jj] : 0.0;
+        Z += e[b];
+        sl = fma(e[b], x[jj], sl);
+        em = e[b] > em ? e[b] : em;
+      }
+    }
+#pragma unroll
+    for (int qd = 0; qd < NB / 2; ++qd)
+      *reinterpret_cast<dvec2*>(&E[lane * ES + 2 * qd]) = dvec2{e[2 * qd], e[2 * qd + 1]};
+    const double rZ = recip(Z);
+    if (inr) {
+      logacc += log(Z);
+      entq = fma(sl, rZ, entq);
+      const double mr = em * rZ;
+      mxr = mr > mxr ? mr : mxr;
+    }
+#pragma unroll
+    for (int k = 0; k < NF; ++k) F[k * kFusedFS + lane] *= rZ;  // own column: no cross-lane hazard
+    lds_wave_sync();
+#pragma unroll 2
+    for (int s = 0; s < 16; ++s) {
+      const int pl = s * 4 + g;
+      const double fb = F[bl * kFusedFS + pl];  // B: feature bl of point 4s + g
+      double fk[NX];
+#pragma unroll
+      for (int t = 0; t < NX; ++t) fk[t] = F[(16 + t) * kFusedFS + pl];
+#pragma unroll
+      for (int jt = 0; jt < BPL; ++jt) {
+        const double a = E[pl * ES + 16 * jt + bl];  // A: e of bin 16 jt + bl, point 4s + g
+        acc4[s & 1][jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb, acc4[s & 1][jt], 0, 0, 0);
+#pragma unroll
+        for (int t = 0; t < NX; ++t) accx[jt][t] = fma(a, fk[t], accx[jt][t]);
+      }
+    }
+  }
+  // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
+  int64_t npts = n_cap - chunk0;
+  npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
+  const double ent = logacc - entq - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
+  const int RL = B * NF + REC_EXTRA;
+#pragma unroll
+  for (int jt = 0; jt < BPL; ++jt) acc4[0][jt] += acc4[1][jt];
+  __syncthreads();
+  write_partial_record_mfma<BPL, NX>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds,
+                                     partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
+}
+
+// bins / τ, zero-padded to 16 * BPL rows (the lane-per-point kernel's scalar-load operand)
+__global__ void k_scale_bins(int B, int NB, const double* __restrict__ bins, double inv_tau, double* out) {
+  const int i = threadIdx.x;
+  if (i < 3 * NB) out[i] = (i < 3 * B) ? bins[i] * inv_tau : 0.0;
 }
 
 // ================================================================ finalize (a6 + certs)
@@ -1080,16 +1303,23 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const int64_t chunks = (n_cap + iters * 256 - 1) / (iters * 256);
   const int NF = NF_BASE;
   const int RL = B * NF + REC_EXTRA;
+  const int bpl = bpl_for(B);
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
   const size_t sh = sizeof(double) * std::max<size_t>(4 * kFusedFS * (NF + 4) + kExpTab + 192, 4 * (size_t)B * NF + 12);
   dim3 grid((unsigned)chunks, H);
   const double inv_tau = 1.0 / tau;
-#define GC_FUSED(BP)                                                                                     \
-  hipLaunchKernelGGL((k_bins_fused<BP>), grid, dim3(256), sh, ctx->stream, n_cap, B, iters, d_points_raw, \
-                     d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins, inv_tau, h_origin3[0],     \
+#define GC_FUSED(BP, FULL)                                                                                     \
+  hipLaunchKernelGGL((k_bins_fused<BP, FULL>), grid, dim3(256), sh, ctx->stream, n_cap, B, iters, d_points_raw, \
+                     d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins, inv_tau, h_origin3[0],            \
                      h_origin3[1], h_origin3[2], (double*)scr)
-  switch (bpl_for(B)) { case 1: GC_FUSED(1); break; case 2: GC_FUSED(2); break; case 3: GC_FUSED(3); break; default: GC_FUSED(4); }
+  const bool full = B == 16 * bpl;
+  switch (bpl) {
+    case 1: if (full) { GC_FUSED(1, true); } else { GC_FUSED(1, false); } break;
+    case 2: if (full) { GC_FUSED(2, true); } else { GC_FUSED(2, false); } break;
+    case 3: if (full) { GC_FUSED(3, true); } else { GC_FUSED(3, false); } break;
+    default: if (full) { GC_FUSED(4, true); } else { GC_FUSED(4, false); } break;
+  }
 #undef GC_FUSED
   GC_LAUNCH_CHECK(ctx);
   return launch_finalize(ctx, H, B, NF, chunks, (const double*)scr, eps_psd, eps_mass, d_stats_out, d_cert_out);

@@ -1,5 +1,6 @@
 // Dev probe (not product): the fused a1->a6 bins kernel at C3 size (64k points x 256 hypotheses),
-// built per tuning variant with -DGC_FUSED_OCC / -DGC_FUSED_NACC.
+// built per tuning variant with -DGC_FUSED_OCC / -DGC_FUSED_NACC / -DGC_LP_OCC; times the
+// bin-distributed kernel (k_bins_fused) and the lane-per-point product kernel (k_bins_fused_lp).
 #include "../../fl-slam_amd/csrc/gc_points.hip"
 #include <cstdio>
 #include <vector>
@@ -30,10 +31,20 @@ int main() {
   hipMemcpy(xi, hx.data(), 8 * 6 * H, hipMemcpyHostToDevice); hipMemcpy(bins, hb.data(), 8 * 3 * B, hipMemcpyHostToDevice);
   const size_t sh = sizeof(double) * std::max<size_t>(4 * gc::kFusedFS * (gc::NF_BASE + 4) + gc::kExpTab + 192, 4 * (size_t)B * gc::NF_BASE + 12);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
-  auto run = [&] { hipLaunchKernelGGL((gc::k_bins_fused<3>), dim3(chunks, H), dim3(256), sh, 0, n, B, iters, p, t, w, bs, 100.0, 100.1, xi, bins, 10.0, -0.06, -0.1, 0.1, part); };
+  auto run = [&] { hipLaunchKernelGGL((gc::k_bins_fused<3, true>), dim3(chunks, H), dim3(256), sh, 0, n, B, iters, p, t, w, bs, 100.0, 100.1, xi, bins, 10.0, -0.06, -0.1, 0.1, part); };
   run(); hipDeviceSynchronize();
   hipEventRecord(e0); for (int r = 0; r < 10; ++r) run(); hipEventRecord(e1); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
   printf("k_bins_fused<3> occ=%d nacc=%d: %.3f ms/launch (%s)\n", GC_FUSED_OCC, GC_FUSED_NACC, ms / 10, hipGetErrorString(hipGetLastError()));
+  // lane-per-point variant (product path)
+  double* bsc; hipMalloc(&bsc, 8 * 3 * 64);
+  hipLaunchKernelGGL(gc::k_scale_bins, dim3(1), dim3(192), 0, 0, B, 48, bins, 10.0, bsc);
+  const size_t sh2 = sizeof(double) * (4 * gc::kFusedFS * gc::NF_BASE + 4 * 64 * 50 + gc::kExpTab);
+  hipFuncSetAttribute((const void*)gc::k_bins_fused_lp<3, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh2);
+  auto run2 = [&] { hipLaunchKernelGGL((gc::k_bins_fused_lp<3, true>), dim3(chunks, H), dim3(256), sh2, 0, n, B, iters, p, t, w, bs, 100.0, 100.1, xi, bsc, 10.0, -0.06, -0.1, 0.1, part); };
+  run2(); hipDeviceSynchronize();
+  hipEventRecord(e0); for (int r = 0; r < 10; ++r) run2(); hipEventRecord(e1); hipEventSynchronize(e1);
+  hipEventElapsedTime(&ms, e0, e1);
+  printf("k_bins_fused_lp<3,full> occ=%d: %.3f ms/launch (%s)\n", GC_LP_OCC, ms / 10, hipGetErrorString(hipGetLastError()));
   return 0;
 }
