@@ -274,7 +274,9 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     for (int k = 0; k < 3; ++k) dg[24 + k] = wmf[k];      // log R_mf
     for (int k = 0; k < 3; ++k) dg[27 + k] = mf[24 + k];  // MF singular values
     for (int k = 0; k < 6; ++k) dg[30 + k] = P.xi[(int64_t)hl * 6 + k];
-    dg[36] = sc[54]; dg[37] = sc[55]; dg[38] = 0.0; dg[39] = 0.0;
+    double mu2 = 0.0;
+    for (int k = 0; k < n; ++k) mu2 += mufin[k] * mufin[k];
+    dg[36] = sc[54]; dg[37] = sc[55]; dg[38] = mu2; dg[39] = 0.0;  // |μ|² for the combine's spread
   }
 }
 
@@ -292,28 +294,41 @@ __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
   const double wsum = wg_sum(loc, red);
   const int e = blockIdx.x * 64 + lane;
   const int PLn = partial_len(P.B);
-  double s = 0.0;
-  if (e < kPMAP) {
-    for (int k = g; k < Hl; k += 4) {
-      const double wr = P.weights[P.h_begin + k];
-      const double wn = fmax(wr, P.weight_floor) / wsum;
-      double v = 0.0;
-      if (e < kPH) v = wn * P.L[(int64_t)k * NN + e];
-      else if (e < kPZ) v = wn * P.h[(int64_t)k * n + (e - kPH)];
-      else if (e < kPMU) v = wn * P.z[(int64_t)k * n + (e - kPZ)];
-      else if (e < kPMU2) v = wn * P.mu_fin[(int64_t)k * n + (e - kPMU)];
-      else if (e == kPMU2) {
-        double q = 0.0;
-        for (int i = 0; i < n; ++i) q += P.mu_fin[(int64_t)k * n + i] * P.mu_fin[(int64_t)k * n + i];
-        v = wn * q;
-      } else if (e < kPDNUP) v = wr * P.dPsiP[(int64_t)k * 252 + (e - kPDPSIP)];
-      else if (e < kPDPSIM) v = wr;
-      else if (e < kPDNUM) v = wr * P.dPsiM[(int64_t)k * 27 + (e - kPDPSIM)];
-      else if (e < kPDNUM + 3) v = (e - kPDNUM < 2) ? wr : 0.0;
-      s += v;
+  // this lane's record entry as (source row, stride, weight kind), resolved once; the hypothesis
+  // loop is then branch-free (clamped rows, 0/1 masks) with 16 independent loads in flight
+  const double* W = P.weights + P.h_begin;
+  const double* src = W;
+  int64_t stride = 0;
+  double use_src = 0.0, use_norm = 0.0, live = 1.0;  // value = w * (use_src ? src : 1)
+  if (e < kPH) { src = P.L + e; stride = NN; use_src = 1.0; use_norm = 1.0; }
+  else if (e < kPZ) { src = P.h + (e - kPH); stride = n; use_src = 1.0; use_norm = 1.0; }
+  else if (e < kPMU) { src = P.z + (e - kPZ); stride = n; use_src = 1.0; use_norm = 1.0; }
+  else if (e < kPMU2) { src = P.mu_fin + (e - kPMU); stride = n; use_src = 1.0; use_norm = 1.0; }
+  else if (e == kPMU2) { src = P.diag + 38; stride = kHypDiag; use_src = 1.0; use_norm = 1.0; }  // |μ|², k_evidence
+  else if (e < kPDNUP) { src = P.dPsiP + (e - kPDPSIP); stride = 252; use_src = 1.0; }
+  else if (e < kPDPSIM) { }  // dν_proc: w
+  else if (e < kPDNUM) { src = P.dPsiM + (e - kPDPSIM); stride = 27; use_src = 1.0; }
+  else if (e < kPDNUM + 2) { }  // dν_meas gyro/accel: w
+  else live = 0.0;
+  const double inv_wsum = 1.0 / wsum;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int k0 = g; k0 < Hl; k0 += 64) {
+    double v[16], wr[16], m[16];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int k = k0 + 4 * j;
+      const int kc = k < Hl ? k : Hl - 1;
+      m[j] = k < Hl ? live : 0.0;
+      wr[j] = W[kc];
+      v[j] = src[(int64_t)kc * stride];
+    }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const double wk = use_norm != 0.0 ? fmax(wr[j], P.weight_floor) * inv_wsum : wr[j];
+      acc[j & 3] += m[j] * wk * (use_src != 0.0 ? v[j] : 1.0);
     }
   }
-  part[g][lane] = s;
+  part[g][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
   if (g == 0 && e < PLn) {
     double r = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);

@@ -1042,8 +1042,16 @@ __global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t ch
     double v = 0.0;
     if (i == B * NF + 1) {
       for (int64_t c = 0; c < chunks; ++c) v = fmax(v, P[c * RL + i]);
-    } else {
-      for (int64_t c = 0; c < chunks; ++c) v += P[c * RL + i];
+    } else {  // chunk order fixed; 8 loads in flight per lane
+      int64_t c = 0;
+      for (; c + 8 <= chunks; c += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = P[(c + u) * RL + i];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v += x[u];
+      }
+      for (; c < chunks; ++c) v += P[c * RL + i];
     }
     sm[i] = v;
   }
@@ -1067,7 +1075,24 @@ __global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t ch
         if (NF > NF_BASE) v += a[NF_BASE + 3 * i + j] * invN;
         Sr[3 * i + j] = v;
       }
-    psd_project3(Sr, eps_psd, Sp, c6);
+    // certified shortcut (as wg_psd_project_fast): Cholesky of Σ_sym - εI succeeds => the clamp
+    // is inactive and the projection is Σ_sym itself (projection delta 0 up to rounding)
+    {
+      double S[9];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) S[3 * i + j] = 0.5 * (Sr[3 * i + j] + Sr[3 * j + i]);
+      const double a00 = S[0] - eps_psd;
+      const double l10 = S[3] / sqrt(fmax(a00, 1e-300)), l20 = S[6] / sqrt(fmax(a00, 1e-300));
+      const double a11 = S[4] - eps_psd - l10 * l10;
+      const double l21 = (S[7] - l20 * l10) / sqrt(fmax(a11, 1e-300));
+      const double a22 = S[8] - eps_psd - l20 * l20 - l21 * l21;
+      if (a00 > 0.0 && a11 > 0.0 && a22 > 0.0) {
+        for (int k = 0; k < 9; ++k) Sp[k] = S[k];
+        c6[0] = 0.0;
+      } else {
+        psd_project3(Sr, eps_psd, Sp, c6);
+      }
+    }
     const double Rbar = sqrt(sd[0] * sd[0] + sd[1] * sd[1] + sd[2] * sd[2]) * invN;
     const double kap = kappa_blend(Rbar, 1e-6, 3.0, 0.8, 0.03);
     double* o = stats + ((int64_t)h * B + b) * GC_BIN_STATS;

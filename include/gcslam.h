@@ -189,7 +189,7 @@ typedef struct {
  * 9 s_dt, 10 s_ex, 11 anchor rho, 12 frobenius strength, 13 cond_pose6, 14 ess_total,
  * 15 dt_asymmetry, 16 z_to_xy, 17 nll_per_ess, 18 MF trigger, 19 planar trigger,
  * 20 fusion psd delta, [21:24] t_wls, [24:27] log R_mf, [27:30] MF singular values,
- * [30:36] xi_body, 36 support_frac, 37 excitation_total */
+ * [30:36] xi_body, 36 support_frac, 37 excitation_total, 38 |mu_final|^2 (barycenter spread) */
 #define GC_HYP_DIAG 40
 /* combined output (GC_COMB_LEN): L 484, h 22, z_lin 22, X_anchor(hyp 0) 6, then
  * [stamp, psd_delta, eig_min, eig_max, cond, nnc, ess, support_frac, mass_eps_ratio,
