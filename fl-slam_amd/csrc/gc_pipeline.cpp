@@ -20,6 +20,8 @@ struct gc_pipeline {
   struct Slot {
     double *pts = nullptr, *t = nullptr, *w = nullptr, *imu_t = nullptr, *imu_g = nullptr, *imu_a = nullptr;
     double* odom = nullptr;  // kOdomLen doubles (device), staged by gc_pipeline_stage_odom
+    uint8_t *bytes = nullptr, *ring = nullptr, *tag = nullptr;  // PointCloud2 staging
+    size_t bytes_cap = 0;
     int64_t n_in = 0;
   } slots[GC_PIPE_MAX_SLOTS];
   int io_mode = GC_IO_COMPUTED;
@@ -122,6 +124,8 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
   for (void* a : p->allocs) (void)hipFree(a);
   for (auto& s : p->slots) {
     for (double* d : {s.pts, s.t, s.w, s.imu_t, s.imu_g, s.imu_a, s.odom})
+      if (d) (void)hipFree(d);
+    for (uint8_t* d : {s.bytes, s.ring, s.tag})
       if (d) (void)hipFree(d);
   }
   delete p;
@@ -258,6 +262,46 @@ int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_pts
   GC_TRY(up(p, s.pts, h_pts, 3 * (size_t)n_in));
   GC_TRY(up(p, s.t, h_t, (size_t)n_in));
   GC_TRY(up(p, s.w, h_w, (size_t)n_in));
+  GC_TRY(up(p, s.imu_t, h_imu_t, (size_t)p->P.M));
+  GC_TRY(up(p, s.imu_g, h_imu_g, 3 * (size_t)p->P.M));
+  return up(p, s.imu_a, h_imu_a, 3 * (size_t)p->P.M);
+}
+
+int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_t* h_data, int64_t n_points,
+                                      int32_t point_step, const int32_t* h_fields, double header_stamp,
+                                      const double* h_R9, const double* h_t3, const double* h_imu_t,
+                                      const double* h_imu_g, const double* h_imu_a) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS, "slot out of range");
+  GC_CHECK_ARG(p->ctx, n_points >= 0 && n_points <= p->P.n_in, "n_points must be in [0, n_in_max]");
+  GC_CHECK_ARG(p->ctx, h_fields && h_R9 && h_t3 && h_imu_t && h_imu_g && h_imu_a, "NULL argument");
+  GC_CHECK_ARG(p->ctx, n_points == 0 || (h_data && point_step > 0), "NULL message data");
+  if (n_points == 0) {  // one zero-weight dummy point (backend_node.py:1700-1707)
+    const double z3[3] = {0.0, 0.0, 0.0}, z1 = 0.0;
+    return gc_pipeline_stage_scan(p, slot, z3, &z1, &z1, 1, h_imu_t, h_imu_g, h_imu_a);
+  }
+  auto& s = p->slots[slot];
+  if (!s.pts) {
+    const size_t n = (size_t)p->P.n_in, M = (size_t)p->P.M;
+    double** bufs[] = {&s.pts, &s.t, &s.w, &s.imu_t, &s.imu_g, &s.imu_a};
+    const size_t cnt[] = {3 * n, n, n, M, 3 * M, 3 * M};
+    for (int i = 0; i < 6; ++i) GC_HIP(p->ctx, hipMalloc((void**)bufs[i], cnt[i] * sizeof(double)));
+  }
+  if (!s.ring) {
+    GC_HIP(p->ctx, hipMalloc((void**)&s.ring, (size_t)p->P.n_in));
+    GC_HIP(p->ctx, hipMalloc((void**)&s.tag, (size_t)p->P.n_in));
+  }
+  const size_t nb = (size_t)n_points * (size_t)point_step;
+  if (s.bytes_cap < nb) {
+    if (s.bytes) GC_HIP(p->ctx, hipFree(s.bytes));
+    GC_HIP(p->ctx, hipMalloc((void**)&s.bytes, nb));
+    s.bytes_cap = nb;
+  }
+  GC_HIP(p->ctx, hipMemcpyAsync(s.bytes, h_data, nb, hipMemcpyHostToDevice, p->ctx->stream));
+  GC_TRY(gc_pointcloud2_parse(p->ctx, s.bytes, n_points, point_step, h_fields, header_stamp, h_R9, h_t3, s.pts,
+                              s.t, s.w, s.ring, s.tag));
+  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
+  s.n_in = n_points;
   GC_TRY(up(p, s.imu_t, h_imu_t, (size_t)p->P.M));
   GC_TRY(up(p, s.imu_g, h_imu_g, 3 * (size_t)p->P.M));
   return up(p, s.imu_a, h_imu_a, 3 * (size_t)p->P.M);

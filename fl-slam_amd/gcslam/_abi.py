@@ -68,6 +68,8 @@ SIGNATURES = {
     "gc_pipeline_set_map": [_vp, _vp],
     "gc_pipeline_get_map": [_vp, _vp, _vp, _vp],
     "gc_pipeline_stage_scan": [_vp, _i32, _vp, _vp, _vp, _i64, _vp, _vp, _vp],
+    "gc_pointcloud2_parse": [_vp, _vp, _i64, _i32, _vp, _f64, _dptr, _dptr, _vp, _vp, _vp, _vp, _vp],
+    "gc_pipeline_stage_pointcloud2": [_vp, _i32, _vp, _i64, _i32, _vp, _f64, _dptr, _dptr, _vp, _vp, _vp],
     "gc_pipeline_run_scan": [_vp, _i32, _f64, _f64, _f64, _f64, _f64, _i64],
     "gc_pipeline_get_combined": [_vp, _vp],
     "gc_pipeline_get_hyp_diag": [_vp, _vp],

@@ -1,0 +1,95 @@
+"""PointCloud2 (VLP-16 layout) parsing on the GPU: parse_pointcloud2_vlp16
+(backend/backend_node.py:377-468) and the no-TF base transform (backend_node.py:1677-1690).
+
+The message is duck-typed like sensor_msgs/PointCloud2: ``width``, ``height``, ``point_step``,
+``fields`` (objects with ``name``, ``offset``, ``datatype``), ``data`` (bytes) and
+``header.stamp.sec`` / ``header.stamp.nanosec``. ``PointField`` / ``PointCloud2Msg`` below are
+minimal stand-ins for callers without ROS message classes. All per-point arithmetic runs in
+``gc_pointcloud2_parse``; the host only resolves the field table.
+"""
+
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Tuple
+
+import numpy as np
+
+from .. import _abi
+
+INT8, UINT8, INT16, UINT16, INT32, UINT32, FLOAT32, FLOAT64 = range(1, 9)
+
+
+@dataclass
+class PointField:
+    name: str
+    offset: int
+    datatype: int
+    count: int = 1
+
+
+@dataclass
+class _Stamp:
+    sec: int = 0
+    nanosec: int = 0
+
+
+@dataclass
+class _Header:
+    stamp: _Stamp = field(default_factory=_Stamp)
+    frame_id: str = "velodyne"
+
+
+@dataclass
+class PointCloud2Msg:
+    width: int
+    height: int
+    point_step: int
+    fields: List[PointField]
+    data: bytes
+    header: _Header = field(default_factory=_Header)
+    is_bigendian: bool = False
+
+
+def header_stamp_sec(msg) -> float:
+    return msg.header.stamp.sec + msg.header.stamp.nanosec * 1e-9
+
+
+def field_table(msg) -> np.ndarray:
+    """int32[10] = [x_off, x_type, y_off, y_type, z_off, z_type, ring_off, ring_type, time_off,
+    time_type] (time_off = -1 without a t/time field), the layout of gc_pointcloud2_parse.
+    Raises RuntimeError when a VLP-16 field is missing (backend_node.py:396-403)."""
+    fmap = {f.name: (int(f.offset), int(f.datatype)) for f in msg.fields}
+    missing = [k for k in ("x", "y", "z", "ring") if k not in fmap]
+    if missing:
+        raise RuntimeError(f"PointCloud2 (VLP-16 layout) missing required fields: {missing}. "
+                           f"Present fields: {sorted(fmap)}")
+    for k, (_, dt) in fmap.items():
+        if not 1 <= dt <= 8:
+            raise ValueError(f"Unsupported PointField datatype: {dt}")
+    tf = "t" if "t" in fmap else ("time" if "time" in fmap else None)
+    t_off, t_type = fmap[tf] if tf else (-1, 0)
+    return np.array([*fmap["x"], *fmap["y"], *fmap["z"], *fmap["ring"], t_off, t_type], dtype=np.int32)
+
+
+def parse_pointcloud2_vlp16(msg, R_base_lidar=None, t_base_lidar=None, ctx=None
+                            ) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray, np.ndarray]:
+    """(points, timestamps, weights, ring, tag) as the reference returns them; with an extrinsic
+    (R_base_lidar (3,3), t_base_lidar (3,)) the points come out in the base frame."""
+    ctx = ctx or _abi.default_context()
+    n = int(msg.width) * int(msg.height)
+    if n <= 0:
+        return (np.zeros((0, 3)), np.zeros(0), np.zeros(0), np.zeros(0, np.uint8), np.zeros(0, np.uint8))
+    ft = field_table(msg)
+    step = int(msg.point_step)
+    raw = np.frombuffer(bytes(msg.data), dtype=np.uint8, count=n * step)
+    R = np.eye(3) if R_base_lidar is None else np.ascontiguousarray(R_base_lidar, np.float64).reshape(3, 3)
+    t = np.zeros(3) if t_base_lidar is None else np.ascontiguousarray(t_base_lidar, np.float64).reshape(3)
+    d_raw = _abi.DeviceArray.from_host(ctx, raw, np.uint8)
+    pts, ts, ws = _abi.DeviceArray(ctx, (n, 3)), _abi.DeviceArray(ctx, n), _abi.DeviceArray(ctx, n)
+    rg, tg = _abi.DeviceArray(ctx, n, np.uint8), _abi.DeviceArray(ctx, n, np.uint8)
+    Ra, Rp = _abi.f64p(R)  # keep the host arrays alive across the call
+    ta, tp = _abi.f64p(t)
+    _abi.call("gc_pointcloud2_parse", ctx.handle, d_raw.ptr, n, step, ft.ctypes.data, header_stamp_sec(msg), Rp, tp,
+              pts.ptr, ts.ptr, ws.ptr, rg.ptr, tg.ptr, ctx=ctx)
+    return pts.download(), ts.download(), ws.download(), rg.download(), tg.download()

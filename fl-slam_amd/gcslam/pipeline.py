@@ -168,6 +168,24 @@ class BatchedScanPipeline:
                        _p(_f(scan["odom_cov"], (6, 6))), _p(_f(scan["odom_twist"], (6,))),
                        _p(_f(scan["odom_twist_cov"], (6, 6))))
 
+    def stage_pointcloud2(self, slot: int, msg, imu: dict, R_base_lidar, t_base_lidar):
+        """Stage a slot from a PointCloud2 message (raw bytes parsed on the device,
+        backend_node.py:377-468 + :1677-1690) and the slot's IMU window (imu_stamps, imu_gyro,
+        imu_accel arrays of M rows)."""
+        from .ops.pointcloud import field_table, header_stamp_sec
+        n = int(msg.width) * int(msg.height)
+        ft = field_table(msg) if n > 0 else np.full(10, -1, np.int32)
+        raw = np.frombuffer(bytes(msg.data), dtype=np.uint8) if n > 0 else np.zeros(1, np.uint8)
+        Ra, Rp = _abi.f64p(np.asarray(R_base_lidar, np.float64).reshape(9))
+        ta, tp = _abi.f64p(np.asarray(t_base_lidar, np.float64).reshape(3))
+        self._call("gc_pipeline_stage_pointcloud2", int(slot), raw.ctypes.data, n, int(msg.point_step), ft.ctypes.data,
+                   header_stamp_sec(msg), Rp, tp, _p(_f(imu["imu_stamps"], (self.M,))),
+                   _p(_f(imu["imu_gyro"], (self.M, 3))), _p(_f(imu["imu_accel"], (self.M, 3))))
+        if "odom_pose" in imu:
+            self._call("gc_pipeline_stage_odom", int(slot), _p(_f(imu["odom_pose"], (6,))),
+                       _p(_f(imu["odom_cov"], (6, 6))), _p(_f(imu["odom_twist"], (6,))),
+                       _p(_f(imu["odom_twist_cov"], (6, 6))))
+
     def run_scan(self, slot: int, scan: dict, scan_count: int):
         self._call("gc_pipeline_run_scan", int(slot), float(scan["scan_start"]), float(scan["scan_end"]),
                    float(scan["t_last"]), float(scan["t_scan"]), float(scan["dt_sec"]), int(scan_count))

@@ -104,3 +104,51 @@ def make_io_evidence(H: int, seed: int = SEED0):
         h[k] = L[k] @ rng.normal(0.0, 1e-3, size=D_Z)
         cert[k] = [1.0, 20.0, 1.0, 1.0, 1.0, 1.0, 0.0, 0.0, 0.01, 0.5]
     return L, h, cert
+
+
+def make_pointcloud2(scan: dict, T_base_lidar=None, time_mode: str = "relative", layout: str = "vlp16",
+                     n_nonfinite: int = 0, seed: int = SEED0):
+    """The scan as a PointCloud2 message in the Velodyne VLP-16 driver layout (x, y, z, intensity
+    f32; ring u16; time f32 relative to the header stamp; point_step 22 — unaligned fields) or
+    layout="f64" (x, y, z f64, ring u8, t f64 absolute; point_step 33). Points are expressed in the
+    LiDAR frame (inverse of T_base_lidar), so parse + base transform returns the scan.
+    time_mode: "relative" (s from the header stamp), "ns" (absolute ns, exercises the 1e-9 rule),
+    "none" (no time field). n_nonfinite points get NaN / ±inf coordinates."""
+    from .ops.pointcloud import FLOAT32, FLOAT64, UINT8, UINT16, PointCloud2Msg, PointField, _Header, _Stamp
+    from scipy.spatial.transform import Rotation
+    T = np.asarray(T_BASE_LIDAR if T_base_lidar is None else T_base_lidar, np.float64)
+    R = Rotation.from_rotvec(T[3:6]).as_matrix()
+    p_lidar = (scan["points"] - T[None, :3]) @ R  # R^T (p - t)
+    n = p_lidar.shape[0]
+    stamp = float(scan["scan_start"])
+    sec = int(np.floor(stamp)); nsec = int(round((stamp - sec) * 1e9))
+    hdr = _Header(stamp=_Stamp(sec=sec, nanosec=nsec))
+    rng = np.random.default_rng(seed + 99)
+    if layout == "vlp16":
+        names = ["x", "y", "z", "intensity", "ring"] + ([] if time_mode == "none" else ["time"])
+        fmts = ["<f4", "<f4", "<f4", "<f4", "<u2"] + ([] if time_mode == "none" else ["<f4" if time_mode == "relative" else "<f8"])
+        offs = [0, 4, 8, 12, 16] + ([] if time_mode == "none" else [18])
+        step = 22 if time_mode == "relative" else (26 if time_mode == "ns" else 18)
+        types = [FLOAT32, FLOAT32, FLOAT32, FLOAT32, UINT16] + ([] if time_mode == "none" else
+                                                             [FLOAT32 if time_mode == "relative" else FLOAT64])
+    else:
+        names = ["x", "y", "z", "ring"] + ([] if time_mode == "none" else ["t"])
+        fmts = ["<f8", "<f8", "<f8", "u1"] + ([] if time_mode == "none" else ["<f8"])
+        offs = [0, 8, 16, 24] + ([] if time_mode == "none" else [25])
+        step = 33 if time_mode != "none" else 25
+        types = [FLOAT64, FLOAT64, FLOAT64, UINT8] + ([] if time_mode == "none" else [FLOAT64])
+    arr = np.zeros(n, dtype=np.dtype({"names": names, "formats": fmts, "offsets": offs, "itemsize": step}))
+    arr["x"], arr["y"], arr["z"] = p_lidar[:, 0], p_lidar[:, 1], p_lidar[:, 2]
+    if "intensity" in names:
+        arr["intensity"] = rng.uniform(0, 100, n)
+    arr["ring"] = scan["ring"].astype(np.uint16) + (256 if layout == "vlp16" else 0)  # wraps to u8
+    if time_mode == "relative":
+        arr[names[-1]] = scan["timestamps"] - stamp
+    elif time_mode == "ns":
+        arr[names[-1]] = scan["timestamps"] * 1e9
+    if n_nonfinite:
+        idx = rng.choice(n, n_nonfinite, replace=False)
+        for k, i in enumerate(idx):
+            arr[["x", "y", "z"][k % 3]][i] = [np.nan, np.inf, -np.inf][k % 3]
+    fields = [PointField(nm, o, ty) for nm, o, ty in zip(names, offs, types)]
+    return PointCloud2Msg(width=n, height=1, point_step=step, fields=fields, data=arr.tobytes(), header=hdr)

@@ -76,6 +76,20 @@ int32_t gc_point_budget_resample(gc_ctx* ctx, const double* d_points, const doub
                                  double* d_w_out, uint8_t* d_ring_out, uint8_t* d_tag_out,
                                  int64_t* d_idx_out, double* d_scalars_out);
 
+/* ------------------------------------------------------------- PointCloud2
+ * parse_pointcloud2_vlp16 (backend/backend_node.py:377-468) + the no-TF base transform
+ * p_base = R p + t (backend_node.py:1677-1690) on the device. d_data: the message's raw bytes
+ * (n_points * point_step, little-endian). h_fields (10 int32): [x_off, x_type, y_off, y_type,
+ * z_off, z_type, ring_off, ring_type, time_off, time_type] with sensor_msgs/PointField datatype
+ * codes (1 INT8 .. 8 FLOAT64); time_off = -1 when the cloud has no t/time field (every point gets
+ * header_stamp). Times are divided by 1e9 when any raw time exceeds 1e6 (ns-stamped drivers).
+ * Non-finite coordinates become ±1e6 (GC_NONFINITE_SENTINEL); weights are the range sigmoid of
+ * the sensor-frame distance; ring is the field cast to uint8; tag = 0. */
+int32_t gc_pointcloud2_parse(gc_ctx* ctx, const uint8_t* d_data, int64_t n_points, int32_t point_step,
+                             const int32_t* h_fields, double header_stamp, const double* h_R9, const double* h_t3,
+                             double* d_points_out, double* d_t_out, double* d_w_out, uint8_t* d_ring_out,
+                             uint8_t* d_tag_out);
+
 /* ------------------------------------------------------------------ a4 DeskewConstantTwist
  * Replaces backend/operators/deskew_constant_twist.py:31-69 for H twists over one point set:
  * p0 = Exp(α ξ_h)^{-1} p, α = (t - t0)/max(t1 - t0, 1e-12); w_out = w · window(t).
@@ -234,6 +248,14 @@ int32_t gc_pipeline_get_map(gc_pipeline* p, double* h_map, double* h_map_der, do
 int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_points, const double* h_t,
                                const double* h_w, int64_t n_in, const double* h_imu_t, const double* h_imu_gyro,
                                const double* h_imu_accel);
+/* Stage a scan slot straight from a PointCloud2 message (the on-wire format): the raw bytes are
+ * uploaded once and parsed on the device into the slot (gc_pointcloud2_parse layout of h_fields;
+ * h_R9/h_t3 = T_base_lidar). An empty cloud stages one zero-weight dummy point, as the node does
+ * (backend_node.py:1700-1707). */
+int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_t* h_data, int64_t n_points,
+                                      int32_t point_step, const int32_t* h_fields, double header_stamp,
+                                      const double* h_R9, const double* h_t3, const double* h_imu_t,
+                                      const double* h_imu_gyro, const double* h_imu_accel);
 /* Enqueue one scan (all local hypotheses, exchange, combine, IW apply, map update). */
 int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
                              double t_scan, double dt_sec, int64_t scan_count);

@@ -255,6 +255,59 @@ def trigger(lift=0.0, psd=0.0, nu=0.0, mass=0.0, rho=0.0, dt=1.0, ex=1.0, alpha=
 
 
 # ---------------------------------------------------------------------------------------
+# PointCloud2 parse — backend_node.py:356-468 (parse_pointcloud2_vlp16,
+# _pointfield_to_dtype) and the no-TF base transform :1677-1690 (_parse_T_base_sensor_6d :247-258)
+# ---------------------------------------------------------------------------------------
+_PF_DTYPES = {1: "i1", 2: "u1", 3: "<i2", 4: "<u2", 5: "<i4", 6: "<u4", 7: "<f4", 8: "<f8"}
+NONFINITE_SENTINEL = 1e6
+
+
+def parse_pointcloud2_vlp16(data: bytes, fields, point_step: int, n_points: int, header_stamp: float):
+    """fields: iterable of (name, offset, datatype). Returns (points, timestamps, weights, ring, tag)."""
+    if n_points <= 0:
+        return (np.zeros((0, 3)), np.zeros(0), np.zeros(0), np.zeros(0, np.uint8), np.zeros(0, np.uint8))
+    fmap = {name: (off, dt) for name, off, dt in fields}
+    missing = [k for k in ("x", "y", "z", "ring") if k not in fmap]
+    if missing:
+        raise RuntimeError(f"PointCloud2 (VLP-16 layout) missing required fields: {missing}")
+    needed = ["x", "y", "z", "ring"] + (["intensity"] if "intensity" in fmap else [])
+    tf = "t" if "t" in fmap else ("time" if "time" in fmap else None)
+    if tf:
+        needed.append(tf)
+    dtype = np.dtype({"names": needed, "formats": [_PF_DTYPES[fmap[k][1]] for k in needed],
+                      "offsets": [fmap[k][0] for k in needed], "itemsize": point_step})
+    arr = np.frombuffer(data, dtype=dtype, count=n_points)
+    s = NONFINITE_SENTINEL
+    x = np.nan_to_num(np.asarray(arr["x"], np.float64), nan=s, posinf=s, neginf=-s)
+    y = np.nan_to_num(np.asarray(arr["y"], np.float64), nan=s, posinf=s, neginf=-s)
+    z = np.nan_to_num(np.asarray(arr["z"], np.float64), nan=s, posinf=s, neginf=-s)
+    ring = np.asarray(arr["ring"]).astype(np.uint8)
+    if tf is not None:
+        t_raw = np.asarray(arr[tf], np.float64)
+        t = t_raw * 1e-9 if np.any(t_raw > 1e6) else t_raw
+    else:
+        t = np.full(n_points, header_stamp, np.float64)
+    dist = np.sqrt(x * x + y * y + z * z)
+    with np.errstate(over="ignore"):  # sentinel ranges: exp overflows to inf, weight -> floor
+      w_raw = (1.0 / (1.0 + np.exp(-(dist - RANGE_MIN_R) / RANGE_SIGMA))) * \
+              (1.0 / (1.0 + np.exp(-(RANGE_MAX_R - dist) / RANGE_SIGMA)))
+    w = w_raw * (1.0 - WEIGHT_FLOOR) + WEIGHT_FLOOR
+    return np.stack([x, y, z], axis=1), t, w, ring, np.zeros(n_points, np.uint8)
+
+
+def T_base_sensor(xyz_rxyz):
+    """_parse_T_base_sensor_6d (backend_node.py:247-258): (R, t), R = Rotation.from_rotvec."""
+    from scipy.spatial.transform import Rotation
+    v = np.asarray(xyz_rxyz, np.float64).reshape(6)
+    return Rotation.from_rotvec(v[3:6]).as_matrix(), v[:3].copy()
+
+
+def to_base(points, R, t):
+    """pts_base = (R @ p.T).T + t (backend_node.py:1680)."""
+    return (R @ points.T).T + t[None, :]
+
+
+# ---------------------------------------------------------------------------------------
 # a1 PointBudgetResample — backend/operators/point_budget.py:50-221
 # ---------------------------------------------------------------------------------------
 def point_budget_resample(points, t, w, ring=None, tag=None, n_points_cap=8192):
