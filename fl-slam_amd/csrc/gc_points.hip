@@ -94,16 +94,23 @@ GC_DEV double exp_neg(double x, const double* T) {
   return ldexp(T[k & (kExpTab - 1)] * p, k >> 8);
 }
 // exp_neg over N independent arguments, phased so the N table reads are in flight together
-// (one LDS round trip per step instead of one per bin).
-template <int N>
+// (one LDS round trip per step instead of one per bin). MAGIC: k by the rounding constant (one
+// FMA + one add, k from the low word) instead of mul + rint + cvt; the soft-assign kernel keeps
+// the rint form (its register budget at 3 waves/SIMD is tighter with the extra integer row).
+template <int N, bool MAGIC = true>
 GC_DEV void exp_neg_n(const double (&x)[N], const double* T, double (&out)[N]) {
   double kf[N], tv[N];
   int ki[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    const double ks = fma(x[j], kTabOverLn2, kRoundMagic);
-    kf[j] = ks - kRoundMagic;
-    ki[j] = __double2loint(ks);
+    if constexpr (MAGIC) {
+      const double ks = fma(x[j], kTabOverLn2, kRoundMagic);
+      kf[j] = ks - kRoundMagic;
+      ki[j] = __double2loint(ks);
+    } else {
+      kf[j] = rint(x[j] * kTabOverLn2);
+      ki[j] = (int)kf[j];
+    }
     tv[j] = T[ki[j] & (kExpTab - 1)];
   }
 #pragma unroll
@@ -418,7 +425,7 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
       }
       asm volatile("" : "+v"(best), "+v"(bidx));  // keep the argmax chain per group (no 48 live S)
       double e8[8];
-      exp_neg_n<8>(x, Tx, e8);
+      exp_neg_n<8, false>(x, Tx, e8);
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int j = j0 + jj;
@@ -433,7 +440,7 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
     {
       const double xb[1] = {fma(best, inv_tau, -inv_tau)};
       double o1[1];
-      exp_neg_n<1>(xb, Tx, o1);  // = ex[bidx] bit for bit (same argument, same evaluation)
+      exp_neg_n<1, false>(xb, Tx, o1);  // = ex[bidx] bit for bit (same argument, same evaluation)
       eb = o1[0];
     }
     if (valid) {
