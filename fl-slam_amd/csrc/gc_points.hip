@@ -25,6 +25,14 @@ typedef double v4d __attribute__((ext_vector_type(4)));  // f64 MFMA accumulator
 constexpr int NF_BASE = 19;   // [1, d(3), dd(6: 00 01 02 11 12 22), p(3), pp(6)] x w
 constexpr int NF_COV = 9;     // full 3x3 point covariance x w
 constexpr int REC_EXTRA = 4;  // [entropy_sum, max_resp, sum_w, n_points]
+#ifndef GC_NT_RESP
+#define GC_NT_RESP 0  // non-temporal responsibility stream (tuning knob, probes)
+#endif
+#if GC_NT_RESP
+#define GC_RESP_LOAD(ptr) __builtin_nontemporal_load(ptr)
+#else
+#define GC_RESP_LOAD(ptr) (*(ptr))
+#endif
 
 // 16-lane (DPP row) butterflies: quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror,
 // row_mirror. Every step pairs each lane with a distinct partner holding a disjoint partial, so
@@ -467,7 +475,13 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
 #pragma unroll
         for (int m = 0; m < 8; ++m) {
           const dvec2 v = *reinterpret_cast<const dvec2*>(&S[(i0 + 8 * m) * RS + 2 * q]);
-          if (8 * m < lim) *reinterpret_cast<dvec2*>(rowp + 8 * m * NB) = v;
+          if (8 * m < lim) {
+#if GC_NT_RESP
+            __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(rowp + 8 * m * NB));
+#else
+            *reinterpret_cast<dvec2*>(rowp + 8 * m * NB) = v;
+#endif
+          }
         }
       } else {
 #pragma unroll
@@ -562,7 +576,7 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
       int64_t p_ = (BASE) + 4 * s_ + g;                                         \
       p_ = p_ < wend ? p_ : wend - 1; /* prefetch past the range re-reads a line */ \
       const double* row_ = Rh + p_ * B;                                         \
-      _Pragma("unroll") for (int j_ = 0; j_ < BPL; ++j_) RR[s_][j_] = row_[cb[j_]]; \
+      _Pragma("unroll") for (int j_ = 0; j_ < BPL; ++j_) RR[s_][j_] = GC_RESP_LOAD(row_ + cb[j_]); \
     }                                                                           \
   }
   // raw inputs of one 32-point group (point = lane & 31), loaded by every lane into registers and

@@ -162,3 +162,18 @@ def test_hypothesis_weight_floor():
 # ---- test_geometric_compositional_invariants.py:197-212
 def test_total_trigger_at_least_lift_plus_psd():
     assert O.trigger(lift=1e-8, psd=0.3) >= 1e-8 + 0.3
+
+
+# ---- archive/legacy_tests/test_operators.py:300-327 (gyro residual direction: pred^{-1} ∘ meas)
+def test_gyro_residual_is_pred_inverse_composed_with_meas():
+    pred = np.array([0.01, -0.02, 0.005])
+    r = O.imu_gyro_rotation_evidence(np.zeros(3), pred, np.zeros(3), np.eye(3), 1.0)
+    assert np.allclose(r["r_rot"], -pred, atol=1e-6)
+
+
+@pytest.mark.gpu
+def test_gpu_gyro_residual_direction(ctx):
+    from gcslam.ops import imu_gyro_rotation_evidence
+    pred = np.array([0.01, -0.02, 0.005])
+    res, _, _ = imu_gyro_rotation_evidence(np.zeros(3), pred, np.zeros(3), np.eye(3), 1.0, ctx=ctx)
+    assert np.allclose(res.r_rot, -pred, atol=1e-6)
