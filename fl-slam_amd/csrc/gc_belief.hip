@@ -76,12 +76,14 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   double* hpred = vec + 2 * kDZ;
   double* mu_inc = vec + 3 * kDZ;
 
+  GC_PHASE(P, 0);
   for (int i = t; i < N2; i += kWG) Lp[i] = P.L[(int64_t)h * N2 + i];
   if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
   __syncthreads();
   // --- a2 predict (predict.py:43-98): L_pred -> W1, h_pred, mu_prev, cert
   wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,
              P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2);
+  GC_PHASE(P, 1);
   if (t == 0) compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);  // pose0 = world pose of belief_prev
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + t] = mu_prev[t];
   for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
@@ -89,8 +91,11 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   // --- predicted moments: Σ_pred[15,15] and mu_inc (pipeline.py:436-453) from chol(L_pred+εI)
   for (int i = t; i < N2; i += kWG) W4[i] = W1[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
   __syncthreads();
+  GC_PHASE(P, 2);
   wg_chol(W4, n);
+  GC_PHASE(P, 3);
   wg_chol_solve(W4, hpred, mu_inc, n);
+  GC_PHASE(P, 4);
   if (t == 0) {
     const double s1515 = inv_diag_from_chol(W4, n, 15);
     misc[6] = fmax(sqrt(s1515), 0.01);                  // sigma_warp
@@ -127,7 +132,9 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   const double* R0 = misc + 16;
   double* pre = misc + 32;  // kPreint
   const double kG[3] = {0.0, 0.0, -9.81 * P.gravity_scale};  // GC_GRAVITY_W · imu_gravity_scale
+  GC_PHASE(P, 5);
   wg_preintegrate(M, S.imu_t, S.imu_g, S.imu_a, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, red, pre);
+  GC_PHASE(P, 6);
   const double ess_scan = wg_sum(wa + wb, red);
   if (t == 0) {
     double dR[9], dpose[6], xi[6];
@@ -171,7 +178,9 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
         rr[6 + q] = (wia / wsum) * raa[i] * raa[j] + (wib / wsum) * rab[i] * rab[j];
       }
   }
+  GC_PHASE(P, 7);
   for (int q = 0; q < 12; ++q) rr[q] = wg_sum(rr[q], red);
+  GC_PHASE(P, 8);
   if (t == 0) {
     double* out = P.dPsiM + (int64_t)h * 27;
     for (int blk = 0; blk < 2; ++blk) {

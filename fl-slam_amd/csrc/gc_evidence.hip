@@ -70,6 +70,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     zl[t] = P.z[(int64_t)hl * n + t];
   }
   const double* st = P.stats + (int64_t)hl * B * 38;
+  GC_PHASE(P, 10);
   // ---------------------------------------------- a7 MatrixFisher: per-bin cross-covariance
   if (t < B) {
     const double* s = st + t * 38;
@@ -84,6 +85,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     mf_finalize(acc, Rp, eps, P.eps_psd, mf);
   }
   __syncthreads();
+  GC_PHASE(P, 11);
   // ---------------------------------------------- a8 planar translation WLS (R_hat = R_mf)
   if (t < B) {
     const double* s = st + t * 38;
@@ -95,6 +97,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   sum_bins(tab, B, 13, acc);
   if (t == 0) planar_finalize(acc, P.map_misc[0], P.pose_pred + (int64_t)hl * 6, eps, P.eps_psd, pt);
   __syncthreads();
+  GC_PHASE(P, 12);
   // ---------------------------------------------- a9 evidence sum: L_raw = L_io + L_lidar
   if (t < 9) {
     const int i = t / 3, j = t % 3;
@@ -152,6 +155,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   }
   if (t < n) hps[t] = afac(t) * P.hpred[(int64_t)hl * n + t];
   __syncthreads();
+  GC_PHASE(P, 13);
   // a10: pose-6 conditioning of L_ev and the fusion scale α
   {
     double* P6 = W3;
@@ -182,11 +186,13 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     __syncthreads();
   }
   const double alpha = sc[59];
+  GC_PHASE(P, 14);
   // a11 InfoFusionAdditive
   for (int i = t; i < NN; i += kWG) W2[i] = Lps[i] + alpha * Lev[i];
   if (t < n) hpo[t] = hps[t] + alpha * hev[t];
   __syncthreads();
   wg_psd_project_fast(W2, Lpo, P.eps_psd, n, Sx, red, c6);
+  GC_PHASE(P, 15);
   // a12 recompose: T from every operator's trigger magnitude (pipeline.py:1211)
   if (t == 0) {
     const double* bc = P.bincert + (int64_t)hl * 8;
@@ -217,6 +223,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     zl[t] = zl[t] - sh;
   }
   __syncthreads();
+  GC_PHASE(P, 16);
   // a15 process-noise IW statistics (inverse_wishart_jax.py:71-123)
   wg_chol_solve(Wc, hrec, mupo, n);
   for (int i = t; i < NN; i += kWG) W3[i] = Lps[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
@@ -225,6 +232,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   wg_chol_solve(W3, hps, mups, n);
   wg_chol_inverse(Wc, W2, Sx, n);  // Σ_post -> W2
   for (int idx = t; idx < 7 * 36; idx += kWG) P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
+  GC_PHASE(P, 17);
   // a13 map increment from hypothesis 0 only (backend_node.py:2081-2083), build-defined pushforward
   if (P.h_begin + hl == 0) {
     if (t == 0) {
@@ -237,6 +245,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     __syncthreads();
     if (t < B) pushforward_bin(st + t * 38, sc + 80, sc + 89, W2, n, P.map_inc + t * kMapRec);
   }
+  GC_PHASE(P, 18);
   // a14 anchor drift (anchor_drift.py:93-191): δz = μ_post of the recomposed belief
   if (t == 0) {
     const double rho = drift_rho(mupo, nullptr, nullptr);
@@ -251,6 +260,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   __syncthreads();
   wg_matvec(Lpo, zl, hfin, n);
   wg_chol_solve(Wc, hfin, mufin, n);
+  GC_PHASE(P, 19);
   // write the final belief and per-hypothesis outputs
   for (int i = t; i < NN; i += kWG) P.L[(int64_t)hl * NN + i] = Lpo[i];
   if (t < n) {

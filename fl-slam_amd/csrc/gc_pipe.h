@@ -61,6 +61,20 @@ struct ScanArgs {
   double w_process;                        // min(1, scan_count)
 };
 
+// dev instrumentation: -DGC_PHASE_TIMING records s_memtime at phase boundaries of hypothesis 0
+// into io_parts[slot] (read with the pipeline in GC_IO_GIVEN mode); compiled out otherwise
+#ifdef GC_PHASE_TIMING
+#define GC_PHASE(P, i)                                                                   \
+  do {                                                                                   \
+    __syncthreads();                                                                     \
+    if (blockIdx.x == 0 && threadIdx.x == 0) (P).io_parts[i] = (double)__builtin_readcyclecounter(); \
+  } while (0)
+#else
+#define GC_PHASE(P, i) \
+  do {                 \
+  } while (0)
+#endif
+
 // launchers (gc_belief.hip)
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st);
 hipError_t launch_io_branch(const PipeDev& P, const ScanArgs& S, const double* d_odom, hipStream_t st);

@@ -56,33 +56,57 @@ GC_DEV void wg_copy(double* dst, const double* src, int count) {
   __syncthreads();
 }
 
+// ---- register-resident factorizations (n <= 22). Wave 0 holds one matrix row per lane (row i
+// in lane i, rows >= n padded with the identity, which leaves the leading block's factors
+// unchanged); column broadcasts are v_readlane (compile-time lane, loops fully unrolled). No LDS
+// traffic or workgroup barriers inside the factorization: ~5x shorter latency than the
+// LDS/barrier-per-column form on the 22x22 information matrices of the per-hypothesis kernels.
+GC_DEV double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// Right-looking Cholesky of the lane rows a (lower triangle significant). CHECKED: a pivot <= 0
+// (or NaN) clears ok and is replaced by 1 so the rest stays finite (wg_chol_checked semantics).
+template <bool CHECKED>
+GC_DEV void lane_chol22(double (&a)[kDZ], int lane, bool& ok) {
+#pragma unroll
+  for (int k = 0; k < kDZ; ++k) {
+    double piv = readlane_f64(a[k], k);
+    if constexpr (CHECKED) {
+      if (!(piv > 0.0)) { ok = false; piv = 1.0; }
+    }
+    const double d = sqrt(piv);
+    a[k] = lane == k ? d : (lane > k ? a[k] / d : a[k]);
+#pragma unroll
+    for (int j = k + 1; j < kDZ; ++j) a[j] -= a[k] * readlane_f64(a[k], j);
+  }
+}
+
+GC_DEV void lane_load_rows(const double* A, int n, int lane, double (&a)[kDZ]) {
+#pragma unroll
+  for (int j = 0; j < kDZ; ++j)
+    a[j] = (lane < n && j < n) ? (j <= lane ? A[lane * n + j] : 0.0) : (lane == j ? 1.0 : 0.0);
+}
+
+GC_DEV void lane_store_lower(double* A, int n, int lane, const double (&a)[kDZ]) {
+  if (lane < n) {
+#pragma unroll
+    for (int j = 0; j < kDZ; ++j)
+      if (j < n) A[lane * n + j] = j <= lane ? a[j] : 0.0;
+  }
+}
+
 // In-place lower Cholesky of the n x n (row-major) A; upper triangle zeroed.
 GC_DEV void wg_chol(double* A, int n) {
-  for (int k = 0; k < n; ++k) {
-    if (threadIdx.x == 0) A[k * n + k] = sqrt(A[k * n + k]);
-    __syncthreads();
-    const double dk = A[k * n + k];
-    const int m = n - k - 1;
-    if ((int)threadIdx.x < m) {
-      const int i = k + 1 + threadIdx.x;
-      A[i * n + k] = A[i * n + k] / dk;
-    }
-    __syncthreads();
-    const int tri = m * (m + 1) / 2;
-    for (int idx = threadIdx.x; idx < tri; idx += kWG) {
-      // decode lower-triangular (i, j) with j <= i inside the trailing block
-      int i = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
-      while ((i + 1) * (i + 2) / 2 <= idx) ++i;
-      while (i * (i + 1) / 2 > idx) --i;
-      const int j = idx - i * (i + 1) / 2;
-      const int gi = k + 1 + i, gj = k + 1 + j;
-      A[gi * n + gj] -= A[gi * n + k] * A[gj * n + k];
-    }
-    __syncthreads();
-  }
-  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
-    const int i = idx / n, j = idx % n;
-    if (j > i) A[idx] = 0.0;
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double a[kDZ];
+    lane_load_rows(A, n, lane, a);
+    bool ok = true;
+    lane_chol22<false>(a, lane, ok);
+    lane_store_lower(A, n, lane, a);
   }
   __syncthreads();
 }
@@ -90,66 +114,73 @@ GC_DEV void wg_chol(double* A, int n) {
 // In-place lower Cholesky that reports failure (a pivot <= 0 or NaN): returns true on success
 // on every thread. flag: one LDS double.
 GC_DEV bool wg_chol_checked(double* A, int n, double* flag) {
-  if (threadIdx.x == 0) flag[0] = 0.0;
-  __syncthreads();
-  for (int k = 0; k < n; ++k) {
-    if (threadIdx.x == 0) {
-      double d = A[k * n + k];
-      if (!(d > 0.0)) { flag[0] = 1.0; d = 1.0; }
-      A[k * n + k] = sqrt(d);
-    }
-    __syncthreads();
-    const double dk = A[k * n + k];
-    const int m = n - k - 1;
-    if ((int)threadIdx.x < m) {
-      const int i = k + 1 + threadIdx.x;
-      A[i * n + k] = A[i * n + k] / dk;
-    }
-    __syncthreads();
-    const int tri = m * (m + 1) / 2;
-    for (int idx = threadIdx.x; idx < tri; idx += kWG) {
-      int i = (int)((sqrt(8.0 * idx + 1.0) - 1.0) * 0.5);
-      while ((i + 1) * (i + 2) / 2 <= idx) ++i;
-      while (i * (i + 1) / 2 > idx) --i;
-      const int j = idx - i * (i + 1) / 2;
-      const int gi = k + 1 + i, gj = k + 1 + j;
-      A[gi * n + gj] -= A[gi * n + k] * A[gj * n + k];
-    }
-    __syncthreads();
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    double a[kDZ];
+    lane_load_rows(A, n, lane, a);
+    bool ok = true;
+    lane_chol22<true>(a, lane, ok);
+    lane_store_lower(A, n, lane, a);
+    if (lane == 0) flag[0] = ok ? 0.0 : 1.0;
   }
+  __syncthreads();
   const bool ok = flag[0] == 0.0;
   __syncthreads();
   return ok;
 }
 
-// x = (C Cᵀ)^{-1} b for lower-triangular C (thread 0; result visible to all on return).
+// x = (C Cᵀ)^{-1} b for lower-triangular C (result visible to all on return). Wave 0, lane i holds
+// row i and column i of C: forward substitution broadcasts y_j, backward x_j, one readlane each.
 GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
-  if (threadIdx.x == 0) {
-    double y[kDZ];
-    for (int i = 0; i < n; ++i) {
-      double v = b[i];
-      for (int j = 0; j < i; ++j) v -= C[i * n + j] * y[j];
-      y[i] = v / C[i * n + i];
+  if (threadIdx.x < 64) {
+    const int lane = threadIdx.x;
+    const bool live = lane < n;
+    double c[kDZ], ct[kDZ];
+#pragma unroll
+    for (int j = 0; j < kDZ; ++j) {
+      const bool in = live && j < n;
+      c[j] = in ? (j <= lane ? C[lane * n + j] : 0.0) : (lane == j ? 1.0 : 0.0);
+      ct[j] = in ? (j >= lane ? C[j * n + lane] : 0.0) : (lane == j ? 1.0 : 0.0);
     }
-    for (int i = n - 1; i >= 0; --i) {
-      double v = y[i];
-      for (int j = i + 1; j < n; ++j) v -= C[j * n + i] * x[j];
-      x[i] = v / C[i * n + i];
+    const double diag = live ? C[lane * n + lane] : 1.0;
+    double r = live ? b[lane] : 0.0, y = 0.0;
+#pragma unroll
+    for (int j = 0; j < kDZ; ++j) {  // y_j = (b_j - Σ_{k<j} C_jk y_k) / C_jj
+      const double yj = readlane_f64(r / diag, j);
+      if (lane == j) y = yj;
+      r -= c[j] * yj;
     }
+    r = y;
+    double xv = 0.0;
+#pragma unroll
+    for (int j = kDZ - 1; j >= 0; --j) {  // x_j = (y_j - Σ_{k>j} C_kj x_k) / C_jj
+      const double xj = readlane_f64(r / diag, j);
+      if (lane == j) xv = xj;
+      r -= ct[j] * xj;
+    }
+    if (live) x[lane] = xv;
   }
   __syncthreads();
 }
 
 // Ainv = C^{-ᵀ} C^{-1} (primitives.py:186-191: L_chol_inv.T @ L_chol_inv). scratch: n*n.
 GC_DEV void wg_chol_inverse(const double* C, double* Ainv, double* scratch, int n) {
-  // scratch <- C^{-1} (lower), column j solved by thread j
+  // scratch <- C^{-1} (lower): column j by thread j, the column held in registers, C read by
+  // LDS broadcast (every active lane reads the same C[i][k])
   if ((int)threadIdx.x < n) {
     const int j = threadIdx.x;
-    for (int i = 0; i < n; ++i) {
+    double col[kDZ];
+#pragma unroll
+    for (int i = 0; i < kDZ; ++i) {
       double v = (i == j) ? 1.0 : 0.0;
-      if (i >= j)
-        for (int k = j; k < i; ++k) v -= C[i * n + k] * scratch[k * n + j];
-      scratch[i * n + j] = (i >= j) ? v / C[i * n + i] : 0.0;
+      if (i < n) {
+#pragma unroll
+        for (int k = 0; k < i; ++k) v -= (k >= j ? C[i * n + k] * col[k] : 0.0);
+        col[i] = i >= j ? v / C[i * n + i] : 0.0;
+        scratch[i * n + j] = col[i];
+      } else {
+        col[i] = 0.0;
+      }
     }
   }
   __syncthreads();

@@ -1,0 +1,46 @@
+"""Dev helper: per-phase cycle counts of hypothesis 0's workgroup in k_predict_imu (slots 0-8) and
+k_evidence (10-19), from a library built with -DGC_PHASE_TIMING (tools/probe/libgcslam_timing.so):
+    make -C fl-slam_amd BUILD=build_timing OUT=../tools/probe/libgcslam_timing.so \
+        CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -I../include -DGC_PHASE_TIMING"
+Runs the bench workload (64k points x 256 hypotheses) with the IMU/odom branch given (GC_IO_GIVEN
+leaves io_parts to the instrumentation)."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
+sys.path.insert(0, ROOT)
+from gcslam import _abi  # noqa: E402
+
+_abi.LIB_PATH = os.path.join(ROOT, "tools", "probe", "libgcslam_timing.so")
+import numpy as np  # noqa: E402
+from gcslam.pipeline import BatchedScanPipeline, PipelineConfig, iw_meas_prior, iw_process_prior  # noqa: E402
+from gcslam.synth import make_hypotheses, make_io_evidence, make_scan  # noqa: E402
+from oracle import cases  # noqa: E402
+
+H = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+ctx = _abi.Context(0)
+scans = [make_scan(k + 1) for k in range(3)]
+n = scans[0]["points"].shape[0]
+pipe = BatchedScanPipeline(H, n, PipelineConfig(n_points_cap=n), ctx=ctx)
+hy = make_hypotheses(H)
+pipe.set_beliefs(hy["X_anchor"], hy["z_lin"], hy["L"], hy["h"], hy["stamp"])
+pipe.set_io_evidence(*make_io_evidence(H))
+pipe.set_iw(*iw_process_prior(), *iw_meas_prior())
+m0 = cases.warmup_map(make_scan(0), n, np.asarray(pipe.cfg.lidar_origin), cases.O.fibonacci_atlas(48))
+pipe.set_map(cases.map_to_record(m0))
+for k, s in enumerate(scans):
+    pipe.stage_scan(k, s)
+for r in range(6):
+    pipe.run_scan(r % 3, scans[r % 3], r)
+ctx.sync()
+t = pipe.io_parts()[0]
+names = {1: "predict: wg_predict", 2: "predict: compose", 3: "predict: chol", 4: "predict: chol_solve",
+         5: "predict: moments+dt_imu", 6: "predict: preintegrate", 7: "predict: xi+omega", 8: "predict: meas IW",
+         11: "evidence: start..MF", 12: "evidence: MF..planar", 13: "evidence: L_raw,beta,excitation",
+         14: "evidence: pose6 cond+alpha", 15: "evidence: fusion PSD", 16: "evidence: recompose+IW stats",
+         17: "evidence: IW solves/inverse", 18: "evidence: map increment", 19: "evidence: drift+final solves"}
+for i in sorted(names):
+    if t[i] and t[i - 1]:
+        print(f"{names[i]:36s} {t[i] - t[i - 1]:10.0f} cycles")
+print("predict total", t[8] - t[0], "evidence 10..19", t[19] - t[10])
