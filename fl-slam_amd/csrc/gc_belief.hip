@@ -156,10 +156,11 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
     return (i < M) ? window_weight(ti, S.t_last, S.t_scan, sigma_warp) * (ti > 0.0 ? 1.0 : 0.0) : 0.0;
   };
   const double wia = wint(ia), wib = wint(ib);
-  const double wsum = wg_sum(wia + wib, red) + P.eps_mass;
-  double om[3];
-  for (int k = 0; k < 3; ++k)
-    om[k] = wg_sum(wia * (ga[k] - bg[k]) + wib * (gb[k] - bg[k]), red) / wsum;
+  double om[4] = {wia + wib, 0.0, 0.0, 0.0};
+  for (int k = 0; k < 3; ++k) om[1 + k] = wia * (ga[k] - bg[k]) + wib * (gb[k] - bg[k]);
+  wg_sum_n<4>(om, A);  // A: preintegration scratch, free again
+  const double wsum = om[0] + P.eps_mass;
+  for (int k = 0; k < 3; ++k) om[k] = om[1 + k] / wsum;
   double rr[12];
   {
     const double f0 = -(R0[0] * kG[0] + R0[3] * kG[1] + R0[6] * kG[2]);
@@ -179,7 +180,7 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
       }
   }
   GC_PHASE(P, 7);
-  for (int q = 0; q < 12; ++q) rr[q] = wg_sum(rr[q], red);
+  wg_sum_n<12>(rr, A);
   GC_PHASE(P, 8);
   if (t == 0) {
     double* out = P.dPsiM + (int64_t)h * 27;

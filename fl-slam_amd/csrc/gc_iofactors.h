@@ -445,8 +445,10 @@ GC_DEV void wg_imu_vmf_tr(int M, const double* accel, const double* gyro, const 
     S[0] += wr * (a0 / n); S[1] += wr * (a1 / n); S[2] += wr * (a2 / n);
     rel_s += rel; wr_s += wr; w_s += w[i];
   }
-  const double ess_w = wg_sum(wr_s, red), ess_raw = wg_sum(w_s, red), mrel = wg_sum(rel_s, red) / (double)M;
-  for (int k = 0; k < 3; ++k) S[k] = wg_sum(S[k], red);
+  double sums[6] = {wr_s, w_s, rel_s, S[0], S[1], S[2]};
+  wg_sum_n<6>(sums, sc);  // e / dev no longer needed
+  const double ess_w = sums[0], ess_raw = sums[1], mrel = sums[2] / (double)M;
+  S[0] = sums[3]; S[1] = sums[4]; S[2] = sums[5];
   if (t == 0) {
     const double Sn = norm3(S);
     const double xb[3] = {S[0] / (Sn + eps_mass), S[1] / (Sn + eps_mass), S[2] / (Sn + eps_mass)};

@@ -51,6 +51,23 @@ GC_DEV double wg_max(double v, double* red) {
   return r;
 }
 
+// N workgroup sums with two barriers instead of 3N (fixed shuffle tree + fixed wave order, as
+// wg_sum). scratch: 4N doubles of LDS not otherwise live. Results replace v on every thread.
+template <int N>
+GC_DEV void wg_sum_n(double (&v)[N], double* scratch) {
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) scratch[(threadIdx.x >> 6) * N + i] = v[i];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < N; ++i) v[i] = (scratch[i] + scratch[N + i]) + (scratch[2 * N + i] + scratch[3 * N + i]);
+  __syncthreads();
+}
+
 GC_DEV void wg_copy(double* dst, const double* src, int count) {
   for (int i = threadIdx.x; i < count; i += kWG) dst[i] = src[i];
   __syncthreads();
