@@ -86,18 +86,33 @@ GC_DEV double readlane_f64(double v, int lane) {
 
 // Right-looking Cholesky of the lane rows a (lower triangle significant). CHECKED: a pivot <= 0
 // (or NaN) clears ok and is replaced by 1 so the rest stays finite (wg_chol_checked semantics).
+// The pivot scale is one v_rsq_f64 + a Goldschmidt step (d = √p and 1/d to ~1 ulp) instead of a
+// correctly rounded sqrt and a per-lane division. Column k is broadcast as: L[k+1][k] by
+// readlane (it feeds the next pivot), L[k+2..][k] through a 22-double LDS row (one ds_write per
+// lane, then same-address broadcast reads, no readlane hazard NOPs). Wave 0 only, in program
+// order, so the LDS row needs no barrier.
 template <bool CHECKED>
 GC_DEV void lane_chol22(double (&a)[kDZ], int lane, bool& ok) {
+  __shared__ __attribute__((aligned(16))) double colbuf[kDZ + 2];
 #pragma unroll
   for (int k = 0; k < kDZ; ++k) {
     double piv = readlane_f64(a[k], k);
     if constexpr (CHECKED) {
       if (!(piv > 0.0)) { ok = false; piv = 1.0; }
     }
-    const double d = sqrt(piv);
-    a[k] = lane == k ? d : (lane > k ? a[k] / d : a[k]);
+    const double y = __builtin_amdgcn_rsq(piv);
+    double g = piv * y, h = 0.5 * y;
+    const double r = fma(-g, h, 0.5);
+    g = fma(g, r, g);
+    h = fma(h, r, h);
+    const double inv = h + h;
+    a[k] = lane == k ? g : (lane > k ? a[k] * inv : a[k]);
+    if (k + 1 < kDZ) {
+      if (k + 2 < kDZ) colbuf[lane < kDZ ? lane : kDZ + 1] = a[k];
+      a[k + 1] -= a[k] * (lane == k + 1 ? a[k] : readlane_f64(a[k], k + 1));  // next pivot: no readlane
 #pragma unroll
-    for (int j = k + 1; j < kDZ; ++j) a[j] -= a[k] * readlane_f64(a[k], j);
+      for (int j = k + 2; j < kDZ; ++j) a[j] -= a[k] * colbuf[j];
+    }
   }
 }
 
@@ -159,11 +174,11 @@ GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
       c[j] = in ? (j <= lane ? C[lane * n + j] : 0.0) : (lane == j ? 1.0 : 0.0);
       ct[j] = in ? (j >= lane ? C[j * n + lane] : 0.0) : (lane == j ? 1.0 : 0.0);
     }
-    const double diag = live ? C[lane * n + lane] : 1.0;
+    const double idiag = 1.0 / (live ? C[lane * n + lane] : 1.0);  // off the dependency chain
     double r = live ? b[lane] : 0.0, y = 0.0;
 #pragma unroll
     for (int j = 0; j < kDZ; ++j) {  // y_j = (b_j - Σ_{k<j} C_jk y_k) / C_jj
-      const double yj = readlane_f64(r / diag, j);
+      const double yj = readlane_f64(r * idiag, j);
       if (lane == j) y = yj;
       r -= c[j] * yj;
     }
@@ -171,7 +186,7 @@ GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
     double xv = 0.0;
 #pragma unroll
     for (int j = kDZ - 1; j >= 0; --j) {  // x_j = (y_j - Σ_{k>j} C_kj x_k) / C_jj
-      const double xj = readlane_f64(r / diag, j);
+      const double xj = readlane_f64(r * idiag, j);
       if (lane == j) xv = xj;
       r -= ct[j] * xj;
     }
@@ -181,32 +196,47 @@ GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
 }
 
 // Ainv = C^{-ᵀ} C^{-1} (primitives.py:186-191: L_chol_inv.T @ L_chol_inv). scratch: n*n.
+// Phase 1 (wave 0): lane j forward-substitutes column j of W = C^{-1} in registers, C read by
+// same-address LDS broadcast, the row sums split over 4 accumulators (short dependency chain) and
+// the 1/C_ii off the chain; W is stored transposed (scratch row j = column j). Phase 2 (all 4
+// waves): thread (g = t/32, j = t%32) forms Ainv[i][j] = Σ_k W[k][i] W[k][j] for i ≡ g (mod 8),
+// its column j of W in registers and column i broadcast; k ascends over the full range (the
+// entries below the triangles are exact zeros), the order of the reference's product.
 GC_DEV void wg_chol_inverse(const double* C, double* Ainv, double* scratch, int n) {
-  // scratch <- C^{-1} (lower): column j by thread j, the column held in registers, C read by
-  // LDS broadcast (every active lane reads the same C[i][k])
   if ((int)threadIdx.x < n) {
     const int j = threadIdx.x;
     double col[kDZ];
 #pragma unroll
     for (int i = 0; i < kDZ; ++i) {
-      double v = (i == j) ? 1.0 : 0.0;
+      col[i] = 0.0;
       if (i < n) {
+        const double* Ci = C + i * n;
+        double s[4] = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-        for (int k = 0; k < i; ++k) v -= (k >= j ? C[i * n + k] * col[k] : 0.0);
-        col[i] = i >= j ? v / C[i * n + i] : 0.0;
-        scratch[i * n + j] = col[i];
-      } else {
-        col[i] = 0.0;
+        for (int k = 0; k < i; ++k) s[k & 3] = fma(Ci[k], col[k], s[k & 3]);
+        const double v = ((i == j) ? 1.0 : 0.0) - ((s[0] + s[1]) + (s[2] + s[3]));
+        const double inv = 1.0 / Ci[i];
+        col[i] = i >= j ? v * inv : 0.0;
       }
     }
+#pragma unroll
+    for (int k = 0; k < kDZ; ++k)
+      if (k < n) scratch[j * n + k] = col[k];
   }
   __syncthreads();
-  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
-    const int i = idx / n, j = idx % n;
-    const int k0 = i > j ? i : j;
-    double v = 0.0;
-    for (int k = k0; k < n; ++k) v += scratch[k * n + i] * scratch[k * n + j];
-    Ainv[idx] = v;
+  const int j = threadIdx.x & 31, g = threadIdx.x >> 5;
+  if (j < n) {
+    double wj[kDZ];
+#pragma unroll
+    for (int k = 0; k < kDZ; ++k) wj[k] = k < n ? scratch[j * n + k] : 0.0;
+    for (int i = g; i < n; i += kWG / 32) {
+      const double* wi = scratch + i * n;
+      double v = 0.0;
+#pragma unroll
+      for (int k = 0; k < kDZ; ++k)
+        if (k < n) v = fma(wi[k], wj[k], v);
+      Ainv[i * n + j] = v;
+    }
   }
   __syncthreads();
 }
