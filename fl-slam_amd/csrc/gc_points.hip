@@ -139,6 +139,50 @@ GC_DEV double recip(double z) {
   e = fma(-z, r, 1.0);
   return fma(r, e, r);
 }
+// Fused-kernel exp: a 2048-entry table and arguments pre-scaled to y = x·2048/ln2. Entry j holds
+// 2^(j/2048) with (j << 9) subtracted from its high word, so adding (k << 9) to the high word of
+// T[k & 2047] yields 2^(j/2048)·2^(k >> 11) for any k (one integer add instead of a shift and a
+// v_ldexp). r = y - rint(y) is exact (Sterbenz), |r| <= 1/2, and e^{r ln2/2048} needs only a
+// cubic (truncation (ln2/4096)^4/24 = 3.5e-17). 13 VALU slots per exp with the 3-FMA logit
+// (16 for exp_neg_n). Valid for y in [-2048·700/ln2, 0] (normal results).
+constexpr int kExpTab2 = 2048;
+constexpr double kTab2OverLn2 = 2954.6394437405970;     // 2048 / ln2
+constexpr double kExp2C1 = 3.3845077175902435e-04;     // ln2 / 2048
+constexpr double kExp2C2 = kExp2C1 * kExp2C1 * 0.5;
+constexpr double kExp2C3 = kExp2C1 * kExp2C1 * kExp2C1 * (1.0 / 6.0);
+GC_DEV void exp_table2_init(double* T) {
+  for (int j = threadIdx.x; j < kExpTab2; j += blockDim.x) {
+    const double v = exp2((double)j / kExpTab2);
+    T[j] = __hiloint2double(__double2hiint(v) - (j << 9), __double2loint(v));
+  }
+}
+template <int N>
+GC_DEV void exp2s_n(const double (&y)[N], const double* T, double (&out)[N]) {
+  double r[N], tv[N];
+  int ki[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double ks = y[j] + kRoundMagic;
+    ki[j] = __double2loint(ks);
+    r[j] = y[j] - (ks - kRoundMagic);
+    tv[j] = T[ki[j] & (kExpTab2 - 1)];
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double p = fma(fma(fma(kExp2C3, r[j], kExp2C2), r[j], kExp2C1), r[j], 1.0);
+    const double t = __hiloint2double(__double2hiint(tv[j]) + (ki[j] << 9), __double2loint(tv[j]));
+    out[j] = t * p;
+  }
+}
+// σ(x) = 1 / (1 + e^{-x}) on the 2048 table (e^{-|x|} clamped at e^{-700} ~ 1e-304)
+GC_DEV double sigmoid2(double x, const double* T) {
+  const double y[1] = {fmax(-fabs(x), -700.0) * kTab2OverLn2};
+  double e[1];
+  exp2s_n<1>(y, T, e);
+  const double r = recip(1.0 + e[0]);
+  return x >= 0.0 ? r : e[0] * r;
+}
+
 
 GC_DEV void lds_wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
@@ -214,6 +258,34 @@ GC_DEV void deskew_point_fast(const double* p, double alpha, const double* xi, d
   q[0] = p[0] - t[0]; q[1] = p[1] - t[1]; q[2] = p[2] - t[2];
   mat3_tvec(R, q, out);
 }
+// Series form for the fused kernel: a = sin θ/θ, B = (1 - cos θ)/θ², C = (θ - sin θ)/θ³ are
+// power series in θ² (1/(2k+1)!, 1/(2k+2)!, 1/(2k+3)! of (-θ²)^k); ten terms reach < 1e-17 for
+// θ² <= 1 — three independent Horner chains instead of sqrt + sincos + two reciprocals. Larger
+// rotations (|α ω| > 1 rad within one scan) take the sincos form.
+constexpr double kInvFact[22] = {1.0, 1.0, 0.5, 0.16666666666666666, 0.041666666666666664, 0.008333333333333333, 0.001388888888888889, 0.0001984126984126984, 2.48015873015873e-05, 2.7557319223985893e-06, 2.755731922398589e-07, 2.505210838544172e-08, 2.08767569878681e-09, 1.6059043836821613e-10, 1.1470745597729725e-11, 7.647163731819816e-13, 4.779477332387385e-14, 2.8114572543455206e-15, 1.5619206968586225e-16, 8.22063524662433e-18, 4.110317623312165e-19, 1.9572941063391263e-20};
+GC_DEV void deskew_point_series(const double* p, double alpha, const double* xi, double* out) {
+  const double phi[3] = {alpha * xi[3], alpha * xi[4], alpha * xi[5]};
+  const double ts = dot3(phi, phi);
+  if (ts > 1.0) {
+    deskew_point_fast(p, alpha, xi, out);
+    return;
+  }
+  const double rho[3] = {alpha * xi[0], alpha * xi[1], alpha * xi[2]};
+  const double u = -ts;
+  double a = kInvFact[19], Bv = kInvFact[20], Cv = kInvFact[21];
+#pragma unroll
+  for (int k = 8; k >= 0; --k) {
+    a = fma(a, u, kInvFact[2 * k + 1]);
+    Bv = fma(Bv, u, kInvFact[2 * k + 2]);
+    Cv = fma(Cv, u, kInvFact[2 * k + 3]);
+  }
+  double V[9], R[9], t[3], q[3];
+  rodrigues_form(phi, Bv, Cv, V);
+  mat3_vec(V, rho, t);
+  rodrigues_form(phi, a, Bv, R);
+  q[0] = p[0] - t[0]; q[1] = p[1] - t[1]; q[2] = p[2] - t[2];
+  mat3_tvec(R, q, out);
+}
 GC_DEV void direction_fast(const double* p, const double* o, double eps, double* d) {
   const double r0 = p[0] - o[0], r1 = p[1] - o[1], r2 = p[2] - o[2];
   const double inv = recip(sqrt(r0 * r0 + r1 * r1 + r2 * r2) + eps);
@@ -227,6 +299,11 @@ GC_DEV double sigmoid_fast(double x, const double* T) {
 }
 GC_DEV double window_weight_fast(double t, double t0, double t1, double inv_sig, const double* T) {
   const double wr = sigmoid_fast((t - t0) * inv_sig, T) * sigmoid_fast((t1 - t) * inv_sig, T);
+  return wr * (1.0 - 1e-12) + 1e-12;
+}
+
+GC_DEV double window_weight2(double t, double t0, double t1, double inv_sig, const double* T) {
+  const double wr = sigmoid2((t - t0) * inv_sig, T) * sigmoid2((t1 - t) * inv_sig, T);
   return wr * (1.0 - 1e-12) + 1e-12;
 }
 
@@ -775,13 +852,14 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   const double inv_denom = 1.0 / denom;
   const double inv_sig = 1.0 / fmax(0.1 * denom, 1e-6);
   double* Tx = lds + 4 * kFusedFS * NS;
-  double* Lb = Tx + kExpTab;  // bin directions pre-scaled by 1/τ (x, y, z rows of 64)
-  exp_table_init(Tx);
+  double* Lb = Tx + kExpTab2;  // bin directions pre-scaled by 2048/(τ ln2) (x, y, z rows of 64)
+  exp_table2_init(Tx);
+  const double ysc = inv_tau * kTab2OverLn2;
   if (threadIdx.x < 64) {
     const int b = threadIdx.x;
-    Lb[b] = b < B ? bins[3 * b] * inv_tau : 0.0;
-    Lb[64 + b] = b < B ? bins[3 * b + 1] * inv_tau : 0.0;
-    Lb[128 + b] = b < B ? bins[3 * b + 2] * inv_tau : 0.0;
+    Lb[b] = b < B ? bins[3 * b] * ysc : 0.0;
+    Lb[64 + b] = b < B ? bins[3 * b + 1] * ysc : 0.0;
+    Lb[128 + b] = b < B ? bins[3 * b + 2] * ysc : 0.0;
   }
   __syncthreads();
   constexpr int NACC = GC_FUSED_NACC;
@@ -795,7 +873,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
     for (int t = 0; t < NX; ++t) accx[j][t] = 0.0;
   }
   double sumw = 0.0, logacc = 0.0, entq = 0.0, mxr = 0.0;
-  const double xmax = inv_tau;  // S <= 1 for unit vectors: exp never overflows
+  const double ymax = ysc;  // S <= 1 for unit vectors: y = (S - 1) 2048/(τ ln2) <= 0
   const double Beps = (double)B * 1e-12;
   const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
   for (int it = 0; it < iters; ++it) {
@@ -811,8 +889,8 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
         ww = w_raw[i] * scale;
       }
       double q[3], d[3], f[NF];
-      deskew_point_fast(p, (tt - t0) * inv_denom, xr, q);
-      const double wd = inr ? ww * window_weight_fast(tt, t0, t1, inv_sig, Tx) : 0.0;
+      deskew_point_series(p, (tt - t0) * inv_denom, xr, q);
+      const double wd = inr ? ww * window_weight2(tt, t0, t1, inv_sig, Tx) : 0.0;
       direction_fast(q, o, 1e-12, d);
       point_features(q, d, wd, f);
       sumw += wd;
@@ -831,16 +909,18 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
       const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
       const bool valid = F[(NF + 3) * kFusedFS + pl] != 0.0;
       const double fb = F[bl * kFusedFS + pl];  // MFMA B operand: feature bl of point 4s + g
-      double e[BPL], x[BPL], ex[BPL], zl = 0.0, sl = 0.0, em = 0.0;
+      double e[BPL], x[BPL], ex[BPL];
 #pragma unroll
       for (int j = 0; j < BPL; ++j) {
-        const int b = bl + 16 * j;  // Lb is zero past B: x = -1/τ stays finite, then masked
-        x[j] = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -xmax)));
+        const int b = bl + 16 * j;  // Lb is zero past B: y = -ymax stays in range, then masked
+        x[j] = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -ymax)));
       }
-      exp_neg_n<BPL>(x, Tx, ex);
+      exp2s_n<BPL>(x, Tx, ex);
 #pragma unroll
-      for (int j = 0; j < BPL; ++j) {
-        e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
+      for (int j = 0; j < BPL; ++j) e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
+      double zl = e[0], sl = e[0] * x[0], em = e[0];  // e >= 0
+#pragma unroll
+      for (int j = 1; j < BPL; ++j) {
         zl += e[j];
         sl = fma(e[j], x[j], sl);
         em = fmax(em, e[j]);
@@ -848,7 +928,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
       const double Z = group16_sum(zl);
       const double rZ = recip(Z);
       if (valid) {
-        entq = fma(sl, rZ, entq);  // lane partials of S/Z, summed over lanes at the end
+        entq = fma(sl, rZ, entq);  // lane partials of S/Z (in y units), summed over lanes at the end
         mxr = fmax(mxr, em * rZ);
       }
       if (bl == s) zst = valid ? Z : 1.0;
@@ -871,7 +951,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
   int64_t npts = n_cap - chunk0;
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
-  const double ent = logacc - entq - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
+  const double ent = logacc - entq * kExp2C1 - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
   const int RL = B * NF + REC_EXTRA;
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
@@ -1352,10 +1432,12 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const int bpl = bpl_for(B);
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
-  const size_t sh = sizeof(double) * std::max<size_t>(4 * kFusedFS * (NF + 4) + kExpTab + 192, 4 * (size_t)B * NF + 12);
+  const size_t sh = sizeof(double) * std::max<size_t>(4 * kFusedFS * (NF + 4) + kExpTab2 + 192, 4 * (size_t)B * NF + 12);
   dim3 grid((unsigned)chunks, H);
   const double inv_tau = 1.0 / tau;
 #define GC_FUSED(BP, FULL)                                                                                     \
+  (void)hipFuncSetAttribute((const void*)k_bins_fused<BP, FULL>, hipFuncAttributeMaxDynamicSharedMemorySize,    \
+                            (int)sh);                                                                          \
   hipLaunchKernelGGL((k_bins_fused<BP, FULL>), grid, dim3(256), sh, ctx->stream, n_cap, B, iters, d_points_raw, \
                      d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins, inv_tau, h_origin3[0],            \
                      h_origin3[1], h_origin3[2], (double*)scr)
