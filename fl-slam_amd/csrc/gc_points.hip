@@ -876,18 +876,28 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   const double ymax = ysc;  // S <= 1 for unit vectors: y = (S - 1) 2048/(τ ln2) <= 0
   const double Beps = (double)B * 1e-12;
   const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
+  // raw point of the next iteration, loaded one iteration ahead (its HBM latency hides behind
+  // this iteration's soft assignment)
+  double np[3] = {0.0, 0.0, 0.0}, ntt = 0.0, nww = 0.0;
+  auto fetch = [&](int it2) {
+    const int64_t j = chunk0 + (int64_t)it2 * 256 + wv * 64 + lane;
+    np[0] = 0.0; np[1] = 0.0; np[2] = 0.0; ntt = 0.0; nww = 0.0;
+    if (j < n_cap && j < n_sel) {
+      const int64_t i = j * stride;
+      np[0] = pts_raw[3 * i]; np[1] = pts_raw[3 * i + 1]; np[2] = pts_raw[3 * i + 2];
+      ntt = t_raw[i];
+      nww = w_raw[i];
+    }
+  };
+  fetch(0);
   for (int it = 0; it < iters; ++it) {
     const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
     {  // phase A
       const int64_t j = wbase + lane;
       const bool inr = j < n_cap;
-      double p[3] = {0.0, 0.0, 0.0}, tt = 0.0, ww = 0.0;
-      if (inr && j < n_sel) {
-        const int64_t i = j * stride;
-        p[0] = pts_raw[3 * i]; p[1] = pts_raw[3 * i + 1]; p[2] = pts_raw[3 * i + 2];
-        tt = t_raw[i];
-        ww = w_raw[i] * scale;
-      }
+      double p[3] = {np[0], np[1], np[2]};
+      const double tt = ntt, ww = nww * scale;
+      if (it + 1 < iters) fetch(it + 1);
       double q[3], d[3], f[NF];
       deskew_point_series(p, (tt - t0) * inv_denom, xr, q);
       const double wd = inr ? ww * window_weight2(tt, t0, t1, inv_sig, Tx) : 0.0;

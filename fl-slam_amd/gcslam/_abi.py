@@ -98,6 +98,11 @@ SIGNATURES = {
     "gc_iw_meas_apply": [_vp, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp],
     "gc_hypothesis_barycenter": [_vp, _i32, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp],
     "gc_primitive_map_fuse": [_vp, _vp, _vp, _vp, _f64, _f64, _f64, _i64, _vp],
+    "gc_primitive_map_forget": [_vp, _vp, _i64, _i64, _f64],
+    "gc_primitive_map_recency_inflate": [_vp, _vp, _i64, _i64, _i64, _f64, _f64, _vp],
+    "gc_primitive_map_cull": [_vp, _vp, _i64, _i64, _f64, _i64, _vp],
+    "gc_primitive_map_insert_masked": [_vp, _vp, _i64, _i64, _vp, _f64, _i64, _f64, _i64, _vp, _vp, _vp],
+    "gc_primitive_map_merge_reduce": [_vp, _vp, _i64, _i64, _f64, _i32, _f64, _f64, _vp],
 }
 
 GC_PCFG_LEN = 22

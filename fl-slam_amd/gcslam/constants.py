@@ -44,6 +44,16 @@ GC_IMU_ACCEL_NOISE_DENSITY = 9.5e-5  # constants.py:201
 GC_PLANAR_Z_REF = 0.0                # constants.py:294
 GC_PLANAR_Z_SIGMA = 0.1              # constants.py:305
 GC_PLANAR_VZ_SIGMA = 0.01            # constants.py:310
+# PrimitiveMap maintenance (constants.py:392-477)
+GC_PRIMITIVE_MAP_MAX_SIZE = 50000
+GC_RECENCY_DECAY_LAMBDA = 0.02
+GC_RECENCY_MIN_SCALE = 0.05
+GC_PRIMITIVE_FORGETTING_FACTOR = 0.995
+GC_PRIMITIVE_MERGE_THRESHOLD = 0.1
+GC_K_MERGE_PAIRS_PER_TILE = 4
+GC_PRIMITIVE_MERGE_MAX_TILE_SIZE = 2048
+GC_PRIMITIVE_CULL_WEIGHT_THRESHOLD = 1e-4
+GC_K_INSERT_TILE = 64
 
 # PipelineConfig defaults (pipeline.py:118-131; gc_unified.yaml:41-57)
 POWER_BETA_MIN = 0.25

@@ -1,30 +1,43 @@
-"""Device-resident PrimitiveMap and primitive_map_fuse (backend/structures/primitive_map.py:
-992-1163) with the world pushforward of transform_gaussian_to_world (backend/pipeline.py:
-1248-1256) fused in: the C5 map update. The map lives in HBM as one flat array of
-n_tiles * m_tile slots (tile t, local slot j -> t * m_tile + j); the fuse runs in place."""
+"""Device-resident PrimitiveMap and its operators (backend/structures/primitive_map.py):
+primitive_map_fuse (:992-1163) with the world pushforward of transform_gaussian_to_world
+(backend/pipeline.py:1248-1256) fused in (the C5 map update), and the maintenance operators
+primitive_map_insert_masked (:807-982), primitive_map_cull (:1175-1305), primitive_map_forget
+(:1314-1390), primitive_map_recency_inflate (:1400-1490) and primitive_map_merge_reduce
+(:1809-2030). The map lives in HBM as one flat array of n_tiles * m_tile slots (tile t, local
+slot j -> t * m_tile + j); every operator runs in place on its tile. The AtlasMap bookkeeping
+(next_global_id, total_count, per-tile count) stays on the host, as in the reference."""
 
 from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import Dict, Tuple
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 
 from . import _abi
-from .certificates import CertBundle, ExpectedEffect
-from .constants import GC_CHART_ID, GC_EPS_LIFT, GC_EPS_MASS, GC_EPS_PSD
+from .certificates import CertBundle, ExpectedEffect, InfluenceCert
+from .constants import (GC_CHART_ID, GC_EPS_LIFT, GC_EPS_MASS, GC_EPS_PSD, GC_K_MERGE_PAIRS_PER_TILE,
+                        GC_PRIMITIVE_CULL_WEIGHT_THRESHOLD, GC_PRIMITIVE_FORGETTING_FACTOR,
+                        GC_PRIMITIVE_MERGE_MAX_TILE_SIZE, GC_PRIMITIVE_MERGE_THRESHOLD, GC_RECENCY_DECAY_LAMBDA,
+                        GC_RECENCY_MIN_SCALE)
 
 GC_VMF_N_LOBES = 3
 
 _F64 = ("Lambdas", "thetas", "etas", "weights", "timestamps")
 _I64 = ("last_supported_scan_seq", "last_update_scan_seq")
 _COL = ("cam_mass", "lidar_mass", "rgb_cam_accum", "rgb_cam_denom", "rgb", "colors")
+_MAINT = ("valid_mask", "created_timestamps", "primitive_ids")
 
 
 class _MapStruct(C.Structure):
     _fields_ = [("m_slots", C.c_int64), ("n_lobes", C.c_int32), ("pad_", C.c_int32)] + \
-               [(k, C.c_void_p) for k in _F64 + _I64 + _COL]
+               [(k, C.c_void_p) for k in _F64 + _I64 + _COL + _MAINT]
+
+
+class _InsertStruct(C.Structure):
+    _fields_ = [("K", C.c_int64)] + [(k, C.c_void_p) for k in (
+        "Lambdas", "thetas", "etas", "weights", "valid_mask", "colors", "sources")]
 
 
 class _FuseStruct(C.Structure):
@@ -43,17 +56,24 @@ class DevicePrimitiveMap:
         M = self.M = self.n_tiles * self.m_tile
         shapes = dict(Lambdas=(M, 3, 3), thetas=(M, 3), etas=(M, n_lobes, 3), weights=(M,), timestamps=(M,),
                       last_supported_scan_seq=(M,), last_update_scan_seq=(M,), cam_mass=(M,), lidar_mass=(M,),
-                      rgb_cam_accum=(M, 3), rgb_cam_denom=(M,), rgb=(M, 3), colors=(M, 3))
+                      rgb_cam_accum=(M, 3), rgb_cam_denom=(M,), rgb=(M, 3), colors=(M, 3),
+                      valid_mask=(M,), created_timestamps=(M,), primitive_ids=(M,))
+        dtypes = dict(last_supported_scan_seq=np.int64, last_update_scan_seq=np.int64, primitive_ids=np.int64,
+                      valid_mask=np.uint8)
         self.fields: Dict[str, _abi.DeviceArray] = {}
         for k, shp in shapes.items():
             if k in _COL and not track_colors:
                 continue
-            self.fields[k] = _abi.DeviceArray(self.ctx, shp, np.int64 if k in _I64 else np.float64)
+            self.fields[k] = _abi.DeviceArray(self.ctx, shp, dtypes.get(k, np.float64))
             self.fields[k].zero()
         if track_colors:
             self.fields["rgb"].upload(np.full((M, 3), 0.5))
         self._struct = _MapStruct(M, self.n_lobes, 0, *[self.fields[k].ptr if k in self.fields else None
-                                                        for k in _F64 + _I64 + _COL])
+                                                        for k in _F64 + _I64 + _COL + _MAINT])
+        # AtlasMap bookkeeping (primitive_map.py:183-201): host integers, as in the reference
+        self.next_global_id = 0
+        self.total_count = 0
+        self.tile_count: Dict[int, int] = {}
 
     def upload(self, **arrays):
         for k, v in arrays.items():
@@ -64,6 +84,16 @@ class DevicePrimitiveMap:
 
     def tile_slot(self, tile_id: int, slots) -> np.ndarray:
         return int(tile_id) * self.m_tile + np.asarray(slots, dtype=np.int64)
+
+    def tile_range(self, tile_id: int) -> Tuple[int, int]:
+        t = int(tile_id)
+        if not 0 <= t < self.n_tiles:
+            raise ValueError(f"tile_id {t} outside [0, {self.n_tiles})")
+        return t * self.m_tile, self.m_tile
+
+    def download_tile(self, tile_id: int, *names) -> Dict[str, np.ndarray]:
+        s0, n = self.tile_range(tile_id)
+        return {k: v[s0:s0 + n] for k, v in self.download(*names).items()}
 
 
 @dataclass
@@ -137,3 +167,191 @@ def primitive_map_fuse(atlas_map: DevicePrimitiveMap, tile_id: int, target_slots
     return (PrimitiveMapFuseResult(atlas_map, int(tile_id), n),
             CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
             ExpectedEffect(objective_name="primitive_map_fuse", predicted=float(K), realized=float(n)))
+
+
+# ----------------------------------------------------------------------------- maintenance
+def _no_op(result, chart_id: str, anchor_id: str, name: str, predicted: float = 0.0):
+    """_exact_no_op_result (primitive_map.py:624-640)."""
+    return (result, CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
+            ExpectedEffect(objective_name=name, predicted=predicted, realized=0.0))
+
+
+@dataclass
+class PrimitiveMapForgetResult:
+    atlas_map: DevicePrimitiveMap
+    tile_id: int
+
+
+def primitive_map_forget(atlas_map: DevicePrimitiveMap, tile_id: int,
+                         forgetting_factor: float = GC_PRIMITIVE_FORGETTING_FACTOR, chart_id: str = GC_CHART_ID,
+                         anchor_id: str = "primitive_map"
+                         ) -> Tuple[PrimitiveMapForgetResult, CertBundle, ExpectedEffect]:
+    """primitive_map_forget (primitive_map.py:1314-1390): weights *= γ on the tile."""
+    s0, n = atlas_map.tile_range(tile_id)
+    gamma = float(forgetting_factor)
+    _abi.call("gc_primitive_map_forget", atlas_map.ctx.handle, C.byref(atlas_map._struct), s0, n, gamma,
+              ctx=atlas_map.ctx)
+    return (PrimitiveMapForgetResult(atlas_map, int(tile_id)),
+            CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
+            ExpectedEffect(objective_name="primitive_map_forget", predicted=1.0 - gamma, realized=1.0 - gamma))
+
+
+@dataclass
+class PrimitiveMapRecencyInflateStats:
+    staleness_inflation_strength: float
+    staleness_cov_inflation_trace: float
+    stale_precision_downscale_total: float
+
+
+def primitive_map_recency_inflate(atlas_map: DevicePrimitiveMap, tile_ids: List[int], scan_seq: int,
+                                  recency_decay_lambda: float = GC_RECENCY_DECAY_LAMBDA,
+                                  min_scale: float = GC_RECENCY_MIN_SCALE, chart_id: str = GC_CHART_ID,
+                                  anchor_id: str = "primitive_map_recency_inflate"):
+    """primitive_map_recency_inflate (primitive_map.py:1400-1490) -> (atlas_map, cert, effect, stats)."""
+    n_valid = downscale = trace = 0.0
+    for tid in tile_ids:
+        s0, n = atlas_map.tile_range(tid)
+        st = np.zeros(3)
+        _abi.call("gc_primitive_map_recency_inflate", atlas_map.ctx.handle, C.byref(atlas_map._struct), s0, n,
+                  int(scan_seq), float(recency_decay_lambda), float(min_scale), st.ctypes.data, ctx=atlas_map.ctx)
+        n_valid += st[0]
+        downscale += st[1]
+        trace += st[2]
+    stats = PrimitiveMapRecencyInflateStats(staleness_inflation_strength=float(downscale / max(n_valid, 1.0)),
+                                            staleness_cov_inflation_trace=float(trace),
+                                            stale_precision_downscale_total=float(downscale))
+    return (atlas_map, CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
+            ExpectedEffect(objective_name="primitive_map_recency_inflate", predicted=float(n_valid),
+                           realized=float(n_valid)), stats)
+
+
+@dataclass
+class PrimitiveMapCullResult:
+    atlas_map: DevicePrimitiveMap
+    tile_id: int
+    n_culled: int
+    mass_dropped: float
+
+
+def primitive_map_cull(atlas_map: DevicePrimitiveMap, tile_id: int,
+                       weight_threshold: float = GC_PRIMITIVE_CULL_WEIGHT_THRESHOLD,
+                       max_primitives: Optional[int] = None, chart_id: str = GC_CHART_ID,
+                       anchor_id: str = "primitive_map") -> Tuple[PrimitiveMapCullResult, CertBundle, ExpectedEffect]:
+    """primitive_map_cull (primitive_map.py:1175-1305)."""
+    s0, n = atlas_map.tile_range(tile_id)
+    out = np.zeros(4)
+    _abi.call("gc_primitive_map_cull", atlas_map.ctx.handle, C.byref(atlas_map._struct), s0, n,
+              float(weight_threshold), -1 if max_primitives is None else int(max_primitives), out.ctypes.data,
+              ctx=atlas_map.ctx)
+    n_culled, mass_dropped, sum_w, n_valid = int(out[0]), float(out[1]), float(out[2]), int(out[3])
+    if n_valid == 0 or n_culled == 0:
+        return _no_op(PrimitiveMapCullResult(atlas_map, int(tile_id), 0, 0.0), chart_id, anchor_id,
+                      "primitive_map_cull")
+    atlas_map.tile_count[int(tile_id)] = n_valid - n_culled
+    atlas_map.total_count -= n_culled
+    cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=["budgeting", "mass_drop"],
+                                    influence=InfluenceCert.identity().with_overrides(
+                                        mass_epsilon_ratio=mass_dropped / (sum_w + GC_EPS_MASS)))
+    return (PrimitiveMapCullResult(atlas_map, int(tile_id), n_culled, mass_dropped), cert,
+            ExpectedEffect(objective_name="primitive_map_cull", predicted=float(n_culled), realized=float(n_culled)))
+
+
+@dataclass
+class PrimitiveMapInsertResult:
+    atlas_map: DevicePrimitiveMap
+    tile_id: int
+    n_inserted: int
+    new_ids: np.ndarray
+    target_slots: Optional[np.ndarray] = None  # tile-local eviction slots (extra field)
+
+
+def primitive_map_insert_masked(atlas_map: DevicePrimitiveMap, tile_id: int, Lambdas_new, thetas_new, etas_new,
+                                weights_new, timestamp: float, valid_new_mask, scan_seq: int = 0,
+                                recency_decay_lambda: float = GC_RECENCY_DECAY_LAMBDA, colors_new=None,
+                                sources_new=None, chart_id: str = GC_CHART_ID,
+                                anchor_id: str = "primitive_map_insert_masked"
+                                ) -> Tuple[PrimitiveMapInsertResult, CertBundle, ExpectedEffect]:
+    """primitive_map_insert_masked (primitive_map.py:807-982)."""
+    s0, n = atlas_map.tile_range(tile_id)
+    L = atlas_map.n_lobes
+    w = np.ascontiguousarray(weights_new, np.float64).reshape(-1)
+    K = w.shape[0]
+    mask = np.ascontiguousarray(valid_new_mask).reshape(-1).astype(np.uint8)
+    if mask.shape[0] != K or K > n or K == 0:
+        raise ValueError(f"insert_masked: K={K} proposals, mask {mask.shape[0]}, tile {n}")
+    ctx = atlas_map.ctx
+    arrs = [np.ascontiguousarray(Lambdas_new, np.float64).reshape(K, 9),
+            np.ascontiguousarray(thetas_new, np.float64).reshape(K, 3),
+            np.ascontiguousarray(etas_new, np.float64).reshape(K, 3 * L), w, mask,
+            None if colors_new is None else np.ascontiguousarray(colors_new, np.float64).reshape(K, 3),
+            None if sources_new is None else np.ascontiguousarray(sources_new, np.int32).reshape(K)]
+    dev = [None if a is None else _abi.DeviceArray.from_host(ctx, a, a.dtype) for a in arrs]
+    batch = _InsertStruct(K, *[None if d is None else d.ptr for d in dev])
+    d_slots = _abi.DeviceArray(ctx, K, np.int32)
+    d_ids = _abi.DeviceArray(ctx, K, np.int64)
+    out = np.zeros(2, np.int64)
+    _abi.call("gc_primitive_map_insert_masked", ctx.handle, C.byref(atlas_map._struct), s0, n, C.byref(batch),
+              float(timestamp), int(scan_seq), float(recency_decay_lambda), int(atlas_map.next_global_id),
+              d_slots.ptr, d_ids.ptr, out.ctypes.data, ctx=ctx)
+    n_ins, count = int(out[0]), int(out[1])
+    atlas_map.next_global_id += n_ins
+    atlas_map.total_count += n_ins
+    atlas_map.tile_count[int(tile_id)] = count
+    dropped = int(np.sum(mask == 0))
+    cert = (CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=["insert_unfilled_budget"],
+                                     frobenius_applied=False) if dropped > 0
+            else CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id))
+    return (PrimitiveMapInsertResult(atlas_map, int(tile_id), n_ins, d_ids.download(), d_slots.download()), cert,
+            ExpectedEffect(objective_name="primitive_map_insert_masked", predicted=float(int(mask.sum())),
+                           realized=float(n_ins)))
+
+
+@dataclass
+class PrimitiveMapMergeReduceResult:
+    atlas_map: DevicePrimitiveMap
+    tile_id: int
+    n_merged: int
+    frobenius_correction: float
+
+
+def primitive_map_merge_reduce(atlas_map: DevicePrimitiveMap, tile_id: int,
+                               merge_threshold: float = GC_PRIMITIVE_MERGE_THRESHOLD,
+                               max_pairs: int = GC_K_MERGE_PAIRS_PER_TILE,
+                               max_tile_size: int = GC_PRIMITIVE_MERGE_MAX_TILE_SIZE, eps_psd: float = GC_EPS_PSD,
+                               eps_lift: float = GC_EPS_LIFT, chart_id: str = GC_CHART_ID,
+                               anchor_id: str = "primitive_map"
+                               ) -> Tuple[PrimitiveMapMergeReduceResult, CertBundle, ExpectedEffect]:
+    """primitive_map_merge_reduce (primitive_map.py:1809-2030)."""
+    s0, M = atlas_map.tile_range(tile_id)
+
+    def no_op(predicted, triggers=None, influence=None):
+        res = PrimitiveMapMergeReduceResult(atlas_map, int(tile_id), 0, 0.0)
+        cert = (CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=triggers,
+                                         frobenius_applied=True, influence=influence or InfluenceCert.identity())
+                if triggers else CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id))
+        return res, cert, ExpectedEffect(objective_name="primitive_map_merge_reduce", predicted=predicted,
+                                         realized=0.0)
+
+    if int(max_tile_size) > 0 and M > int(max_tile_size):
+        # the budget cap (:1881-1890) applies after the M / valid count / max_pairs no-op test (:1879)
+        n_valid = int(atlas_map.download_tile(tile_id, "valid_mask")["valid_mask"].sum())
+        if M < 2 or n_valid < 2 or int(max_pairs) <= 0:
+            return no_op(float(max_pairs))
+        over = float(M - int(max_tile_size)) / float(max(M, 1))
+        return no_op(float(max_pairs), ["merge_reduce_budget_cap"],
+                     InfluenceCert.identity().with_overrides(mass_epsilon_ratio=over))
+    out = np.zeros(2, np.int64)
+    _abi.call("gc_primitive_map_merge_reduce", atlas_map.ctx.handle, C.byref(atlas_map._struct), s0, M,
+              float(merge_threshold), int(max_pairs), float(eps_psd), float(eps_lift), out.ctypes.data,
+              ctx=atlas_map.ctx)
+    n_merged, count = int(out[0]), int(out[1])
+    if n_merged <= 0:
+        return no_op(float(max_pairs))
+    atlas_map.tile_count[int(tile_id)] = count
+    atlas_map.total_count -= n_merged
+    cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=["primitive_map_merge_reduce"],
+                                    frobenius_applied=True, influence=InfluenceCert.identity().with_overrides(
+                                        mass_epsilon_ratio=float(n_merged) / float(max(M, 1))))
+    return (PrimitiveMapMergeReduceResult(atlas_map, int(tile_id), n_merged, float(n_merged)), cert,
+            ExpectedEffect(objective_name="primitive_map_merge_reduce", predicted=float(max_pairs),
+                           realized=float(n_merged)))

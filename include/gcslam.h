@@ -442,6 +442,11 @@ typedef struct gc_primitive_map {
   double* rgb_cam_denom;    /* (M) or NULL */
   double* rgb;              /* (M, 3) or NULL */
   double* colors;           /* (M, 3) or NULL */
+  /* maintenance fields (primitive_map_insert_masked / cull / recency / merge; the fuse ignores
+     them): valid_mask is required by those entries, the other two may be NULL */
+  uint8_t* valid_mask;      /* (M) */
+  double* created_timestamps;        /* (M) or NULL */
+  int64_t* primitive_ids;            /* (M) or NULL */
 } gc_primitive_map;
 
 typedef struct gc_fuse_batch {
@@ -463,6 +468,58 @@ typedef struct gc_fuse_batch {
 int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc_fuse_batch* meas,
                               const double* h_pose6, double eps_lift, double eps_mass, double timestamp,
                               int64_t scan_seq, int64_t* n_fused_out);
+
+/* ------------------------------------------------------------------------------------------
+ * PrimitiveMap maintenance. Each entry works on one reference tile: the slot
+ * range [slot0, slot0 + n_slots) of the flat map (tile t -> slot0 = t * m_tile). Reductions are
+ * fixed-order (no float atomics); host outputs synchronise the stream.
+ * ------------------------------------------------------------------------------------------ */
+/* primitive_map_forget (primitive_map.py:1314-1390): weights *= gamma on every slot. */
+int32_t gc_primitive_map_forget(gc_ctx* ctx, const gc_primitive_map* map, int64_t slot0, int64_t n_slots,
+                                double gamma);
+/* primitive_map_recency_inflate (primitive_map.py:1400-1490) on one tile: decay =
+   clip(exp(-lambda max(0, scan_seq - last_supported)), min_scale, 1) on valid slots (1 elsewhere);
+   Lambdas, thetas *= decay. h_stats3 (host, may be NULL) = [n_valid, sum (1 - decay), sum (1/decay - 1)]
+   over valid slots. */
+int32_t gc_primitive_map_recency_inflate(gc_ctx* ctx, const gc_primitive_map* map, int64_t slot0, int64_t n_slots,
+                                         int64_t scan_seq, double decay_lambda, double min_scale,
+                                         double* h_stats3);
+/* primitive_map_cull (primitive_map.py:1175-1305): clears valid on valid slots with weight <
+   threshold; with max_primitives >= 0 (< 0 = None) and more survivors than that, the threshold
+   becomes the (max_primitives+1)-th largest of weight*valid. h_out4 (host) = [n_culled,
+   mass_dropped, sum of all tile weights, n_valid before]. */
+int32_t gc_primitive_map_cull(gc_ctx* ctx, const gc_primitive_map* map, int64_t slot0, int64_t n_slots,
+                              double weight_threshold, int64_t max_primitives, double* h_out4);
+
+typedef struct gc_insert_batch {
+  int64_t K;
+  const double* Lambdas;            /* (K, 3, 3) */
+  const double* thetas;             /* (K, 3) */
+  const double* etas;               /* (K, n_lobes, 3) */
+  const double* weights;            /* (K) */
+  const uint8_t* valid_mask;        /* (K) proposals with 0 are ignored */
+  const double* colors;             /* (K, 3) or NULL (zeros) */
+  const int32_t* sources;           /* (K) 0 = camera, 1 = lidar, or NULL (all lidar) */
+} gc_insert_batch;
+
+/* primitive_map_insert_masked (primitive_map.py:807-982): proposal k goes to the k-th slot of the
+   tile ordered by retention key (valid ? w exp(-lambda max(0, seq - last_supported)) : -inf),
+   ties by slot (_select_lowest_mass_slots_fixed :325-353, a stable sort on the key). Inserted
+   proposals get ids next_global_id + (number inserted before them). d_target_slots_out (K, tile-
+   local) and d_new_ids_out (K, -1 where not inserted) may be NULL. h_out2 (host) = [n_inserted,
+   valid count of the tile after]. Requires 1 <= K <= n_slots. */
+int32_t gc_primitive_map_insert_masked(gc_ctx* ctx, const gc_primitive_map* map, int64_t slot0, int64_t n_slots,
+                                       const gc_insert_batch* batch, double timestamp, int64_t scan_seq,
+                                       double recency_decay_lambda, int64_t next_global_id,
+                                       int32_t* d_target_slots_out, int64_t* d_new_ids_out, int64_t* h_out2);
+/* primitive_map_merge_reduce (primitive_map.py:1809-2030 -> _merge_reduce_jax :1501-1807):
+   Bhattacharyya distances of all slot pairs i < j (+inf unless both valid), a stable ascending
+   sort, greedy disjoint selection of up to max_pairs pairs with finite distance < threshold, and
+   moment-matched merges into the lower slot. The caller applies the reference's tile-size cap.
+   h_out2 (host) = [n_merged, valid count after]. Requires n_slots <= 65536. */
+int32_t gc_primitive_map_merge_reduce(gc_ctx* ctx, const gc_primitive_map* map, int64_t slot0, int64_t n_slots,
+                                      double merge_threshold, int32_t max_pairs, double eps_psd, double eps_lift,
+                                      int64_t* h_out2);
 
 #ifdef __cplusplus
 }

@@ -1338,3 +1338,173 @@ def primitive_map_fuse(tile: dict, slots, Lambdas, thetas, etas, weights, resp, 
         out["rgb"] = np.where((out["cam_mass"] > 0.0)[:, None], est, 0.5)
         out["colors"] = out["rgb"].copy()
     return out, int(np.unique(idx).shape[0])
+
+
+# ---------------------------------------------------------------------------------------
+# PrimitiveMap maintenance (structures/primitive_map.py), SURVEY §8f rank 3. A tile is a dict of
+# the create_empty_tile fields (valid_mask bool); each function returns a new tile dict.
+# ---------------------------------------------------------------------------------------
+def empty_tile(m_tile, L=3):
+    """create_empty_tile (primitive_map.py:148-175)."""
+    return dict(Lambdas=np.zeros((m_tile, 3, 3)), thetas=np.zeros((m_tile, 3)), etas=np.zeros((m_tile, L, 3)),
+                weights=np.zeros(m_tile), timestamps=np.zeros(m_tile), created_timestamps=np.zeros(m_tile),
+                last_supported_scan_seq=np.zeros(m_tile, np.int64), last_update_scan_seq=np.zeros(m_tile, np.int64),
+                primitive_ids=np.zeros(m_tile, np.int64), valid_mask=np.zeros(m_tile, bool),
+                colors=np.zeros((m_tile, 3)), cam_mass=np.zeros(m_tile), lidar_mass=np.zeros(m_tile),
+                rgb_cam_accum=np.zeros((m_tile, 3)), rgb_cam_denom=np.zeros(m_tile), rgb=np.full((m_tile, 3), 0.5))
+
+
+def _tile_copy(tile):
+    return {k: np.array(v, copy=True) for k, v in tile.items()}
+
+
+def primitive_map_forget(tile, gamma):
+    """primitive_map_forget (primitive_map.py:1314-1390): weights = γ · weights."""
+    out = _tile_copy(tile)
+    out["weights"] = gamma * tile["weights"]
+    return out
+
+
+def _recency_decay(scan_seq, last_supported, lam):
+    dt = np.maximum(np.int64(0), np.int64(scan_seq) - np.asarray(last_supported, np.int64))
+    return np.exp(-lam * dt.astype(np.float64))
+
+
+def primitive_map_recency_inflate(tile, scan_seq, lam, min_scale):
+    """primitive_map_recency_inflate (primitive_map.py:1400-1490) for one tile -> (tile, (n_valid,
+    Σ(1 - decay), Σ(1/decay - 1)))."""
+    valid = np.asarray(tile["valid_mask"], bool)
+    decay = np.clip(_recency_decay(scan_seq, tile["last_supported_scan_seq"], lam), float(min_scale), 1.0)
+    decay = np.where(valid, decay, 1.0)
+    out = _tile_copy(tile)
+    out["Lambdas"] = tile["Lambdas"] * decay[:, None, None]
+    out["thetas"] = tile["thetas"] * decay[:, None]
+    vf = valid.astype(np.float64)
+    return out, (float(vf.sum()), float(np.sum((1.0 - decay) * vf)), float(np.sum((1.0 / decay - 1.0) * vf)))
+
+
+def primitive_map_cull(tile, weight_threshold, max_primitives=None):
+    """primitive_map_cull (primitive_map.py:1175-1305) -> (tile, n_culled, mass_dropped)."""
+    valid = np.asarray(tile["valid_mask"], bool)
+    w = tile["weights"]
+    out = _tile_copy(tile)
+    count = int(valid.sum())
+    if count == 0:
+        return out, 0, 0.0
+    below = valid & (w < weight_threshold)
+    if max_primitives is not None and count - int(below.sum()) > max_primitives:
+        sw = np.sort(w * valid.astype(np.float64))[::-1]
+        if max_primitives < len(sw):
+            below = valid & (w < float(sw[max_primitives]))
+    n = int(below.sum())
+    if n == 0:
+        return out, 0, 0.0
+    out["valid_mask"] = valid & ~below
+    return out, n, float(np.sum(w * below.astype(np.float64)))
+
+
+def select_lowest_mass_slots(tile, scan_seq, lam, k):
+    """_select_lowest_mass_slots_fixed (primitive_map.py:325-353). jax.lax.sort with the default
+    num_keys=1 is a stable sort on the key alone, so ties keep slot order."""
+    ret = tile["weights"] * _recency_decay(scan_seq, tile["last_supported_scan_seq"], lam)
+    key = np.where(np.asarray(tile["valid_mask"], bool), ret, -np.inf)
+    return np.argsort(key, kind="stable")[:k].astype(np.int32)
+
+
+def primitive_map_insert_masked(tile, Lambdas, thetas, etas, weights, timestamp, valid_new, scan_seq, lam,
+                                next_global_id, colors=None, sources=None):
+    """primitive_map_insert_masked (primitive_map.py:807-982) -> (tile, n_inserted, new_ids, slots)."""
+    w = np.asarray(weights, np.float64).reshape(-1)
+    K = w.shape[0]
+    slots = select_lowest_mass_slots(tile, scan_seq, lam, K)
+    do = np.asarray(valid_new, bool).reshape(-1)
+    ids = np.where(do, np.int64(next_global_id) + np.cumsum(do.astype(np.int64)) - 1, np.int64(-1))
+    col = np.zeros((K, 3)) if colors is None else np.asarray(colors, np.float64).reshape(K, 3)
+    if sources is None:
+        is_cam, is_lid = np.zeros(K), np.ones(K)
+    else:
+        src = np.asarray(sources).reshape(-1)
+        is_cam, is_lid = (src == 0).astype(np.float64), (src == 1).astype(np.float64)
+    cam, lid = w * is_cam, w * is_lid
+    rgb_new = np.where((cam > 0.0)[:, None], np.clip(col, 0.0, 1.0), 0.5)
+    out = _tile_copy(tile)
+    s = slots[do]
+    out["Lambdas"][s] = np.asarray(Lambdas, np.float64).reshape(K, 3, 3)[do]
+    out["thetas"][s] = np.asarray(thetas, np.float64).reshape(K, 3)[do]
+    out["etas"][s] = np.asarray(etas, np.float64).reshape(K, -1, 3)[do]
+    out["weights"][s] = w[do]
+    out["timestamps"][s] = float(timestamp)
+    out["created_timestamps"][s] = float(timestamp)
+    out["last_supported_scan_seq"][s] = scan_seq
+    out["last_update_scan_seq"][s] = scan_seq
+    out["primitive_ids"][s] = ids[do]
+    out["valid_mask"][s] = True
+    out["colors"][s] = rgb_new[do]
+    out["cam_mass"][s] = cam[do]
+    out["lidar_mass"][s] = lid[do]
+    out["rgb_cam_accum"][s] = (col * cam[:, None])[do]
+    out["rgb_cam_denom"][s] = cam[do]
+    out["rgb"][s] = rgb_new[do]
+    return out, int(do.sum()), ids, slots
+
+
+def primitive_map_merge_reduce(tile, merge_threshold, max_pairs, eps_psd=EPS_PSD, eps_lift=EPS_LIFT):
+    """primitive_map_merge_reduce (primitive_map.py:1809-2030 -> _merge_reduce_jax :1501-1807)
+    -> (tile, n_merged). The caller applies the tile-size budget cap."""
+    valid = np.asarray(tile["valid_mask"], bool)
+    M = valid.shape[0]
+    out = _tile_copy(tile)
+    if M < 2 or int(valid.sum()) < 2 or max_pairs <= 0:
+        return out, 0
+    Lr = tile["Lambdas"] + eps_lift * np.eye(3)[None]
+    mu = np.linalg.solve(Lr, tile["thetas"][..., None])[..., 0]
+    Sig = np.linalg.inv(Lr)
+    det = np.linalg.det(Sig)
+    ii, jj = np.triu_indices(M, k=1)
+    S = 0.5 * (Sig[ii] + Sig[jj])
+    detS = np.linalg.det(S)
+    Sinv = np.linalg.inv(S + eps_lift * np.eye(3)[None])
+    dmu = (mu[ii] - mu[jj])[:, :, None]
+    quad = 0.125 * np.squeeze(np.matmul(np.matmul(dmu.transpose(0, 2, 1), Sinv), dmu), axis=(1, 2))
+    with np.errstate(invalid="ignore", divide="ignore"):
+        logt = 0.5 * np.log(detS / np.sqrt(det[ii] * det[jj] + 1e-24))
+    dist = np.where(valid[ii] & valid[jj], quad + logt, np.inf)
+    used = np.zeros(M, bool)
+    sel = []
+    for idx in np.argsort(dist, kind="stable"):  # select_body (:1560-1585)
+        if len(sel) >= max_pairs:
+            break
+        d, i, j = dist[idx], ii[idx], jj[idx]
+        if np.isfinite(d) and d < merge_threshold and not used[i] and not used[j]:
+            used[i] = used[j] = True
+            sel.append((i, j))
+    for i, j in sel:  # merge_body (:1603-1726)
+        w1, w2 = out["weights"][i], out["weights"][j]
+        ws = w1 + w2
+        if not ws > 0.0:
+            continue
+        mm = (w1 * mu[i] + w2 * mu[j]) / ws
+        d1, d2 = (mu[i] - mm)[:, None], (mu[j] - mm)[:, None]
+        Sm = (w1 * (Sig[i] + d1 @ d1.T) + w2 * (Sig[j] + d2 @ d2.T)) / ws + eps_psd * np.eye(3)
+        Lm = np.linalg.inv(Sm)
+        out["Lambdas"][i] = Lm
+        out["thetas"][i] = Lm @ mm
+        out["etas"][i] = (w1 * out["etas"][i] + w2 * out["etas"][j]) / ws
+        cm = out["cam_mass"][i] + out["cam_mass"][j]
+        acc = out["rgb_cam_accum"][i] + out["rgb_cam_accum"][j]
+        den = out["rgb_cam_denom"][i] + out["rgb_cam_denom"][j]
+        rgb = np.clip(acc / max(den, eps_psd), 0.0, 1.0) if cm > 0.0 else np.full(3, 0.5)
+        out["cam_mass"][i] = cm
+        out["lidar_mass"][i] = out["lidar_mass"][i] + out["lidar_mass"][j]
+        out["rgb_cam_accum"][i] = acc
+        out["rgb_cam_denom"][i] = den
+        out["rgb"][i] = rgb
+        out["colors"][i] = rgb
+        out["timestamps"][i] = max(out["timestamps"][i], out["timestamps"][j])
+        out["created_timestamps"][i] = min(out["created_timestamps"][i], out["created_timestamps"][j])
+        out["last_supported_scan_seq"][i] = max(out["last_supported_scan_seq"][i], out["last_supported_scan_seq"][j])
+        out["last_update_scan_seq"][i] = max(out["last_update_scan_seq"][i], out["last_update_scan_seq"][j])
+        out["weights"][i] = ws
+        out["weights"][j] = 0.0
+        out["valid_mask"][j] = False
+    return out, len(sel)
