@@ -1,5 +1,6 @@
 """PointCloud2 (VLP-16 layout) parsing on the GPU: parse_pointcloud2_vlp16
-(backend/backend_node.py:377-468) and the no-TF base transform (backend_node.py:1677-1690).
+(backend/backend_node.py:377-468) and the no-TF base transform (backend_node.py:1677-1690); the
+IMU window slicing/padding of the same per-scan staging (backend_node.py:1927-1951).
 
 The message is duck-typed like sensor_msgs/PointCloud2: ``width``, ``height``, ``point_step``,
 ``fields`` (objects with ``name``, ``offset``, ``datatype``), ``data`` (bytes) and
@@ -16,6 +17,7 @@ from typing import List, Tuple
 import numpy as np
 
 from .. import _abi
+from ..constants import GC_MAX_IMU_PREINT_LEN
 
 INT8, UINT8, INT16, UINT16, INT32, UINT32, FLOAT32, FLOAT64 = range(1, 9)
 
@@ -93,3 +95,25 @@ def parse_pointcloud2_vlp16(msg, R_base_lidar=None, t_base_lidar=None, ctx=None
     _abi.call("gc_pointcloud2_parse", ctx.handle, d_raw.ptr, n, step, ft.ctypes.data, header_stamp_sec(msg), Rp, tp,
               pts.ptr, ts.ptr, ws.ptr, rg.ptr, tg.ptr, ctx=ctx)
     return pts.download(), ts.download(), ws.download(), rg.download(), tg.download()
+
+
+def imu_window_padded(imu_buffer, t_last_scan: float, scan_start_time: float, t_scan: float,
+                      scan_end_time: float, M: int = GC_MAX_IMU_PREINT_LEN
+                      ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:
+    """The node's IMU slicing and padding (backend_node.py:1927-1951): samples (t, gyro, accel)
+    with t in [min(t_last_scan, scan_start) - 1e-9, max(t_scan, scan_end) + 1e-9], the last M of
+    them, zero-padded to M rows -> (stamps (M,), gyro (M, 3), accel (M, 3)), the arrays
+    stage_pointcloud2 / stage_scan take as imu_stamps / imu_gyro / imu_accel. Host bookkeeping
+    over the node's Python ring buffer (no arithmetic to offload)."""
+    t_min = min(t_last_scan, scan_start_time)
+    t_max = max(t_scan, scan_end_time)
+    eps_t = 1e-9
+    window = [(t, g, a) for (t, g, a) in imu_buffer if t_min - eps_t <= t <= t_max + eps_t]
+    if len(window) > M:
+        window = window[-M:]
+    stamps, gyro, accel = np.zeros(M), np.zeros((M, 3)), np.zeros((M, 3))
+    for i, (t, g, a) in enumerate(window):
+        stamps[i] = float(t)
+        gyro[i] = np.asarray(g, np.float64)
+        accel[i] = np.asarray(a, np.float64)
+    return stamps, gyro, accel

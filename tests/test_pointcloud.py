@@ -122,3 +122,19 @@ def test_gpu_pipeline_staged_from_pointcloud2(ctx):
         ctx.sync()
         out.append(pipe.bin_stats()[0])
     assert np.max(np.abs(out[0] - out[1]) / np.maximum(np.abs(out[1]), 1e-300)) < 1e-12
+
+
+def test_imu_window_padded_slicing():
+    """backend_node.py:1927-1951: window [min(t_last, start) - 1e-9, max(t_scan, end) + 1e-9], last M
+    samples, zero padding."""
+    from gcslam.ops import imu_window_padded
+    buf = [(0.005 * k, (k, 0.0, 1.0), (0.0, k, 9.81)) for k in range(400)]
+    st, gy, ac = imu_window_padded(buf, t_last_scan=0.5, scan_start_time=0.6, t_scan=0.7, scan_end_time=0.65, M=512)
+    sel = [t for (t, _, _) in buf if 0.5 - 1e-9 <= t <= 0.7 + 1e-9]
+    assert np.count_nonzero(st) == len(sel) and np.allclose(st[:len(sel)], sel)
+    assert np.all(st[len(sel):] == 0.0) and np.all(gy[len(sel):] == 0.0)
+    assert gy[0, 0] == 100 and ac[0, 1] == 100
+    st, _, _ = imu_window_padded(buf, 0.0, 0.0, 2.0, 2.0, M=64)  # more samples than M: the last 64
+    assert st[0] == buf[-64][0] and st[-1] == buf[-1][0]
+    st, _, _ = imu_window_padded([], 0.0, 0.0, 1.0, 1.0, M=8)
+    assert st.shape == (8,) and not st.any()
