@@ -103,6 +103,9 @@ SIGNATURES = {
     "gc_primitive_map_cull": [_vp, _vp, _i64, _i64, _f64, _i64, _vp],
     "gc_primitive_map_insert_masked": [_vp, _vp, _i64, _i64, _vp, _f64, _i64, _f64, _i64, _vp, _vp, _vp],
     "gc_primitive_map_merge_reduce": [_vp, _vp, _i64, _i64, _f64, _i32, _f64, _f64, _vp],
+    "gc_extract_map_view": [_vp, _vp, _i64, _vp, _vp, _f64, _f64, _vp],
+    "gc_associate_primitives_ot": [_vp, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp,
+                                   _vp, _vp],
 }
 
 GC_PCFG_LEN = 22

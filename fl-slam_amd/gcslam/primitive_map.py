@@ -74,6 +74,21 @@ class DevicePrimitiveMap:
         self.next_global_id = 0
         self.total_count = 0
         self.tile_count: Dict[int, int] = {}
+        # tile keys of the dense tiles (the reference's packed MA-hex tile ids); default 0..n-1
+        self.tile_keys: List[int] = list(range(self.n_tiles))
+
+    def set_tile_keys(self, keys) -> None:
+        keys = [int(k) for k in keys]
+        if len(keys) != self.n_tiles or len(set(keys)) != len(keys):
+            raise ValueError("tile keys must be n_tiles distinct ids")
+        self.tile_keys = keys
+
+    def dense_tile(self, key: int) -> int:
+        """Dense tile index holding tile key `key`, or -1 (an empty tile for the view)."""
+        try:
+            return self.tile_keys.index(int(key))
+        except ValueError:
+            return -1
 
     def upload(self, **arrays):
         for k, v in arrays.items():

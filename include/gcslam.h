@@ -521,6 +521,54 @@ int32_t gc_primitive_map_merge_reduce(gc_ctx* ctx, const gc_primitive_map* map, 
                                       double merge_threshold, int32_t max_pairs, double eps_psd, double eps_lift,
                                       int64_t* h_out2);
 
+/* ------------------------------------------------------------------------------------------
+ * Map view + OT association (the current PrimitiveMap pose-evidence path).
+ * ------------------------------------------------------------------------------------------ */
+/* AtlasMapView (primitive_map.py:236-300) in device memory: V = n_tiles * m_tile_view entries,
+   tile-major. The caller allocates every array; tile_ids is a device copy of the view tile ids. */
+typedef struct gc_map_view {
+  int32_t n_tiles;
+  int32_t m_tile_view;
+  int32_t n_lobes;
+  int32_t pad_;
+  int64_t* tile_ids;                /* (T) packed MA-hex tile ids */
+  int64_t* candidate_tile_ids;      /* (V) */
+  int64_t* candidate_slots;         /* (V) tile-local slot */
+  uint8_t* valid_mask;              /* (V) */
+  double* positions;                /* (V, 3) solve(Λ + εI, θ) */
+  double* covariances;              /* (V, 3, 3) inv(Λ + εI) */
+  double* directions;               /* (V, 3) η_sum / (‖η_sum‖ + ε_mass) */
+  double* kappas;                   /* (V) ‖η_sum‖ */
+  double* weights;                  /* (V) */
+  int64_t* primitive_ids;           /* (V) */
+  int64_t* last_supported_scan_seq; /* (V) */
+  double* etas;                     /* (V, n_lobes, 3) */
+  double* colors;                   /* (V, 3) rgb (0.5 where the map has no colour fields) */
+} gc_map_view;
+
+/* extract_atlas_map_view (primitive_map.py:356-451): for view tile t, the top m_tile_view slots of
+   dense map tile h_dense_tiles[t] (slot range [d * m_tile, (d+1) * m_tile); -1 = missing, an empty
+   tile) by weight, invalid slots last, ties by slot (_select_topk_slots_fixed :304-322). */
+int32_t gc_extract_map_view(gc_ctx* ctx, const gc_primitive_map* map, int64_t m_tile, const int64_t* h_dense_tiles,
+                            const int64_t* h_tile_ids, double eps_lift, double eps_mass, const gc_map_view* view);
+
+#define GC_OT_CFG_LEN 15  /* [k_assoc, k_sinkhorn, beta, epsilon, tau_a, tau_b, cost_subtract_row_min,
+                             weight_proportional, eps_mass, h_tile, r_stencil_xy, r_stencil_z, scan_seq,
+                             recency_decay_lambda, eps_lift] (AssociationConfig, primitive_association.py:205-236) */
+#define GC_OT_CERT_LEN 13 /* [marginal_defect_a, marginal_defect_b, transport_mass_total, sum_a, sum_b, sum_m,
+                             sum_novel, ess_ot, nonzero_a, nonzero_b, total_cost, n_valid_meas, n_valid_map] */
+/* associate_primitives_ot (operators/primitive_association.py:239-553): N measurement primitives
+   (info form + vMF lobes) against a map view. Outputs (device, caller-allocated, K = k_assoc <= 16):
+   responsibilities (N, K), candidate pool indices int32 (N, K), candidate tile ids / slots int64
+   (N, K), row masses (N), cost matrix (N, K). h_cert_out (host) = GC_OT_CERT_LEN values; with no
+   valid measurement or map entry every output is zero and n_valid_* tell which. */
+int32_t gc_associate_primitives_ot(gc_ctx* ctx, int64_t N, int32_t n_lobes, const double* d_Lambdas,
+                                   const double* d_thetas, const double* d_etas, const double* d_weights,
+                                   const uint8_t* d_valid, const gc_map_view* view, const double* h_cfg,
+                                   double* d_resp_out, int32_t* d_cand_out, int64_t* d_cand_tile_out,
+                                   int64_t* d_cand_slot_out, double* d_row_mass_out, double* d_cost_out,
+                                   double* h_cert_out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1508,3 +1508,172 @@ def primitive_map_merge_reduce(tile, merge_threshold, max_pairs, eps_psd=EPS_PSD
         out["weights"][j] = 0.0
         out["valid_mask"][j] = False
     return out, len(sel)
+
+
+# ---------------------------------------------------------------------------------------
+# Map view + OT association: extract_atlas_map_view
+# (structures/primitive_map.py:356-451 + _extract_primitive_map_view_core :475-498) and
+# associate_primitives_ot (operators/primitive_association.py:105-553) with the MA-hex tiling
+# helpers (common/tiling.py:72-186).
+# ---------------------------------------------------------------------------------------
+PACK_BITS, PACK_BIAS = 21, 1 << 20
+PACK_MASK = (1 << PACK_BITS) - 1
+
+
+def hex_disk_axial(radius):
+    """tiling.py:171-186: axial (q, r) of a hex disk, sorted."""
+    r = int(radius)
+    out = []
+    for q in range(-r, r + 1):
+        for rr in range(max(-r, -q - r), min(r, -q + r) + 1):
+            out.append((q, rr))
+    return sorted(out)
+
+
+def tile_ids_from_cells(c1, c2, cz):
+    """tile_ids_from_cells_jax (tiling.py:148-168): biased, masked 21-bit fields packed in int64."""
+    u1 = (np.asarray(c1, np.int64) + PACK_BIAS) & PACK_MASK
+    u2 = (np.asarray(c2, np.int64) + PACK_BIAS) & PACK_MASK
+    uz = (np.asarray(cz, np.int64) + PACK_BIAS) & PACK_MASK
+    return (u1 << (2 * PACK_BITS)) | (u2 << PACK_BITS) | uz
+
+
+def tile_cells_from_xyz(xyz, h_tile):
+    """The cell coordinates of associate_primitives_ot (primitive_association.py:317-323)."""
+    h = max(float(h_tile), 1e-12)
+    s1 = xyz[:, 0]
+    s2 = xyz[:, 0] * 0.5 + xyz[:, 1] * (np.sqrt(3.0) * 0.5)
+    return (np.floor(s1 / h).astype(np.int64), np.floor(s2 / h).astype(np.int64),
+            np.floor(xyz[:, 2] / h).astype(np.int64))
+
+
+def extract_atlas_map_view(tiles: dict, tile_ids, m_tile_view, m_tile, L=3, eps_lift=EPS_LIFT, eps_mass=EPS_MASS):
+    """tiles: {tile_id: tile dict}; missing ids are empty tiles. Top m_tile_view slots per tile by
+    weight (_select_topk_slots_fixed :304-322: a stable sort on -score, invalid = -1e30)."""
+    k = int(m_tile_view)
+    parts = {n: [] for n in ("slots", "tile", "valid", "Lambdas", "thetas", "etas", "weights", "ids", "last", "rgb")}
+    for tid in tile_ids:
+        t = tiles.get(int(tid))
+        if t is None:
+            t = empty_tile(m_tile, L)
+        score = np.where(t["valid_mask"], t["weights"], -1e30)
+        slots = np.argsort(-score, kind="stable")[:k]
+        parts["slots"].append(slots)
+        parts["tile"].append(np.full(k, int(tid), np.int64))
+        parts["valid"].append(t["valid_mask"][slots])
+        parts["Lambdas"].append(t["Lambdas"][slots])
+        parts["thetas"].append(t["thetas"][slots])
+        parts["etas"].append(t["etas"][slots])
+        parts["weights"].append(t["weights"][slots])
+        parts["ids"].append(t["primitive_ids"][slots])
+        parts["last"].append(t["last_supported_scan_seq"][slots])
+        parts["rgb"].append(t["rgb"][slots])
+    cat = {n: np.concatenate(v, axis=0) for n, v in parts.items()}
+    Lr = cat["Lambdas"] + eps_lift * np.eye(3)[None]
+    eta_sum = cat["etas"].sum(axis=1)
+    kap = np.linalg.norm(eta_sum, axis=1)
+    return dict(candidate_tile_ids=cat["tile"], candidate_slots=cat["slots"].astype(np.int64),
+                valid_mask=cat["valid"].astype(bool), tile_ids=np.asarray(tile_ids, np.int64), m_tile_view=k,
+                positions=np.linalg.solve(Lr, cat["thetas"][..., None])[..., 0], covariances=np.linalg.inv(Lr),
+                directions=eta_sum / (kap[:, None] + eps_mass), kappas=kap, weights=cat["weights"],
+                primitive_ids=cat["ids"], last_supported_scan_seq=cat["last"], etas=cat["etas"], colors=cat["rgb"])
+
+
+def _A_vmf(k, eps=1e-12):
+    """_A_vmf_vec_jax (primitive_association.py:141-149)."""
+    k = np.maximum(np.asarray(k, np.float64), eps)
+    with np.errstate(over="ignore", invalid="ignore"):
+        log_sinh = np.where(k > 20.0, k - np.log(2.0),
+                            np.where(k >= 1e-2, np.log(np.sinh(np.minimum(k, 20.0))), np.log(k + k ** 3 / 6.0)))
+    return np.log(4.0 * np.pi) + log_sinh - np.log(k)
+
+
+def ot_cost(mp, md, mk, vp, vd, vk, beta=0.5, eig_min=1e-12):
+    """_compute_sparse_cost_matrix_jax (:152-197) on gathered candidates: mp (N,3), vp (N,C,3)."""
+    diff = mp[:, None, :] - vp
+    d_pos = np.sum(diff * diff, axis=-1)
+    km = 0.5 * np.linalg.norm(mk[:, None, None] * md[:, None, :] + vk[:, :, None] * vd, axis=-1)
+    bc = np.exp(_A_vmf(np.maximum(km, eig_min), eig_min) -
+                0.5 * (_A_vmf(np.maximum(mk[:, None], eig_min), eig_min) + _A_vmf(np.maximum(vk, eig_min), eig_min)))
+    d_dir = np.maximum(0.0, 1.0 - bc)
+    d_dir = np.where((mk[:, None] > 0.0) & (vk > 0.0), d_dir, 0.0)
+    return d_pos + float(beta) * d_dir
+
+
+OT_DEFAULTS = dict(k_assoc=8, k_sinkhorn=50, beta=0.5, epsilon=0.1, tau_a=0.5, tau_b=0.5, cost_subtract_row_min=True,
+                   weight_proportional=False, eps_mass=EPS_MASS, h_tile=2.0, r_xy=1, r_z=0, scan_seq=0,
+                   recency_decay_lambda=0.02)
+
+
+def associate_primitives_ot(meas: dict, view: dict, cfg: dict = None, eps_lift=EPS_LIFT, eps_mass=EPS_MASS):
+    """associate_primitives_ot (primitive_association.py:239-553): meas = {Lambdas, thetas, etas,
+    weights, valid_mask}. Returns the result arrays and the OT cert scalars."""
+    c = dict(OT_DEFAULTS, **(cfg or {}))
+    K = int(c["k_assoc"])
+    valid = np.asarray(meas["valid_mask"], bool)
+    N = valid.shape[0]
+    zeros = dict(responsibilities=np.zeros((N, K)), candidate_pool_indices=np.zeros((N, K), np.int32),
+                 candidate_tile_ids=np.zeros((N, K), np.int64), candidate_slots=np.zeros((N, K), np.int64),
+                 row_masses=np.zeros(N), cost_matrix=np.zeros((N, K)))
+    if valid.sum() == 0 or view["valid_mask"].sum() == 0:
+        return zeros, None
+    Lr = meas["Lambdas"] + eps_lift * np.eye(3)[None]
+    mp = np.linalg.solve(Lr, meas["thetas"][..., None])[..., 0]
+    es = meas["etas"].sum(axis=1)
+    mk = np.linalg.norm(es, axis=1)
+    md = es / (np.linalg.norm(es, axis=1, keepdims=True) + eps_mass)
+    vf = valid.astype(np.float64)
+    disk = hex_disk_axial(c["r_xy"])
+    dq = np.array([d[0] for d in disk], np.int64)
+    dr = np.array([d[1] for d in disk], np.int64)
+    dz = np.arange(-int(c["r_z"]), int(c["r_z"]) + 1, dtype=np.int64)
+    c1, c2, cz = tile_cells_from_xyz(mp, c["h_tile"])
+    g1 = c1[:, None, None] + dq[None, None, :] + 0 * dz[None, :, None]
+    g2 = c2[:, None, None] + dr[None, None, :] + 0 * dz[None, :, None]
+    gz = cz[:, None, None] + dz[None, :, None] + 0 * dq[None, None, :]
+    st = tile_ids_from_cells(g1, g2, gz).reshape(N, -1)
+    pool_tiles = view["tile_ids"]
+    kv = int(view["m_tile_view"])
+    eq = st[:, :, None] == pool_tiles[None, None, :]
+    has = eq.any(axis=2)
+    tix = np.where(has, eq.argmax(axis=2), 0)
+    pool = ((tix * kv)[:, :, None] + np.arange(kv)[None, None, :]).reshape(N, -1)
+    cost_pool = ot_cost(mp, md, mk, view["positions"][pool], view["directions"][pool], view["kappas"][pool], c["beta"])
+    pv = view["valid_mask"][pool] & np.repeat(has, kv, axis=1)
+    cost_pool = np.where(pv, cost_pool, 1e12)
+    order = np.argsort(cost_pool, axis=1, kind="stable")  # lax.sort, num_keys=1: cost only, stable
+    cand = np.take_along_axis(pool, order, axis=1)[:, :K].astype(np.int32)
+    cand = np.where(valid[:, None], cand, 0).astype(np.int32)
+    C = ot_cost(mp, md, mk, view["positions"][cand], view["directions"][cand], view["kappas"][cand], c["beta"])
+    dt = np.maximum(0, np.int64(c["scan_seq"]) - view["last_supported_scan_seq"][cand]).astype(np.float64)
+    C = C + float(c["epsilon"]) * float(c["recency_decay_lambda"]) * dt
+    if c["cost_subtract_row_min"]:
+        C = C - C.min(axis=1, keepdims=True)
+    if c["weight_proportional"]:
+        wv = vf * np.asarray(meas["weights"], np.float64)
+        sum_a = max(wv.sum(), c["eps_mass"])
+        a = wv / sum_a
+    else:
+        sum_a = max(vf.sum(), c["eps_mass"])
+        a = vf / sum_a
+    b = np.ones(K) / K
+    eps = max(float(c["epsilon"]), 1e-12)
+    Km = np.exp(-C / eps)
+    ua, vb = 1.0 / (1.0 + c["tau_a"] / eps), 1.0 / (1.0 + c["tau_b"] / eps)
+    u, v = np.ones(N), np.ones(K)
+    for _ in range(int(c["k_sinkhorn"])):
+        u = (a / (Km @ v + 1e-12)) ** ua
+        v = (b / (Km.T @ u + 1e-12)) ** vb
+    pi = u[:, None] * Km * v[None, :]
+    rows = pi.sum(axis=1)
+    res = dict(responsibilities=pi * valid[:, None], candidate_pool_indices=cand,
+               candidate_tile_ids=view["candidate_tile_ids"][cand], candidate_slots=view["candidate_slots"][cand],
+               row_masses=rows, cost_matrix=C)
+    em = c["eps_mass"]
+    cols = pi.sum(axis=0)
+    cert = dict(marginal_defect_a=float(np.linalg.norm(rows - a)), marginal_defect_b=float(np.linalg.norm(cols - b)),
+                transport_mass_total=float(pi.sum()), sum_a=float(sum_a), sum_b=float(b.sum()),
+                sum_m=float(rows.sum()), sum_novel=float(np.maximum(a - rows, 0.0).sum()),
+                ess=float(rows.sum() ** 2 / (np.sum(rows ** 2) + em)), nonzero_a=int(np.sum(a > em)),
+                nonzero_b=int(np.sum(b > em)), total_cost=float(np.sum(pi * C)))
+    return res, cert
