@@ -78,6 +78,9 @@ struct ScanArgs {
 // launchers (gc_belief.hip)
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st);
 hipError_t launch_io_branch(const PipeDev& P, const ScanArgs& S, const double* d_odom, hipStream_t st);
+// a1 budget scalars into out (8) with 3 x 64 partials in part (gc_points.hip)
+hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, double* part, double* out,
+                               hipStream_t st);
 hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st);
 hipError_t launch_combine_local(const PipeDev& P, hipStream_t st);
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st);

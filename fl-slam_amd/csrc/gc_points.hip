@@ -1279,21 +1279,26 @@ static int pick_iters(int64_t n, int H, int max_iters = 8) {
   return iters;
 }
 
+namespace gc {
+hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, double* part, double* out,
+                               hipStream_t st) {
+  const int64_t stride = std::max<int64_t>(1, (n_in + n_cap - 1) / n_cap);
+  hipLaunchKernelGGL(k_budget_partials, dim3(kBudgetBlocks), dim3(256), 0, st, d_w, n_in, stride, part);
+  hipLaunchKernelGGL(k_budget_final, dim3(1), dim3(64), 0, st, (const double*)part, kBudgetBlocks, n_in, n_cap,
+                     stride, out);
+  return hipGetLastError();
+}
+}  // namespace gc
+
 extern "C" {
 
 int32_t gc_budget_stats(gc_ctx* ctx, const double* d_w, int64_t n_in, int64_t n_cap, double* d_out) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   GC_CHECK_ARG(ctx, n_in > 0 && n_cap > 0, "n_in and n_cap must be positive");
   GC_CHECK_ARG(ctx, d_w && d_out, "NULL buffer");
-  const int64_t stride = std::max<int64_t>(1, (n_in + n_cap - 1) / n_cap);
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * 3 * kBudgetBlocks, &scr)) return rc;
-  hipLaunchKernelGGL(k_budget_partials, dim3(kBudgetBlocks), dim3(256), 0, ctx->stream, d_w, n_in, stride,
-                     (double*)scr);
-  GC_LAUNCH_CHECK(ctx);
-  hipLaunchKernelGGL(k_budget_final, dim3(1), dim3(64), 0, ctx->stream, (const double*)scr, kBudgetBlocks, n_in,
-                     n_cap, stride, d_out);
-  GC_LAUNCH_CHECK(ctx);
+  GC_HIP(ctx, gc::launch_budget_stats(d_w, n_in, n_cap, (double*)scr, d_out, ctx->stream));
   return GC_OK;
 }
 
