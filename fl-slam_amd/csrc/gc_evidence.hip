@@ -417,6 +417,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
   double* Qp = Qs + NN;     // NN
   const int t = threadIdx.x, n = kDZ;
   const int PLn = partial_len(P.B);
+  GC_PHASE(P, 20);
   // fixed rank-order reduction of the gathered partial records
   for (int e = t; e < PLn; e += kWG) {
     double s = 0.0;
@@ -428,6 +429,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
   for (int i = t; i < NN; i += kWG) Lr[i] = R[kPL + i];
   __syncthreads();
   wg_psd_project_fast(Lr, Lc, P.eps_psd, n, Sx, red, c6);
+  GC_PHASE(P, 21);
   double* cb = P.comb;
   for (int i = t; i < NN; i += kWG) cb[i] = Lc[i];
   if (t < n) { cb[NN + t] = R[kPH + t]; cb[NN + n + t] = R[kPZ + t]; }
@@ -451,17 +453,22 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     cc[10] = R[kPMU2] - mm;  // spread proxy Σ w‖μ_j‖² − ‖Σ w μ_j‖²
   }
   __syncthreads();
+  GC_PHASE(P, 22);
   // ---- process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
   wg_iw_proc_apply(P.nu_proc, P.Psi_proc, R + kPDPSIP, R + kPDNUP, S.w_process, P.eps_psd, P.nu_max, P.nu_proc,
                    P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab);
+  GC_PHASE(P, 23);
   // ---- measurement-noise IW apply (measurement_noise_iw_jax.py:59-100)
   wg_iw_meas_apply(P.nu_meas, P.Psi_meas, R + kPDPSIM, R + kPDNUM, P.eps_psd, P.nu_max, P.nu_meas, P.Psi_meas,
                    P.iw_cert + 2, tab);
+  GC_PHASE(P, 24);
   iw_Q_wg(P, Qs, Qp, Sx, red);
+  GC_PHASE(P, 25);
   // ---- map update: γ·map + increments of hypothesis 0 (bin_atlas.py:137-163, :232-257)
   for (int e = t; e < P.B * kMapRec; e += kWG) P.map[e] = P.forgetting * P.map[e] + R[kPMAP + e];
   __syncthreads();
   map_derive_wg(P, red, tab);
+  GC_PHASE(P, 26);
 }
 
 // ------------------------------------------------------------------------------ launchers

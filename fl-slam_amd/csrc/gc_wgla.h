@@ -91,11 +91,11 @@ GC_DEV double readlane_f64(double v, int lane) {
 // readlane (it feeds the next pivot), L[k+2..][k] through a 22-double LDS row (one ds_write per
 // lane, then same-address broadcast reads, no readlane hazard NOPs). Wave 0 only, in program
 // order, so the LDS row needs no barrier.
-template <bool CHECKED>
-GC_DEV void lane_chol22(double (&a)[kDZ], int lane, bool& ok) {
-  __shared__ __attribute__((aligned(16))) double colbuf[kDZ + 2];
+template <int NM, bool CHECKED>
+GC_DEV void lane_chol(double (&a)[NM], int lane, bool& ok) {
+  __shared__ __attribute__((aligned(16))) double colbuf[NM + 2];
 #pragma unroll
-  for (int k = 0; k < kDZ; ++k) {
+  for (int k = 0; k < NM; ++k) {
     double piv = readlane_f64(a[k], k);
     if constexpr (CHECKED) {
       if (!(piv > 0.0)) { ok = false; piv = 1.0; }
@@ -107,38 +107,49 @@ GC_DEV void lane_chol22(double (&a)[kDZ], int lane, bool& ok) {
     h = fma(h, r, h);
     const double inv = h + h;
     a[k] = lane == k ? g : (lane > k ? a[k] * inv : a[k]);
-    if (k + 1 < kDZ) {
-      if (k + 2 < kDZ) colbuf[lane < kDZ ? lane : kDZ + 1] = a[k];
+    if (k + 1 < NM) {
+      if (k + 2 < NM) colbuf[lane < NM ? lane : NM + 1] = a[k];
       a[k + 1] -= a[k] * (lane == k + 1 ? a[k] : readlane_f64(a[k], k + 1));  // next pivot: no readlane
 #pragma unroll
-      for (int j = k + 2; j < kDZ; ++j) a[j] -= a[k] * colbuf[j];
+      for (int j = k + 2; j < NM; ++j) a[j] -= a[k] * colbuf[j];
     }
   }
 }
 
-GC_DEV void lane_load_rows(const double* A, int n, int lane, double (&a)[kDZ]) {
+template <int NM>
+GC_DEV void lane_load_rows(const double* A, int n, int lane, double (&a)[NM]) {
 #pragma unroll
-  for (int j = 0; j < kDZ; ++j)
+  for (int j = 0; j < NM; ++j)
     a[j] = (lane < n && j < n) ? (j <= lane ? A[lane * n + j] : 0.0) : (lane == j ? 1.0 : 0.0);
 }
 
-GC_DEV void lane_store_lower(double* A, int n, int lane, const double (&a)[kDZ]) {
+template <int NM>
+GC_DEV void lane_store_lower(double* A, int n, int lane, const double (&a)[NM]) {
   if (lane < n) {
 #pragma unroll
-    for (int j = 0; j < kDZ; ++j)
+    for (int j = 0; j < NM; ++j)
       if (j < n) A[lane * n + j] = j <= lane ? a[j] : 0.0;
   }
+}
+
+// wave-0 factorization padded to NM = 8 (the 6x6 / 3x3 blocks of IW, Q, pose-6) or kDZ = 22:
+// the padded identity costs full columns, so small blocks take the short form
+template <int NM, bool CHECKED>
+GC_DEV bool wave0_chol(double* A, int n) {
+  const int lane = threadIdx.x;
+  double a[NM];
+  lane_load_rows<NM>(A, n, lane, a);
+  bool ok = true;
+  lane_chol<NM, CHECKED>(a, lane, ok);
+  lane_store_lower<NM>(A, n, lane, a);
+  return ok;
 }
 
 // In-place lower Cholesky of the n x n (row-major) A; upper triangle zeroed.
 GC_DEV void wg_chol(double* A, int n) {
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    double a[kDZ];
-    lane_load_rows(A, n, lane, a);
-    bool ok = true;
-    lane_chol22<false>(a, lane, ok);
-    lane_store_lower(A, n, lane, a);
+    if (n <= 8) (void)wave0_chol<8, false>(A, n);
+    else (void)wave0_chol<kDZ, false>(A, n);
   }
   __syncthreads();
 }
@@ -147,13 +158,8 @@ GC_DEV void wg_chol(double* A, int n) {
 // on every thread. flag: one LDS double.
 GC_DEV bool wg_chol_checked(double* A, int n, double* flag) {
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    double a[kDZ];
-    lane_load_rows(A, n, lane, a);
-    bool ok = true;
-    lane_chol22<true>(a, lane, ok);
-    lane_store_lower(A, n, lane, a);
-    if (lane == 0) flag[0] = ok ? 0.0 : 1.0;
+    const bool ok = n <= 8 ? wave0_chol<8, true>(A, n) : wave0_chol<kDZ, true>(A, n);
+    if (threadIdx.x == 0) flag[0] = ok ? 0.0 : 1.0;
   }
   __syncthreads();
   const bool ok = flag[0] == 0.0;
@@ -163,34 +169,39 @@ GC_DEV bool wg_chol_checked(double* A, int n, double* flag) {
 
 // x = (C Cᵀ)^{-1} b for lower-triangular C (result visible to all on return). Wave 0, lane i holds
 // row i and column i of C: forward substitution broadcasts y_j, backward x_j, one readlane each.
+template <int NM>
+GC_DEV void wave0_chol_solve(const double* C, const double* b, double* x, int n) {
+  const int lane = threadIdx.x;
+  const bool live = lane < n;
+  double c[NM], ct[NM];
+#pragma unroll
+  for (int j = 0; j < NM; ++j) {
+    const bool in = live && j < n;
+    c[j] = in ? (j <= lane ? C[lane * n + j] : 0.0) : (lane == j ? 1.0 : 0.0);
+    ct[j] = in ? (j >= lane ? C[j * n + lane] : 0.0) : (lane == j ? 1.0 : 0.0);
+  }
+  const double idiag = 1.0 / (live ? C[lane * n + lane] : 1.0);  // off the dependency chain
+  double r = live ? b[lane] : 0.0, y = 0.0;
+#pragma unroll
+  for (int j = 0; j < NM; ++j) {  // y_j = (b_j - Σ_{k<j} C_jk y_k) / C_jj
+    const double yj = readlane_f64(r * idiag, j);
+    if (lane == j) y = yj;
+    r -= c[j] * yj;
+  }
+  r = y;
+  double xv = 0.0;
+#pragma unroll
+  for (int j = NM - 1; j >= 0; --j) {  // x_j = (y_j - Σ_{k>j} C_kj x_k) / C_jj
+    const double xj = readlane_f64(r * idiag, j);
+    if (lane == j) xv = xj;
+    r -= ct[j] * xj;
+  }
+  if (live) x[lane] = xv;
+}
 GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
   if (threadIdx.x < 64) {
-    const int lane = threadIdx.x;
-    const bool live = lane < n;
-    double c[kDZ], ct[kDZ];
-#pragma unroll
-    for (int j = 0; j < kDZ; ++j) {
-      const bool in = live && j < n;
-      c[j] = in ? (j <= lane ? C[lane * n + j] : 0.0) : (lane == j ? 1.0 : 0.0);
-      ct[j] = in ? (j >= lane ? C[j * n + lane] : 0.0) : (lane == j ? 1.0 : 0.0);
-    }
-    const double idiag = 1.0 / (live ? C[lane * n + lane] : 1.0);  // off the dependency chain
-    double r = live ? b[lane] : 0.0, y = 0.0;
-#pragma unroll
-    for (int j = 0; j < kDZ; ++j) {  // y_j = (b_j - Σ_{k<j} C_jk y_k) / C_jj
-      const double yj = readlane_f64(r * idiag, j);
-      if (lane == j) y = yj;
-      r -= c[j] * yj;
-    }
-    r = y;
-    double xv = 0.0;
-#pragma unroll
-    for (int j = kDZ - 1; j >= 0; --j) {  // x_j = (y_j - Σ_{k>j} C_kj x_k) / C_jj
-      const double xj = readlane_f64(r * idiag, j);
-      if (lane == j) xv = xj;
-      r -= ct[j] * xj;
-    }
-    if (live) x[lane] = xv;
+    if (n <= 8) wave0_chol_solve<8>(C, b, x, n);
+    else wave0_chol_solve<kDZ>(C, b, x, n);
   }
   __syncthreads();
 }
