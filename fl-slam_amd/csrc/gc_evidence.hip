@@ -163,6 +163,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
       const int i = idx / 6, j = idx % 6;
       double v = 0.5 * (Lev[i * n + j] + Lev[j * n + i]);
       P6[idx] = isfinite(v) ? v : 0.0;
+      P.lpose[(int64_t)hl * 36 + idx] = Lev[i * n + j];  // L_evidence[pose, pose] for the tape
     }
     __syncthreads();
     double* w6 = acc;
@@ -175,6 +176,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
         mn = fmin(mn, e); mx = fmax(mx, e);
       }
       const double cond6 = mx / mn;
+      P.diag[(int64_t)hl * kHypDiag + 39] = mn;  // eigmin_pose6
       const double ess_ev = sc[53], exc = sc[55];
       double q = sqrt((P.c0_cond / (cond6 + P.c0_cond)) * (ess_ev / (ess_ev + 1.0)));
       q *= exp(-sc[56]) * clampd(sc[51], 0.0, 1.0);
@@ -286,7 +288,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     for (int k = 0; k < 6; ++k) dg[30 + k] = P.xi[(int64_t)hl * 6 + k];
     double mu2 = 0.0;
     for (int k = 0; k < n; ++k) mu2 += mufin[k] * mufin[k];
-    dg[36] = sc[54]; dg[37] = sc[55]; dg[38] = mu2; dg[39] = 0.0;  // |μ|² for the combine's spread
+    dg[36] = sc[54]; dg[37] = sc[55]; dg[38] = mu2;  // |μ|² for the combine's spread; [39] eigmin_pose6
   }
 }
 

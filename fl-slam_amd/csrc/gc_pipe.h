@@ -41,6 +41,7 @@ struct PipeDev {
   double *io_L, *io_h, *io_cert;           // IMU/odom-branch evidence (computed or given)
   double *mu_aux, *io_parts;               // (Hl, kMuAux), (Hl, kIoParts)
   double *dPsiP, *mu_fin, *diag;
+  double *lpose;                           // (Hl, 36) pose block of L_evidence (diagnostics tape)
   // shared
   double *weights;                         // (H)
   double *Q;                               // (22, 22)

@@ -98,13 +98,13 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   int rc = GC_OK;
   double** fields[] = {&P.X, &P.z, &P.L, &P.h, &P.stamp, &P.Lpred, &P.hpred, &P.pred_cert, &P.pose_pred, &P.xi,
                        &P.imu_out, &P.dPsiM, &P.stats, &P.bincert, &P.io_L, &P.io_h, &P.io_cert, &P.dPsiP,
-                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts};
+                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose};
   const size_t sizes[] = {(size_t)Hl * 6, (size_t)Hl * 22, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl,
                           (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kPredCert, (size_t)Hl * 6,
                           (size_t)Hl * 6, (size_t)Hl * gc::kImuOut, (size_t)Hl * 27, (size_t)Hl * B * 38,
                           (size_t)Hl * 8, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kIoCert,
                           (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag, (size_t)Hl * gc::kMuAux,
-                          (size_t)Hl * gc::kIoParts};
+                          (size_t)Hl * gc::kIoParts, (size_t)Hl * 36};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert};
@@ -387,6 +387,11 @@ int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out) {
 int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag) {
   GC_CHECK_ARG(nullptr, p && h_diag, "NULL argument");
   return down(p, h_diag, p->P.diag, (size_t)p->P.Hl * gc::kHypDiag);
+}
+
+int32_t gc_pipeline_get_lpose6(gc_pipeline* p, double* h_lpose) {
+  GC_CHECK_ARG(nullptr, p && h_lpose, "NULL argument");
+  return down(p, h_lpose, p->P.lpose, (size_t)p->P.Hl * 36);
 }
 
 int32_t gc_pipeline_get_bin_stats(gc_pipeline* p, double* h_stats, double* h_cert, double* h_xi) {

@@ -73,6 +73,7 @@ SIGNATURES = {
     "gc_pipeline_run_scan": [_vp, _i32, _f64, _f64, _f64, _f64, _f64, _i64],
     "gc_pipeline_get_combined": [_vp, _vp],
     "gc_pipeline_get_hyp_diag": [_vp, _vp],
+    "gc_pipeline_get_lpose6": [_vp, _vp],
     "gc_pipeline_get_bin_stats": [_vp, _vp, _vp, _vp],
     "gc_pipeline_attach_comm": [_vp, _vp],
     "gc_comm_unique_id": [_vp],

@@ -1,0 +1,261 @@
+"""Per-scan diagnostics tape, runtime manifest and TUM trajectory export:
+MinimalScanTape / DiagnosticsLog (backend/diagnostics.py:18-329), the tape fill of
+process_scan_single_hypothesis (backend/pipeline.py:1527-1570), RuntimeManifest
+(pipeline.py:1629-1793) and the node's TUM writer (backend_node.py:1257-1260, 2287-2293).
+
+The tape fields come from the batched pipeline's device diagnostics of one hypothesis (hyp_diag,
+lpose6, bin cert); the file formats (JSONL, npz) match the reference's so its tools read them.
+Fields the device pipeline does not evaluate keep the reference's defaults and are listed in
+TAPE_NOT_COMPUTED."""
+
+from __future__ import annotations
+
+import dataclasses
+import json
+import os
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+from . import constants as K
+
+
+@dataclass
+class MinimalScanTape:
+    """diagnostics.py:18-67 (same fields, defaults and JSON keys)."""
+    scan_number: int
+    timestamp: float
+    dt_sec: float
+    n_points_raw: int
+    n_points_budget: int
+    fusion_alpha: float
+    cond_pose6: float
+    conditioning_number: float
+    eigmin_pose6: float
+    L_pose6: np.ndarray
+    total_trigger_magnitude: float
+    cert_exact: bool
+    cert_frobenius_applied: bool
+    cert_n_triggers: int
+    support_ess_total: float
+    support_frac: float
+    mismatch_nll_per_ess: float
+    mismatch_directional_score: float
+    excitation_dt_effect: float
+    excitation_extrinsic_effect: float
+    influence_psd_projection_delta: float
+    influence_mass_epsilon_ratio: float
+    influence_anchor_drift_rho: float
+    influence_dt_scale: float
+    influence_extrinsic_scale: float
+    influence_trust_alpha: float
+    influence_power_beta: float
+    overconfidence_excitation_total: float
+    overconfidence_ess_to_excitation: float
+    overconfidence_cond_to_support: float
+    overconfidence_dt_asymmetry: float
+    overconfidence_z_to_xy_ratio: float
+    t_total_ms: float = 0.0
+    t_point_budget_ms: float = 0.0
+    t_deskew_ms: float = 0.0
+    t_imu_preint_scan_ms: float = 0.0
+    t_imu_preint_int_ms: float = 0.0
+    t_surfel_extraction_ms: float = 0.0
+    t_association_ms: float = 0.0
+    t_visual_pose_ms: float = 0.0
+    t_map_branch_ms: float = 0.0
+    t_map_update_ms: float = 0.0
+
+    def to_dict(self) -> Dict[str, Any]:
+        d = {f.name: getattr(self, f.name) for f in dataclasses.fields(self)}
+        d["L_pose6"] = np.asarray(self.L_pose6, np.float64).tolist()
+        for f in dataclasses.fields(self):
+            v = d[f.name]
+            if isinstance(v, (np.floating, np.integer, np.bool_)):
+                d[f.name] = v.item()
+        return d
+
+    @classmethod
+    def from_dict(cls, d: Dict[str, Any]) -> "MinimalScanTape":
+        kw = {}
+        for f in dataclasses.fields(cls):
+            if f.name == "L_pose6":
+                kw[f.name] = np.array(d["L_pose6"], dtype=np.float64)
+            elif f.name in d:
+                kw[f.name] = _TYPES[f.name](d[f.name])
+            elif f.default is not dataclasses.MISSING:
+                kw[f.name] = f.default
+            else:
+                kw[f.name] = _TYPES[f.name](_LOAD_DEFAULTS.get(f.name, 0))
+        return cls(**kw)
+
+
+_TYPES = {f.name: (int if f.type == "int" else bool if f.type == "bool" else float)
+          for f in dataclasses.fields(MinimalScanTape) if f.name != "L_pose6"}
+# defaults the reference's loaders use for absent keys (diagnostics.py:129-159, :294-322)
+_LOAD_DEFAULTS = dict(cert_exact=True, influence_dt_scale=1.0, influence_extrinsic_scale=1.0,
+                      influence_trust_alpha=1.0, influence_power_beta=1.0)
+# npz array names that differ from the field names (diagnostics.py:216-222)
+_NPZ_NAME = dict(scan_number="scan_numbers", timestamp="timestamps", dt_sec="dt_secs")
+
+# reference tape fields the device pipeline does not evaluate (defaults kept)
+TAPE_NOT_COMPUTED = ("cert_n_triggers", "mismatch_directional_score", "overconfidence_ess_to_excitation",
+                     "overconfidence_cond_to_support")
+
+
+@dataclass
+class DiagnosticsLog:
+    """diagnostics.py:163-329."""
+    tape: List[MinimalScanTape] = field(default_factory=list)
+    run_id: str = ""
+    start_time: float = 0.0
+    end_time: float = 0.0
+    total_scans: int = 0
+
+    def append_tape(self, entry: MinimalScanTape) -> None:
+        self.tape.append(entry)
+        self.total_scans = len(self.tape)
+
+    def save_jsonl(self, path: str) -> None:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        with open(path, "w") as f:
+            f.write(json.dumps({"_type": "header", "run_id": self.run_id, "start_time": self.start_time,
+                                "total_scans": self.total_scans}) + "\n")
+            for e in self.tape:
+                f.write(json.dumps(e.to_dict()) + "\n")
+
+    @classmethod
+    def load_jsonl(cls, path: str) -> "DiagnosticsLog":
+        log = cls()
+        with open(path) as f:
+            for line in f:
+                line = line.strip()
+                if not line:
+                    continue
+                d = json.loads(line)
+                if d.get("_type") == "header":
+                    log.run_id, log.start_time = d.get("run_id", ""), d.get("start_time", 0.0)
+                else:
+                    log.tape.append(MinimalScanTape.from_dict(d))
+        log.total_scans = len(log.tape)
+        return log
+
+    def save_npz(self, path: str) -> None:
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        n = len(self.tape)
+        if n == 0:
+            np.savez_compressed(path, format="minimal_tape", n_scans=0)
+            return
+        data: Dict[str, Any] = dict(format="minimal_tape", n_scans=n, run_id=self.run_id, start_time=self.start_time)
+        for f in dataclasses.fields(MinimalScanTape):
+            col = [getattr(t, f.name) for t in self.tape]
+            data[_NPZ_NAME.get(f.name, f.name)] = np.stack(col) if f.name == "L_pose6" else np.array(col)
+        np.savez_compressed(path, **data)
+
+    @classmethod
+    def load_npz(cls, path: str) -> "DiagnosticsLog":
+        data = np.load(path)  # no pickles: every array is numeric or a unicode scalar
+        if str(data["format"]) != "minimal_tape":
+            raise ValueError("Unsupported diagnostics format; only minimal_tape is supported.")
+        log = cls()
+        n = int(data["n_scans"])
+        if n == 0:
+            return log
+        log.run_id = str(data["run_id"]) if "run_id" in data else ""
+        log.start_time = float(data["start_time"]) if "start_time" in data else 0.0
+        for i in range(n):
+            d = {}
+            for f in dataclasses.fields(MinimalScanTape):
+                key = _NPZ_NAME.get(f.name, f.name)
+                if key in data:
+                    d[f.name] = data[key][i] if f.name == "L_pose6" else data[key][i].item()
+            log.tape.append(MinimalScanTape.from_dict(d))
+        log.total_scans = len(log.tape)
+        return log
+
+
+def tape_from_pipeline(pipe, scan_number: int, timestamp: float, dt_sec: float, n_points_raw: int,
+                       n_points_budget: int, hyp: int = 0, timing_ms: Optional[Dict[str, float]] = None
+                       ) -> MinimalScanTape:
+    """The tape entry of hypothesis `hyp` after BatchedScanPipeline.run_scan (pipeline.py:1527-1570).
+    Mapping (include/gcslam.h GC_HYP_DIAG): α = diag[8], cond_pose6 = diag[13] (also the
+    aggregated conditioning: the pose-6 FusionScale cert is the one that carries it), eigmin =
+    diag[39], L_pose6 = L_evidence[pose, pose], T = diag[6], ess = diag[14], support = diag[36],
+    nll/ess = diag[17], excitation effects (s_dt, s_ex) = diag[9], diag[10] with the scales
+    1 - s, psd Δ = diag[20], drift ρ = diag[11], β = diag[7], mass-ε ratio = bin cert[3],
+    excitation total / dt asymmetry / z-to-xy = diag[37], diag[15], diag[16]."""
+    d = pipe.hyp_diag()[hyp]
+    lp = pipe.lpose6()[hyp]
+    bin_cert = pipe.bin_stats()[1][hyp]
+    tm = timing_ms or {}
+    return MinimalScanTape(
+        scan_number=int(scan_number), timestamp=float(timestamp), dt_sec=float(dt_sec),
+        n_points_raw=int(n_points_raw), n_points_budget=int(n_points_budget), fusion_alpha=float(d[8]),
+        cond_pose6=float(d[13]), conditioning_number=float(d[13]), eigmin_pose6=float(d[39]), L_pose6=lp,
+        total_trigger_magnitude=float(d[6]), cert_exact=bool(d[6] == 0.0), cert_frobenius_applied=bool(d[12] > 0.0),
+        cert_n_triggers=0, support_ess_total=float(d[14]), support_frac=float(d[36]),
+        mismatch_nll_per_ess=float(d[17]), mismatch_directional_score=1.0, excitation_dt_effect=float(d[9]),
+        excitation_extrinsic_effect=float(d[10]), influence_psd_projection_delta=float(d[20]),
+        influence_mass_epsilon_ratio=float(bin_cert[3]), influence_anchor_drift_rho=float(d[11]),
+        influence_dt_scale=float(1.0 - d[9]), influence_extrinsic_scale=float(1.0 - d[10]),
+        influence_trust_alpha=float(d[8]), influence_power_beta=float(d[7]),
+        overconfidence_excitation_total=float(d[37]), overconfidence_ess_to_excitation=0.0,
+        overconfidence_cond_to_support=0.0, overconfidence_dt_asymmetry=float(d[15]),
+        overconfidence_z_to_xy_ratio=float(d[16]),
+        **{f"t_{k}": float(v) for k, v in tm.items() if f"t_{k}" in _TYPES})
+
+
+def runtime_manifest(**overrides) -> Dict[str, Any]:
+    """RuntimeManifest.to_dict (pipeline.py:1629-1793) for the batched GPU pipeline: the constants it
+    runs with and the device implementation behind each backend key."""
+    m: Dict[str, Any] = dict(
+        chart_id=K.GC_CHART_ID, D_Z=K.GC_D_Z, K_HYP=K.GC_K_HYP, HYP_WEIGHT_FLOOR=K.GC_HYP_WEIGHT_FLOOR,
+        N_POINTS_CAP=K.GC_N_POINTS_CAP, eps_psd=K.GC_EPS_PSD, eps_lift=K.GC_EPS_LIFT, eps_mass=K.GC_EPS_MASS,
+        eps_r=K.GC_EPS_R, alpha_min=K.GC_ALPHA_MIN, alpha_max=K.GC_ALPHA_MAX, kappa_scale=K.GC_KAPPA_SCALE,
+        c0_cond=K.GC_C0_COND, c_dt=K.GC_C_DT, c_ex=K.GC_C_EX, c_frob=K.GC_C_FROB,
+        power_beta_min=K.POWER_BETA_MIN, power_beta_exc_c=K.POWER_BETA_EXC_C, power_beta_z_c=K.POWER_BETA_Z_C,
+        K_INSERT_TILE=K.GC_K_INSERT_TILE, K_MERGE_PAIRS_TILE=K.GC_K_MERGE_PAIRS_PER_TILE,
+        MERGE_MAX_TILE_SIZE=K.GC_PRIMITIVE_MERGE_MAX_TILE_SIZE, M_TILE=K.GC_PRIMITIVE_MAP_MAX_SIZE,
+        MAX_IMU_PREINT_LEN=K.GC_MAX_IMU_PREINT_LEN, B_BINS=K.GC_B_BINS, TAU_SOFT_ASSIGN=K.GC_TAU_SOFT_ASSIGN,
+        backends={
+            "core_array": "libgcslam (HIP, gfx950)",
+            "bins": "k_bins_fused (a1+a4+a5+a6, f64 MFMA moments)",
+            "predict": "k_predict_imu (wave-0 register Cholesky)",
+            "imu_odom_evidence": "k_io_branch",
+            "evidence": "k_evidence (a7-a15)",
+            "hypothesis_barycenter": "k_combine_local + RCCL all-gather + k_combine_final",
+            "map_update": "gc_map.hip / gc_mapops.hip (Fuse/Insert/Cull/Forget/Recency/MergeReduce)",
+            "association": "gc_assoc.hip (unbalanced fixed-K Sinkhorn)",
+            "pointcloud_parser": "gc_cloud.hip",
+            "sinkhorn_backend": "unbalanced_fixed_k",
+        })
+    m.update(overrides)
+    return m
+
+
+def _rotvec_to_quat(w: np.ndarray) -> np.ndarray:
+    th = float(np.linalg.norm(w))
+    if th < 1e-12:
+        return np.array([0.5 * w[0], 0.5 * w[1], 0.5 * w[2], 1.0])
+    s = np.sin(0.5 * th) / th
+    return np.array([w[0] * s, w[1] * s, w[2] * s, np.cos(0.5 * th)])
+
+
+class TumTrajectoryWriter:
+    """The node's TUM export (backend_node.py:1257-1260, 2287-2293): a header line, then
+    `stamp x y z qx qy qz qw` per scan from the world pose [t, rotvec]."""
+
+    def __init__(self, path: str):
+        os.makedirs(os.path.dirname(path) or ".", exist_ok=True)
+        self._f = open(path, "w")
+        self._f.write("# timestamp x y z qx qy qz qw\n")
+
+    def write(self, stamp_sec: float, pose6) -> None:
+        p = np.asarray(pose6, np.float64).reshape(6)
+        q = _rotvec_to_quat(p[3:6])
+        self._f.write(f"{stamp_sec:.9f} {p[0]:.6f} {p[1]:.6f} {p[2]:.6f} {q[0]:.6f} {q[1]:.6f} {q[2]:.6f} {q[3]:.6f}\n")
+        self._f.flush()
+
+    def close(self) -> None:
+        self._f.close()

@@ -203,6 +203,12 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_get_hyp_diag", _p(o))
         return o
 
+    def lpose6(self):
+        """L_evidence[pose, pose] per hypothesis of the last scan (Hl, 6, 6)."""
+        o = np.empty((self.Hl, 6, 6))
+        self._call("gc_pipeline_get_lpose6", _p(o))
+        return o
+
     def bin_stats(self):
         s, c, x = np.empty((self.Hl, self.B, 38)), np.empty((self.Hl, 8)), np.empty((self.Hl, 6))
         self._call("gc_pipeline_get_bin_stats", _p(s), _p(c), _p(x))

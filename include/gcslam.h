@@ -203,7 +203,8 @@ typedef struct {
  * 9 s_dt, 10 s_ex, 11 anchor rho, 12 frobenius strength, 13 cond_pose6, 14 ess_total,
  * 15 dt_asymmetry, 16 z_to_xy, 17 nll_per_ess, 18 MF trigger, 19 planar trigger,
  * 20 fusion psd delta, [21:24] t_wls, [24:27] log R_mf, [27:30] MF singular values,
- * [30:36] xi_body, 36 support_frac, 37 excitation_total, 38 |mu_final|^2 (barycenter spread) */
+ * [30:36] xi_body, 36 support_frac, 37 excitation_total, 38 |mu_final|^2 (barycenter spread),
+ * 39 eigmin_pose6 (clipped at eps_psd, pipeline.py:1157-1168) */
 #define GC_HYP_DIAG 40
 /* combined output (GC_COMB_LEN): L 484, h 22, z_lin 22, X_anchor(hyp 0) 6, then
  * [stamp, psd_delta, eig_min, eig_max, cond, nnc, ess, support_frac, mass_eps_ratio,
@@ -261,6 +262,9 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
                              double t_scan, double dt_sec, int64_t scan_count);
 int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out);
 int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag);
+/* L_evidence[pose, pose] (Hl, 6, 6) of the last scan, as the reference's MinimalScanTape.L_pose6
+   (pipeline.py:1537). */
+int32_t gc_pipeline_get_lpose6(gc_pipeline* p, double* h_lpose);
 int32_t gc_pipeline_get_bin_stats(gc_pipeline* p, double* h_stats, double* h_cert, double* h_xi);
 int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm);
 

@@ -982,10 +982,14 @@ def fusion_alpha(cond_ev, ess_ev, exc_total, dt_asym, z_xy, beta, nll,
     return min(max(amin + (amax - amin) * q, amin), amax)
 
 
-def pose6_cond(L_ev, eps=EPS_PSD):
-    """pipeline.py:1157-1170: eigvalsh of the symmetrised pose block, clipped at eps_psd."""
+def pose6_eigs(L_ev, eps=EPS_PSD):
+    """pipeline.py:1157-1168: eigvalsh of the symmetrised pose block, clipped at eps_psd."""
     P = 0.5 * (L_ev[0:6, 0:6] + L_ev[0:6, 0:6].T)
-    ev = np.maximum(np.linalg.eigvalsh(P), eps)
+    return np.maximum(np.linalg.eigvalsh(P), eps)
+
+
+def pose6_cond(L_ev, eps=EPS_PSD):
+    ev = pose6_eigs(L_ev, eps)
     return ev[-1] / ev[0]
 
 
@@ -1241,7 +1245,7 @@ def scan_hypothesis(b_prev: Belief, scan: ScanInput, Q, io: IOEvidence, mapst: M
                 map_inc=inc, T=T, beta=beta, alpha=alpha, s_dt=s_dt, s_ex=s_ex, xi_body=xi,
                 moments=mm, assign=sa, mf=mf, planar=tr, rho=dr["rho"], frob=rc["frobenius_strength"],
                 budget=bud, retained=retained, pose=world_pose(b_fin), L_post=L_post, h_post=h_post,
-                io=io, io_parts=io_parts)
+                io=io, io_parts=io_parts, L_ev=L_ev, cond6=cond6, eigmin6=pose6_eigs(L_ev)[0])
 
 
 @dataclass

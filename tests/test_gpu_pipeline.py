@@ -47,8 +47,13 @@ def test_pipeline_matches_oracle_over_scans(ctx, H):
         diag = pipe.hyp_diag()
         stats, bcert, xi = pipe.bin_stats()
         bel = pipe.get_beliefs()
+        lpose = pipe.lpose6()
         for i in range(H):
             r = res[i]
+            # diagnostics-tape inputs: L_evidence pose block, pose-6 conditioning and eig min
+            _close(lpose[i], r["L_ev"][0:6, 0:6], 1e-8, 1e-10, f"scan{k} hyp{i} L_pose6")
+            _close(diag[i, 13], r["cond6"], 1e-6, 0, f"scan{k} hyp{i} cond_pose6")
+            _close(diag[i, 39], r["eigmin6"], 1e-7, 1e-12, f"scan{k} hyp{i} eigmin_pose6")
             _close(xi[i], r["xi_body"], 1e-9, 1e-12, f"scan{k} hyp{i} xi_body")
             _close(stats[i, :, 0], r["moments"]["N"], 1e-10, 0, f"scan{k} hyp{i} bin N")
             _close(stats[i, :, 16:25].reshape(-1, 3, 3), r["moments"]["Sigma_p"], 1e-7, 1e-12, f"Sigma_p {k}/{i}")
