@@ -1149,22 +1149,40 @@ __global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t ch
   const int h = blockIdx.x;
   const int RL = B * NF + REC_EXTRA;
   const double* P = partials + (int64_t)h * chunks * RL;
-  for (int i = threadIdx.x; i < RL; i += kWG) {
-    double v = 0.0;
-    if (i == B * NF + 1) {
-      for (int64_t c = 0; c < chunks; ++c) v = fmax(v, P[c * RL + i]);
-    } else {  // chunk order fixed; 8 loads in flight per lane
-      int64_t c = 0;
-      for (; c + 8 <= chunks; c += 8) {
-        double x[8];
+  // chunk order fixed per entry; a lane's (up to 4) entries advance together, 8 chunks at a time:
+  // 32 loads in flight per lane (the reduction is L2-latency-bound at small H)
+  constexpr int kE = 4;
+  int ie[kE];
+  double v[kE];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) x[u] = P[(c + u) * RL + i];
+  for (int e = 0; e < kE; ++e) {
+    ie[e] = threadIdx.x + e * kWG;
+    v[e] = 0.0;
+  }
+  const int imax = B * NF + 1;  // the max-responsibility entry reduces by fmax
+  int64_t c = 0;
+  for (; c + 8 <= chunks; c += 8) {
+    double x[kE][8];
 #pragma unroll
-        for (int u = 0; u < 8; ++u) v += x[u];
-      }
-      for (; c < chunks; ++c) v += P[c * RL + i];
-    }
-    sm[i] = v;
+    for (int e = 0; e < kE; ++e)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) x[e][u] = ie[e] < RL ? P[(c + u) * RL + ie[e]] : 0.0;
+#pragma unroll
+    for (int e = 0; e < kE; ++e)
+#pragma unroll
+      for (int u = 0; u < 8; ++u) v[e] = ie[e] == imax ? fmax(v[e], x[e][u]) : v[e] + x[e][u];
+  }
+  for (; c < chunks; ++c)
+#pragma unroll
+    for (int e = 0; e < kE; ++e)
+      if (ie[e] < RL) v[e] = ie[e] == imax ? fmax(v[e], P[c * RL + ie[e]]) : v[e] + P[c * RL + ie[e]];
+#pragma unroll
+  for (int e = 0; e < kE; ++e)
+    if (ie[e] < RL) sm[ie[e]] = v[e];
+  for (int i = threadIdx.x + kE * kWG; i < RL; i += kWG) {  // B * NF + 4 > 1024 (not at B <= 53)
+    double w = 0.0;
+    for (int64_t cc = 0; cc < chunks; ++cc) w = i == imax ? fmax(w, P[cc * RL + i]) : w + P[cc * RL + i];
+    sm[i] = w;
   }
   __syncthreads();
   double Nl = 0.0, N2l = 0.0, psdl = 0.0, epsl = 0.0, sfl = 0.0;
