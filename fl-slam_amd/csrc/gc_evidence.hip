@@ -368,7 +368,7 @@ GC_DEV void map_derive_wg(const PipeDev& P, double* red, double* tab) {
     for (int k = 0; k < 3; ++k) c[k] = m[14 + k] * invp;
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) Sr[3 * i + j] = m[17 + 3 * i + j] * invp - c[i] * c[j];
-    psd_project3(Sr, P.eps_psd, Sp, nullptr);
+    psd_project3_fast(Sr, P.eps_psd, Sp, nullptr);
     for (int k = 0; k < 3; ++k) d[4 + k] = c[k];
     for (int k = 0; k < 9; ++k) d[7 + k] = Sp[k];
     d[16] = 0.0;

@@ -289,6 +289,34 @@ GC_DEV void psd_project3(const double* M, double eps, double* Mp, double* cert) 
   }
 }
 
+// psd_project3 with the certified shortcut of wg_psd_project_fast: if the Cholesky of
+// S_sym - eps I succeeds, every eigenvalue exceeds eps, the clamp is inactive and the projection is
+// S_sym (the reference's V diag(λ) Vᵀ reconstructs it up to rounding); projection delta 0 and the
+// eigen fields of cert NaN. Otherwise the Jacobi form.
+GC_DEV void psd_project3_fast(const double* M, double eps, double* Mp, double* cert) {
+  double S[9], symd = 0.0;
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      S[3 * i + j] = 0.5 * (M[3 * i + j] + M[3 * j + i]);
+      const double d = S[3 * i + j] - M[3 * i + j];
+      symd += d * d;
+    }
+  const double a00 = S[0] - eps;
+  const double l10 = S[3] / sqrt(fmax(a00, 1e-300)), l20 = S[6] / sqrt(fmax(a00, 1e-300));
+  const double a11 = S[4] - eps - l10 * l10;
+  const double l21 = (S[7] - l20 * l10) / sqrt(fmax(a11, 1e-300));
+  const double a22 = S[8] - eps - l20 * l20 - l21 * l21;
+  if (a00 > 0.0 && a11 > 0.0 && a22 > 0.0) {
+    for (int k = 0; k < 9; ++k) Mp[k] = S[k];
+    if (cert) {
+      const double nan = __builtin_nan("");
+      cert[0] = 0.0; cert[1] = sqrt(symd); cert[2] = nan; cert[3] = nan; cert[4] = nan; cert[5] = nan;
+    }
+    return;
+  }
+  psd_project3(M, eps, Mp, cert);
+}
+
 // Sorted (descending) eigenvalues of a symmetric 3x3.
 GC_DEV void eigvalsh3_desc(const double* M, double* lam) {
   double V[9], w[3];

@@ -375,7 +375,7 @@ GC_DEV double psd_padded_small(const double* A6, int d, double eps, double* out6
     double A[9], Pp[9], c[6];
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) A[3 * i + j] = A6[6 * i + j];
-    psd_project3(A, eps, Pp, c);
+    psd_project3_fast(A, eps, Pp, c);
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) out6[6 * i + j] = Pp[3 * i + j];
     d2 += c[0] * c[0];
@@ -438,7 +438,7 @@ GC_DEV void wg_iw_meas_apply(const double* nu, const double* Psi, const double* 
     for (int k = 0; k < 9; ++k) Mr[k] = kIwRhoMeas[t] * Psi[t * 9 + k] + dPsi[t * 9 + k];
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) Ms[3 * i + j] = 0.5 * (Mr[3 * i + j] + Mr[3 * j + i]);
-    psd_project3(Ms, eps_psd, Mp, cc);
+    psd_project3_fast(Ms, eps_psd, Mp, cc);
     const double nr = kIwRhoMeas[t] * nu[t] + dnu[t];
     const double nn = nu_project(nr, 3.0, nu_max);
     tab[t] = cc[0];
@@ -473,7 +473,7 @@ GC_DEV void wg_iw_Q(const double* nu, const double* Psi, double eps_psd, double*
       double A[9], Pp[9];
       for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) A[3 * i + j] = Psi[b * 36 + 6 * i + j] / dn;
-      psd_project3(A, eps_psd, Pp, nullptr);
+      psd_project3_fast(A, eps_psd, Pp, nullptr);
       for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) Qp[(s0 + i) * n + (s0 + j)] = Pp[3 * i + j];
     }
