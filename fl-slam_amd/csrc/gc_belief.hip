@@ -188,7 +188,7 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
       const double* r = rr + 6 * blk;
       const double M3[9] = {r[0], r[1], r[2], r[1], r[3], r[4], r[2], r[4], r[5]};
       double Pp[9];
-      psd_project3(M3, P.eps_psd, Pp, nullptr);
+      psd_project3_fast(M3, P.eps_psd, Pp, nullptr);
       for (int k = 0; k < 9; ++k) out[9 * blk + k] = Pp[k] * dt_imu;
     }
     for (int k = 0; k < 9; ++k) out[18 + k] = 0.0;

@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(256) k_io_branch(PipeDev P, ScanArgs S, const 
     double Sg[9];
     const double den = P.nu_meas[idx] + 3.0 + 1.0;
     for (int k = 0; k < 9; ++k) Sg[k] = P.Psi_meas[9 * idx + k] / den;
-    psd_project3(Sg, P.eps_psd, out, nullptr);
+    psd_project3_fast(Sg, P.eps_psd, out, nullptr);
   };
   const double* od_pose = odom;
   const double* od_cov = odom + 6;

@@ -264,7 +264,7 @@ GC_DEV void iof_gyro(const double* rv_start, const double* rv_end_pred, const do
   double mn = 0.0, mx = 0.0, nb = 0.0;
   if constexpr (CERT) {
     double Lpp[9];
-    psd_project3(Lr, eps_psd, Lpp, nullptr);
+    psd_project3_fast(Lr, eps_psd, Lpp, nullptr);
     eig_stats<3>(Lpp, eps_psd, &mn, &mx, &nb);
   }
   ex[0] = r[0]; ex[1] = r[1]; ex[2] = r[2];
@@ -296,9 +296,9 @@ GC_DEV void iof_preint(const double* p_start, const double* rv_start, const doub
   double mn1 = 0.0, mx1 = 0.0, nb1 = 0.0, mn2 = 0.0, mx2 = 0.0, nb2 = 0.0;
   if constexpr (CERT) {
     double A[9];
-    psd_project3(Lv, eps_psd, A, nullptr);
+    psd_project3_fast(Lv, eps_psd, A, nullptr);
     eig_stats<3>(A, eps_psd, &mn1, &mx1, &nb1);
-    psd_project3(Lp, eps_psd, A, nullptr);
+    psd_project3_fast(Lp, eps_psd, A, nullptr);
     eig_stats<3>(A, eps_psd, &mn2, &mx2, &nb2);
   }
   for (int k = 0; k < 3; ++k) { ex[k] = rv[k]; ex[3 + k] = rp[k]; }

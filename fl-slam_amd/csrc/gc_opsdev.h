@@ -52,7 +52,7 @@ GC_DEV void mf_finalize(const double* acc, const double* Rp, double eps, double 
   double Rerr[9], dl[3], Lrot[9], cc[6];
   mat3_mul_tn(Rp, Rmf, Rerr);
   so3_log(Rerr, dl);
-  psd_project3(Lr, eps_psd, Lrot, cc);
+  psd_project3_fast(Lr, eps_psd, Lrot, cc);
   double hr[3];
   mat3_vec(Lrot, dl, hr);
   const double Neff = acc[9];
@@ -100,7 +100,7 @@ GC_DEV void planar_finalize(const double* acc, double zsc, const double* tp, dou
     for (int j = 0; j < 3; ++j) Lm[3 * i + j] = acc[3 * i + j] * msk[i] * msk[j];
   const double dl[3] = {tw[0] - tp[0], tw[1] - tp[1], tw[2] - tp[2]};
   double Lt[9], cc[6], ht[3];
-  psd_project3(Lm, eps_psd, Lt, cc);
+  psd_project3_fast(Lm, eps_psd, Lt, cc);
   mat3_vec(Lt, dl, ht);
   const double Neff = acc[12];
   const double nll = 0.5 * (dl[0] * ht[0] + dl[1] * ht[1] + dl[2] * ht[2]);

@@ -441,6 +441,65 @@ GC_DEV void wg_psd_project_fast(const double* M, double* Mp, double eps, int n, 
   wg_psd_project(M, Mp, eps, n, scratch, red, cert6);
 }
 
+GC_DEV void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// The parallel cyclic Jacobi of wg_jacobi_eigh (eigenvalues only) on wave 0 for n <= 16: the
+// same round-robin rotations and convergence test, with wave barriers and shuffle sums in place of
+// workgroup barriers (a 6x6 needs ~40 rounds; the workgroup form pays two barriers per round).
+GC_DEV void wave_jacobi_eigvals(double* A, double* w, int n, double* cs) {
+  const int lane = threadIdx.x;  // caller: threadIdx.x < 64
+  const int half = n / 2, tiles = half * half;
+  int* pq = reinterpret_cast<int*>(cs + 2 * half);
+  double dloc = 0.0, offloc = 0.0;
+  for (int i = lane; i < n; i += 64) dloc += A[i * n + i] * A[i * n + i];
+  for (int idx = lane; idx < n * n; idx += 64)
+    if (idx / n != idx % n) offloc += A[idx] * A[idx];
+  const double fro2 = wave_sum(dloc + offloc);
+  double off = wave_sum(offloc);
+  for (int sweep = 0; sweep < 20 && off > 1e-30 * fro2 && off > 1e-300; ++sweep) {
+    for (int r = 0; r < n - 1; ++r) {
+      if (lane < half) {
+        int p, q;
+        rr_pair(n, r, lane, &p, &q);
+        const double apq = A[p * n + q], app = A[p * n + p], aqq = A[q * n + q];
+        double c = 1.0, s = 0.0;
+        if (apq != 0.0 && fabs(apq) > 1e-300 && fabs(apq) > 1e-18 * sqrt(fabs(app * aqq))) {
+          const double th = (aqq - app) / (2.0 * apq);
+          const double t = (th >= 0.0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1.0));
+          c = 1.0 / sqrt(t * t + 1.0);
+          s = t * c;
+        }
+        cs[2 * lane] = c;
+        cs[2 * lane + 1] = s;
+        pq[2 * lane] = p;
+        pq[2 * lane + 1] = q;
+      }
+      wave_lds_sync();
+      for (int t = lane; t < tiles; t += 64) {
+        const int I = t / half, J = t % half;
+        const int pi = pq[2 * I], qi = pq[2 * I + 1], pj = pq[2 * J], qj = pq[2 * J + 1];
+        const double ci = cs[2 * I], si = cs[2 * I + 1], cj = cs[2 * J], sj = cs[2 * J + 1];
+        const double b00 = A[pi * n + pj], b01 = A[pi * n + qj], b10 = A[qi * n + pj], b11 = A[qi * n + qj];
+        const double c00 = cj * b00 - sj * b01, c01 = sj * b00 + cj * b01;
+        const double c10 = cj * b10 - sj * b11, c11 = sj * b10 + cj * b11;
+        double n00 = ci * c00 - si * c10, n01 = ci * c01 - si * c11;
+        double n10 = si * c00 + ci * c10, n11 = si * c01 + ci * c11;
+        if (I == J) { n01 = 0.0; n10 = 0.0; }
+        A[pi * n + pj] = n00; A[pi * n + qj] = n01; A[qi * n + pj] = n10; A[qi * n + qj] = n11;
+      }
+      wave_lds_sync();
+    }
+    offloc = 0.0;
+    for (int idx = lane; idx < n * n; idx += 64)
+      if (idx / n != idx % n) offloc += A[idx] * A[idx];
+    off = wave_sum(offloc);
+  }
+  for (int i = lane; i < n; i += 64) w[i] = A[i * n + i];
+}
+
 // eigvalsh (ascending not required) of the symmetrised n x n M -> w. scratch: n*n + 3n.
 GC_DEV void wg_eigvalsh(const double* M, double* w, int n, double* scratch, double* red) {
   double* S = scratch;
@@ -450,6 +509,11 @@ GC_DEV void wg_eigvalsh(const double* M, double* w, int n, double* scratch, doub
     S[idx] = 0.5 * (M[i * n + j] + M[j * n + i]);
   }
   __syncthreads();
+  if (n <= 16) {
+    if (threadIdx.x < 64) wave_jacobi_eigvals(S, w, n, cs);
+    __syncthreads();
+    return;
+  }
   wg_jacobi_eigh(S, nullptr, w, n, cs, red);
 }
 
