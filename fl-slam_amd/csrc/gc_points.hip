@@ -917,7 +917,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
     for (int s = 0; s < 16; ++s) {
       const int pl = s * 4 + g;
       const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
-      const bool valid = F[(NF + 3) * kFusedFS + pl] != 0.0;
+      const double vf = F[(NF + 3) * kFusedFS + pl];  // 1 for a point of the chunk, 0 for padding
       const double fb = F[bl * kFusedFS + pl];  // MFMA B operand: feature bl of point 4s + g
       double e[BPL], x[BPL], ex[BPL];
 #pragma unroll
@@ -928,30 +928,33 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
       exp2s_n<BPL>(x, Tx, ex);
 #pragma unroll
       for (int j = 0; j < BPL; ++j) e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
-      double zl = e[0], sl = e[0] * x[0], em = e[0];  // e >= 0
+      double zl = e[0], sl = e[0] * x[0];
 #pragma unroll
       for (int j = 1; j < BPL; ++j) {
         zl += e[j];
         sl = fma(e[j], x[j], sl);
-        em = fmax(em, e[j]);
       }
       const double Z = group16_sum(zl);
       const double rZ = recip(Z);
-      if (valid) {
-        entq = fma(sl, rZ, entq);  // lane partials of S/Z (in y units), summed over lanes at the end
-        mxr = fmax(mxr, em * rZ);
-      }
-      if (bl == s) zst = valid ? Z : 1.0;
+      double r[BPL];
 #pragma unroll
-      for (int j = 0; j < BPL; ++j) {
-        const double r = e[j] * rZ;
-        acc4[s % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r, fb, acc4[s % NACC][j], 0, 0, 0);
-      }
+      for (int j = 0; j < BPL; ++j) r[j] = e[j] * rZ;
+      double rm = r[0];  // max responsibility: max(e) rZ == max(e rZ) exactly (monotone rounding)
+#pragma unroll
+      for (int j = 1; j < BPL; ++j) rm = fmax(rm, r[j]);
+      // padding points (vf = 0) add nothing: S/Z scaled by 0, r >= 0 scaled to 0 under the max,
+      // and log Z replaced by log 1
+      entq = fma(sl * vf, rZ, entq);  // lane partials of S/Z (in y units), summed over lanes at the end
+      mxr = fmax(mxr, rm * vf);
+      if (bl == s) zst = fma(Z - 1.0, vf, 1.0);
+#pragma unroll
+      for (int j = 0; j < BPL; ++j)
+        acc4[s % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[j], fb, acc4[s % NACC][j], 0, 0, 0);
 #pragma unroll
       for (int t = 0; t < NX; ++t) {
         const double fk = F[(16 + t) * kFusedFS + pl];
 #pragma unroll
-        for (int j = 0; j < BPL; ++j) accx[j][t] = fma(e[j] * rZ, fk, accx[j][t]);
+        for (int j = 0; j < BPL; ++j) accx[j][t] = fma(r[j], fk, accx[j][t]);
       }
     }
     // each lane stashed the Z of one point per 16 steps: one log per lane per iteration
