@@ -19,6 +19,7 @@
 #include "gc_pipe.h"
 #include "gc_wgla.h"
 #include "gc_opsdev.h"
+#include "gc_budget.h"
 
 namespace gc {
 
@@ -71,6 +72,24 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   const int h = blockIdx.x;
   const int t = threadIdx.x;
   const int n = kDZ;
+  if (h >= P.Hl) {
+    // a1 budget statistics (point_budget.py:60-113) on kBudgetBlocks extra workgroups of this
+    // grid: they only read the staged weights, so they run beside the hypotheses' chains with no
+    // second stream. The last workgroup to arrive (agent-scope acq_rel ticket) sums the partials
+    // in block order — the same fixed order as k_budget_final — and re-arms the ticket.
+    const int b = h - P.Hl;
+    const int64_t stride = budget_stride(S.n_in, P.n_cap);
+    budget_partial_block(S.w_raw, S.n_in, stride, b, P.budget_part, sm);
+    if (t == 0) {
+      const unsigned prev =
+          __hip_atomic_fetch_add(P.budget_ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      if (prev == kBudgetBlocks - 1) {
+        budget_final_values(P.budget_part, S.n_in, P.n_cap, stride, P.budget);
+        __hip_atomic_store(P.budget_ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
+    return;
+  }
   double* hprev = vec;
   double* mu_prev = vec + kDZ;
   double* hpred = vec + 2 * kDZ;
@@ -205,7 +224,8 @@ static size_t lds_predict() {
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
   (void)hipFuncSetAttribute((const void*)k_predict_imu, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)lds_predict());
-  hipLaunchKernelGGL(k_predict_imu, dim3(P.Hl), dim3(256), lds_predict(), st, P, S);
+  // P.Hl hypothesis workgroups + kBudgetBlocks a1 budget workgroups (S.w_raw, S.n_in)
+  hipLaunchKernelGGL(k_predict_imu, dim3(P.Hl + kBudgetBlocks), dim3(256), lds_predict(), st, P, S);
   return hipGetLastError();
 }
 

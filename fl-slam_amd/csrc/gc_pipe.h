@@ -16,6 +16,7 @@ constexpr int kMuAux = 50;    // [mu_prev 22 (belief_prev increment), mu_inc 22 
 constexpr int kIoParts = 40;  // GC_IO_PARTS layout (include/gcslam.h)
 constexpr int kOdomLen = 84;  // [pose 6, cov 36, twist 6, twist_cov 36]  // see include/gcslam.h GC_HYP_DIAG layout
 constexpr int kCombCert = 16;
+constexpr int kBudgetBlocks = 64;  // a1 budget partial workgroups (gc_budget.h)
 
 // Partial-sum record exchanged between ranks once per scan (doubles).
 constexpr int kPL = 0, kPH = 484, kPZ = 506, kPMU = 528, kPMU2 = 550, kPDPSIP = 551, kPDNUP = 803,
@@ -50,6 +51,8 @@ struct PipeDev {
   double *map_inc;                         // (B, 26) written by hypothesis 0's owner
   double *nu_proc, *Psi_proc, *nu_meas, *Psi_meas;  // (7), (7,36), (3), (3,9)
   double *budget;                          // 8 budget scalars
+  double *budget_part;                     // (64, 3) a1 partials, written by predict's extra workgroups
+  unsigned *budget_ticket;                 // arrival counter of those workgroups (reset by the last)
   double *send, *gather;                   // (P), (G, P)
   int G;                                   // ranks
   double *comb;                            // combined belief: L 484, h 22, z 22, X 6, stamp, cert 16
@@ -60,6 +63,8 @@ struct ScanArgs {
   const double *imu_t, *imu_g, *imu_a;     // (M), (M,3), (M,3)
   double t0, t1, t_last, t_scan, dt;
   double w_process;                        // min(1, scan_count)
+  const double* w_raw;                     // (n_in) raw point weights (a1 budget, fused into predict)
+  int64_t n_in;                            // raw points of this scan
 };
 
 // dev instrumentation: -DGC_PHASE_TIMING records s_memtime at phase boundaries of hypothesis 0

@@ -27,11 +27,11 @@ struct gc_pipeline {
   int io_mode = GC_IO_COMPUTED;
   gc_comm* comm = nullptr;
   double* d_cfg_origin = nullptr;
-  // side stream: the a1 budget statistics run beside predict, and the IMU/odom branch beside the
-  // fused bins kernel (independent inputs and outputs); events order them into the main stream
+  // side stream: the IMU/odom branch runs beside the fused bins kernel (independent inputs and
+  // outputs); events order it into the main stream. The a1 budget statistics need no stream of
+  // their own: they are extra workgroups of the predict grid.
   hipStream_t side = nullptr;
-  hipEvent_t ev_start = nullptr, ev_budget = nullptr, ev_pred = nullptr, ev_io = nullptr;
-  double* budget_part = nullptr;
+  hipEvent_t ev_pred = nullptr, ev_io = nullptr;
 };
 
 namespace {
@@ -119,9 +119,12 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   if (P.G == 1) {  // single rank: the combine reads its own partial record in place
     P.gather = P.send;
   }
-  if (rc == GC_OK) rc = dalloc(p, 3 * 64, &p->budget_part);
+  if (rc == GC_OK) rc = dalloc(p, 3 * gc::kBudgetBlocks, &P.budget_part);
+  double* ticket = nullptr;
+  if (rc == GC_OK) rc = dalloc(p, 1, &ticket);  // zeroed: the predict grid's budget arrival counter
+  P.budget_ticket = reinterpret_cast<unsigned*>(ticket);
   hipError_t e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
-  for (hipEvent_t* ev : {&p->ev_start, &p->ev_budget, &p->ev_pred, &p->ev_io})
+  for (hipEvent_t* ev : {&p->ev_pred, &p->ev_io})
     if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
   if (rc == GC_OK && e != hipSuccess) {
     gc::set_error(p->ctx, std::string("side stream / events: ") + hipGetErrorString(e));
@@ -139,7 +142,7 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
   if (!p) return GC_OK;
   (void)hipStreamSynchronize(p->ctx->stream);
   if (p->side) (void)hipStreamSynchronize(p->side);
-  for (hipEvent_t ev : {p->ev_start, p->ev_budget, p->ev_pred, p->ev_io})
+  for (hipEvent_t ev : {p->ev_pred, p->ev_io})
     if (ev) (void)hipEventDestroy(ev);
   if (p->side) (void)hipStreamDestroy(p->side);
   for (void* a : p->allocs) (void)hipFree(a);
@@ -345,16 +348,11 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
   gc_ctx* ctx = p->ctx;
   const auto& s = p->slots[slot];
   gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
-                 scan_count >= 1 ? 1.0 : 0.0};
+                 scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in};
   gc::PipeDev& P = p->P;
   const bool io = p->io_mode == GC_IO_COMPUTED;
-  // a1 budget scalars (the fused kernel reads the selection / mass scale from them), on the side
-  // stream beside predict
-  GC_HIP(ctx, hipEventRecord(p->ev_start, ctx->stream));
-  GC_HIP(ctx, hipStreamWaitEvent(p->side, p->ev_start, 0));
-  GC_HIP(ctx, gc::launch_budget_stats(s.w, s.n_in, P.n_cap, p->budget_part, P.budget, p->side));
-  GC_HIP(ctx, hipEventRecord(p->ev_budget, p->side));
-  // a2 + a3
+  // a1 budget scalars (the fused kernel reads the selection / mass scale from them) on extra
+  // workgroups of the predict grid; a2 + a3
   GC_HIP(ctx, gc::launch_predict_imu(P, S, ctx->stream));
   // a9a IMU/odom evidence branch (pipeline.py:595-776): needs the prediction, not the bins, so it
   // runs on the side stream beside the fused kernel
@@ -365,7 +363,6 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
     GC_HIP(ctx, hipEventRecord(p->ev_io, p->side));
   }
   // a1 -> a4 -> a5 -> a6 fused over all local hypotheses
-  GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, p->ev_budget, 0));
   const double origin[3] = {P.o0, P.o1, P.o2};
   GC_TRY(gc_scan_bins_fused(ctx, P.Hl, s.n_in, P.n_cap, P.B, s.pts, s.t, s.w, P.budget, scan_start, scan_end,
                             P.xi, P.bins, P.tau, origin, P.eps_psd, P.eps_mass, P.stats, P.bincert));

@@ -17,6 +17,7 @@
 #include <type_traits>
 #include "gc_internal.h"
 #include "gc_wgla.h"
+#include "gc_budget.h"
 
 namespace gc {
 
@@ -326,44 +327,17 @@ GC_DEV void direction(const double* p, const double* o, double eps, double* d) {
 
 // =============================================================================== a1 budget
 // Two-level deterministic reduction: 64 workgroups write [Σw_in, Σw_sel, Σw_sel²] partials, one
-// workgroup finishes. ess = 1 / Σ_cap (ŵ² + ε) is evaluated as (scale/(m_in+ε))² Σw_sel² + cap·ε
-// (algebraically the reference's sum, point_budget.py:100-101).
-constexpr int kBudgetBlocks = 64;
+// thread finishes (gc_budget.h).
 __global__ void __launch_bounds__(256) k_budget_partials(const double* __restrict__ w, int64_t n_in,
                                                          int64_t stride, double* part) {
   __shared__ double red[4];
-  const int64_t n_sel = (n_in + stride - 1) / stride;
-  double a = 0.0, b = 0.0, c = 0.0;
-  for (int64_t i = (int64_t)blockIdx.x * kWG + threadIdx.x; i < n_in; i += (int64_t)gridDim.x * kWG) a += w[i];
-  for (int64_t j = (int64_t)blockIdx.x * kWG + threadIdx.x; j < n_sel; j += (int64_t)gridDim.x * kWG) {
-    const double v = w[j * stride];
-    b += v;
-    c += v * v;
-  }
-  a = wg_sum(a, red);
-  b = wg_sum(b, red);
-  c = wg_sum(c, red);
-  if (threadIdx.x == 0) {
-    part[3 * blockIdx.x] = a; part[3 * blockIdx.x + 1] = b; part[3 * blockIdx.x + 2] = c;
-  }
+  budget_partial_block(w, n_in, stride, blockIdx.x, part, red);
 }
 
-__global__ void k_budget_final(const double* __restrict__ part, int blocks, int64_t n_in, int64_t n_cap,
-                               int64_t stride, double* out) {
+__global__ void k_budget_final(const double* __restrict__ part, int64_t n_in, int64_t n_cap, int64_t stride,
+                               double* out) {
   if (threadIdx.x != 0) return;
-  double a = 0.0, b = 0.0, c = 0.0;
-  for (int k = 0; k < blocks; ++k) { a += part[3 * k]; b += part[3 * k + 1]; c += part[3 * k + 2]; }
-  const int64_t n_sel = (n_in + stride - 1) / stride;
-  const double scale = a / (b + 1e-12);
-  const double f = scale / (a + 1e-12);
-  out[0] = a;
-  out[1] = b;
-  out[2] = scale;
-  out[3] = 1.0 / (f * f * c + (double)n_cap * 1e-12);
-  out[4] = scale * b;
-  out[5] = (double)n_sel;
-  out[6] = (double)stride;
-  out[7] = fmin(1.0, (double)n_cap / ((double)n_in + 1e-12));
+  budget_final_values(part, n_in, n_cap, stride, out);
 }
 
 __global__ void k_budget_gather(const double* __restrict__ pts, const double* __restrict__ t,
@@ -1291,22 +1265,23 @@ static int bpl_for(int B) { return (B + 15) / 16; }
 
 using namespace gc;
 
-static int pick_iters(int64_t n, int H, int max_iters = 8) {
+static int pick_iters(int64_t n, int H, int max_iters = 8, int64_t min_wgs = 2048) {
   // Aim for >= ~4 workgroups per CU-slot while keeping partial records small. The fused kernel
   // takes 16 (its per-workgroup prologue, the 16 KB exp table and the bin directions, and the
-  // partial-record epilogue amortise over twice the points: 1.667 -> 1.604 ms/scan, 32 no better).
+  // partial-record epilogue amortise over twice the points: 1.667 -> 1.604 ms/scan, 32 no better)
+  // and halves only below 1024 workgroups (a 32-hypothesis shard: 8 iterations, 0.404 -> 0.395
+  // ms/scan against 4).
   int iters = max_iters;
-  while (iters > 1 && ((n + iters * 256 - 1) / (iters * 256)) * (int64_t)H < 2048) iters >>= 1;
+  while (iters > 1 && ((n + iters * 256 - 1) / (iters * 256)) * (int64_t)H < min_wgs) iters >>= 1;
   return iters;
 }
 
 namespace gc {
 hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, double* part, double* out,
                                hipStream_t st) {
-  const int64_t stride = std::max<int64_t>(1, (n_in + n_cap - 1) / n_cap);
+  const int64_t stride = budget_stride(n_in, n_cap);
   hipLaunchKernelGGL(k_budget_partials, dim3(kBudgetBlocks), dim3(256), 0, st, d_w, n_in, stride, part);
-  hipLaunchKernelGGL(k_budget_final, dim3(1), dim3(64), 0, st, (const double*)part, kBudgetBlocks, n_in, n_cap,
-                     stride, out);
+  hipLaunchKernelGGL(k_budget_final, dim3(1), dim3(64), 0, st, (const double*)part, n_in, n_cap, stride, out);
   return hipGetLastError();
 }
 }  // namespace gc
@@ -1463,7 +1438,8 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   GC_CHECK_ARG(ctx, d_points_raw && d_t_raw && d_w_raw && d_budget_scalars && d_xi && d_bins && h_origin3 &&
                         d_stats_out && d_cert_out, "NULL buffer");
   (void)n_in;
-  const int iters = pick_iters(n_cap, H, 16);
+  int iters = pick_iters(n_cap, H, 16, 1024);
+  if (const char* e = getenv("GC_FUSED_ITERS")) iters = std::max(1, atoi(e));  // dev tuning knob
   const int64_t chunks = (n_cap + iters * 256 - 1) / (iters * 256);
   const int NF = NF_BASE;
   const int RL = B * NF + REC_EXTRA;
