@@ -46,6 +46,7 @@ def parse():
     ap.add_argument("--no-map", action="store_true", help="skip the C5 PrimitiveMap fuse leg")
     ap.add_argument("--roofline-only", action="store_true",
                     help="run only the contract-pair roofline leg (PMC traffic passes, tools/pmc_traffic.sh)")
+    ap.add_argument("--io-given", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--roofline-reps", type=int, default=10)
     return ap.parse_args()
 
@@ -144,7 +145,11 @@ def main():
     hy = make_hypotheses(H_total)
     pipe.set_beliefs(hy["X_anchor"][h0:h1], hy["z_lin"][h0:h1], hy["L"][h0:h1], hy["h"][h0:h1], hy["stamp"][h0:h1])
     pipe.set_weights(hy["weights"])
-    pipe.set_io_mode(True)  # IMU/odom branch evaluated on the device from each scan's odometry + IMU
+    if args.io_given:  # dev: IMU/odom-branch evidence given (isolates the branch's share of the step)
+        from gcslam.synth import make_io_evidence
+        pipe.set_io_evidence(*make_io_evidence(H))
+    else:
+        pipe.set_io_mode(True)  # IMU/odom branch evaluated on the device from each scan's odometry + IMU
     pipe.set_iw(*iw_process_prior(), *iw_meas_prior())
     pipe.set_map(warmup_map_record(ctx, _abi, make_scan(0, n_az=args.n_az), n, B, bins, origin))
     if dist.world > 1:

@@ -101,7 +101,8 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   __syncthreads();
   // --- a2 predict (predict.py:43-98): L_pred -> W1, h_pred, mu_prev, cert
   wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,
-             P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2);
+             P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2, false,
+             S.sig_cached ? P.Sig + (int64_t)h * N2 : nullptr, S.sig_cached ? P.mu_fin + (int64_t)h * n : nullptr);
   GC_PHASE(P, 1);
   if (t == 0) compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);  // pose0 = world pose of belief_prev
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + t] = mu_prev[t];

@@ -228,11 +228,19 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   GC_PHASE(P, 16);
   // a15 process-noise IW statistics (inverse_wishart_jax.py:71-123)
   wg_chol_solve(Wc, hrec, mupo, n);
-  for (int i = t; i < NN; i += kWG) W3[i] = Lps[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
-  __syncthreads();
-  wg_chol(W3, n);
-  wg_chol_solve(W3, hps, mups, n);
-  wg_chol_inverse(Wc, W2, Sx, n);  // Σ_post -> W2
+  if (s_dt == 0.0 && s_ex == 0.0) {
+    // no dt / extrinsic excitation: every afac is 1.0, so Lps and hps are L_pred and h_pred bit for
+    // bit and μ_pred = (L_pred + εI)⁻¹ h_pred is predict's μ_inc (same routines, same operands)
+    if (t < n) mups[t] = P.mu_aux[(int64_t)hl * kMuAux + 22 + t];
+    __syncthreads();
+  } else {
+    for (int i = t; i < NN; i += kWG) W3[i] = Lps[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
+    __syncthreads();
+    wg_chol(W3, n);
+    wg_chol_solve(W3, hps, mups, n);
+  }
+  wg_chol_inverse(Wc, W2, Sx, n);  // Σ_post -> W2 (also the next scan's predict Σ, P.Sig)
+  for (int i = t; i < NN; i += kWG) P.Sig[(int64_t)hl * NN + i] = W2[i];
   for (int idx = t; idx < 7 * 36; idx += kWG) P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
   GC_PHASE(P, 17);
   // a13 map increment from hypothesis 0 only (backend_node.py:2081-2083), build-defined pushforward

@@ -223,10 +223,19 @@ constexpr int kPredCertLen = 8;  // [lift, psd Δ, eig_min, eig_max, cond, nnc, 
 GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, double dt, double eps_psd,
                        double eps_lift, double lambda_ou, double* Lout, double* hout, double* mu, double* cert,
                        double* W1, double* W2, double* W3, double* Sx, double* red, double* c1, double* c2,
-                       bool full_cert = false) {
+                       bool full_cert = false, const double* Sig_cached = nullptr,
+                       const double* mu_cached = nullptr) {
   const int t = threadIdx.x, n = kDZ;
-  wg_solve_lifted(Lp, hprev, mu, eps_lift, n, W1);  // W1 = chol(L + εI)
-  wg_chol_inverse(W1, W2, W3, n);                    // W2 = Σ
+  if (Sig_cached) {
+    // The batched pipeline's evidence kernel already factorised this very (L + εI) with the same
+    // routines (Σ_post and μ_fin of the previous scan): bit-identical, so reuse them.
+    for (int i = t; i < kNN; i += kWG) W2[i] = Sig_cached[i];
+    if (t < n) mu[t] = mu_cached[t];
+    __syncthreads();
+  } else {
+    wg_solve_lifted(Lp, hprev, mu, eps_lift, n, W1);  // W1 = chol(L + εI)
+    wg_chol_inverse(W1, W2, W3, n);                    // W2 = Σ
+  }
   const double ef = exp(-2.0 * lambda_ou * dt);
   const double dc = (1.0 - ef) / (2.0 * lambda_ou + kF64Eps);
   for (int i = t; i < kNN; i += kWG) W2[i] = ef * W2[i] + dc * Q[i];

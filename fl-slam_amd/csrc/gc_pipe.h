@@ -43,6 +43,7 @@ struct PipeDev {
   double *mu_aux, *io_parts;               // (Hl, kMuAux), (Hl, kIoParts)
   double *dPsiP, *mu_fin, *diag;
   double *lpose;                           // (Hl, 36) pose block of L_evidence (diagnostics tape)
+  double *Sig;                             // (Hl, 22, 22) Σ_post = (L_post + εI)⁻¹ of the last scan
   // shared
   double *weights;                         // (H)
   double *Q;                               // (22, 22)
@@ -65,6 +66,7 @@ struct ScanArgs {
   double w_process;                        // min(1, scan_count)
   const double* w_raw;                     // (n_in) raw point weights (a1 budget, fused into predict)
   int64_t n_in;                            // raw points of this scan
+  int sig_cached;                          // P.Sig / P.mu_fin hold (P.L + εI)⁻¹ and its solve with P.h
 };
 
 // dev instrumentation: -DGC_PHASE_TIMING records s_memtime at phase boundaries of hypothesis 0

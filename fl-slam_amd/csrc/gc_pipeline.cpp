@@ -32,6 +32,9 @@ struct gc_pipeline {
   // their own: they are extra workgroups of the predict grid.
   hipStream_t side = nullptr;
   hipEvent_t ev_pred = nullptr, ev_io = nullptr;
+  // P.Sig / P.mu_fin were written by the last scan's evidence kernel from the current P.L / P.h
+  // (cleared whenever the beliefs are set from the host)
+  bool sig_cached = false;
 };
 
 namespace {
@@ -98,13 +101,13 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   int rc = GC_OK;
   double** fields[] = {&P.X, &P.z, &P.L, &P.h, &P.stamp, &P.Lpred, &P.hpred, &P.pred_cert, &P.pose_pred, &P.xi,
                        &P.imu_out, &P.dPsiM, &P.stats, &P.bincert, &P.io_L, &P.io_h, &P.io_cert, &P.dPsiP,
-                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose};
+                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose, &P.Sig};
   const size_t sizes[] = {(size_t)Hl * 6, (size_t)Hl * 22, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl,
                           (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kPredCert, (size_t)Hl * 6,
                           (size_t)Hl * 6, (size_t)Hl * gc::kImuOut, (size_t)Hl * 27, (size_t)Hl * B * 38,
                           (size_t)Hl * 8, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kIoCert,
                           (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag, (size_t)Hl * gc::kMuAux,
-                          (size_t)Hl * gc::kIoParts, (size_t)Hl * 36};
+                          (size_t)Hl * gc::kIoParts, (size_t)Hl * 36, (size_t)Hl * NN};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert};
@@ -165,6 +168,7 @@ int32_t gc_pipeline_set_beliefs(gc_pipeline* p, const double* h_X, const double*
                                 const double* h_h, const double* h_stamp) {
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
   const size_t Hl = p->P.Hl;
+  p->sig_cached = false;
   GC_TRY(up(p, p->P.X, h_X, Hl * 6));
   GC_TRY(up(p, p->P.z, h_z, Hl * 22));
   GC_TRY(up(p, p->P.L, h_L, Hl * 484));
@@ -348,7 +352,7 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
   gc_ctx* ctx = p->ctx;
   const auto& s = p->slots[slot];
   gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
-                 scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in};
+                 scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in, p->sig_cached ? 1 : 0};
   gc::PipeDev& P = p->P;
   const bool io = p->io_mode == GC_IO_COMPUTED;
   // a1 budget scalars (the fused kernel reads the selection / mass scale from them) on extra
@@ -369,6 +373,7 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
   if (io) GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, p->ev_io, 0));
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
+  p->sig_cached = true;
   // a16: partial sums, exchange, fixed-order reduction + IW apply + map update
   GC_HIP(ctx, gc::launch_combine_local(P, ctx->stream));
   if (P.G > 1) GC_TRY(gc::comm_allgather(p->comm, ctx, P.send, P.gather, gc::partial_len(P.B)));

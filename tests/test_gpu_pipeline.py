@@ -78,3 +78,26 @@ def test_pipeline_matches_oracle_over_scans(ctx, H):
         _close(iw["Q"], O.iw_process_Q(st.nu_proc, st.Psi_proc), 1e-7, 1e-18, "Q")
         mp = pipe.get_map()
         _close(mp["map"], cases.map_to_record(st.map), 1e-8, 1e-12, f"scan{k} map")
+
+
+def test_predict_reuses_posterior_factorisation_bit_exactly(ctx):
+    """The predict kernel reuses the previous scan's Σ_post = (L_post + εI)⁻¹ and μ_fin from the
+    evidence kernel instead of refactorising P.L (gc_opsdev.h wg_predict, Sig_cached). Re-setting
+    the beliefs from the host clears that cache, so a run that round-trips the beliefs before every
+    scan refactorises; both runs must agree bit for bit (same routines on the same operands)."""
+    case = cases.build(H=4, n_az=256, n_scans=3)
+    outs = []
+    for refactor in (False, True):
+        pipe = _gpu_pipeline(case, ctx)
+        st = case["state"]
+        for k, s in enumerate(case["scans"]):
+            if refactor and k > 0:
+                b = pipe.get_beliefs()
+                pipe.set_beliefs(b["X_anchor"], b["z_lin"], b["L"], b["h"], b["stamp"])
+            pipe.stage_scan(0, s)
+            pipe.run_scan(0, s, st.scan_count + k)
+        ctx.sync()
+        b = pipe.get_beliefs()
+        outs.append((b["L"], b["h"], b["z_lin"], b["X_anchor"], pipe.combined()["L"], pipe.get_iw()["Psi_proc"]))
+    for a, b in zip(*outs):
+        assert np.array_equal(a, b)
