@@ -114,20 +114,26 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   GC_PHASE(P, 2);
   wg_chol(W4, n);
   GC_PHASE(P, 3);
-  wg_chol_solve(W4, hpred, mu_inc, n);
-  GC_PHASE(P, 4);
-  if (t == 0) {
+  // μ_inc on wave 0; beside it, one lane each of waves 1 and 2: σ_warp from (L_pred+εI)⁻¹[15,15]
+  // and R0 = Exp(rotvec of pose0) (pose0 from phase 1)
+  if (t < 64) {
+    wave0_chol_solve<kDZ>(W4, hpred, mu_inc, n);
+  } else if (t == 64) {
     const double s1515 = inv_diag_from_chol(W4, n, 15);
-    misc[6] = fmax(sqrt(s1515), 0.01);                  // sigma_warp
-    compose_exp(P.X + (int64_t)h * 6, mu_inc, misc + 8);  // pose_pred (for MF / planar)
-    for (int k = 0; k < 6; ++k) P.pose_pred[(int64_t)h * 6 + k] = misc[8 + k];
+    misc[6] = fmax(sqrt(s1515), 0.01);  // sigma_warp
+  } else if (t == 128) {
     for (int k = 0; k < 6; ++k) P.mu_aux[(int64_t)h * kMuAux + 44 + k] = misc[k];
     double R0[9];
     so3_exp(misc + 3, R0);
     for (int k = 0; k < 9; ++k) misc[16 + k] = R0[k];
   }
-  if (t < n) P.mu_aux[(int64_t)h * kMuAux + 22 + t] = mu_inc[t];
   __syncthreads();
+  GC_PHASE(P, 4);
+  if (t == 0) {
+    compose_exp(P.X + (int64_t)h * 6, mu_inc, misc + 8);  // pose_pred (for MF / planar)
+    for (int k = 0; k < 6; ++k) P.pose_pred[(int64_t)h * 6 + k] = misc[8 + k];
+  }
+  if (t < n) P.mu_aux[(int64_t)h * kMuAux + 22 + t] = mu_inc[t];
   // ------------------------------------------------------------------ IMU (a3)
   const double sigma_warp = misc[6];
   const double bg[3] = {mu_inc[9], mu_inc[10], mu_inc[11]};
@@ -139,9 +145,10 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
     const double ti = S.imu_t[i];
     if (ti > 0.0) { cnt += 1.0; tmin = fmin(tmin, ti); tmax = fmax(tmax, ti); }
   }
-  const double nvalid = wg_sum(cnt, red);
-  tmin = -wg_max(-tmin, red);
-  tmax = wg_max(tmax, red);
+  double ntmin = -tmin;
+  wg_sum_max2(cnt, ntmin, tmax, A);  // A: preintegration scratch, not yet live
+  const double nvalid = cnt;
+  tmin = -ntmin;
   const double dt_imu = fmax(nvalid >= 2.0 ? (tmax - tmin) / fmax(nvalid - 1.0, 1.0) : 0.0, 1e-12);
   // two samples per thread: a = 2t, b = 2t+1
   const int ia = 2 * t, ib = 2 * t + 1;
@@ -155,15 +162,6 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   GC_PHASE(P, 5);
   wg_preintegrate(M, S.imu_t, S.imu_g, S.imu_a, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, red, pre);
   GC_PHASE(P, 6);
-  const double ess_scan = wg_sum(wa + wb, red);
-  if (t == 0) {
-    double dR[9], dpose[6], xi[6];
-    mat3_mul_tn(R0, pre, dR);
-    mat3_tvec(R0, pre + 9, dpose);
-    so3_log(dR, dpose + 3);
-    se3_log(dpose, xi);
-    for (int k = 0; k < 6; ++k) P.xi[(int64_t)h * 6 + k] = xi[k];
-  }
   double ga[3] = {0, 0, 0}, gb[3] = {0, 0, 0}, aa[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
   for (int k = 0; k < 3; ++k) {
     if (ia < M) { ga[k] = S.imu_g[3 * ia + k]; aa[k] = S.imu_a[3 * ia + k]; }
@@ -176,9 +174,10 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
     return (i < M) ? window_weight(ti, S.t_last, S.t_scan, sigma_warp) * (ti > 0.0 ? 1.0 : 0.0) : 0.0;
   };
   const double wia = wint(ia), wib = wint(ib);
-  double om[4] = {wia + wib, 0.0, 0.0, 0.0};
+  double om[5] = {wia + wib, 0.0, 0.0, 0.0, wa + wb};
   for (int k = 0; k < 3; ++k) om[1 + k] = wia * (ga[k] - bg[k]) + wib * (gb[k] - bg[k]);
-  wg_sum_n<4>(om, A);  // A: preintegration scratch, free again
+  wg_sum_n<5>(om, A);  // A: preintegration scratch, free again (om[4]: ess_scan, wg_sum's order)
+  const double ess_scan = om[4];
   const double wsum = om[0] + P.eps_mass;
   for (int k = 0; k < 3; ++k) om[k] = om[1 + k] / wsum;
   double rr[12];
@@ -202,6 +201,14 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   GC_PHASE(P, 7);
   wg_sum_n<12>(rr, A);
   GC_PHASE(P, 8);
+  if (t == 64) {  // ξ_body = se3_log(R0ᵀ Δpose) on wave 1 beside thread 0's IW statistics
+    double dR[9], dpose[6], xi[6];
+    mat3_mul_tn(R0, pre, dR);
+    mat3_tvec(R0, pre + 9, dpose);
+    so3_log(dR, dpose + 3);
+    se3_log(dpose, xi);
+    for (int k = 0; k < 6; ++k) P.xi[(int64_t)h * 6 + k] = xi[k];
+  }
   if (t == 0) {
     double* out = P.dPsiM + (int64_t)h * 27;
     for (int blk = 0; blk < 2; ++blk) {

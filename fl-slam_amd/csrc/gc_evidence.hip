@@ -227,7 +227,6 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   __syncthreads();
   GC_PHASE(P, 16);
   // a15 process-noise IW statistics (inverse_wishart_jax.py:71-123)
-  wg_chol_solve(Wc, hrec, mupo, n);
   if (s_dt == 0.0 && s_ex == 0.0) {
     // no dt / extrinsic excitation: every afac is 1.0, so Lps and hps are L_pred and h_pred bit for
     // bit and μ_pred = (L_pred + εI)⁻¹ h_pred is predict's μ_inc (same routines, same operands)
@@ -239,7 +238,8 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     wg_chol(W3, n);
     wg_chol_solve(W3, hps, mups, n);
   }
-  wg_chol_inverse(Wc, W2, Sx, n);  // Σ_post -> W2 (also the next scan's predict Σ, P.Sig)
+  // Σ_post -> W2 (also the next scan's predict Σ, P.Sig); μ_post = (L_post + εI)⁻¹ h_rec on wave 1
+  wg_chol_inverse_and_solve(Wc, W2, Sx, n, hrec, mupo);
   for (int i = t; i < NN; i += kWG) P.Sig[(int64_t)hl * NN + i] = W2[i];
   for (int idx = t; idx < 7 * 36; idx += kWG) P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
   GC_PHASE(P, 17);

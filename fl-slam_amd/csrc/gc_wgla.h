@@ -51,6 +51,24 @@ GC_DEV double wg_max(double v, double* red) {
   return r;
 }
 
+// Workgroup sum of s (wg_sum's order) and maxima of m1, m2 with three barriers instead of nine.
+// scratch: 12 doubles of LDS not otherwise live.
+GC_DEV void wg_sum_max2(double& s, double& m1, double& m2, double* scratch) {
+  s = wave_sum(s);
+  m1 = wave_max(m1);
+  m2 = wave_max(m2);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) {
+    const int w = threadIdx.x >> 6;
+    scratch[w] = s; scratch[4 + w] = m1; scratch[8 + w] = m2;
+  }
+  __syncthreads();
+  s = (scratch[0] + scratch[1]) + (scratch[2] + scratch[3]);
+  m1 = fmax(fmax(scratch[4], scratch[5]), fmax(scratch[6], scratch[7]));
+  m2 = fmax(fmax(scratch[8], scratch[9]), fmax(scratch[10], scratch[11]));
+  __syncthreads();
+}
+
 // N workgroup sums with two barriers instead of 3N (fixed shuffle tree + fixed wave order, as
 // wg_sum). scratch: 4N doubles of LDS not otherwise live. Results replace v on every thread.
 template <int N>
@@ -171,7 +189,7 @@ GC_DEV bool wg_chol_checked(double* A, int n, double* flag) {
 // row i and column i of C: forward substitution broadcasts y_j, backward x_j, one readlane each.
 template <int NM>
 GC_DEV void wave0_chol_solve(const double* C, const double* b, double* x, int n) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;  // any single wave (callers: wave 0, or wave 1 beside wave-0 work)
   const bool live = lane < n;
   double c[NM], ct[NM];
 #pragma unroll
@@ -213,7 +231,7 @@ GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
 // waves): thread (g = t/32, j = t%32) forms Ainv[i][j] = Σ_k W[k][i] W[k][j] for i ≡ g (mod 8),
 // its column j of W in registers and column i broadcast; k ascends over the full range (the
 // entries below the triangles are exact zeros), the order of the reference's product.
-GC_DEV void wg_chol_inverse(const double* C, double* Ainv, double* scratch, int n) {
+GC_DEV void chol_inverse_phase1(const double* C, double* scratch, int n) {
   if ((int)threadIdx.x < n) {
     const int j = threadIdx.x;
     double col[kDZ];
@@ -234,7 +252,8 @@ GC_DEV void wg_chol_inverse(const double* C, double* Ainv, double* scratch, int 
     for (int k = 0; k < kDZ; ++k)
       if (k < n) scratch[j * n + k] = col[k];
   }
-  __syncthreads();
+}
+GC_DEV void chol_inverse_phase2(double* Ainv, const double* scratch, int n) {
   const int j = threadIdx.x & 31, g = threadIdx.x >> 5;
   if (j < n) {
     double wj[kDZ];
@@ -249,6 +268,24 @@ GC_DEV void wg_chol_inverse(const double* C, double* Ainv, double* scratch, int 
       Ainv[i * n + j] = v;
     }
   }
+}
+GC_DEV void wg_chol_inverse(const double* C, double* Ainv, double* scratch, int n) {
+  chol_inverse_phase1(C, scratch, n);
+  __syncthreads();
+  chol_inverse_phase2(Ainv, scratch, n);
+  __syncthreads();
+}
+// wg_chol_inverse(C) and, on wave 1 while wave 0 forward-substitutes, x = (C Cᵀ)⁻¹ b
+// (wave0_chol_solve): the two results are exactly those of the separate calls.
+GC_DEV void wg_chol_inverse_and_solve(const double* C, double* Ainv, double* scratch, int n, const double* b,
+                                      double* x) {
+  if (threadIdx.x < 64) chol_inverse_phase1(C, scratch, n);
+  else if (threadIdx.x < 128) {
+    if (n <= 8) wave0_chol_solve<8>(C, b, x, n);
+    else wave0_chol_solve<kDZ>(C, b, x, n);
+  }
+  __syncthreads();
+  chol_inverse_phase2(Ainv, scratch, n);
   __syncthreads();
 }
 
