@@ -166,15 +166,11 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
       P.lpose[(int64_t)hl * 36 + idx] = Lev[i * n + j];  // L_evidence[pose, pose] for the tape
     }
     __syncthreads();
-    double* w6 = acc;
-    wg_eigvalsh(P6, w6, 6, Sx, red);
+    double lmin = 0.0, lmax = 0.0;
+    if (t < 64) wave_extreme_eigvals<6>(P6, lmin, lmax);  // only λ_min / λ_max are consumed
     if (t == 0) {
-      double mn = 1e308, mx = -1e308;
-      for (int k = 0; k < 6; ++k) {
-        double e = isfinite(w6[k]) ? w6[k] : P.eps_psd;
-        e = fmax(e, P.eps_psd);
-        mn = fmin(mn, e); mx = fmax(mx, e);
-      }
+      const double mn = fmax(isfinite(lmin) ? lmin : P.eps_psd, P.eps_psd);
+      const double mx = fmax(isfinite(lmax) ? lmax : P.eps_psd, P.eps_psd);
       const double cond6 = mx / mn;
       P.diag[(int64_t)hl * kHypDiag + 39] = mn;  // eigmin_pose6
       const double ess_ev = sc[53], exc = sc[55];

@@ -554,6 +554,99 @@ GC_DEV void wg_eigvalsh(const double* M, double* w, int n, double* scratch, doub
   wg_jacobi_eigh(S, nullptr, w, n, cs, red);
 }
 
+// Extreme eigenvalues of a symmetric N x N (N <= 8) in LDS, wave 0 only (no workgroup barrier):
+// every lane runs the same Householder tridiagonalisation in registers (the Lanczos/LAPACK
+// reduction, so no broadcast is needed afterwards), then lanes 0-31 multisect for λ_min and lanes
+// 32-63 for λ_max with Sturm counts (the inertia of T − σI, as LAPACK dstebz): 33 sections per
+// round, 11 rounds take the Gershgorin interval to 2^-55 of its width (absolute accuracy ~u‖A‖,
+// that of eigh). Replaces the full Jacobi sweep where only the conditioning is consumed.
+template <int N>
+GC_DEV void wave_extreme_eigvals(const double* S, double& lmin, double& lmax) {
+  double A[N][N];
+#pragma unroll
+  for (int i = 0; i < N; ++i)
+#pragma unroll
+    for (int j = 0; j < N; ++j) A[i][j] = S[i * N + j];
+  double d[N], e[N];
+#pragma unroll
+  for (int k = 0; k < N - 2; ++k) {
+    double ss = 0.0;
+#pragma unroll
+    for (int i = k + 2; i < N; ++i) ss = fma(A[i][k], A[i][k], ss);
+    const double x0 = A[k + 1][k];
+    const double sigma = sqrt(fma(x0, x0, ss));
+    if (ss == 0.0) {  // already tridiagonal in this column
+      e[k] = x0;
+      continue;
+    }
+    const double alpha = x0 >= 0.0 ? -sigma : sigma;
+    double v[N];
+#pragma unroll
+    for (int i = 0; i < N; ++i) v[i] = i > k + 1 ? A[i][k] : 0.0;
+    v[k + 1] = x0 - alpha;
+    const double beta = 1.0 / (sigma * (sigma + fabs(x0)));  // 2 / vᵀv
+    double p[N];
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) {
+      double acc = 0.0;
+#pragma unroll
+      for (int j = k + 1; j < N; ++j) acc = fma(A[i][j], v[j], acc);
+      p[i] = beta * acc;
+    }
+    double pv = 0.0;
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) pv = fma(p[i], v[i], pv);
+    const double K = 0.5 * beta * pv;
+#pragma unroll
+    for (int i = k + 1; i < N; ++i) p[i] = fma(-K, v[i], p[i]);  // w
+#pragma unroll
+    for (int i = k + 1; i < N; ++i)
+#pragma unroll
+      for (int j = k + 1; j < N; ++j) A[i][j] = A[i][j] - (v[i] * p[j] + p[i] * v[j]);
+    e[k] = alpha;
+  }
+  e[N - 2] = A[N - 1][N - 2];
+  e[N - 1] = 0.0;
+#pragma unroll
+  for (int i = 0; i < N; ++i) d[i] = A[i][i];
+  double lo = d[0] - fabs(e[0]), hi = d[0] + fabs(e[0]), emax2 = 0.0;
+#pragma unroll
+  for (int i = 1; i < N; ++i) {
+    const double r = fabs(e[i - 1]) + fabs(e[i]);
+    lo = fmin(lo, d[i] - r);
+    hi = fmax(hi, d[i] + r);
+    emax2 = fmax(emax2, e[i - 1] * e[i - 1]);
+  }
+  const double pivmin = 2.2250738585072014e-308 * fmax(1.0, emax2);
+  const int lane = threadIdx.x & 63, half = lane >> 5, l = lane & 31;
+  double a = lo, b = hi;  // this half's bracket: λ_min (half 0) or λ_max (half 1)
+  const int target = half == 0 ? 1 : N;  // first σ with count(σ) >= target lies above the eigenvalue
+  for (int round = 0; round < 11; ++round) {
+    const double step = (b - a) * (1.0 / 33.0);
+    const double sig = fma((double)(l + 1), step, a);
+    int cnt = 0;
+    double q = d[0] - sig;
+    if (fabs(q) < pivmin) q = -pivmin;
+    cnt += q < 0.0;
+#pragma unroll
+    for (int i = 1; i < N; ++i) {
+      q = (d[i] - sig) - e[i - 1] * e[i - 1] / q;
+      if (fabs(q) < pivmin) q = -pivmin;
+      cnt += q < 0.0;
+    }
+    const uint64_t m = __builtin_amdgcn_ballot_w64(cnt >= target);
+    const uint32_t mh = (uint32_t)(half == 0 ? m : (m >> 32));
+    const int f = mh ? __builtin_ctz(mh) : 32;  // first section point above the eigenvalue
+    const double na = f == 0 ? a : fma((double)f, step, a);
+    const double nb = f == 32 ? b : fma((double)(f + 1), step, a);
+    a = na;
+    b = nb;
+  }
+  const double mid = 0.5 * (a + b);
+  lmin = readlane_f64(mid, 0);
+  lmax = readlane_f64(mid, 32);
+}
+
 // y = A x (n x n, LDS), threads < n
 GC_DEV void wg_matvec(const double* A, const double* x, double* y, int n) {
   if ((int)threadIdx.x < n) {
