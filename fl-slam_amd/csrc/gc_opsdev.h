@@ -259,7 +259,7 @@ GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, d
 
 // ------------------------------------------------------------------------------------ a3
 // Weighted IMU preintegration (imu_preintegration.py:46-147) over M <= 512 samples, two per
-// thread (a = 2t, b = 2t+1): rotation by an inclusive Hillis-Steele scan of the 3x3 factors
+// thread (a = 2t, b = 2t+1): rotation by an inclusive wave-shuffle + cross-wave scan of the 3x3 factors
 // Exp((ω−b_g) w dt), velocity by a prefix sum, position by the closed-form sum
 // p = Σ v_i de_i + ½ a_i de_i². wa/wb are the two samples' weights, R0 the start rotation.
 // Thread 0 writes out[kPreint] = [R_end 9, p_end 3, v_end 3, Σde, Σa_body de 3,
@@ -289,21 +289,39 @@ GC_DEV void wg_preintegrate(int M, const double* stamps, const double* gyro, con
     so3_exp(wv2, dRb);
     mat3_mul(dRa, dRb, Pl);
   }
-  for (int k = 0; k < 9; ++k) A[t * 9 + k] = Pl[k];
-  __syncthreads();
-  // inclusive Hillis-Steele scan of 3x3 products: X_t = Pl_0 ... Pl_t
+  // inclusive scan of 3x3 products X_t = Pl_0 ... Pl_t: 6 shuffle levels inside each wave, then the
+  // wave totals (left to right) applied on the left; result rows in A for the reads below
   double* src = A;
-  double* dst = Bm;
-  for (int off = 1; off < kWG; off <<= 1) {
-    double Xn[9];
-    if (t >= off) {
-      mat3_mul(src + (t - off) * 9, src + t * 9, Xn);
-    } else {
-      for (int k = 0; k < 9; ++k) Xn[k] = src[t * 9 + k];
+  {
+    const int lane = t & 63, w = t >> 6;
+    double X[9];
+    for (int k = 0; k < 9; ++k) X[k] = Pl[k];
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      double Y[9], Z[9];
+#pragma unroll
+      for (int k = 0; k < 9; ++k) Y[k] = __shfl_up(X[k], off, 64);
+      if (lane >= off) {
+        mat3_mul(Y, X, Z);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) X[k] = Z[k];
+      }
     }
-    for (int k = 0; k < 9; ++k) dst[t * 9 + k] = Xn[k];
+    if (lane == 63)
+      for (int k = 0; k < 9; ++k) Bm[w * 9 + k] = X[k];
     __syncthreads();
-    double* tmp = src; src = dst; dst = tmp;
+    if (w > 0) {
+      double W[9], Z[9];
+      for (int k = 0; k < 9; ++k) W[k] = Bm[k];
+      for (int v = 1; v < w; ++v) {
+        mat3_mul(W, Bm + v * 9, Z);
+        for (int k = 0; k < 9; ++k) W[k] = Z[k];
+      }
+      mat3_mul(W, X, Z);
+      for (int k = 0; k < 9; ++k) X[k] = Z[k];
+    }
+    for (int k = 0; k < 9; ++k) A[t * 9 + k] = X[k];
+    __syncthreads();
   }
   double Ea[9], Rb[9];
   if (t == 0) {
@@ -318,17 +336,28 @@ GC_DEV void wg_preintegrate(int M, const double* stamps, const double* gyro, con
   mat3_vec(Ea, aba, nga);
   mat3_vec(Rb, abb, ngb);
   for (int k = 0; k < 3; ++k) { awa[k] = nga[k] + g[k]; awb[k] = ngb[k] + g[k]; }
-  // exclusive prefix sum of velocity increments
-  for (int k = 0; k < 3; ++k) V1[t * 3 + k] = awa[k] * dea + awb[k] * deb;
-  __syncthreads();
+  // prefix sum of velocity increments (inclusive rows in V1; the reads below take row t-1):
+  // shuffle levels inside each wave, then the preceding waves' totals
   double* vs = V1;
-  double* vd = V2;
-  for (int off = 1; off < kWG; off <<= 1) {
+  {
+    const int lane = t & 63, w = t >> 6;
     double v[3];
-    for (int k = 0; k < 3; ++k) v[k] = vs[t * 3 + k] + ((t >= off) ? vs[(t - off) * 3 + k] : 0.0);
-    for (int k = 0; k < 3; ++k) vd[t * 3 + k] = v[k];
+    for (int k = 0; k < 3; ++k) v[k] = awa[k] * dea + awb[k] * deb;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const double y = __shfl_up(v[k], off, 64);
+        if (lane >= off) v[k] = y + v[k];
+      }
+    }
+    if (lane == 63)
+      for (int k = 0; k < 3; ++k) V2[w * 3 + k] = v[k];
     __syncthreads();
-    double* tp = vs; vs = vd; vd = tp;
+    for (int u = 0; u < w; ++u)
+      for (int k = 0; k < 3; ++k) v[k] = V2[u * 3 + k] + v[k];
+    for (int k = 0; k < 3; ++k) V1[t * 3 + k] = v[k];
+    __syncthreads();
   }
   double pc[3];
   for (int k = 0; k < 3; ++k) {
@@ -344,7 +373,7 @@ GC_DEV void wg_preintegrate(int M, const double* stamps, const double* gyro, con
     sums[9 + k] = awa[k] * dea + awb[k] * deb;
   }
   sums[12] = dea + deb;
-  for (int q = 0; q < 13; ++q) sums[q] = wg_sum(sums[q], red);
+  wg_sum_n<13>(sums, Bm);  // 13 sums in wg_sum's order with two barriers (Bm: free again)
   if (t == 0) {
     mat3_mul(R0, src + (kWG - 1) * 9, out);  // R_end
     for (int k = 0; k < 3; ++k) {
