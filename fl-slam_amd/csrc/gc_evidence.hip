@@ -423,6 +423,20 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
   double* Qp = Qs + NN;     // NN
   const int t = threadIdx.x, n = kDZ;
   const int PLn = partial_len(P.B);
+  if (blockIdx.x == 1) {
+    // ---- map update on a second workgroup, beside the IW / Q chain of workgroup 0 (nothing there
+    // reads the map): γ·map + increments of hypothesis 0 (bin_atlas.py:137-163, :232-257), the
+    // increments reduced in the same rank order as workgroup 0's record (0.0 + Σ_g, so the value
+    // is the same whether or not workgroup 0 has already rewritten an aliased single-rank record)
+    for (int e = t; e < P.B * kMapRec; e += kWG) {
+      double s = 0.0;
+      for (int g = 0; g < P.G; ++g) s += P.gather[(int64_t)g * PLn + kPMAP + e];
+      P.map[e] = P.forgetting * P.map[e] + s;
+    }
+    __syncthreads();
+    map_derive_wg(P, red, tab);
+    return;
+  }
   GC_PHASE(P, 20);
   // fixed rank-order reduction of the gathered partial records
   for (int e = t; e < PLn; e += kWG) {
@@ -470,11 +484,6 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
   GC_PHASE(P, 24);
   iw_Q_wg(P, Qs, Qp, Sx, red);
   GC_PHASE(P, 25);
-  // ---- map update: γ·map + increments of hypothesis 0 (bin_atlas.py:137-163, :232-257)
-  for (int e = t; e < P.B * kMapRec; e += kWG) P.map[e] = P.forgetting * P.map[e] + R[kPMAP + e];
-  __syncthreads();
-  map_derive_wg(P, red, tab);
-  GC_PHASE(P, 26);
 }
 
 // ------------------------------------------------------------------------------ launchers
@@ -498,7 +507,8 @@ hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
 }
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
   allow_big_lds((const void*)k_combine_final, lds_final());
-  hipLaunchKernelGGL(k_combine_final, dim3(1), dim3(256), lds_final(), st, P, S);
+  // workgroup 0: record reduction, certificates, IW apply, Q; workgroup 1: map update + derive
+  hipLaunchKernelGGL(k_combine_final, dim3(2), dim3(256), lds_final(), st, P, S);
   return hipGetLastError();
 }
 hipError_t launch_map_derive(const PipeDev& P, hipStream_t st) {
