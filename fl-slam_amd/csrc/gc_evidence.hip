@@ -462,7 +462,9 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     const double wf = fmax(P.weights[k], P.weight_floor), wn = wf / wsum;
     l2 += wn * wn; lc += (wn > P.weight_floor) ? 1.0 : 0.0; la += fabs(wf - P.weights[k]);
   }
-  const double s2 = wg_sum(l2, red), scnt = wg_sum(lc, red), sadj = wg_sum(la, red);
+  double s3[3] = {l2, lc, la};
+  wg_sum_n<3>(s3, tab);  // wg_sum's order, two barriers (tab: free until the IW apply)
+  const double s2 = s3[0], scnt = s3[1], sadj = s3[2];
   if (t == 0) {
     double* cc = cb + NN + 2 * n + 6;
     cc[0] = R[kPSTAMP0];
