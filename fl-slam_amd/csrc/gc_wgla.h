@@ -453,16 +453,29 @@ GC_DEV void wg_psd_project(const double* M, double* Mp, double eps, int n, doubl
 // (not computed). Otherwise the full Jacobi projection runs. scratch: 2n*n + 4n doubles.
 GC_DEV void wg_psd_project_fast(const double* M, double* Mp, double eps, int n, double* scratch,
                                 double* red, double* cert6) {
-  double symloc = 0.0;
   for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
     const int i = idx / n, j = idx % n;
-    const double sv = 0.5 * (M[i * n + j] + M[j * n + i]);
-    const double d = sv - M[idx];
-    symloc += d * d;
-    scratch[idx] = sv - ((i == j) ? eps : 0.0);
+    scratch[idx] = 0.5 * (M[i * n + j] + M[j * n + i]) - ((i == j) ? eps : 0.0);
   }
-  const double symd = wg_sum(symloc, red);
-  const bool spd = wg_chol_checked(scratch, n, red + 4);
+  __syncthreads();
+  // Cholesky on wave 0; the symmetry deviation (cert field 1) on wave 1 meanwhile
+  if (threadIdx.x < 64) {
+    const bool okc = n <= 8 ? wave0_chol<8, true>(scratch, n) : wave0_chol<kDZ, true>(scratch, n);
+    if (threadIdx.x == 0) red[4] = okc ? 0.0 : 1.0;
+  } else if (threadIdx.x < 128) {
+    double symloc = 0.0;
+    for (int idx = threadIdx.x - 64; idx < n * n; idx += 64) {
+      const int i = idx / n, j = idx % n;
+      const double d = 0.5 * (M[i * n + j] + M[j * n + i]) - M[idx];
+      symloc += d * d;
+    }
+    symloc = wave_sum(symloc);
+    if (threadIdx.x == 64) red[5] = symloc;
+  }
+  __syncthreads();
+  const bool spd = red[4] == 0.0;
+  const double symd = red[5];
+  __syncthreads();
   if (spd) {
     for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
       const int i = idx / n, j = idx % n;
