@@ -96,6 +96,9 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   double* mu_inc = vec + 3 * kDZ;
 
   GC_PHASE(P, 0);
+  // this thread's IMU slots, loaded beside the belief (one exposed latency for both) and parked in
+  // the preintegration scratch (Bm..V2, 15 doubles per thread, not live before the IMU section)
+  imu_pair_store(load_imu_pair(P.M, S.imu_t, S.imu_g, S.imu_a), Bm + 15 * t);
   for (int i = t; i < N2; i += kWG) Lp[i] = P.L[(int64_t)h * N2 + i];
   if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
   __syncthreads();
@@ -135,16 +138,15 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   }
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + 22 + t] = mu_inc[t];
   // ------------------------------------------------------------------ IMU (a3)
+  const ImuPair q = imu_pair_load(Bm + 15 * t);  // own slots: no barrier needed
   const double sigma_warp = misc[6];
   const double bg[3] = {mu_inc[9], mu_inc[10], mu_inc[11]};
   const double ba[3] = {mu_inc[12], mu_inc[13], mu_inc[14]};
   const int M = P.M;
   // dt_imu over valid (stamp > 0) samples (pipeline.py:526-535)
-  double cnt = 0.0, tmin = 1e308, tmax = -1e308;
-  for (int i = t; i < M; i += kWG) {
-    const double ti = S.imu_t[i];
-    if (ti > 0.0) { cnt += 1.0; tmin = fmin(tmin, ti); tmax = fmax(tmax, ti); }
-  }
+  double cnt = 0.0, tmin = 1e308, tmax = -1e308;  // over this thread's slots 2t, 2t+1 (exact in any order)
+  if (2 * t < M && q.ta > 0.0) { cnt += 1.0; tmin = fmin(tmin, q.ta); tmax = fmax(tmax, q.ta); }
+  if (2 * t + 1 < M && q.tb > 0.0) { cnt += 1.0; tmin = fmin(tmin, q.tb); tmax = fmax(tmax, q.tb); }
   double ntmin = -tmin;
   wg_sum_max2(cnt, ntmin, tmax, A);  // A: preintegration scratch, not yet live
   const double nvalid = cnt;
@@ -152,28 +154,22 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   const double dt_imu = fmax(nvalid >= 2.0 ? (tmax - tmin) / fmax(nvalid - 1.0, 1.0) : 0.0, 1e-12);
   // two samples per thread: a = 2t, b = 2t+1
   const int ia = 2 * t, ib = 2 * t + 1;
-  auto stamp = [&](int i) { return i < M ? S.imu_t[i] : 0.0; };
-  const double ta = stamp(ia), tb = stamp(ib);
+  const double ta = q.ta, tb = q.tb;
   const double wa = ia < M ? window_weight(ta, S.t0, S.t1, sigma_warp) : 0.0;
   const double wb = ib < M ? window_weight(tb, S.t0, S.t1, sigma_warp) : 0.0;
   const double* R0 = misc + 16;
   double* pre = misc + 32;  // kPreint
   const double kG[3] = {0.0, 0.0, -9.81 * P.gravity_scale};  // GC_GRAVITY_W · imu_gravity_scale
   GC_PHASE(P, 5);
-  wg_preintegrate(M, S.imu_t, S.imu_g, S.imu_a, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, red, pre);
+  wg_preintegrate(M, q, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, pre);
   GC_PHASE(P, 6);
-  double ga[3] = {0, 0, 0}, gb[3] = {0, 0, 0}, aa[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
-  for (int k = 0; k < 3; ++k) {
-    if (ia < M) { ga[k] = S.imu_g[3 * ia + k]; aa[k] = S.imu_a[3 * ia + k]; }
-    if (ib < M) { gb[k] = S.imu_g[3 * ib + k]; ab[k] = S.imu_a[3 * ib + k]; }
-  }
+  const double *ga = q.ga, *gb = q.gb, *aa = q.aa, *ab = q.ab;
   // --- scan-to-scan window: omega_avg and measurement-noise IW statistics
   //     (pipeline.py:537-566, measurement_noise_iw_jax.py:130-218)
-  auto wint = [&](int i) {
-    const double ti = stamp(i);
+  auto wint = [&](int i, double ti) {
     return (i < M) ? window_weight(ti, S.t_last, S.t_scan, sigma_warp) * (ti > 0.0 ? 1.0 : 0.0) : 0.0;
   };
-  const double wia = wint(ia), wib = wint(ib);
+  const double wia = wint(ia, q.ta), wib = wint(ib, q.tb);
   double om[5] = {wia + wib, 0.0, 0.0, 0.0, wa + wb};
   for (int k = 0; k < 3; ++k) om[1 + k] = wia * (ga[k] - bg[k]) + wib * (gb[k] - bg[k]);
   wg_sum_n<5>(om, A);  // A: preintegration scratch, free again (om[4]: ess_scan, wg_sum's order)

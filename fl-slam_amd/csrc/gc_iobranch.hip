@@ -64,7 +64,8 @@ __global__ void __launch_bounds__(256) k_io_branch(PipeDev P, ScanArgs S, const 
   const double ba[3] = {mu_inc[12], mu_inc[13], mu_inc[14]};
   const double g[3] = {0.0, 0.0, -9.81 * P.gravity_scale};
   double* pre = misc + 16;  // kPreint = 25
-  wg_preintegrate(M, S.imu_t, S.imu_g, S.imu_a, wa, wb, misc, bg, ba, g, A, Bm, V1, V2, red, pre);
+  const ImuPair q = load_imu_pair(M, S.imu_t, S.imu_g, S.imu_a);
+  wg_preintegrate(M, q, wa, wb, misc, bg, ba, g, A, Bm, V1, V2, pre);
   // time-resolved vMF gravity (imu_evidence.py:402-559): all threads; w = w_imu_int per slot
   {
     double* w = A;  // preint scratch is free again

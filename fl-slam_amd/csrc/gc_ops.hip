@@ -123,7 +123,8 @@ __global__ void __launch_bounds__(256) k_op_preintegrate(int M, const double* st
   const int ia = 2 * t, ib = 2 * t + 1;
   const double wa = ia < M ? wk[ia] : 0.0, wb = ib < M ? wk[ib] : 0.0;
   const double g[3] = {g0, g1, g2};
-  wg_preintegrate(M, stamps, gyro, accel, wa, wb, R0, bg + 3 * k, ba + 3 * k, g, A, Bm, V1, V2, red, pre);
+  const ImuPair q = load_imu_pair(M, stamps, gyro, accel);
+  wg_preintegrate(M, q, wa, wb, R0, bg + 3 * k, ba + 3 * k, g, A, Bm, V1, V2, pre);
   double ess_l = 0.0;
   for (int i = t; i < M; i += kWG) ess_l += wk[i];
   const double ess = wg_sum(ess_l, red);

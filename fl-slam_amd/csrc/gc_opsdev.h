@@ -265,22 +265,48 @@ GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, d
 // Thread 0 writes out[kPreint] = [R_end 9, p_end 3, v_end 3, Σde, Σa_body de 3,
 // Σa_world_nog de 3, Σa_world de 3]. Scratch A, Bm: 256 x 9; V1, V2: 256 x 3.
 constexpr int kPreint = 25;
-GC_DEV void wg_preintegrate(int M, const double* stamps, const double* gyro, const double* accel, double wa,
-                            double wb, const double* R0, const double* bg, const double* ba, const double* g,
-                            double* A, double* Bm, double* V1, double* V2, double* red, double* out) {
+// A thread's two IMU slots a = 2t, b = 2t+1 (and the stamp of 2t+2), zero past M. Loaded once; the
+// batched predict issues the loads at kernel entry so their latency hides behind the 22x22 algebra.
+struct ImuPair {
+  double ta, tb, tn;
+  double ga[3], gb[3], aa[3], ab[3];
+};
+GC_DEV ImuPair load_imu_pair(int M, const double* stamps, const double* gyro, const double* accel) {
+  const int ia = 2 * threadIdx.x, ib = ia + 1;
+  ImuPair q;
+  q.ta = ia < M ? stamps[ia] : 0.0;
+  q.tb = ib < M ? stamps[ib] : 0.0;
+  q.tn = ib + 1 < M ? stamps[ib + 1] : 0.0;
+  for (int k = 0; k < 3; ++k) {
+    q.ga[k] = ia < M ? gyro[3 * ia + k] : 0.0;
+    q.aa[k] = ia < M ? accel[3 * ia + k] : 0.0;
+    q.gb[k] = ib < M ? gyro[3 * ib + k] : 0.0;
+    q.ab[k] = ib < M ? accel[3 * ib + k] : 0.0;
+  }
+  return q;
+}
+// Park / restore an ImuPair in 15 doubles of LDS (per thread), so it need not stay in registers.
+GC_DEV void imu_pair_store(const ImuPair& q, double* d) {
+  d[0] = q.ta; d[1] = q.tb; d[2] = q.tn;
+  for (int k = 0; k < 3; ++k) { d[3 + k] = q.ga[k]; d[6 + k] = q.gb[k]; d[9 + k] = q.aa[k]; d[12 + k] = q.ab[k]; }
+}
+GC_DEV ImuPair imu_pair_load(const double* d) {
+  ImuPair q;
+  q.ta = d[0]; q.tb = d[1]; q.tn = d[2];
+  for (int k = 0; k < 3; ++k) { q.ga[k] = d[3 + k]; q.gb[k] = d[6 + k]; q.aa[k] = d[9 + k]; q.ab[k] = d[12 + k]; }
+  return q;
+}
+GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const double* R0, const double* bg,
+                            const double* ba, const double* g, double* A, double* Bm, double* V1, double* V2,
+                            double* out) {
   const int t = threadIdx.x;
   const int ia = 2 * t, ib = 2 * t + 1;
-  auto stamp = [&](int i) { return i < M ? stamps[i] : 0.0; };
-  const double ta = stamp(ia), tb = stamp(ib);
+  const double ta = q.ta, tb = q.tb;
   // dt_i = max(t_{i+1} - t_i, 0), last slot 0 (imu_preintegration.py:84-85)
   const double dta = (ib < M) ? fmax(tb - ta, 0.0) : 0.0;
-  const double dtb = ib < M ? ((ib + 1 < M) ? fmax(stamp(ib + 1) - tb, 0.0) : 0.0) : 0.0;
+  const double dtb = ib < M ? ((ib + 1 < M) ? fmax(q.tn - tb, 0.0) : 0.0) : 0.0;
   const double dea = (ia < M ? wa : 0.0) * dta, deb = (ib < M ? wb : 0.0) * dtb;
-  double ga[3] = {0, 0, 0}, gb[3] = {0, 0, 0}, aa[3] = {0, 0, 0}, ab[3] = {0, 0, 0};
-  for (int k = 0; k < 3; ++k) {
-    if (ia < M) { ga[k] = gyro[3 * ia + k]; aa[k] = accel[3 * ia + k]; }
-    if (ib < M) { gb[k] = gyro[3 * ib + k]; ab[k] = accel[3 * ib + k]; }
-  }
+  const double *ga = q.ga, *gb = q.gb, *aa = q.aa, *ab = q.ab;
   double dRa[9], dRb[9], Pl[9];
   {
     double wv[3] = {(ga[0] - bg[0]) * dea, (ga[1] - bg[1]) * dea, (ga[2] - bg[2]) * dea};
