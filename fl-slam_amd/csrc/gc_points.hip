@@ -864,77 +864,85 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
     }
   };
   fetch(0);
-  for (int it = 0; it < iters; ++it) {
-    const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
-    {  // phase A
-      const int64_t j = wbase + lane;
-      const bool inr = j < n_cap;
-      double p[3] = {np[0], np[1], np[2]};
-      const double tt = ntt, ww = nww * scale;
-      if (it + 1 < iters) fetch(it + 1);
-      double q[3], d[3], f[NF];
-      deskew_point_series(p, (tt - t0) * inv_denom, xr, q);
-      const double wd = inr ? ww * window_weight2(tt, t0, t1, inv_sig, Tx) : 0.0;
-      direction_fast(q, o, 1e-12, d);
-      point_features(q, d, wd, f);
-      sumw += wd;
-#pragma unroll
-      for (int k = 0; k < NF; ++k) F[k * kFusedFS + lane] = f[k];
-      F[(NF + 0) * kFusedFS + lane] = d[0];
-      F[(NF + 1) * kFusedFS + lane] = d[1];
-      F[(NF + 2) * kFusedFS + lane] = d[2];
-      F[(NF + 3) * kFusedFS + lane] = inr ? 1.0 : 0.0;
+  // A chunk without padding points (all of it below n_cap: every chunk but the last) runs with
+  // the valid flag folded to 1.0 — the masking multiplies vanish (x·1 = x, fma(Z−1, 1, 1) = Z
+  // exactly), bit-identical to the masked form
+  auto run_iters = [&](auto pad_tag) {
+    constexpr bool PAD = decltype(pad_tag)::value;
+    for (int it = 0; it < iters; ++it) {
+      const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
+      {  // phase A
+        const int64_t j = wbase + lane;
+        const bool inr = j < n_cap;
+        double p[3] = {np[0], np[1], np[2]};
+        const double tt = ntt, ww = nww * scale;
+        if (it + 1 < iters) fetch(it + 1);
+        double q[3], d[3], f[NF];
+        deskew_point_series(p, (tt - t0) * inv_denom, xr, q);
+        const double wd = inr ? ww * window_weight2(tt, t0, t1, inv_sig, Tx) : 0.0;
+        direction_fast(q, o, 1e-12, d);
+        point_features(q, d, wd, f);
+        sumw += wd;
+  #pragma unroll
+        for (int k = 0; k < NF; ++k) F[k * kFusedFS + lane] = f[k];
+        F[(NF + 0) * kFusedFS + lane] = d[0];
+        F[(NF + 1) * kFusedFS + lane] = d[1];
+        F[(NF + 2) * kFusedFS + lane] = d[2];
+        F[(NF + 3) * kFusedFS + lane] = inr ? 1.0 : 0.0;
+      }
+      lds_wave_sync();
+      double zst = 1.0;
+  #pragma unroll 2
+      for (int s = 0; s < 16; ++s) {
+        const int pl = s * 4 + g;
+        const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
+        const double vf = PAD ? F[(NF + 3) * kFusedFS + pl] : 1.0;  // 1 for a point of the chunk, 0 for padding
+        const double fb = F[bl * kFusedFS + pl];  // MFMA B operand: feature bl of point 4s + g
+        double e[BPL], x[BPL], ex[BPL];
+  #pragma unroll
+        for (int j = 0; j < BPL; ++j) {
+          const int b = bl + 16 * j;  // Lb is zero past B: y = -ymax stays in range, then masked
+          x[j] = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -ymax)));
+        }
+        exp2s_n<BPL>(x, Tx, ex);
+  #pragma unroll
+        for (int j = 0; j < BPL; ++j) e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
+        double zl = e[0], sl = e[0] * x[0];
+  #pragma unroll
+        for (int j = 1; j < BPL; ++j) {
+          zl += e[j];
+          sl = fma(e[j], x[j], sl);
+        }
+        const double Z = group16_sum(zl);
+        const double rZ = recip(Z);
+        double r[BPL];
+  #pragma unroll
+        for (int j = 0; j < BPL; ++j) r[j] = e[j] * rZ;
+        double rm = r[0];  // max responsibility: max(e) rZ == max(e rZ) exactly (monotone rounding)
+  #pragma unroll
+        for (int j = 1; j < BPL; ++j) rm = fmax(rm, r[j]);
+        // padding points (vf = 0) add nothing: S/Z scaled by 0, r >= 0 scaled to 0 under the max,
+        // and log Z replaced by log 1
+        entq = fma(sl * vf, rZ, entq);  // lane partials of S/Z (in y units), summed over lanes at the end
+        mxr = fmax(mxr, rm * vf);
+        if (bl == s) zst = fma(Z - 1.0, vf, 1.0);
+  #pragma unroll
+        for (int j = 0; j < BPL; ++j)
+          acc4[s % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[j], fb, acc4[s % NACC][j], 0, 0, 0);
+  #pragma unroll
+        for (int t = 0; t < NX; ++t) {
+          const double fk = F[(16 + t) * kFusedFS + pl];
+  #pragma unroll
+          for (int j = 0; j < BPL; ++j) accx[j][t] = fma(r[j], fk, accx[j][t]);
+        }
+      }
+      // each lane stashed the Z of one point per 16 steps: one log per lane per iteration
+      logacc += log(zst);
+      lds_wave_sync();
     }
-    lds_wave_sync();
-    double zst = 1.0;
-#pragma unroll 2
-    for (int s = 0; s < 16; ++s) {
-      const int pl = s * 4 + g;
-      const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
-      const double vf = F[(NF + 3) * kFusedFS + pl];  // 1 for a point of the chunk, 0 for padding
-      const double fb = F[bl * kFusedFS + pl];  // MFMA B operand: feature bl of point 4s + g
-      double e[BPL], x[BPL], ex[BPL];
-#pragma unroll
-      for (int j = 0; j < BPL; ++j) {
-        const int b = bl + 16 * j;  // Lb is zero past B: y = -ymax stays in range, then masked
-        x[j] = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -ymax)));
-      }
-      exp2s_n<BPL>(x, Tx, ex);
-#pragma unroll
-      for (int j = 0; j < BPL; ++j) e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
-      double zl = e[0], sl = e[0] * x[0];
-#pragma unroll
-      for (int j = 1; j < BPL; ++j) {
-        zl += e[j];
-        sl = fma(e[j], x[j], sl);
-      }
-      const double Z = group16_sum(zl);
-      const double rZ = recip(Z);
-      double r[BPL];
-#pragma unroll
-      for (int j = 0; j < BPL; ++j) r[j] = e[j] * rZ;
-      double rm = r[0];  // max responsibility: max(e) rZ == max(e rZ) exactly (monotone rounding)
-#pragma unroll
-      for (int j = 1; j < BPL; ++j) rm = fmax(rm, r[j]);
-      // padding points (vf = 0) add nothing: S/Z scaled by 0, r >= 0 scaled to 0 under the max,
-      // and log Z replaced by log 1
-      entq = fma(sl * vf, rZ, entq);  // lane partials of S/Z (in y units), summed over lanes at the end
-      mxr = fmax(mxr, rm * vf);
-      if (bl == s) zst = fma(Z - 1.0, vf, 1.0);
-#pragma unroll
-      for (int j = 0; j < BPL; ++j)
-        acc4[s % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[j], fb, acc4[s % NACC][j], 0, 0, 0);
-#pragma unroll
-      for (int t = 0; t < NX; ++t) {
-        const double fk = F[(16 + t) * kFusedFS + pl];
-#pragma unroll
-        for (int j = 0; j < BPL; ++j) accx[j][t] = fma(r[j], fk, accx[j][t]);
-      }
-    }
-    // each lane stashed the Z of one point per 16 steps: one log per lane per iteration
-    logacc += log(zst);
-    lds_wave_sync();
-  }
+  };
+  if (chunk0 + (int64_t)iters * 256 <= n_cap) run_iters(std::false_type{});
+  else run_iters(std::true_type{});
   // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
   int64_t npts = n_cap - chunk0;
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);

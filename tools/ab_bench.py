@@ -1,0 +1,15 @@
+"""Dev helper: run bench.py's main against another build of the library (A/B on one box).
+Usage: python3 tools/ab_bench.py <path/to/libgcslam.so> [bench args]"""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
+sys.path.insert(0, ROOT)
+from gcslam import _abi  # noqa: E402
+
+_abi.LIB_PATH = os.path.abspath(sys.argv[1])
+sys.argv = ["bench.py"] + sys.argv[2:]
+import bench  # noqa: E402
+
+bench.main()
