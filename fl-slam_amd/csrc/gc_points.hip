@@ -132,6 +132,12 @@ GC_DEV void exp_neg_n(const double (&x)[N], const double* T, double (&out)[N]) {
     out[j] = ldexp(tv[j] * p, ki[j] >> 8);
   }
 }
+// 1/z for z > 0 in a normal range, one Newton step on the hardware reciprocal (a few ulp; the
+// fused kernel's softmax normaliser, where it is one of ~140 issue slots per step)
+GC_DEV double recip1(double z) {
+  const double r = __builtin_amdgcn_rcp(z);
+  return fma(r, fma(-z, r, 1.0), r);
+}
 // 1/z for z > 0 in a normal range: hardware reciprocal + two Newton steps (<= 1 ulp).
 GC_DEV double recip(double z) {
   double r = __builtin_amdgcn_rcp(z);
@@ -907,14 +913,11 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
         exp2s_n<BPL>(x, Tx, ex);
   #pragma unroll
         for (int j = 0; j < BPL; ++j) e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
-        double zl = e[0], sl = e[0] * x[0];
+        double zl = e[0];
   #pragma unroll
-        for (int j = 1; j < BPL; ++j) {
-          zl += e[j];
-          sl = fma(e[j], x[j], sl);
-        }
+        for (int j = 1; j < BPL; ++j) zl += e[j];
         const double Z = group16_sum(zl);
-        const double rZ = recip(Z);
+        const double rZ = recip1(Z);
         double r[BPL];
   #pragma unroll
         for (int j = 0; j < BPL; ++j) r[j] = e[j] * rZ;
@@ -923,7 +926,9 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
         for (int j = 1; j < BPL; ++j) rm = fmax(rm, r[j]);
         // padding points (vf = 0) add nothing: S/Z scaled by 0, r >= 0 scaled to 0 under the max,
         // and log Z replaced by log 1
-        entq = fma(sl * vf, rZ, entq);  // lane partials of S/Z (in y units), summed over lanes at the end
+  #pragma unroll
+        for (int j = 0; j < BPL; ++j)  // lane partials of Σ R·x (in y units), summed over lanes at the end
+          entq = fma(r[j] * vf, x[j], entq);
         mxr = fmax(mxr, rm * vf);
         if (bl == s) zst = fma(Z - 1.0, vf, 1.0);
   #pragma unroll
