@@ -930,7 +930,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
         for (int j = 0; j < BPL; ++j)  // lane partials of Σ R·x (in y units), summed over lanes at the end
           entq = fma(r[j] * vf, x[j], entq);
         mxr = fmax(mxr, rm * vf);
-        if (bl == s) zst = fma(Z - 1.0, vf, 1.0);
+        zst *= PAD ? fma(Z - 1.0, vf, 1.0) : Z;  // Π Z of the group's 16 points (<= 48^16)
   #pragma unroll
         for (int j = 0; j < BPL; ++j)
           acc4[s % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[j], fb, acc4[s % NACC][j], 0, 0, 0);
@@ -941,7 +941,8 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
           for (int j = 0; j < BPL; ++j) accx[j][t] = fma(r[j], fk, accx[j][t]);
         }
       }
-      // each lane stashed the Z of one point per 16 steps: one log per lane per iteration
+      // the 16 lanes of a point group hold the same product: one log per lane per iteration, and
+      // only bin-lane 0 of each group contributes it below
       logacc += log(zst);
       lds_wave_sync();
     }
@@ -951,7 +952,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
   int64_t npts = n_cap - chunk0;
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
-  const double ent = logacc - entq * kExp2C1 - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
+  const double ent = (bl == 0 ? logacc : 0.0) - entq * kExp2C1 - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
   const int RL = B * NF + REC_EXTRA;
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
