@@ -300,15 +300,18 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
 // grid: ceil(P_len / 64) blocks x 256 threads; block covers 64 record entries, its 4 waves sum
 // interleaved hypothesis subsets, combined in fixed order (deterministic).
 __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
-  __shared__ double part[4][64];
+  // 16 record entries per workgroup x 16 hypothesis groups (hypotheses g, g+16, ...): at H = 256 a
+  // thread's 16 hypotheses are one batch of loads in flight; the 16 group partials are then
+  // summed in a fixed tree
+  __shared__ double part[16][16];
   __shared__ double red[8];
-  const int t = threadIdx.x, lane = t & 63, g = t >> 6;
+  const int t = threadIdx.x, lane = t & 15, g = t >> 4;
   const int n = kDZ, Hl = P.Hl;
   // floored / renormalised weights over ALL hypotheses (hypothesis.py:77-82), replicated
   double loc = 0.0;
   for (int k = t; k < P.H; k += kWG) loc += fmax(P.weights[k], P.weight_floor);
   const double wsum = wg_sum(loc, red);
-  const int e = blockIdx.x * 64 + lane;
+  const int e = blockIdx.x * 16 + lane;
   const int PLn = partial_len(P.B);
   // this lane's record entry as (source row, stride, weight kind), resolved once; the hypothesis
   // loop is then branch-free (clamped rows, 0/1 masks) with 16 independent loads in flight
@@ -328,11 +331,11 @@ __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
   else live = 0.0;
   const double inv_wsum = 1.0 / wsum;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = g; k0 < Hl; k0 += 64) {
+  for (int k0 = g; k0 < Hl; k0 += 256) {
     double v[16], wr[16], m[16];
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
-      const int k = k0 + 4 * j;
+      const int k = k0 + 16 * j;
       const int kc = k < Hl ? k : Hl - 1;
       m[j] = k < Hl ? live : 0.0;
       wr[j] = W[kc];
@@ -347,7 +350,11 @@ __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
   part[g][lane] = (acc[0] + acc[1]) + (acc[2] + acc[3]);
   __syncthreads();
   if (g == 0 && e < PLn) {
-    double r = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
+    double q[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+      q[a] = (part[4 * a][lane] + part[4 * a + 1][lane]) + (part[4 * a + 2][lane] + part[4 * a + 3][lane]);
+    double r = (q[0] + q[1]) + (q[2] + q[3]);
     if (e >= kPX0 && e < kPX0 + 6) r = (P.h_begin == 0) ? P.X[e - kPX0] : 0.0;
     else if (e == kPSTAMP0) r = (P.h_begin == 0) ? P.stamp[0] : 0.0;
     else if (e >= kPMAP) r = (P.h_begin == 0) ? P.map_inc[e - kPMAP] : 0.0;
@@ -504,7 +511,7 @@ hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) 
   return hipGetLastError();
 }
 hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
-  hipLaunchKernelGGL(k_combine_local, dim3((partial_len(P.B) + 63) / 64), dim3(256), 0, st, P);
+  hipLaunchKernelGGL(k_combine_local, dim3((partial_len(P.B) + 15) / 16), dim3(256), 0, st, P);
   return hipGetLastError();
 }
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
