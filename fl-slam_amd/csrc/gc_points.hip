@@ -181,6 +181,27 @@ GC_DEV void exp2s_n(const double (&y)[N], const double* T, double (&out)[N]) {
     out[j] = t * p;
   }
 }
+// exp2s_n of y - m for an integer-valued shift m (Mp = kRoundMagic - m): ks = y + Mp rounds to
+// Mp + rint(y), so r = y - (ks - Mp) = y - rint(y) exactly and lo(ks) = rint(y) - m. The shift rides
+// in the rounding constant, so the fused logit needs no "- ymax" term of its own.
+template <int N>
+GC_DEV void exp2s_shift_n(const double (&y)[N], double Mp, const double* T, double (&out)[N]) {
+  double r[N], tv[N];
+  int ki[N];
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double ks = y[j] + Mp;
+    ki[j] = __double2loint(ks);
+    r[j] = y[j] - (ks - Mp);
+    tv[j] = T[ki[j] & (kExpTab2 - 1)];
+  }
+#pragma unroll
+  for (int j = 0; j < N; ++j) {
+    const double p = fma(fma(fma(kExp2C3, r[j], kExp2C2), r[j], kExp2C1), r[j], 1.0);
+    const double t = __hiloint2double(__double2hiint(tv[j]) + (ki[j] << 9), __double2loint(tv[j]));
+    out[j] = t * p;
+  }
+}
 // σ(x) = 1 / (1 + e^{-x}) on the 2048 table (e^{-|x|} clamped at e^{-700} ~ 1e-304)
 GC_DEV double sigmoid2(double x, const double* T) {
   const double y[1] = {fmax(-fabs(x), -700.0) * kTab2OverLn2};
@@ -853,7 +874,10 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
     for (int t = 0; t < NX; ++t) accx[j][t] = 0.0;
   }
   double sumw = 0.0, logacc = 0.0, entq = 0.0, mxr = 0.0;
-  const double ymax = ysc;  // S <= 1 for unit vectors: y = (S - 1) 2048/(τ ln2) <= 0
+  // S <= 1 for unit vectors: the exp argument y - ymax = (S·ysc - ymax) <= 0 with an integer ymax
+  // >= ysc (the shift cancels in R and is added back to the entropy below)
+  const double ymax = ceil(ysc);
+  const double Mp = kRoundMagic - ymax;
   const double Beps = (double)B * 1e-12;
   const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
   // raw point of the next iteration, loaded one iteration ahead (its HBM latency hides behind
@@ -908,9 +932,9 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   #pragma unroll
         for (int j = 0; j < BPL; ++j) {
           const int b = bl + 16 * j;  // Lb is zero past B: y = -ymax stays in range, then masked
-          x[j] = fma(d0, Lb[b], fma(d1, Lb[64 + b], fma(d2, Lb[128 + b], -ymax)));
+          x[j] = fma(d0, Lb[b], fma(d1, Lb[64 + b], d2 * Lb[128 + b]));
         }
-        exp2s_n<BPL>(x, Tx, ex);
+        exp2s_shift_n<BPL>(x, Mp, Tx, ex);
   #pragma unroll
         for (int j = 0; j < BPL; ++j) e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
         double zl = e[0];
@@ -952,7 +976,9 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
   int64_t npts = n_cap - chunk0;
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
-  const double ent = (bl == 0 ? logacc : 0.0) - entq * kExp2C1 - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
+  // Σ log Z' (shifted by ymax) - Σ R y + ymax per valid point - B ε per point (lane 0 of each wave)
+  const double ent = (bl == 0 ? logacc : 0.0) - entq * kExp2C1 +
+                     ((lane == 0) ? (ymax * kExp2C1 - Beps) * (double)npts * 0.25 : 0.0);
   const int RL = B * NF + REC_EXTRA;
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
