@@ -922,7 +922,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
       }
       lds_wave_sync();
       double zst = 1.0;
-  #pragma unroll 4
+  #pragma unroll 8
       for (int s = 0; s < 16; ++s) {
         const int pl = s * 4 + g;
         const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
