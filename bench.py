@@ -100,7 +100,7 @@ def warmup_map_record(ctx, _abi, scan, n, B, bins, origin):
     # a wide deskew window (t0 - 1000 s .. t1 + 1000 s) weights every point by the same ~0.987
     _abi.call("gc_scan_bins_fused", ctx.handle, 1, n, n, B, d["points"].ptr, d["timestamps"].ptr, d["weights"].ptr,
               scal.ptr, scan["scan_start"] - 1e3, scan["scan_end"] + 1e3, xi.ptr, db.ptr, GC_TAU_SOFT_ASSIGN, op,
-              1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
+              1e-12, 1e-12, st.ptr, ce.ptr, 0, ctx=ctx)
     s = st.download()[0]
     N, pb, Sp = s[:, 0], s[:, 13:16], s[:, 16:25].reshape(B, 3, 3)
     from gcslam.pipeline import map_record

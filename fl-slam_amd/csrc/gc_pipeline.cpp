@@ -81,6 +81,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   GC_CHECK_ARG(ctx, dims->M >= 2 && dims->M <= 512, "IMU slots M must be in [2, 512]");
   GC_CHECK_ARG(ctx, dims->n_in_max > 0 && dims->n_cap > 0, "point counts must be positive");
   GC_CHECK_ARG(ctx, dims->world_size >= 1 && dims->rank >= 0 && dims->rank < dims->world_size, "bad rank");
+  GC_CHECK_ARG(ctx, cfg[GC_PCFG_TAU] >= GC_FUSED_TAU_MIN, "tau must be >= GC_FUSED_TAU_MIN (3e-3)");
   GC_HIP(ctx, hipSetDevice(ctx->device));
   gc_pipeline* p = new gc_pipeline();
   p->ctx = ctx;
@@ -369,7 +370,7 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
   // a1 -> a4 -> a5 -> a6 fused over all local hypotheses
   const double origin[3] = {P.o0, P.o1, P.o2};
   GC_TRY(gc_scan_bins_fused(ctx, P.Hl, s.n_in, P.n_cap, P.B, s.pts, s.t, s.w, P.budget, scan_start, scan_end,
-                            P.xi, P.bins, P.tau, origin, P.eps_psd, P.eps_mass, P.stats, P.bincert));
+                            P.xi, P.bins, P.tau, origin, P.eps_psd, P.eps_mass, P.stats, P.bincert, 0));
   if (io) GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, p->ev_io, 0));
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
@@ -394,6 +395,15 @@ int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag) {
 int32_t gc_pipeline_get_lpose6(gc_pipeline* p, double* h_lpose) {
   GC_CHECK_ARG(nullptr, p && h_lpose, "NULL argument");
   return down(p, h_lpose, p->P.lpose, (size_t)p->P.Hl * 36);
+}
+
+int32_t gc_pipeline_get_hyp_stats(gc_pipeline* p, double* h_dPsi_proc, double* h_dPsi_meas, double* h_Sigma) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const size_t Hl = p->P.Hl;
+  GC_TRY(down(p, h_dPsi_proc, p->P.dPsiP, Hl * 252));
+  GC_TRY(down(p, h_dPsi_meas, p->P.dPsiM, Hl * 27));
+  GC_CHECK_ARG(p->ctx, h_Sigma == nullptr || p->sig_cached, "no scan has run since the beliefs were set");
+  return down(p, h_Sigma, p->P.Sig, Hl * 484);
 }
 
 int32_t gc_pipeline_get_bin_stats(gc_pipeline* p, double* h_stats, double* h_cert, double* h_xi) {

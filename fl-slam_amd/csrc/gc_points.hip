@@ -455,8 +455,15 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
   typedef double dvec2 __attribute__((ext_vector_type(2)));
   __shared__ double red[8];
   __shared__ double Tx[kExpTab];
+  __shared__ double Lb[3 * 64];  // bin directions, x / y / z rows of 64 (zero past B)
   __shared__ __attribute__((aligned(16))) double Sl[4][64 * RS];
   exp_table_init(Tx);
+  if (threadIdx.x < 64) {
+    const int b = threadIdx.x;
+    Lb[b] = b < B ? bins[3 * b] : 0.0;
+    Lb[64 + b] = b < B ? bins[3 * b + 1] : 0.0;
+    Lb[128 + b] = b < B ? bins[3 * b + 2] : 0.0;
+  }
   __syncthreads();
   const int h = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -490,26 +497,29 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
     GC_LOAD_DIRS(wbase + 256)
     const int64_t pt = wbase + lane;
     const bool valid = pt < n;
-    // bin directions: wave-uniform scalar loads (constant address space), re-issued every
-    // iteration rather than hoisted into 288 registers
-    const __attribute__((address_space(4))) double* bp = (const __attribute__((address_space(4))) double*)bins;
-    asm volatile("" : "+s"(bp));
-    double ex[NB];
-    double best = -1e308, Z = 0.0, sl = 0.0;
+    // pass 1: the row maximum of the exact un-fused similarities and the integer bin index; pass 2
+    // recomputes each similarity (bit-identical) and exponentiates x = (S - S_max)/τ, the
+    // reference's jax.nn.softmax shift (binning.py:68-69): any τ > 0 and any direction norm. The
+    // bin directions are wave-uniform LDS reads (broadcast, no bank conflicts).
+    double best = -1e308;
     int bidx = 0;
+#pragma unroll 8
+    for (int j = 0; j < (FULL ? NB : B); ++j) {
+      const double s = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
+      if (s > best) { best = s; bidx = j; }
+    }
+    double ex[NB];
+    double Z = 0.0, sl = 0.0;
 #pragma unroll
     for (int j0 = 0; j0 < NB; j0 += 8) {
-      asm volatile("" : "+s"(bp));  // this group's scalar loads are issued here, not all up front
       double x[8];
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int j = j0 + jj;
-        const bool ok = FULL || j < B;  // wave-uniform
-        const double s = ok ? sim_nofma(d0, d1, d2, bp[3 * j], bp[3 * j + 1], bp[3 * j + 2]) : -4.0;
-        if (s > best) { best = s; bidx = j; }
-        x[jj] = fma(s, inv_tau, -inv_tau);
+        const double s = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
+        // e^-745 underflows to 0 in f64; the clamp keeps the table index in range for tiny τ
+        x[jj] = (FULL || j < B) ? fmax((s - best) * inv_tau, -1000.0) : 0.0;
       }
-      asm volatile("" : "+v"(best), "+v"(bidx));  // keep the argmax chain per group (no 48 live S)
       double e8[8];
       exp_neg_n<8, false>(x, Tx, e8);
 #pragma unroll
@@ -521,14 +531,9 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
       }
       asm volatile("" : "+v"(Z), "+v"(sl));  // accumulate now: the x of a group die here
     }
+    // the maximal bin has x = 0 and e = 1 exactly: Z >= 1 and max_b R = 1/Z
     const double rZ = recip(Z);
-    double eb;
-    {
-      const double xb[1] = {fma(best, inv_tau, -inv_tau)};
-      double o1[1];
-      exp_neg_n<1, false>(xb, Tx, o1);  // = ex[bidx] bit for bit (same argument, same evaluation)
-      eb = o1[0];
-    }
+    const double eb = 1.0;
     if (valid) {
       // entropy of the point: log Z - S/Z - B ε   (-Σ R log(R+ε) up to ≤ B·ε)
       int e;
@@ -873,7 +878,12 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
 #pragma unroll
     for (int t = 0; t < NX; ++t) accx[j][t] = 0.0;
   }
-  double sumw = 0.0, logacc = 0.0, entq = 0.0, mxr = 0.0;
+  double sumw = 0.0, entq = 0.0, mxr = 0.0;
+  // Π Z of the lane's point group over the whole chunk as mantissa x 2^zex: renormalised every 8
+  // points (Z >= e^{(S_max - 1)/τ} per point, so 8 factors stay normal for every τ the exp table
+  // admits unless a direction lies almost opposite every bin), one log at the end
+  double zst = 1.0;
+  int zex = 0;
   // S <= 1 for unit vectors: the exp argument y - ymax = (S·ysc - ymax) <= 0 with an integer ymax
   // >= ysc (the shift cancels in R and is added back to the entropy below)
   const double ymax = ceil(ysc);
@@ -921,9 +931,9 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
         F[(NF + 3) * kFusedFS + lane] = inr ? 1.0 : 0.0;
       }
       lds_wave_sync();
-      double zst = 1.0;
-  #pragma unroll 8
-      for (int s = 0; s < 16; ++s) {
+      for (int s8 = 0; s8 < 16; s8 += 8) {
+  #pragma unroll
+      for (int s = s8; s < s8 + 8; ++s) {
         const int pl = s * 4 + g;
         const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
         const double vf = PAD ? F[(NF + 3) * kFusedFS + pl] : 1.0;  // 1 for a point of the chunk, 0 for padding
@@ -954,7 +964,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
         for (int j = 0; j < BPL; ++j)  // lane partials of Σ R·x (in y units), summed over lanes at the end
           entq = fma(r[j] * vf, x[j], entq);
         mxr = fmax(mxr, rm * vf);
-        zst *= PAD ? fma(Z - 1.0, vf, 1.0) : Z;  // Π Z of the group's 16 points (<= 48^16)
+        zst *= PAD ? fma(Z - 1.0, vf, 1.0) : Z;  // Π Z of the group's points (<= 48^8 per renormalisation)
   #pragma unroll
         for (int j = 0; j < BPL; ++j)
           acc4[s % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[j], fb, acc4[s % NACC][j], 0, 0, 0);
@@ -965,9 +975,10 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
           for (int j = 0; j < BPL; ++j) accx[j][t] = fma(r[j], fk, accx[j][t]);
         }
       }
-      // the 16 lanes of a point group hold the same product: one log per lane per iteration, and
-      // only bin-lane 0 of each group contributes it below
-      logacc += log(zst);
+        int e8;
+        zst = frexp(zst, &e8);
+        zex += e8;
+      }
       lds_wave_sync();
     }
   };
@@ -976,7 +987,10 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
   int64_t npts = n_cap - chunk0;
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
-  // Σ log Z' (shifted by ymax) - Σ R y + ymax per valid point - B ε per point (lane 0 of each wave)
+  // the 16 lanes of a point group hold the same product: only bin-lane 0 of each group contributes
+  // its log. Σ log Z' (shifted by ymax) - Σ R y + ymax per valid point - B ε per point (lane 0 of
+  // each wave)
+  const double logacc = log(zst) + (double)zex * 0.69314718055994530942;
   const double ent = (bl == 0 ? logacc : 0.0) - entq * kExp2C1 +
                      ((lane == 0) ? (ymax * kExp2C1 - Beps) * (double)npts * 0.25 : 0.0);
   const int RL = B * NF + REC_EXTRA;
@@ -985,173 +999,6 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
     if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
   write_partial_record_mfma<BPL, NX>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds,
                                      partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
-}
-
-// Lane-per-point fused kernel (the product path). Phase A as in k_bins_fused (lane = point:
-// budget gather, deskew, direction, 19 features). Phase B keeps the whole softmax of a point in
-// its lane: the 16*BPL similarities against the 1/τ-prescaled bins (wave-uniform scalar loads),
-// exps (LDS table), Z, the entropy partial and the max responsibility are lane-local, so there
-// is no cross-lane butterfly and one reciprocal per point instead of one per 4-point step. The
-// features are pre-multiplied by 1/Z (Σ_p e_pb (F_pk / Z_p) = Σ_p R_pb F_pk, rounding order
-// only), so the MFMA A operand is the raw e. The point's e row is transposed through a
-// wave-private LDS slab (row stride NB + 2: conflict-free ds_write_b128 rows and ds_read_b64
-// columns) and consumed by 16 steps of BPL v_mfma_f64_16x16x4_f64 (features 0..15) plus VALU
-// FMAs (16..18), 2*BPL independent accumulation chains. f64 MFMA and f64 VALU share the DP
-// pipe on gfx950 (tools/probe/probe_rates.hip), so the kernel is bound by issued DP
-// instructions; this layout issues ~1/3 fewer than k_bins_fused. The e row (2 NB VGPRs) and the
-// full slab (36 KB per wave) size it for one wave per SIMD (up to 512 VGPR+AGPR); the next
-// iteration's point loads are issued before the softmax to cover their latency.
-#ifndef GC_LP_OCC
-#define GC_LP_OCC 1
-#endif
-template <int BPL>
-constexpr int lp_es() { return 16 * BPL + 2; }
-template <int BPL, bool FULL>
-__global__ void __launch_bounds__(256, GC_LP_OCC) k_bins_fused_lp(int64_t n_cap, int B, int iters,
-                                                          const double* __restrict__ pts_raw,
-                                                          const double* __restrict__ t_raw,
-                                                          const double* __restrict__ w_raw,
-                                                          const double* __restrict__ bscal, double t0, double t1,
-                                                          const double* __restrict__ xi,
-                                                          const double* __restrict__ bins_scaled, double inv_tau,
-                                                          double o0, double o1, double o2, double* partials) {
-  constexpr int NF = NF_BASE;
-  constexpr int NX = NF - 16;  // features on the VALU
-  constexpr int NB = 16 * BPL;
-  constexpr int ES = lp_es<BPL>();
-  typedef double dvec2 __attribute__((ext_vector_type(2)));
-  extern __shared__ double lds[];
-  const int h = blockIdx.y;
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int g = lane >> 4, bl = lane & 15;
-  double* F = lds + wv * (NF * kFusedFS);                    // [feature][point] x 1/Z
-  double* E = lds + 4 * NF * kFusedFS + wv * (64 * ES);       // [point][bin]
-  double* Tx = lds + 4 * NF * kFusedFS + 4 * 64 * ES;         // exp table
-  const double o[3] = {o0, o1, o2};
-  double xr[6];
-#pragma unroll
-  for (int k = 0; k < 6; ++k) xr[k] = xi[6 * h + k];
-  const double scale = bscal[2];
-  const int64_t n_sel = (int64_t)bscal[5];
-  const int64_t stride = (int64_t)bscal[6];
-  const double denom = fmax(t1 - t0, 1e-12);
-  const double inv_denom = 1.0 / denom;
-  const double inv_sig = 1.0 / fmax(0.1 * denom, 1e-6);
-  exp_table_init(Tx);
-  __syncthreads();
-  v4d acc4[2][BPL];  // even / odd steps
-  double accx[BPL][NX];
-#pragma unroll
-  for (int jt = 0; jt < BPL; ++jt) {
-    acc4[0][jt] = v4d{0.0, 0.0, 0.0, 0.0};
-    acc4[1][jt] = v4d{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-    for (int t = 0; t < NX; ++t) accx[jt][t] = 0.0;
-  }
-  double sumw = 0.0, logacc = 0.0, entq = 0.0, mxr = 0.0;
-  const double xmax = inv_tau;  // S <= 1 for unit vectors: exp never overflows
-  const double Beps = (double)B * 1e-12;
-  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
-  // raw point of this lane for iteration `it` (clamped, branch-free; selection applied after)
-  double np0, np1, np2, nt, nw;
-  auto load_raw = [&](int it) {
-    const int64_t j = chunk0 + (int64_t)it * 256 + wv * 64 + lane;
-    const int64_t jj = j < n_sel ? j : (n_sel > 0 ? n_sel - 1 : 0);
-    const int64_t i = jj * stride;
-    np0 = pts_raw[3 * i]; np1 = pts_raw[3 * i + 1]; np2 = pts_raw[3 * i + 2];
-    nt = t_raw[i];
-    nw = w_raw[i];
-  };
-  load_raw(0);
-  for (int it = 0; it < iters; ++it) {
-    const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
-    // ---- phase A: lane = point
-    const int64_t j = wbase + lane;
-    const bool inr = j < n_cap;
-    const bool sel = inr && j < n_sel;
-    double p[3] = {sel ? np0 : 0.0, sel ? np1 : 0.0, sel ? np2 : 0.0};
-    const double tt = sel ? nt : 0.0, ww = sel ? nw * scale : 0.0;
-    if (it + 1 < iters) load_raw(it + 1);  // in flight across this iteration's softmax
-    double q[3], d[3];
-    deskew_point_fast(p, (tt - t0) * inv_denom, xr, q);
-    const double wd = inr ? ww * window_weight_fast(tt, t0, t1, inv_sig, Tx) : 0.0;
-    direction_fast(q, o, 1e-12, d);
-    sumw += wd;
-    lds_wave_sync();  // the previous iteration's operand reads are done
-    {  // features parked in the lane's own slab column until 1/Z is known
-      double f[NF];
-      point_features(q, d, wd, f);
-#pragma unroll
-      for (int k = 0; k < NF; ++k) F[k * kFusedFS + lane] = f[k];
-    }
-    // ---- phase B: the point's softmax, lane-local
-    const __attribute__((address_space(4))) double* bp = (const __attribute__((address_space(4))) double*)bins_scaled;
-    double e[NB];
-    double Z = 0.0, sl = 0.0, em = 0.0;
-#pragma unroll
-    for (int j0 = 0; j0 < NB; j0 += 8) {
-      asm volatile("" : "+s"(bp));  // this group's scalar loads are issued here, not all up front
-      double x[8], e8[8];
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int b = j0 + jj;  // bins past B are zero: x = -1/τ stays finite, then masked
-        x[jj] = fma(d[0], bp[3 * b], fma(d[1], bp[3 * b + 1], fma(d[2], bp[3 * b + 2], -xmax)));
-      }
-      exp_neg_n<8>(x, Tx, e8);
-#pragma unroll
-      for (int jj = 0; jj < 8; ++jj) {
-        const int b = j0 + jj;
-        e[b] = (FULL || b < B) ? e8[jj] : 0.0;
-        Z += e[b];
-        sl = fma(e[b], x[jj], sl);
-        em = e[b] > em ? e[b] : em;
-      }
-    }
-#pragma unroll
-    for (int qd = 0; qd < NB / 2; ++qd)
-      *reinterpret_cast<dvec2*>(&E[lane * ES + 2 * qd]) = dvec2{e[2 * qd], e[2 * qd + 1]};
-    const double rZ = recip(Z);
-    if (inr) {
-      logacc += log(Z);
-      entq = fma(sl, rZ, entq);
-      const double mr = em * rZ;
-      mxr = mr > mxr ? mr : mxr;
-    }
-#pragma unroll
-    for (int k = 0; k < NF; ++k) F[k * kFusedFS + lane] *= rZ;  // own column: no cross-lane hazard
-    lds_wave_sync();
-#pragma unroll 2
-    for (int s = 0; s < 16; ++s) {
-      const int pl = s * 4 + g;
-      const double fb = F[bl * kFusedFS + pl];  // B: feature bl of point 4s + g
-      double fk[NX];
-#pragma unroll
-      for (int t = 0; t < NX; ++t) fk[t] = F[(16 + t) * kFusedFS + pl];
-#pragma unroll
-      for (int jt = 0; jt < BPL; ++jt) {
-        const double a = E[pl * ES + 16 * jt + bl];  // A: e of bin 16 jt + bl, point 4s + g
-        acc4[s & 1][jt] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb, acc4[s & 1][jt], 0, 0, 0);
-#pragma unroll
-        for (int t = 0; t < NX; ++t) accx[jt][t] = fma(a, fk[t], accx[jt][t]);
-      }
-    }
-  }
-  // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
-  int64_t npts = n_cap - chunk0;
-  npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
-  const double ent = logacc - entq - ((lane == 0) ? Beps * (double)npts * 0.25 : 0.0);
-  const int RL = B * NF + REC_EXTRA;
-#pragma unroll
-  for (int jt = 0; jt < BPL; ++jt) acc4[0][jt] += acc4[1][jt];
-  __syncthreads();
-  write_partial_record_mfma<BPL, NX>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds,
-                                     partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
-}
-
-// bins / τ, zero-padded to 16 * BPL rows (the lane-per-point kernel's scalar-load operand)
-__global__ void k_scale_bins(int B, int NB, const double* __restrict__ bins, double inv_tau, double* out) {
-  const int i = threadIdx.x;
-  if (i < 3 * NB) out[i] = (i < 3 * B) ? bins[i] * inv_tau : 0.0;
 }
 
 // ================================================================ finalize (a6 + certs)
@@ -1296,6 +1143,67 @@ __global__ void __launch_bounds__(256) k_psd_wg(int d, const double* __restrict_
   wg_psd_project(Ml, Mp, eps, d, scr, red, c6);
   for (int k = threadIdx.x; k < d * d; k += kWG) Mo[(int64_t)i * d * d + k] = Mp[k];
   if (threadIdx.x < 6) cert[6 * i + threadIdx.x] = c6[threadIdx.x];
+}
+
+// domain_projection_psd_core (primitives.py:80-123) for any d (the per-operator drop-in; the
+// pipeline uses the fixed-size forms above). An odd d is padded to even dp with a zero row and
+// column: every Jacobi rotation touching the pad has a_pq = 0, so it is the identity, the pad stays
+// decoupled with eigenvalue 0, contributes nothing to the d x d reconstruction (V[i][pad] = 0) and
+// is left out of the certificate. Workspace: 3 dp² + 4 dp + 8 doubles of LDS (dp <= 64) or of
+// global scratch (the same code on global pointers; __syncthreads orders the workgroup's accesses).
+__host__ __device__ inline int psd_ws_len(int dp) { return 3 * dp * dp + 4 * dp + 8; }
+__global__ void __launch_bounds__(256) k_psd_any(int d, const double* __restrict__ M, double eps, double* Mo,
+                                                 double* cert, double* gws) {
+  extern __shared__ double lds_psd[];
+  const int dp = d + (d & 1);
+  const int64_t i = blockIdx.x;
+  double* A = gws ? gws + i * psd_ws_len(dp) : lds_psd;
+  double* V = A + dp * dp;
+  double* Ms = V + dp * dp;
+  double* w = Ms + dp * dp;
+  double* cs = w + dp;
+  double* red = cs + 3 * dp;
+  const double* Mi = M + i * d * d;
+  double symloc = 0.0;
+  for (int idx = threadIdx.x; idx < dp * dp; idx += kWG) {
+    const int r = idx / dp, c = idx % dp;
+    double sv = 0.0;
+    if (r < d && c < d) {
+      sv = 0.5 * (Mi[r * d + c] + Mi[c * d + r]);
+      const double dd = sv - Mi[r * d + c];
+      symloc += dd * dd;
+    }
+    A[idx] = sv;
+    Ms[idx] = sv;
+  }
+  __syncthreads();
+  const double symd = wg_sum(symloc, red);
+  wg_jacobi_eigh(A, V, w, dp, cs, red);
+  double mnl = 1e308, mxl = -1e308, nnl = 0.0;
+  for (int k = threadIdx.x; k < dp; k += kWG) {
+    const double wc = fmax(w[k], eps);
+    w[k] = wc;
+    if (k < d) {
+      mnl = fmin(mnl, wc); mxl = fmax(mxl, wc); nnl += (wc < 10.0 * eps) ? 1.0 : 0.0;
+    }
+  }
+  const double mn = -wg_max(-mnl, red);
+  const double mx = wg_max(mxl, red);
+  const double nn = wg_sum(nnl, red);
+  double projloc = 0.0;
+  for (int idx = threadIdx.x; idx < d * d; idx += kWG) {
+    const int r = idx / d, c = idx % d;
+    double v = 0.0;
+    for (int k = 0; k < dp; ++k) v += V[r * dp + k] * w[k] * V[c * dp + k];
+    const double dd = v - Ms[r * dp + c];
+    projloc += dd * dd;
+    Mo[i * d * d + idx] = v;
+  }
+  const double proj = wg_sum(projloc, red);
+  if (threadIdx.x == 0) {
+    double* c6 = cert + 6 * i;
+    c6[0] = sqrt(proj); c6[1] = sqrt(symd); c6[2] = mn; c6[3] = mx; c6[4] = mx / mn; c6[5] = nn;
+  }
 }
 
 // ------------------------------------------------------------------------ launch helpers
@@ -1470,16 +1378,18 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
                            const double* d_points_raw, const double* d_t_raw, const double* d_w_raw,
                            const double* d_budget_scalars, double t0, double t1, const double* d_xi,
                            const double* d_bins, double tau, const double* h_origin3, double eps_psd,
-                           double eps_mass, double* d_stats_out, double* d_cert_out) {
+                           double eps_mass, double* d_stats_out, double* d_cert_out, int32_t iters) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   GC_CHECK_ARG(ctx, H > 0 && n_in > 0 && n_cap > 0, "H, n_in, n_cap must be positive");
   GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
-  GC_CHECK_ARG(ctx, tau > 0.0, "tau must be positive");
+  // the table exp's exponent splice holds for arguments down to -2/τ (in units of ln 2 / 2048 that
+  // is 2^-1022): below the floor the smallest responsibilities would wrap instead of underflowing
+  GC_CHECK_ARG(ctx, tau >= GC_FUSED_TAU_MIN, "tau must be >= GC_FUSED_TAU_MIN (3e-3) for the fused kernel");
+  GC_CHECK_ARG(ctx, iters >= 0 && iters <= 64, "iters must be in [0, 64] (0 = by grid size)");
   GC_CHECK_ARG(ctx, d_points_raw && d_t_raw && d_w_raw && d_budget_scalars && d_xi && d_bins && h_origin3 &&
                         d_stats_out && d_cert_out, "NULL buffer");
   (void)n_in;
-  int iters = pick_iters(n_cap, H, 16, 1024);
-  if (const char* e = getenv("GC_FUSED_ITERS")) iters = std::max(1, atoi(e));  // dev tuning knob
+  if (iters == 0) iters = pick_iters(n_cap, H, 16, 1024);
   const int64_t chunks = (n_cap + iters * 256 - 1) / (iters * 256);
   const int NF = NF_BASE;
   const int RL = B * NF + REC_EXTRA;
@@ -1490,8 +1400,8 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   dim3 grid((unsigned)chunks, H);
   const double inv_tau = 1.0 / tau;
 #define GC_FUSED(BP, FULL)                                                                                     \
-  (void)hipFuncSetAttribute((const void*)k_bins_fused<BP, FULL>, hipFuncAttributeMaxDynamicSharedMemorySize,    \
-                            (int)sh);                                                                          \
+  GC_HIP(ctx, hipFuncSetAttribute((const void*)k_bins_fused<BP, FULL>,                                          \
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));                        \
   hipLaunchKernelGGL((k_bins_fused<BP, FULL>), grid, dim3(256), sh, ctx->stream, n_cap, B, iters, d_points_raw, \
                      d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins, inv_tau, h_origin3[0],            \
                      h_origin3[1], h_origin3[2], (double*)scr)
@@ -1522,13 +1432,26 @@ int32_t gc_domain_projection_psd_batch(gc_ctx* ctx, int32_t batch, int32_t d, co
                                        double* d_M_out, double* d_cert_out) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   GC_CHECK_ARG(ctx, batch >= 0 && d_M && d_M_out && d_cert_out, "bad arguments");
-  GC_CHECK_ARG(ctx, d == 3 || (d >= 2 && d <= 22 && d % 2 == 0), "d must be 3 or even in [2, 22]");
+  GC_CHECK_ARG(ctx, d >= 1 && d <= 512, "d must be in [1, 512]");
   if (batch == 0) return GC_OK;
   if (d == 3) {
     hipLaunchKernelGGL(k_psd3, dim3((batch + 63) / 64), dim3(64), 0, ctx->stream, batch, d_M, eps_psd, d_M_out,
                        d_cert_out);
-  } else {
+  } else if (d <= kDZ && d % 2 == 0) {
     hipLaunchKernelGGL(k_psd_wg, dim3(batch), dim3(256), 0, ctx->stream, d, d_M, eps_psd, d_M_out, d_cert_out);
+  } else {
+    const int dp = d + (d & 1);
+    const size_t ws = sizeof(double) * (size_t)psd_ws_len(dp);
+    if (dp <= 64) {
+      GC_HIP(ctx, hipFuncSetAttribute((const void*)k_psd_any, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ws));
+      hipLaunchKernelGGL(k_psd_any, dim3(batch), dim3(256), ws, ctx->stream, d, d_M, eps_psd, d_M_out, d_cert_out,
+                         (double*)nullptr);
+    } else {
+      void* scr;
+      if (int rc = gc::scratch(ctx, ws * (size_t)batch, &scr)) return rc;
+      hipLaunchKernelGGL(k_psd_any, dim3(batch), dim3(256), 0, ctx->stream, d, d_M, eps_psd, d_M_out, d_cert_out,
+                         (double*)scr);
+    }
   }
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;

@@ -19,6 +19,7 @@ LIB_PATH = os.path.join(_HERE, "libgcslam.so")
 GC_OK, GC_ERR_ARG, GC_ERR_RUNTIME = 0, 1, 2
 GC_BIN_STATS = 38
 GC_BIN_CERT = 8
+GC_FUSED_TAU_MIN = 3e-3
 
 _vp, _dp, _i32, _i64, _u64, _f64 = C.c_void_p, C.c_void_p, C.c_int32, C.c_int64, C.c_uint64, C.c_double
 _dptr = C.POINTER(C.c_double)
@@ -47,7 +48,7 @@ SIGNATURES = {
     "gc_bin_soft_assign": [_vp, _i32, _i64, _i32, _vp, _vp, _f64, _vp, _vp, _vp],
     "gc_scan_bin_moment_match": [_vp, _i32, _i64, _i32, _vp, _vp, _vp, _vp, _vp, _dptr, _f64, _f64, _vp, _vp],
     "gc_scan_bins_fused": [_vp, _i32, _i64, _i64, _i32, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _f64, _dptr,
-                           _f64, _f64, _vp, _vp],
+                           _f64, _f64, _vp, _vp, _i32],
     "gc_kappa_from_resultant_batch": [_vp, _i64, _vp, _f64, _f64, _f64, _f64, _vp],
     "gc_domain_projection_psd_batch": [_vp, _i32, _i32, _vp, _f64, _vp, _vp],
     "gc_pipeline_create": [_vp, _vp, _vp, C.POINTER(_vp)],
@@ -75,6 +76,7 @@ SIGNATURES = {
     "gc_pipeline_get_hyp_diag": [_vp, _vp],
     "gc_pipeline_get_lpose6": [_vp, _vp],
     "gc_pipeline_get_bin_stats": [_vp, _vp, _vp, _vp],
+    "gc_pipeline_get_hyp_stats": [_vp, _vp, _vp, _vp],
     "gc_pipeline_attach_comm": [_vp, _vp],
     "gc_comm_unique_id": [_vp],
     "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],

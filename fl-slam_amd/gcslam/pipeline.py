@@ -214,6 +214,13 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_get_bin_stats", _p(s), _p(c), _p(x))
         return s, c, x
 
+    def hyp_stats(self):
+        """Per-hypothesis process-IW dPsi (Hl,7,6,6), measurement-IW dPsi (Hl,3,3,3) and belief
+        covariance Σ = (L + ε_lift I)⁻¹ (Hl,22,22) of the last scan."""
+        a, b, c = np.empty((self.Hl, 7, 6, 6)), np.empty((self.Hl, 3, 3, 3)), np.empty((self.Hl, 22, 22))
+        self._call("gc_pipeline_get_hyp_stats", _p(a), _p(b), _p(c))
+        return a, b, c
+
     # ---------------------------------------------------------------- multi-GPU
     @staticmethod
     def comm_unique_id() -> bytes:

@@ -105,7 +105,8 @@ int32_t gc_point_directions(gc_ctx* ctx, int64_t rows, const double* d_points, c
 
 /* ------------------------------------------------------------------ a5 BinSoftAssign
  * Replaces archive/legacy_operators/binning.py:56-76 (_bin_soft_assign_core), batched over H.
- * d_dirs (H,n,3); d_bins (B,3), B <= 64; d_resp_out (H,n,B) = softmax(dirs·binsᵀ/τ);
+ * d_dirs (H,n,3), any norm; d_bins (B,3), B <= 64; tau > 0;
+ * d_resp_out (H,n,B) = softmax(dirs·binsᵀ/τ) shifted by the row maximum as jax.nn.softmax;
  * d_bin_index_out (H,n) int32 = argmax_b of the un-fused f64 d0*b0+d1*b1+d2*b2 (lowest index
  * on ties; may be NULL); d_cert_out (H,2) = [avg_entropy, max_resp]. */
 int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const double* d_dirs,
@@ -128,12 +129,18 @@ int32_t gc_scan_bin_moment_match(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, c
  * deskew by d_xi (H,6), directions from h_origin3, soft assignment to d_bins (B,3) at tau and
  * moment accumulation — responsibilities never touch HBM. Same outputs as the contract pair
  * (d_stats_out (H,B,GC_BIN_STATS), d_cert_out (H,GC_BIN_CERT) incl. [4:7]).
- * d_budget_scalars: the 8 scalars written by gc_point_budget_resample / gc_budget_stats. */
+ * d_budget_scalars: the 8 scalars written by gc_point_budget_resample / gc_budget_stats.
+ * tau >= GC_FUSED_TAU_MIN (the table exp's range; the contract gc_bin_soft_assign takes any tau).
+ * iters: 256-point iterations per workgroup (launch geometry; it changes only the summation
+ * order): 0 = chosen from the grid size (16 at 64k points x 256 hypotheses, 1 below ~1024
+ * workgroups), 1..64 = forced. */
+#define GC_FUSED_TAU_MIN 3e-3
 int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, int32_t B,
                            const double* d_points_raw, const double* d_t_raw, const double* d_w_raw,
                            const double* d_budget_scalars, double t0, double t1, const double* d_xi,
                            const double* d_bins, double tau, const double* h_origin3,
-                           double eps_psd, double eps_mass, double* d_stats_out, double* d_cert_out);
+                           double eps_psd, double eps_mass, double* d_stats_out, double* d_cert_out,
+                           int32_t iters);
 
 /* Budget reduction only (no gather): writes the 8 budget scalars. */
 int32_t gc_budget_stats(gc_ctx* ctx, const double* d_w, int64_t n_in, int64_t n_cap,
@@ -143,8 +150,9 @@ int32_t gc_budget_stats(gc_ctx* ctx, const double* d_w, int64_t n_in, int64_t n_
 int32_t gc_kappa_from_resultant_batch(gc_ctx* ctx, int64_t n, const double* d_R, double eps_r,
                                       double d, double r0, double tau, double* d_kappa_out);
 
-/* domain_projection_psd_core (primitives.py:80-123) over `batch` d x d matrices (d <= 22 even, or
- * d == 3). d_cert_out (batch,6) = [projection_delta, sym_delta, eig_min, eig_max, cond, nnc]. */
+/* domain_projection_psd_core (primitives.py:80-123) over `batch` d x d matrices, any 1 <= d <= 512
+ * (cyclic Jacobi; an odd d is padded with a decoupled zero row/column that the certificate
+ * ignores). d_cert_out (batch,6) = [projection_delta, sym_delta, eig_min, eig_max, cond, nnc]. */
 int32_t gc_domain_projection_psd_batch(gc_ctx* ctx, int32_t batch, int32_t d, const double* d_M,
                                        double eps_psd, double* d_M_out, double* d_cert_out);
 
@@ -266,6 +274,11 @@ int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag);
    (pipeline.py:1537). */
 int32_t gc_pipeline_get_lpose6(gc_pipeline* p, double* h_lpose);
 int32_t gc_pipeline_get_bin_stats(gc_pipeline* p, double* h_stats, double* h_cert, double* h_xi);
+/* Per-hypothesis statistics of the last scan (any pointer may be NULL): process-IW sufficient
+ * statistics dPsi (Hl,7,6,6) and measurement-IW dPsi (Hl,3,3,3) before the weighted accumulation
+ * (backend_node.py:2085-2090), and the covariance of each updated belief Σ = (L + ε_lift I)⁻¹
+ * (Hl,22,22) (BeliefGaussianInfo covariance, belief.py:373-386). */
+int32_t gc_pipeline_get_hyp_stats(gc_pipeline* p, double* h_dPsi_proc, double* h_dPsi_meas, double* h_Sigma);
 int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm);
 
 /* ------------------------------------------------------------------ RCCL communicator */

@@ -31,14 +31,15 @@ def map_to_record(m: O.MapStats):
                            m.sum_p, m.sum_ppT.reshape(B, 9)], axis=1)
 
 
-def build(H=4, n_az=256, n_scans=3, seed_scan0=0, io="synthetic"):
+def build(H=4, n_az=256, n_scans=3, seed_scan0=0, io="synthetic", cap=None):
     """io="synthetic": given IMU/odom-branch evidence (ios list); io="computed": the branch is
-    evaluated from each scan's odometry + IMU window (ios=None)."""
+    evaluated from each scan's odometry + IMU window (ios=None). cap: N_POINTS_CAP (default: the
+    scan size, stride 1)."""
     import sys, os
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "fl-slam_amd"))
     from gcslam import synth
     scans = [synth.make_scan(seed_scan0 + k, n_az=n_az) for k in range(n_scans + 1)]
-    n = scans[0]["points"].shape[0]
+    n = scans[0]["points"].shape[0] if cap is None else int(cap)
     cfg = O.PipeConfig(n_points_cap=n)
     bins = O.fibonacci_atlas(48)
     hy = synth.make_hypotheses(H)

@@ -77,6 +77,43 @@ def test_soft_assign_matches_oracle(ctx, B, n):
     np.testing.assert_allclose(resp.sum(-1), 1.0, atol=1e-12)                # rows sum to 1
 
 
+@pytest.mark.parametrize("tau,norm", [(0.01, 1.0), (1.0, 1.0), (0.1, 3.7), (0.1, 0.05), (1e-4, 1.0), (0.01, 40.0)])
+def test_soft_assign_row_max_shift_any_tau_and_norm(ctx, tau, norm):
+    """jax.nn.softmax shifts by the row maximum (binning.py:68-69), so the drop-in must accept any
+    τ > 0 and non-unit directions (at τ = 1e-4 the bound shift (S - 1)/τ would underflow every
+    exp). Tolerance: x = (S - S_max)/τ rounds at ulp(|S|/τ), so |ΔR| <= ~4 ulp(|S|/τ)."""
+    from gcslam.ops.binning import bin_soft_assign_batch
+    rng = np.random.default_rng(11)
+    n = 3000
+    D = (_unit(rng, n) * norm * rng.uniform(0.5, 1.5, (n, 1)))[None]
+    bins = O.fibonacci_atlas(48)
+    resp, idx, cert = bin_soft_assign_batch(D, bins, tau, ctx=ctx)
+    ref = O.bin_soft_assign(D[0], bins, tau)
+    tol = 4 * np.spacing(1.5 * norm / tau) + 1e-15
+    np.testing.assert_array_equal(idx[0], ref["bin_index"])
+    np.testing.assert_allclose(resp[0], ref["resp"], atol=tol, rtol=0)
+    assert np.all(np.isfinite(resp)) and np.all(resp >= 0.0)
+    np.testing.assert_allclose(resp.sum(-1), 1.0, atol=1e-12)
+    assert abs(cert[0, 0] - ref["avg_entropy"]) < 1e-9 + 48 * tol
+    assert abs(cert[0, 1] - ref["max_resp"]) < 1e-14 + tol
+
+
+def test_fused_rejects_tau_below_table_floor(ctx):
+    """The fused kernel's table exp covers arguments down to -2/τ for τ >= GC_FUSED_TAU_MIN; below
+    it the call fails loudly (ValueError) instead of wrapping the exponent."""
+    from gcslam import _abi
+    H, n = 1, 512
+    d = _abi.DeviceArray(ctx, (n, 3)); d.zero()
+    t = _abi.DeviceArray(ctx, n); t.zero()
+    scal = _abi.DeviceArray(ctx, 8); scal.zero()
+    xi, bins = _abi.DeviceArray(ctx, (H, 6)), _abi.DeviceArray.from_host(ctx, O.fibonacci_atlas(48))
+    st, ce = _abi.DeviceArray(ctx, (H, 48, 38)), _abi.DeviceArray(ctx, (H, 8))
+    oa, op = _abi.f64p([0.0, 0.0, 0.0])
+    with pytest.raises(ValueError, match="tau"):
+        _abi.call("gc_scan_bins_fused", ctx.handle, H, n, n, 48, d.ptr, t.ptr, t.ptr, scal.ptr, 0.0, 0.1, xi.ptr,
+                  bins.ptr, 1e-3, op, 1e-12, 1e-12, st.ptr, ce.ptr, 0, ctx=ctx)
+
+
 def test_bin_index_ties_resolve_to_lowest_index(ctx):
     from gcslam.ops.binning import bin_soft_assign_batch
     bins = np.array([[1.0, 0, 0], [0, 1.0, 0], [1.0, 0, 0], [0, 0, 1.0]])
@@ -123,8 +160,17 @@ def test_moment_match_matches_oracle(ctx, B, n, with_cov):
         _check_stats(stats[h], cert[h], ref)
 
 
-@pytest.mark.parametrize("n_in,cap,B", [(4096, 4096, 48), (5000, 2048, 48), (3000, 3500, 48), (2000, 2000, 20)])
-def test_fused_bins_match_contract_chain(ctx, n_in, cap, B):
+@pytest.mark.parametrize("n_in,cap,B,iters,tau", [
+    (4096, 4096, 48, 0, 0.1), (5000, 2048, 48, 0, 0.1), (3000, 3500, 48, 0, 0.1), (2000, 2000, 20, 0, 0.1),
+    # the iteration counts the benchmark runs (16 at 64k x 256, 8 for a 32-hypothesis shard) and
+    # caps that leave a partial last chunk (the PAD specialisation at several iterations)
+    (65536, 65536, 48, 16, 0.1), (65536, 65536, 48, 8, 0.1), (5000, 5000, 48, 2, 0.1),
+    (20000, 20000, 48, 8, 0.1), (65536, 30000, 48, 16, 0.1), (3000, 3000, 20, 4, 0.1),
+    # C2 at full size with the automatic geometry (H = 3 -> one iteration per workgroup)
+    (65536, 65536, 48, 0, 0.1),
+    # other temperatures (down to the fused kernel's floor)
+    (4096, 4096, 48, 4, 0.01), (4096, 4096, 48, 2, 1.0), (4096, 4096, 48, 0, 0.003)])
+def test_fused_bins_match_contract_chain(ctx, n_in, cap, B, iters, tau):
     """Fused a1->a4->a5->a6 == oracle chain budget -> deskew -> dirs -> soft assign -> moments."""
     from gcslam import _abi
     from gcslam.synth import make_scan
@@ -143,27 +189,33 @@ def test_fused_bins_match_contract_chain(ctx, n_in, cap, B):
     st = _abi.DeviceArray(ctx, (H, B, 38)); ce = _abi.DeviceArray(ctx, (H, 8))
     oa, op = _abi.f64p(o)
     _abi.call("gc_scan_bins_fused", ctx.handle, H, n_in, cap, B, dP.ptr, dT.ptr, dW.ptr, scal.ptr,
-              s["scan_start"], s["scan_end"], dX.ptr, dB.ptr, 0.1, op, 1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
+              s["scan_start"], s["scan_end"], dX.ptr, dB.ptr, tau, op, 1e-12, 1e-12, st.ptr, ce.ptr, iters,
+              ctx=ctx)
     stats, cert = st.download(), ce.download()
     bud = O.point_budget_resample(P, T, W, None, None, cap)
     for h in range(H):
         p0, wd, ret = O.deskew_constant_twist(bud["points"], bud["timestamps"], bud["weights"],
                                               s["scan_start"], s["scan_end"], xis[h])
-        sa = O.bin_soft_assign(O.point_directions(p0, o), bins, 0.1)
+        sa = O.bin_soft_assign(O.point_directions(p0, o), bins, tau)
         ref = O.scan_bin_moment_match(p0, None, wd, sa["resp"], None, o)
         _check_stats(stats[h], cert[h], ref, rtol=1e-10)
-        assert abs(cert[h, 4] - sa["avg_entropy"]) < 1e-9
-        assert abs(cert[h, 5] - sa["max_resp"]) < 1e-12
+        # the logits round at ulp(1/τ): entropy within ~B·ulp(1/τ), max responsibility within
+        # a few ulp(1/τ)
+        assert abs(cert[h, 4] - sa["avg_entropy"]) < 1e-9 + 48 * np.spacing(1.0 / tau)
+        assert abs(cert[h, 5] - sa["max_resp"]) < 1e-12 + 4 * np.spacing(1.0 / tau)
         assert abs(cert[h, 6] / (bud["weights"].sum() + 1e-12) - ret) < 1e-12
 
 
 def test_fused_is_bit_reproducible(ctx):
+    """Full-size properties at the benchmark geometry (C3: 65,536 points x 256 hypotheses, 16
+    iterations per workgroup): two runs agree bit for bit and Σ_b N_b = Σ_n w_deskew for every
+    hypothesis (softmax rows sum to one)."""
     from gcslam import _abi
     from gcslam.synth import make_scan
-    s = make_scan(1, n_az=1024)
+    s = make_scan(1, n_az=4096)
     n = s["points"].shape[0]
     bins = O.fibonacci_atlas(48)
-    H = 8
+    H = 256
     xis = np.random.default_rng(9).normal(size=(H, 6)) * 0.02
     dP, dT, dW = (_abi.DeviceArray.from_host(ctx, s[k]) for k in ("points", "timestamps", "weights"))
     scal = _abi.DeviceArray(ctx, 8)
@@ -174,15 +226,18 @@ def test_fused_is_bit_reproducible(ctx):
         st = _abi.DeviceArray(ctx, (H, 48, 38)); ce = _abi.DeviceArray(ctx, (H, 8))
         oa, op = _abi.f64p([-0.065447, -0.100474, 0.108987])
         _abi.call("gc_scan_bins_fused", ctx.handle, H, n, n, 48, dP.ptr, dT.ptr, dW.ptr, scal.ptr,
-                  s["scan_start"], s["scan_end"], dX.ptr, dB.ptr, 0.1, op, 1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
+                  s["scan_start"], s["scan_end"], dX.ptr, dB.ptr, 0.1, op, 1e-12, 1e-12, st.ptr, ce.ptr, 0, ctx=ctx)
         outs.append((st.download(), ce.download()))
     assert np.array_equal(outs[0][0], outs[1][0]) and np.array_equal(outs[0][1], outs[1][1])
     # mass conservation: Σ_b N_b = Σ_n w_deskew (softmax rows sum to one)
     np.testing.assert_allclose(outs[0][0][:, :, 0].sum(1), outs[0][1][:, 6], rtol=1e-12)
 
 
-@pytest.mark.parametrize("d", [22, 6, 3, 2])
+@pytest.mark.parametrize("d", [22, 6, 3, 2, 1, 5, 7, 23, 40, 64, 100])
 def test_psd_projection_matches_oracle(ctx, d):
+    """domain_projection_psd_core takes any square matrix (primitives.py:80-123): even d <= 22 on
+    the fixed-size path, odd / larger d padded (LDS up to 64, global workspace beyond).
+    Tolerance 1e-12 x scale x max(1, d/16) (Jacobi vs LAPACK eigh rounding grows with d)."""
     from gcslam.ops.primitives import domain_projection_psd_batch
     rng = np.random.default_rng(7 + d)
     A = rng.normal(size=(5, d, d))
@@ -193,7 +248,7 @@ def test_psd_projection_matches_oracle(ctx, d):
     Mp, c = domain_projection_psd_batch(M, 1e-12, ctx=ctx)
     for i in range(5):
         rp, rc = O.psd_project(M[i])
-        sc = max(np.max(np.abs(M[i])), 1.0)
+        sc = max(np.max(np.abs(M[i])), 1.0) * max(1.0, d / 16)
         np.testing.assert_allclose(Mp[i], rp, atol=1e-12 * sc, rtol=0)
         np.testing.assert_allclose(c[i, [1, 5]], rc[[1, 5]], atol=1e-12 * sc)
         np.testing.assert_allclose(c[i, 2:4], rc[2:4], atol=1e-12 * sc)
