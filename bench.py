@@ -42,8 +42,9 @@ def parse():
     ap.add_argument("--scans", type=int, default=4, help="distinct resident scans cycled through")
     ap.add_argument("--no-roofline", action="store_true")
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--cpu-budget-s", type=float, default=15.0)
+    ap.add_argument("--cpu-budget-s", type=float, default=30.0)
     ap.add_argument("--no-map", action="store_true", help="skip the C5 PrimitiveMap fuse leg")
+    ap.add_argument("--no-c5", action="store_true", help="skip the C5 single-GPU pipeline leg")
     ap.add_argument("--roofline-only", action="store_true",
                     help="run only the contract-pair roofline leg (PMC traffic passes, tools/pmc_traffic.sh)")
     ap.add_argument("--io-given", action="store_true", help=argparse.SUPPRESS)
@@ -207,8 +208,12 @@ def main():
         d0 = {k: _abi.DeviceArray.from_host(ctx, scans[0][k]) for k in ("points", "timestamps", "weights")}
         dbins = _abi.DeviceArray.from_host(ctx, bins)
         out["roofline"] = roofline_leg(ctx, _abi, scans[0], d0, xi, dbins, B, n, H, origin, reps=args.roofline_reps)
+    if dist.rank == 0 and not args.no_roofline:
+        out["fused_roofline"] = fused_roofline_leg(ctx, _abi, scans[0], B, n, H, bins, origin)
     if dist.rank == 0 and not args.no_map:
         out["c5_map_fuse"] = map_fuse_leg(ctx, _abi)
+    if dist.rank == 0 and dist.world == 1 and not args.no_c5:
+        out["c5"] = c5_leg(ctx, _abi, args)
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args.n_az, H_total, args.cpu_budget_s)
     if dist.rank == 0:
@@ -270,6 +275,78 @@ def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=3):
             "hypotheses": H, "points": n, "bins": B}
 
 
+FP64_PEAK_TFS = 78.6  # MI355X FP64 vector = FP64 matrix peak (16 lanes x FMA per SIMD-cycle, 256 CUs, 2.4 GHz)
+FUSED_FLOP_PER_POINT_BIN = 76  # 5 (dot) + 1 (exp) + 2 (normalise) + 34 x 2 (moment FMAs)
+
+
+def fused_roofline_leg(ctx, _abi, s, B, n, H, bins, origin, reps=10, warm=3):
+    """The product's dominant kernel, k_bins_fused (a1->a4->a5->a6 fused, responsibilities in
+    registers): FP64-issue-bound, so its roofline is flops against the FP64 peak. Timed with HIP
+    events on the library stream around gc_scan_bins_fused (the fused kernel + its ~1 % finalize)."""
+    from gcslam.constants import GC_TAU_SOFT_ASSIGN
+    rng = np.random.default_rng(5)
+    xi = np.zeros((H, 6)); xi[:, 0] = 0.1 + rng.normal(0, 0.005, H); xi[:, 5] = 0.03 + rng.normal(0, 0.002, H)
+    d = {k: _abi.DeviceArray.from_host(ctx, s[k]) for k in ("points", "timestamps", "weights")}
+    scal = _abi.DeviceArray(ctx, 8)
+    _abi.call("gc_budget_stats", ctx.handle, d["weights"].ptr, n, n, scal.ptr, ctx=ctx)
+    dx, db = _abi.DeviceArray.from_host(ctx, xi), _abi.DeviceArray.from_host(ctx, bins)
+    st, ce = _abi.DeviceArray(ctx, (H, B, 38)), _abi.DeviceArray(ctx, (H, 8))
+    oa, op = _abi.f64p(origin)
+    ev = [_abi.Event(ctx) for _ in range(2)]
+    ts = []
+    for r in range(reps + warm):
+        ev[0].record()
+        _abi.call("gc_scan_bins_fused", ctx.handle, H, n, n, B, d["points"].ptr, d["timestamps"].ptr,
+                  d["weights"].ptr, scal.ptr, s["scan_start"], s["scan_end"], dx.ptr, db.ptr, GC_TAU_SOFT_ASSIGN, op,
+                  1e-12, 1e-12, st.ptr, ce.ptr, 0, ctx=ctx)
+        ev[1].record()
+        ctx.sync()
+        if r >= warm:
+            ts.append(ev[0].elapsed_ms(ev[1]))
+    ms = float(np.mean(ts))
+    flop = float(FUSED_FLOP_PER_POINT_BIN) * n * B * H
+    ach = flop / (ms * 1e-3) / 1e12
+    return {"bound": "fp64", "achieved": ach, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFS,
+            "ms": ms, "flop": flop, "flop_per_point_bin": FUSED_FLOP_PER_POINT_BIN,
+            "kernel": "k_bins_fused + k_bins_finalize (gc_scan_bins_fused)", "hypotheses": H, "points": n, "bins": B}
+
+
+def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5):
+    """C5 on one GPU: 131,072-point scans budgeted to 65,536 (stride 2) x 1024
+    hypotheses through the full batched pipeline, plus the 1M-slot PrimitiveMap fuse of
+    map_fuse_leg timed separately. BASELINE.json quotes C5 on 8 GPUs; this is one GPU's
+    whole-job throughput at the full 1024 hypotheses."""
+    from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
+    from gcslam.ops.binning import create_fibonacci_atlas
+    from gcslam.pipeline import BatchedScanPipeline, PipelineConfig, iw_meas_prior, iw_process_prior
+    from gcslam.synth import make_hypotheses, make_scan
+    B = GC_B_BINS
+    scans = [make_scan(k + 1, n_az=n_az) for k in range(2)]
+    n_in = scans[0]["points"].shape[0]
+    pipe = BatchedScanPipeline(H, n_in, PipelineConfig(n_points_cap=cap), ctx=ctx)
+    hy = make_hypotheses(H)
+    pipe.set_beliefs(hy["X_anchor"], hy["z_lin"], hy["L"], hy["h"], hy["stamp"])
+    pipe.set_weights(hy["weights"])
+    pipe.set_io_mode(True)
+    pipe.set_iw(*iw_process_prior(), *iw_meas_prior())
+    pipe.set_map(warmup_map_record(ctx, _abi, make_scan(0, n_az=n_az), n_in, B, create_fibonacci_atlas(B).dirs,
+                                   np.asarray(T_BASE_LIDAR[:3])))
+    for k, sc in enumerate(scans):
+        pipe.stage_scan(k, sc)
+    for i in range(warmup):
+        pipe.run_scan(i % 2, scans[i % 2], i)
+    ctx.sync()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        pipe.run_scan(i % 2, scans[i % 2], warmup + i)
+    ctx.sync()
+    dt = (time.perf_counter() - t0) / steps
+    pipe.close()
+    return {"workload": "C5 shape on 1 GPU: %d-point scans, budget cap %d (stride 2), %d hypotheses, full pipeline"
+                        % (n_in, cap, H), "ms_per_scan": 1e3 * dt, "scans_per_s": 1.0 / dt, "steps": steps,
+            "warmup": warmup}
+
+
 def map_fuse_leg(ctx, _abi, m_slots=1 << 20, rows=1 << 17, reps=5):
     """C5 map update: 1,048,576-slot PrimitiveMap (random SPD Λ with eigenvalues
     10..1e4, θ, 3-lobe η, w in (0, 1]) and 131,072 measurement rows pushed to the world frame and
@@ -306,33 +383,126 @@ def map_fuse_leg(ctx, _abi, m_slots=1 << 20, rows=1 << 17, reps=5):
             "GB/s": b / (ms * 1e-3) / 1e9, "kernel": "k_fuse_keys + radix sort + k_fuse_segments + k_fuse_colors"}
 
 
-def cpu_leg(n_az, H_total, budget_s):
-    """The CPU oracle (NumPy restatement of the reference pipeline) on whole hypotheses of the
-    same workload until the time budget is spent; per-scan time extrapolated to H hypotheses."""
+def cpu_info():
+    """os.cpu_count(), the affinity count, the cgroup CPU quota (cpu.max, if any) and the model."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, int(float(q) / float(per)))
+    except (OSError, ValueError):
+        pass
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    return dict(cpu_count=os.cpu_count(), affinity=aff, cgroup_quota=quota, model=model)
+
+
+_CPU = {}
+
+
+def _cpu_init(n_az, H_total):
+    """Per-process oracle inputs of the C3 scan (spawned pool workers build their own copy)."""
     sys.path.insert(0, ROOT)
     from threadpoolctl import threadpool_limits
     from oracle import cases, gc_oracle as O
+    _CPU["limits"] = threadpool_limits(limits=1)
     case = cases.build(H=H_total, n_az=n_az, n_scans=1, io="computed")
-    st, s = case["state"], case["scans"][0]
-    Q = O.iw_process_Q(st.nu_proc, st.Psi_proc)
-    Sga = (O.iw_meas_mode(st.nu_meas, st.Psi_meas, 0), O.iw_meas_mode(st.nu_meas, st.Psi_meas, 1))
-    md = O.map_derived(st.map)
-    scan = cases.scan_input(s)
-    with threadpool_limits(limits=1):
+    st = case["state"]
+    _CPU.update(case=case, scan=cases.scan_input(case["scans"][0]), Q=O.iw_process_Q(st.nu_proc, st.Psi_proc),
+                Sga=(O.iw_meas_mode(st.nu_meas, st.Psi_meas, 0), O.iw_meas_mode(st.nu_meas, st.Psi_meas, 1)),
+                md=O.map_derived(st.map))
+
+
+def _cpu_hyp(k):
+    """One hypothesis through a1-a15 (+ the IMU/odom branch) in the oracle."""
+    from oracle import gc_oracle as O
+    c = _CPU["case"]
+    st = c["state"]
+    r = O.scan_hypothesis(st.beliefs[k], _CPU["scan"], _CPU["Q"], None, st.map, _CPU["md"], c["bins"], c["cfg"],
+                          _CPU["Sga"])
+    return (r["belief"], r["dPsi_proc"], r["dPsi_meas"], r["map_inc"] if k == 0 else None)
+
+
+def _cpu_combine(outs, st):
+    """a16 barycenter + IW apply + map update of one scan (backend_node.py:2085-2119)."""
+    from oracle import gc_oracle as O
+    H = len(outs)
+    w = st.weights
+    comb = O.hypothesis_barycenter(np.stack([o[0].L for o in outs]), np.stack([o[0].h for o in outs]),
+                                   np.stack([o[0].z_lin for o in outs]), w, 0.01 / H)
+    aP = sum(w[i] * outs[i][1] for i in range(H))
+    aM = sum(w[i] * outs[i][2] for i in range(H))
+    O.iw_process_apply(st.nu_proc, st.Psi_proc, aP, np.full(7, w.sum()))
+    O.iw_meas_apply(st.nu_meas, st.Psi_meas, aM, w.sum() * np.array([1.0, 1.0, 0.0]))
+    O.map_forget_and_add(st.map, outs[0][3])
+    return comb
+
+
+def cpu_leg(n_az, H_total, budget_s):
+    """CPU baseline: the oracle (NumPy restatement of the reference path) on the
+    same C3 scan, both legs of the plan, on this host's cores:
+      (i)  one process, BLAS threads = the usable cores: per-hypothesis a1-a15 timed as the median
+           of 20 hypotheses after 3 warm-ups, plus one timed a16 combine + IW apply + map update
+           over all H; scan time = H x median + combine;
+      (ii) multiprocessing.Pool(usable cores) over the hypotheses (1 BLAS thread per worker): whole
+           scans (all H hypotheses, then the combine in the parent), median of the scans that fit
+           the budget after one warm-up scan.
+    Usable cores = min(affinity, cgroup quota)."""
+    import multiprocessing as mproc
+    import statistics
+    from threadpoolctl import threadpool_limits
+    info = cpu_info()
+    cores = min(info["affinity"], info["cgroup_quota"] or info["affinity"])
+    _cpu_init(n_az, H_total)
+    st = _CPU["case"]["state"]
+    # leg (i)
+    with threadpool_limits(limits=cores):
+        for k in range(3):
+            _cpu_hyp(k)
+        ts, outs = [], []
+        for k in range(20):
+            t0 = time.perf_counter()
+            outs.append(_cpu_hyp(k % H_total))
+            ts.append(time.perf_counter() - t0)
+        t_hyp = statistics.median(ts)
+        full = [outs[0]] + [outs[1 + (k % 19)] for k in range(H_total - 1)]
         t0 = time.perf_counter()
-        done = 0
-        while done < H_total:
-            O.scan_hypothesis(st.beliefs[done], scan, Q, None, st.map, md, case["bins"], case["cfg"], Sga)
-            done += 1
-            if time.perf_counter() - t0 > budget_s:
-                break
-        dt = time.perf_counter() - t0
-    per_hyp = dt / done
-    return {"value": 1.0 / (per_hyp * H_total), "unit": "scans/s", "cores": 1, "kind": "port",
-            "sample": "%d of %d hypotheses of one %d-point scan through the oracle pipeline (a1-a14 + IMU/odom "
-                      "branch per hypothesis, NumPy, 1 BLAS thread), extrapolated to the full scan"
-                      % (done, H_total, case["n"]),
-            "cpu_count": os.cpu_count(), "affinity": len(os.sched_getaffinity(0))}
+        _cpu_combine(full, st)
+        t_comb = time.perf_counter() - t0
+    leg1 = {"scans_per_s": 1.0 / (H_total * t_hyp + t_comb), "median_hyp_ms": 1e3 * t_hyp,
+            "combine_ms": 1e3 * t_comb, "blas_threads": cores,
+            "sample": "20 hypotheses after 3 warm-ups (median) x %d + one combine/IW/map over %d" % (H_total, H_total)}
+    # leg (ii)
+    pctx = mproc.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
+    scans = []
+    with pctx.Pool(cores, initializer=_cpu_init, initargs=(n_az, H_total)) as pool:
+        pool.map(_cpu_hyp, range(cores))  # workers built and warm
+        t_start = time.perf_counter()
+        n = 0
+        while n < 6 and (n < 2 or time.perf_counter() - t_start < budget_s):
+            t0 = time.perf_counter()
+            outs = pool.map(_cpu_hyp, range(H_total), chunksize=max(1, H_total // (4 * cores)))
+            _cpu_combine(outs, st)
+            dt = time.perf_counter() - t0
+            if n > 0:  # the first scan is the warm-up
+                scans.append(dt)
+            n += 1
+    t_scan = statistics.median(scans)
+    leg2 = {"scans_per_s": 1.0 / t_scan, "median_scan_s": t_scan, "workers": cores,
+            "sample": "%d whole %d-hypothesis scans after 1 warm-up (median)" % (len(scans), H_total)}
+    best = max(leg1["scans_per_s"], leg2["scans_per_s"])
+    return {"value": best, "unit": "scans/s", "cores": cores, "kind": "port",
+            "sample": "oracle (NumPy restatement) on the C3 scan, %d points x %d hypotheses, a1-a16 incl. the "
+                      "IMU/odom branch, combine, IW apply and map update; value = the faster of leg (i) %s and "
+                      "leg (ii) Pool(%d) %s" % (_CPU["case"]["n"], H_total, leg1["sample"], cores, leg2["sample"]),
+            "legs": {"single_process": leg1, "pool": leg2}, **info}
 
 
 if __name__ == "__main__":

@@ -35,6 +35,11 @@ struct gc_pipeline {
   // P.Sig / P.mu_fin were written by the last scan's evidence kernel from the current P.L / P.h
   // (cleared whenever the beliefs are set from the host)
   bool sig_cached = false;
+  // a scan whose local part (a1-a15 + partial record) is enqueued and whose exchange + combine
+  // (gc_pipeline_scan_finish) is still due
+  bool pending = false;
+  gc::ScanArgs pending_S{};
+  double* own_gather = nullptr;  // separate gather buffer of a single-rank pipeline with a communicator
 };
 
 namespace {
@@ -339,15 +344,56 @@ int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_
 int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm) {
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
   GC_CHECK_ARG(p->ctx, comm == nullptr || gc::comm_size(comm) == p->P.G, "communicator size != world_size");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   p->comm = comm;
+  if (p->P.G == 1) {
+    // a single-rank pipeline with a communicator runs the real all-gather into a buffer of its own
+    // (without one the combine reads its partial record in place)
+    if (comm && !p->own_gather) GC_TRY(dalloc(p, (size_t)gc::partial_len(p->P.B), &p->own_gather));
+    p->P.gather = comm ? p->own_gather : p->P.send;
+  }
   return GC_OK;
 }
+
+int32_t gc_pipeline_partial_len(const gc_pipeline* p) { return p ? gc::partial_len(p->P.B) : 0; }
 
 int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
                              double t_scan, double dt_sec, int64_t scan_count) {
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
-  GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS && p->slots[slot].pts, "scan slot not staged");
   GC_CHECK_ARG(p->ctx, p->P.G == 1 || p->comm, "world_size > 1 needs gc_pipeline_attach_comm");
+  GC_TRY(gc_pipeline_scan_local(p, slot, scan_start, scan_end, t_last, t_scan, dt_sec, scan_count));
+  return gc_pipeline_scan_finish(p, nullptr);
+}
+
+int32_t gc_pipeline_get_partial(gc_pipeline* p, double* h_record) {
+  GC_CHECK_ARG(nullptr, p && h_record, "NULL argument");
+  GC_CHECK_ARG(p->ctx, p->pending, "no pending scan (gc_pipeline_scan_local)");
+  return down(p, h_record, p->P.send, (size_t)gc::partial_len(p->P.B));
+}
+
+int32_t gc_pipeline_scan_finish(gc_pipeline* p, const double* h_gather) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, p->pending, "no pending scan (gc_pipeline_scan_local)");
+  GC_CHECK_ARG(p->ctx, h_gather || p->P.G == 1 || p->comm,
+               "world_size > 1 needs a communicator or the host-gathered records");
+  gc_ctx* ctx = p->ctx;
+  gc::PipeDev& P = p->P;
+  const int64_t PL = gc::partial_len(P.B);
+  if (h_gather) {  // the G records of this scan, gathered by the caller (rank order)
+    GC_TRY(up(p, P.gather, h_gather, (size_t)PL * P.G));
+  } else if (p->comm) {
+    GC_TRY(gc::comm_allgather(p->comm, ctx, P.send, P.gather, PL));
+  }
+  p->pending = false;
+  GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream));
+  return GC_OK;
+}
+
+int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
+                               double t_scan, double dt_sec, int64_t scan_count) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "the previous scan's exchange is pending (gc_pipeline_scan_finish)");
+  GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS && p->slots[slot].pts, "scan slot not staged");
   GC_CHECK_ARG(p->ctx, p->io_mode == GC_IO_GIVEN || p->slots[slot].odom,
                "GC_IO_COMPUTED needs the slot's odometry (gc_pipeline_stage_odom)");
   gc_ctx* ctx = p->ctx;
@@ -375,10 +421,10 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
   p->sig_cached = true;
-  // a16: partial sums, exchange, fixed-order reduction + IW apply + map update
+  // a16 local part: this rank's partial record (weighted sums, IW statistics, map increment)
   GC_HIP(ctx, gc::launch_combine_local(P, ctx->stream));
-  if (P.G > 1) GC_TRY(gc::comm_allgather(p->comm, ctx, P.send, P.gather, gc::partial_len(P.B)));
-  GC_HIP(ctx, gc::launch_combine_final(P, S, ctx->stream));
+  p->pending_S = S;
+  p->pending = true;
   return GC_OK;
 }
 

@@ -443,8 +443,36 @@ __global__ void k_point_dirs(int64_t rows, const double* __restrict__ pts, doubl
 // is transposed through a wave-private LDS slab one 16-bin block at a time (row stride 18
 // doubles: the 8 lanes of a ds_write_b128 group hit disjoint banks) and leaves as contiguous
 // 128-B row segments, 16 B per lane (FULL: B == 16*BPL) or 8 B per lane (ragged B).
+// One 16-bin block of a wave's 64 normalised rows, from the LDS transpose slab (row stride 18) to
+// HBM as 128-B row segments: 16 B per lane (FULL, B == 16 BPL) or 8 B per lane (ragged B).
+template <int BPL, bool FULL>
+GC_DEV void sa_store_block(const double* S, double* Rh, int64_t wbase, int64_t n, int B, int blk, int lane) {
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
+  constexpr int NB = 16 * BPL, RS = 18;
+  if constexpr (FULL) {
+    // lane writes pieces (point 8m + lane/8, bins 16 blk + 2 (lane%8) +{0,1}); B == NB
+    const int i0 = lane >> 3, q = lane & 7;
+    double* rowp = Rh + (wbase + i0) * NB + 16 * blk + 2 * q;
+    const int64_t lim = n - wbase - i0;
+#pragma unroll
+    for (int m = 0; m < 8; ++m) {
+      const dvec2 v = *reinterpret_cast<const dvec2*>(&S[(i0 + 8 * m) * RS + 2 * q]);
+      if (8 * m < lim) *reinterpret_cast<dvec2*>(rowp + 8 * m * NB) = v;
+    }
+  } else {
+#pragma unroll
+    for (int m = 0; m < 16; ++m) {
+      const int e = lane + 64 * m, i = e >> 4, k = e & 15;
+      const double v = S[i * RS + k];
+      if (wbase + i < n && 16 * blk + k < B) Rh[(wbase + i) * B + 16 * blk + k] = v;
+    }
+  }
+}
 #ifndef GC_SA_OCC
-#define GC_SA_OCC 3  // waves per SIMD the register budget is sized for (tuning knob, probes)
+// 2 waves per SIMD: the 48 similarities / exps of a lane's point stay in registers with no spill
+// (at 3, the 168-VGPR budget spilled ~12-27 VGPRs per point to scratch: 0.6 GB of extra HBM reads and
+// 0.9 GB of extra writes per C3 launch, tools/probe/probe_sa3.hip; 1.74 -> 1.32 ms)
+#define GC_SA_OCC 2
 #endif
 template <int BPL, bool FULL>
 __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
@@ -497,18 +525,18 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
     GC_LOAD_DIRS(wbase + 256)
     const int64_t pt = wbase + lane;
     const bool valid = pt < n;
-    // pass 1: the row maximum of the exact un-fused similarities and the integer bin index; pass 2
-    // recomputes each similarity (bit-identical) and exponentiates x = (S - S_max)/τ, the
-    // reference's jax.nn.softmax shift (binning.py:68-69): any τ > 0 and any direction norm. The
-    // bin directions are wave-uniform LDS reads (broadcast, no bank conflicts).
+    // pass 1: the exact un-fused similarities (kept in ex[]), their row maximum and the integer bin
+    // index; pass 2 exponentiates x = (S - S_max)/τ in place, the reference's jax.nn.softmax shift
+    // (binning.py:68-69): any τ > 0 and any direction norm. The bin directions are wave-uniform LDS
+    // reads (broadcast, no bank conflicts).
+    double ex[NB];
     double best = -1e308;
     int bidx = 0;
-#pragma unroll 8
-    for (int j = 0; j < (FULL ? NB : B); ++j) {
-      const double s = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
-      if (s > best) { best = s; bidx = j; }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      ex[j] = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
+      if ((FULL || j < B) && ex[j] > best) { best = ex[j]; bidx = j; }
     }
-    double ex[NB];
     double Z = 0.0, sl = 0.0;
 #pragma unroll
     for (int j0 = 0; j0 < NB; j0 += 8) {
@@ -516,9 +544,8 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int j = j0 + jj;
-        const double s = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
         // e^-745 underflows to 0 in f64; the clamp keeps the table index in range for tiny τ
-        x[jj] = (FULL || j < B) ? fmax((s - best) * inv_tau, -1000.0) : 0.0;
+        x[jj] = (FULL || j < B) ? fmax((ex[j] - best) * inv_tau, -1000.0) : 0.0;
       }
       double e8[8];
       exp_neg_n<8, false>(x, Tx, e8);
@@ -533,14 +560,13 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
     }
     // the maximal bin has x = 0 and e = 1 exactly: Z >= 1 and max_b R = 1/Z
     const double rZ = recip(Z);
-    const double eb = 1.0;
     if (valid) {
       // entropy of the point: log Z - S/Z - B ε   (-Σ R log(R+ε) up to ≤ B·ε)
       int e;
       zm *= frexp(Z, &e);
       ze += e;
       entq += fma(sl, rZ, Beps);
-      mxr = fmax(mxr, eb * rZ);
+      mxr = fmax(mxr, rZ);
       if (bin_idx) bin_idx[(int64_t)h * n + pt] = bidx;
     }
 #pragma unroll
@@ -550,30 +576,7 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
         *reinterpret_cast<dvec2*>(&S[lane * RS + 2 * q]) =
             dvec2{ex[16 * blk + 2 * q] * rZ, ex[16 * blk + 2 * q + 1] * rZ};
       lds_wave_sync();
-      if constexpr (FULL) {
-        // lane writes pieces (point 8m + lane/8, bins 16 blk + 2 (lane%8) +{0,1}); B == NB
-        const int i0 = lane >> 3, q = lane & 7;
-        double* rowp = Rh + (wbase + i0) * NB + 16 * blk + 2 * q;
-        const int64_t lim = n - wbase - i0;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          const dvec2 v = *reinterpret_cast<const dvec2*>(&S[(i0 + 8 * m) * RS + 2 * q]);
-          if (8 * m < lim) {
-#if GC_NT_RESP
-            __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(rowp + 8 * m * NB));
-#else
-            *reinterpret_cast<dvec2*>(rowp + 8 * m * NB) = v;
-#endif
-          }
-        }
-      } else {
-#pragma unroll
-        for (int m = 0; m < 16; ++m) {
-          const int e = lane + 64 * m, i = e >> 4, k = e & 15;
-          const double v = S[i * RS + k];
-          if (wbase + i < n && 16 * blk + k < B) Rh[(wbase + i) * B + 16 * blk + k] = v;
-        }
-      }
+      sa_store_block<BPL, FULL>(S, Rh, wbase, n, B, blk, lane);
       lds_wave_sync();
     }
     int e;
@@ -1297,7 +1300,7 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
   GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
   GC_CHECK_ARG(ctx, tau > 0.0, "tau must be positive");
   GC_CHECK_ARG(ctx, d_dirs && d_bins && d_resp_out && d_cert_out, "NULL buffer");
-  int iters = 4;
+  int iters = 8;
   while (iters > 1 && ((n + iters * 256 - 1) / (iters * 256)) * (int64_t)H < 4096) iters >>= 1;
   const int64_t blocks = (n + iters * 256 - 1) / (iters * 256);
   void* scr;

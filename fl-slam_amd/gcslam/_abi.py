@@ -72,6 +72,10 @@ SIGNATURES = {
     "gc_pointcloud2_parse": [_vp, _vp, _i64, _i32, _vp, _f64, _dptr, _dptr, _vp, _vp, _vp, _vp, _vp],
     "gc_pipeline_stage_pointcloud2": [_vp, _i32, _vp, _i64, _i32, _vp, _f64, _dptr, _dptr, _vp, _vp, _vp],
     "gc_pipeline_run_scan": [_vp, _i32, _f64, _f64, _f64, _f64, _f64, _i64],
+    "gc_pipeline_scan_local": [_vp, _i32, _f64, _f64, _f64, _f64, _f64, _i64],
+    "gc_pipeline_partial_len": [_vp],
+    "gc_pipeline_get_partial": [_vp, _vp],
+    "gc_pipeline_scan_finish": [_vp, _vp],
     "gc_pipeline_get_combined": [_vp, _vp],
     "gc_pipeline_get_hyp_diag": [_vp, _vp],
     "gc_pipeline_get_lpose6": [_vp, _vp],

@@ -190,6 +190,23 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_run_scan", int(slot), float(scan["scan_start"]), float(scan["scan_end"]),
                    float(scan["t_last"]), float(scan["t_scan"]), float(scan["dt_sec"]), int(scan_count))
 
+    def run_scan_local(self, slot: int, scan: dict, scan_count: int):
+        """a1-a15 for this rank's hypotheses and its partial record; finish with finish_scan."""
+        self._call("gc_pipeline_scan_local", int(slot), float(scan["scan_start"]), float(scan["scan_end"]),
+                   float(scan["t_last"]), float(scan["t_scan"]), float(scan["dt_sec"]), int(scan_count))
+
+    def partial(self) -> np.ndarray:
+        """This rank's partial record of the pending scan (RECORD layout, partial_len(B) doubles)."""
+        o = np.empty(partial_len(self.B))
+        self._call("gc_pipeline_get_partial", _p(o))
+        return o
+
+    def finish_scan(self, gathered: Optional[np.ndarray] = None):
+        """Exchange + combine of the pending scan. gathered: (world_size, partial_len) records in
+        rank order (any transport), or None for the RCCL all-gather / the single-rank record."""
+        g = None if gathered is None else _f(gathered, (self.world, partial_len(self.B)))
+        self._call("gc_pipeline_scan_finish", _p(g))
+
     def combined(self):
         o = np.empty(_abi.GC_COMB_LEN)
         self._call("gc_pipeline_get_combined", _p(o))

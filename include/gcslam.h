@@ -265,9 +265,25 @@ int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_
                                       int32_t point_step, const int32_t* h_fields, double header_stamp,
                                       const double* h_R9, const double* h_t3, const double* h_imu_t,
                                       const double* h_imu_gyro, const double* h_imu_accel);
-/* Enqueue one scan (all local hypotheses, exchange, combine, IW apply, map update). */
+/* Enqueue one scan (all local hypotheses, exchange, combine, IW apply, map update) =
+ * gc_pipeline_scan_local + gc_pipeline_scan_finish(p, NULL). */
 int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
                              double t_scan, double dt_sec, int64_t scan_count);
+/* The two halves of a scan around the per-scan exchange (backend_node.py:2036-2119):
+ *  scan_local   a1-a15 for this rank's hypotheses and its partial record (partial_len doubles:
+ *               weighted L/h/z/μ sums, IW statistics, hypothesis-0 map increment, anchor).
+ *  get_partial  reads that record back (synchronises the stream).
+ *  scan_finish  the exchange and the combine: with h_gather (world_size x partial_len doubles, in
+ *               rank order, gathered by the caller over any transport) the records are uploaded;
+ *               with NULL the pipeline all-gathers over its RCCL communicator (world_size > 1, or a
+ *               single rank with one attached) or reads its own record (one rank, none attached).
+ *               Then the fixed rank-order reduction, barycenter, IW apply, Q and map update.
+ * Every rank ends the scan with a bit-identical combined belief, IW state and map. */
+int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
+                               double t_scan, double dt_sec, int64_t scan_count);
+int32_t gc_pipeline_partial_len(const gc_pipeline* p);
+int32_t gc_pipeline_get_partial(gc_pipeline* p, double* h_record);
+int32_t gc_pipeline_scan_finish(gc_pipeline* p, const double* h_gather);
 int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out);
 int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag);
 /* L_evidence[pose, pose] (Hl, 6, 6) of the last scan, as the reference's MinimalScanTape.L_pose6

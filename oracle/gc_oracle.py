@@ -497,14 +497,17 @@ def kappa_scalar(R, eps_r=EPS_R, d=3.0, r0=KAPPA_R0, tau=KAPPA_TAU):
 
 def moment_sums(points, covs, w, resp, lam, origin):
     """The raw per-bin sums of binning.py:160-173 (sum_cov skipped when covs is None)."""
+    # the three einsums "nb,ni,nj->bij" / "nb,nij->bij" as the (B x N)·(N x 9) products XLA lowers
+    # them to (dot_general), so the CPU baseline runs them through BLAS
     w_r = (w * lam)[:, None] * resp
     d = point_directions(points, origin)
+    n, B = w_r.shape
     N = np.sum(w_r, axis=0)
     s_dir = w_r.T @ d
-    S_sc = np.einsum("nb,ni,nj->bij", w_r, d, d)
+    S_sc = (w_r.T @ (d[:, :, None] * d[:, None, :]).reshape(n, 9)).reshape(B, 3, 3)
     sum_p = w_r.T @ points
-    sum_ppT = np.einsum("nb,ni,nj->bij", w_r, points, points)
-    sum_cov = np.zeros_like(sum_ppT) if covs is None else np.einsum("nb,nij->bij", w_r, covs)
+    sum_ppT = (w_r.T @ (points[:, :, None] * points[:, None, :]).reshape(n, 9)).reshape(B, 3, 3)
+    sum_cov = np.zeros_like(sum_ppT) if covs is None else (w_r.T @ covs.reshape(n, 9)).reshape(B, 3, 3)
     return N, s_dir, S_sc, sum_p, sum_ppT, sum_cov
 
 

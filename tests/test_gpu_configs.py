@@ -115,15 +115,20 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed):
             _close(bcert[i, 4], r["assign"]["avg_entropy"], 1e-9, 0, f"{tag} avg entropy")
             _close(diag[i, 24:27], O.so3_log(r["mf"]["R_mf"]), 1e-7, 1e-10, f"{tag} R_mf")
             _close(diag[i, 21:24], r["planar"]["t_wls"], 1e-7, 1e-10, f"{tag} t_wls")
-            _close(diag[i, 6], r["T"], 1e-8, 1e-10, f"{tag} T")
-            _close(diag[i, 18], r["mf"]["trig"], 1e-8, 1e-12, f"{tag} MF trigger")
-            _close(diag[i, 19], r["planar"]["trig"], 1e-8, 1e-12, f"{tag} planar trigger")
+            # certificate magnitudes: a PSD projection whose clamp is inactive reports the rounding of
+            # the reference's V diag(λ) Vᵀ as its delta (~1e-16 ||M|| per entry, LAPACK-dependent);
+            # the device certifies SPD by Cholesky and reports 0 for it. At 64k points ||L_post||
+            # reaches ~1e8, so T (the sum over every certificate) carries up to ~1e-7 relative of
+            # that rounding; each 3x3 cert (MF, planar, moment Σ_p) up to ~1e-10 absolute
+            _close(diag[i, 6], r["T"], 1e-7, 1e-10, f"{tag} T")
+            _close(diag[i, 18], r["mf"]["trig"], 0, 1e-9, f"{tag} MF trigger")
+            _close(diag[i, 19], r["planar"]["trig"], 0, 1e-9, f"{tag} planar trigger")
             _close(diag[i, 8], r["alpha"], 0, 1e-12, f"{tag} alpha")
             _close(diag[i, 9:11], [r["s_dt"], r["s_ex"]], 0, 1e-12, f"{tag} excitation scales")
             _close(diag[i, 13], r["cond6"], 1e-6, 0, f"{tag} cond_pose6")
-            _close(bcert[i, 2], r["moments"]["psd_delta"], 1e-8, 1e-14, f"{tag} moment psd delta")
+            _close(bcert[i, 2], r["moments"]["psd_delta"], 0, 1e-10, f"{tag} moment psd delta")
             _close(bcert[i, 3], r["moments"]["max_eps_ratio"], 1e-8, 1e-300, f"{tag} moment mass-eps ratio")
-            _close(bcert[i, 7], r["moments"]["trig"], 1e-8, 1e-14, f"{tag} moment trigger")
+            _close(bcert[i, 7], r["moments"]["trig"], 0, 1e-10, f"{tag} moment trigger")
             _close(diag[i, 7], r["beta"], 0, 1e-10, f"{tag} beta")
             b = r["belief"]
             _close(diag[i, 0:6], r["pose"], 0.0, 1e-6, f"{tag} world pose")             # north-star bar
