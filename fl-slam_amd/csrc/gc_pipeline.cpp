@@ -430,7 +430,23 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
 
 int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out) {
   GC_CHECK_ARG(nullptr, p && h_out, "NULL argument");
-  return down(p, h_out, p->P.comb, GC_COMB_LEN);
+  GC_TRY(down(p, h_out, p->P.comb, GC_COMB_LEN));
+  double* cc = h_out + 484 + 22 + 22 + 6;
+  if (cc[2] != cc[2]) {
+    // the combine certified the barycenter PSD by Cholesky (the projection is then the identity and
+    // its eigen-decomposition was skipped on the scan path); the reference's ConditioningCert of the
+    // combined belief (hypothesis.py:186-202) is the clamped spectrum of that same matrix, computed
+    // here on demand by the Jacobi projection of the stored combined L
+    double* ws = nullptr;
+    GC_HIP(p->ctx, hipMalloc((void**)&ws, sizeof(double) * (484 + 6)));
+    int32_t rc = gc_domain_projection_psd_batch(p->ctx, 1, 22, p->P.comb, p->P.eps_psd, ws, ws + 484);
+    double c6[6];
+    if (rc == GC_OK) rc = down(p, c6, ws + 484, 6);
+    (void)hipFree(ws);
+    if (rc != GC_OK) return rc;
+    cc[2] = c6[2]; cc[3] = c6[3]; cc[4] = c6[4]; cc[5] = c6[5];
+  }
+  return GC_OK;
 }
 
 int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag) {

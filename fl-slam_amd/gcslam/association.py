@@ -21,7 +21,7 @@ from typing import Dict, List, Optional, Tuple
 import numpy as np
 
 from . import _abi
-from .certificates import CertBundle, ComputeCert, ExpectedEffect, InfluenceCert, SupportCert
+from .certificates import CertBundle, ComputeCert, ExpectedEffect, InfluenceCert, OTCert, SupportCert
 from .constants import GC_CHART_ID, GC_EPS_LIFT, GC_EPS_MASS, GC_RECENCY_DECAY_LAMBDA
 from .primitive_map import DevicePrimitiveMap
 
@@ -134,30 +134,6 @@ class PrimitiveAssociationResult:
     candidate_slots: np.ndarray
     row_masses: np.ndarray
     cost_matrix: np.ndarray
-
-
-@dataclass
-class OTCert:
-    """The OT block of the reference's cert (primitive_association.py:524-544)."""
-    marginal_defect_a: float = 0.0
-    marginal_defect_b: float = 0.0
-    transport_mass_total: float = 0.0
-    dual_gap_proxy: float = 0.0
-    sum_a: float = 0.0
-    sum_b: float = 0.0
-    sum_m: float = 0.0
-    sum_novel: float = 0.0
-    p95_a: float = 0.0
-    p95_b: float = 0.0
-    nonzero_a: int = 0
-    nonzero_b: int = 0
-    epsilon: float = 0.0
-    tau_a: float = 0.0
-    tau_b: float = 0.0
-    n_iters: int = 0
-    b_policy: str = "uniform"
-    b_recency_decay_lambda: float = 0.0
-    b_recency_p95: float = 0.0
 
 
 def _p95(x: np.ndarray) -> float:

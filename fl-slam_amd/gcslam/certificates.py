@@ -12,6 +12,8 @@ from __future__ import annotations
 from dataclasses import dataclass, field, fields, replace
 from typing import Any, Dict, List, Optional
 
+import numpy as np
+
 
 def _as_dict(obj) -> Dict[str, Any]:
     return {f.name: getattr(obj, f.name) for f in fields(obj)}
@@ -125,6 +127,59 @@ class ComputeCert:
         return d
 
 
+@dataclass
+class OTCert:
+    """OT association block (certificates.py OTCert; filled by primitive_association.py:524-544)."""
+    marginal_defect_a: float = 0.0
+    marginal_defect_b: float = 0.0
+    transport_mass_total: float = 0.0
+    dual_gap_proxy: float = 0.0
+    sum_a: float = 0.0
+    sum_b: float = 0.0
+    sum_m: float = 0.0
+    sum_novel: float = 0.0
+    p95_a: float = 0.0
+    p95_b: float = 0.0
+    nonzero_a: int = 0
+    nonzero_b: int = 0
+    epsilon: float = 0.0
+    tau_a: float = 0.0
+    tau_b: float = 0.0
+    n_iters: int = 0
+    b_policy: str = "uniform"
+    b_recency_decay_lambda: float = 0.0
+    b_recency_p95: float = 0.0
+
+    to_dict = _as_dict
+
+
+@dataclass
+class MapUpdateCert:
+    """Map-maintenance block (certificates.py MapUpdateCert)."""
+    n_active_tiles: int = 0
+    tile_ids_active: List[int] = field(default_factory=list)
+    n_inactive_tiles: int = 0
+    tile_ids_inactive: List[int] = field(default_factory=list)
+    tile_cache_hits: int = 0
+    tile_cache_misses: int = 0
+    candidate_tiles_per_meas_mean: float = 0.0
+    candidate_primitives_per_meas_mean: float = 0.0
+    candidate_primitives_per_meas_p95: float = 0.0
+    insert_count_total: int = 0
+    insert_mass_total: float = 0.0
+    insert_mass_p95: float = 0.0
+    evicted_count: int = 0
+    evicted_mass_total: float = 0.0
+    fused_count: int = 0
+    fused_mass_total: float = 0.0
+    merged_count: int = 0
+    staleness_inflation_strength: float = 0.0
+    staleness_cov_inflation_trace: float = 0.0
+    stale_precision_downscale_total: float = 0.0
+
+    to_dict = _as_dict
+
+
 _TRIGGER_UNIT = ("dt_scale", "extrinsic_scale", "trust_alpha", "power_beta")
 _TRIGGER_ADD = ("lift_strength", "psd_projection_delta", "nu_projection_delta",
                 "mass_epsilon_ratio", "anchor_drift_rho")
@@ -150,8 +205,8 @@ class CertBundle:
     influence: InfluenceCert = field(default_factory=InfluenceCert)
     overconfidence: OverconfidenceCert = field(default_factory=OverconfidenceCert)
     compute: ComputeCert = field(default_factory=ComputeCert)
-    ot: Optional[Any] = None
-    map_update: Optional[Any] = None
+    ot: Optional["OTCert"] = None
+    map_update: Optional["MapUpdateCert"] = None
 
     @classmethod
     def create_exact(cls, chart_id: str, anchor_id: str, **parts) -> "CertBundle":
@@ -214,6 +269,48 @@ def aggregate_certificates(certs: List[CertBundle]) -> CertBundle:
     triggers: List[str] = []
     for c in certs:
         triggers.extend(c.approximation_triggers)
+
+    def nelem(shape) -> int:  # ranking key of largest_tensor_shape (non-integer entries rank 0)
+        try:
+            return int(np.prod([int(v) for v in shape])) if len(shape) else 0
+        except (TypeError, ValueError):
+            return 0
+
+    comp = [c.compute for c in certs]
+    dev = [cc.device_runtime for cc in comp]
+    compute = ComputeCert(
+        alloc_bytes_est=max(cc.alloc_bytes_est for cc in comp),
+        largest_tensor_shape=max((cc.largest_tensor_shape for cc in comp), key=nelem),
+        segment_sum_k=max(cc.segment_sum_k for cc in comp),
+        psd_projection_count=max(cc.psd_projection_count for cc in comp),
+        chol_solve_count=max(cc.chol_solve_count for cc in comp),
+        scan_io=max((cc.scan_io for cc in comp), key=lambda io: io.scan_seq),  # latest scan, first on ties
+        device_runtime=DeviceRuntimeCert(max(d.host_sync_count_est for d in dev),
+                                         max(d.device_to_host_bytes_est for d in dev),
+                                         max(d.host_to_device_bytes_est for d in dev),
+                                         max(d.jit_recompile_count for d in dev)))
+    ots = [c.ot for c in certs if c.ot is not None]
+    ot = None
+    if ots:  # maxima of defects / p95s, sums of masses and counts, parameters of the first
+        o0 = ots[0]
+        mx = ("marginal_defect_a", "marginal_defect_b", "dual_gap_proxy", "p95_a", "p95_b", "b_recency_p95")
+        sm = ("transport_mass_total", "sum_a", "sum_b", "sum_m", "sum_novel", "nonzero_a", "nonzero_b")
+        ot = replace(o0, **{k: max(getattr(o, k) for o in ots) for k in mx},
+                     **{k: sum(getattr(o, k) for o in ots) for k in sm})
+    mus = [c.map_update for c in certs if c.map_update is not None]
+    mu = None
+    if mus:  # union of tile ids, sums of counts / masses, maxima of rates and strengths
+        act = sorted(set(i for m in mus for i in m.tile_ids_active))
+        ina = sorted(set(i for m in mus for i in m.tile_ids_inactive))
+        sm = ("tile_cache_hits", "tile_cache_misses", "insert_count_total", "insert_mass_total", "evicted_count",
+              "evicted_mass_total", "fused_count", "fused_mass_total", "merged_count",
+              "stale_precision_downscale_total")
+        mx = ("candidate_tiles_per_meas_mean", "candidate_primitives_per_meas_mean",
+              "candidate_primitives_per_meas_p95", "insert_mass_p95", "staleness_inflation_strength",
+              "staleness_cov_inflation_trace")
+        mu = MapUpdateCert(n_active_tiles=len(act), tile_ids_active=act, n_inactive_tiles=len(ina),
+                           tile_ids_inactive=ina, **{k: sum(getattr(m, k) for m in mus) for k in sm},
+                           **{k: max(getattr(m, k) for m in mus) for k in mx})
     return CertBundle(
         chart_id=c0.chart_id, anchor_id=c0.anchor_id, exact=all(c.exact for c in certs),
         approximation_triggers=triggers, frobenius_applied=any(c.frobenius_applied for c in certs),
@@ -227,4 +324,4 @@ def aggregate_certificates(certs: List[CertBundle]) -> CertBundle:
                               sum(col(("mismatch", "directional_score"))) / n),
         excitation=ExcitationCert(max(col(("excitation", "dt_effect"))),
                                   max(col(("excitation", "extrinsic_effect")))),
-        influence=inf, overconfidence=over)
+        influence=inf, overconfidence=over, compute=compute, ot=ot, map_update=mu)

@@ -216,7 +216,9 @@ typedef struct {
 #define GC_HYP_DIAG 40
 /* combined output (GC_COMB_LEN): L 484, h 22, z_lin 22, X_anchor(hyp 0) 6, then
  * [stamp, psd_delta, eig_min, eig_max, cond, nnc, ess, support_frac, mass_eps_ratio,
- *  floor_adjustment, spread_proxy, 5 pad] */
+ *  floor_adjustment, spread_proxy, 5 pad]. The conditioning fields are always filled: when the
+ *  scan path certified the barycenter PSD by Cholesky, gc_pipeline_get_combined computes them from
+ *  the stored combined L on demand (one extra launch, off the scan path). */
 #define GC_COMB_LEN (484 + 22 + 22 + 6 + 16)
 
 int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const double* h_cfg, gc_pipeline** out);

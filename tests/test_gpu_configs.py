@@ -150,6 +150,12 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed):
         _close(c["h"], comb["h"], 1e-10, 1e-12, f"scan{k} combined h")
         _close(c["z_lin"], comb["z_lin"], 1e-10, 1e-12, f"scan{k} combined z_lin")
         _close(c["X_anchor"], bel["X_anchor"][0], 0.0, 0.0, f"scan{k} combined anchor = hypothesis 0")
+        # the combined belief's ConditioningCert (hypothesis.py:186-202): eigenvalue extremes of the
+        # projected barycenter (absolute accuracy ~1e-12 of the largest), near-null count exact
+        pc = comb["psd_cert"]
+        _close(c["eig_max"], pc[3], 1e-10, 0.0, f"scan{k} combined eig_max")
+        _close(c["eig_min"], pc[2], 0.0, 1e-12 * pc[3], f"scan{k} combined eig_min")
+        _close(c["near_null"], pc[5], 0.0, 0.0, f"scan{k} combined near-null count")
         Sc = _cov(comb["L"])
         _close(_cov(c["L"])[0:6, 0:6], Sc[0:6, 0:6], 0.0, 1e-6, f"scan{k} combined pose covariance")
         # IW apply from the GPU's per-hypothesis statistics of ALL hypotheses
