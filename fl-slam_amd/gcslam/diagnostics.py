@@ -5,8 +5,8 @@ process_scan_single_hypothesis (backend/pipeline.py:1527-1570), RuntimeManifest
 
 The tape fields come from the batched pipeline's device diagnostics of one hypothesis (hyp_diag,
 lpose6, bin cert); the file formats (JSONL, npz) match the reference's so its tools read them.
-Fields the device pipeline does not evaluate keep the reference's defaults and are listed in
-TAPE_NOT_COMPUTED."""
+Every field of the reference tape is filled (TAPE_NOT_COMPUTED is empty); the certificate-summary
+fields follow the static cert list of the bin-path wiring (BIN_PATH_CERTS)."""
 
 from __future__ import annotations
 
@@ -99,9 +99,50 @@ _LOAD_DEFAULTS = dict(cert_exact=True, influence_dt_scale=1.0, influence_extrins
 # npz array names that differ from the field names (diagnostics.py:216-222)
 _NPZ_NAME = dict(scan_number="scan_numbers", timestamp="timestamps", dt_sec="dt_secs")
 
-# reference tape fields the device pipeline does not evaluate (defaults kept)
-TAPE_NOT_COMPUTED = ("cert_n_triggers", "mismatch_directional_score", "overconfidence_ess_to_excitation",
-                     "overconfidence_cond_to_support")
+# reference tape fields the device pipeline does not evaluate (defaults kept): none
+TAPE_NOT_COMPUTED = ()
+
+# The per-hypothesis certificate list of the bin-path wiring, in pipeline.py's all_certs order
+# (:379-1502 with the legacy bin operators in the map-branch slot): (operator, approximation trigger
+# names, MismatchCert.directional_score). Trigger names are fixed per operator in the reference;
+# "vmf" marks the time-resolved vMF gravity cert, whose directional score is its resultant R̄
+# (imu_evidence.py:518-535; its kappa_from_resultant_v2 trigger is appended, :521).
+BIN_PATH_CERTS = (
+    ("point_budget_resample", ("PointBudgetResample",), 1.0),
+    ("predict_diffusion", ("PredictDiffusion",), 1.0),
+    ("deskew_constant_twist", (), 1.0),
+    ("odom_quadratic_evidence", ("OdomEvidenceGaussian",), 0.0),
+    ("imu_vmf_gravity_evidence_time_resolved",
+     ("ImuAccelDirectionTimeResolved", "TransportConsistencyWeighting", "KappaLowRApproximation"), "vmf"),
+    ("imu_dependence_inflation", ("ImuDependenceInflation",), 1.0),
+    ("imu_gyro_rotation_evidence", ("ImuGyroRotationGaussian",), 0.0),
+    ("imu_preintegration_factor", ("ImuPreintegrationVelPos",), 0.0),
+    ("planar_z_prior", ("PlanarZPrior",), 1.0),
+    ("velocity_z_prior", ("VelocityZPrior",), 1.0),
+    ("odom_velocity_evidence", ("OdomVelocityEvidence",), 1.0),
+    ("odom_yawrate_evidence", ("OdomYawRateEvidence",), 1.0),
+    ("pose_twist_kinematic_consistency", ("PoseTwistKinematicConsistency",), 1.0),
+    ("odom_dependence_inflation", ("OdomDependenceInflation",), 1.0),
+    ("bin_soft_assign", (), 1.0),
+    ("scan_bin_moment_match", ("ScanBinMomentMatch",), 1.0),
+    ("matrix_fisher_rotation_evidence", ("MatrixFisherRotationEvidence",), 1.0),
+    ("planar_translation_evidence", ("PlanarTranslationEvidence",), 1.0),
+    ("power_tempering", ("PowerTempering",), 1.0),
+    ("excitation_prior_scaling", ("ExcitationPriorScaling",), 1.0),
+    ("fusion_scale_from_certificates", (), 1.0),
+    ("info_fusion_additive", ("InfoFusionAdditive",), 1.0),
+    ("pose_update_frobenius_recompose", ("PoseUpdateFrobeniusRecompose",), 1.0),
+    ("pose_cov_inflation_pushforward", (), 1.0),
+    ("anchor_drift_update", ("AnchorDriftUpdate",), 1.0),
+)
+
+
+def cert_summary(vmf_rbar: float = 1.0):
+    """(cert_n_triggers, mismatch_directional_score) of aggregate_certificates over BIN_PATH_CERTS:
+    the concatenated trigger lists and the mean directional score (certificates.py:531-556)."""
+    n = sum(len(t) for _, t, _ in BIN_PATH_CERTS)
+    ds = [vmf_rbar if d == "vmf" else d for _, _, d in BIN_PATH_CERTS]
+    return n, float(sum(ds) / len(ds))
 
 
 @dataclass
@@ -189,19 +230,26 @@ def tape_from_pipeline(pipe, scan_number: int, timestamp: float, dt_sec: float, 
     lp = pipe.lpose6()[hyp]
     bin_cert = pipe.bin_stats()[1][hyp]
     tm = timing_ms or {}
+    # R̄ of the vMF gravity factor when the IMU/odom branch ran on the device (GC_IO_PARTS [11])
+    rbar = float(pipe.io_parts()[hyp][11]) if getattr(pipe, "io_computed", True) else 1.0
+    n_trig, dir_score = cert_summary(rbar)
+    # the FusionScale cert is the only one setting these two sentinels, so the aggregate's max is
+    # its value (fusion.py:121-130): ESS / (excitation + ε_mass), cond / (support + ε_mass)
+    ess_to_exc = float(d[14]) / (float(d[37]) + K.GC_EPS_MASS)
+    cond_to_sup = float(d[13]) / (float(d[36]) + K.GC_EPS_MASS)
     return MinimalScanTape(
         scan_number=int(scan_number), timestamp=float(timestamp), dt_sec=float(dt_sec),
         n_points_raw=int(n_points_raw), n_points_budget=int(n_points_budget), fusion_alpha=float(d[8]),
         cond_pose6=float(d[13]), conditioning_number=float(d[13]), eigmin_pose6=float(d[39]), L_pose6=lp,
         total_trigger_magnitude=float(d[6]), cert_exact=bool(d[6] == 0.0), cert_frobenius_applied=bool(d[12] > 0.0),
-        cert_n_triggers=0, support_ess_total=float(d[14]), support_frac=float(d[36]),
-        mismatch_nll_per_ess=float(d[17]), mismatch_directional_score=1.0, excitation_dt_effect=float(d[9]),
+        cert_n_triggers=n_trig, support_ess_total=float(d[14]), support_frac=float(d[36]),
+        mismatch_nll_per_ess=float(d[17]), mismatch_directional_score=dir_score, excitation_dt_effect=float(d[9]),
         excitation_extrinsic_effect=float(d[10]), influence_psd_projection_delta=float(d[20]),
         influence_mass_epsilon_ratio=float(bin_cert[3]), influence_anchor_drift_rho=float(d[11]),
         influence_dt_scale=float(1.0 - d[9]), influence_extrinsic_scale=float(1.0 - d[10]),
         influence_trust_alpha=float(d[8]), influence_power_beta=float(d[7]),
-        overconfidence_excitation_total=float(d[37]), overconfidence_ess_to_excitation=0.0,
-        overconfidence_cond_to_support=0.0, overconfidence_dt_asymmetry=float(d[15]),
+        overconfidence_excitation_total=float(d[37]), overconfidence_ess_to_excitation=ess_to_exc,
+        overconfidence_cond_to_support=cond_to_sup, overconfidence_dt_asymmetry=float(d[15]),
         overconfidence_z_to_xy_ratio=float(d[16]),
         **{f"t_{k}": float(v) for k, v in tm.items() if f"t_{k}" in _TYPES})
 

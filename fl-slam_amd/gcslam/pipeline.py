@@ -94,6 +94,7 @@ class BatchedScanPipeline:
         _abi.call("gc_pipeline_create", self.ctx.handle, C.addressof(d), cfgv.ctypes.data, C.byref(h), ctx=self.ctx)
         self.handle = h.value
         self._comm = None
+        self.io_computed = True  # GC_IO_COMPUTED is the device default
         self.set_bins(create_fibonacci_atlas(self.B).dirs)
         self.set_weights(np.full(H_total, 1.0 / H_total))
 
@@ -123,9 +124,11 @@ class BatchedScanPipeline:
         """Given (synthetic) IMU/odom-branch evidence; selects GC_IO_GIVEN."""
         self._call("gc_pipeline_set_io_evidence", _p(_f(L, (self.Hl, 22, 22))), _p(_f(h, (self.Hl, 22))),
                    _p(_f(cert, (self.Hl, _abi.GC_IO_CERT))))
+        self.io_computed = False
 
     def set_io_mode(self, computed: bool):
         self._call("gc_pipeline_set_io_mode", _abi.GC_IO_COMPUTED if computed else _abi.GC_IO_GIVEN)
+        self.io_computed = bool(computed)
 
     def io_evidence(self):
         """(L_io (Hl,22,22), h_io (Hl,22), cert (Hl,10)) of the last scan."""

@@ -106,3 +106,45 @@ def test_gpu_tape_from_pipeline_matches_oracle(ctx, tmp_path):
         log.append_tape(t)
     log.save_jsonl(str(tmp_path / "g.jsonl"))
     assert DiagnosticsLog.load_jsonl(str(tmp_path / "g.jsonl")).total_scans == 3
+
+
+def test_cert_summary_of_the_bin_path_wiring():
+    """cert_n_triggers / mismatch_directional_score of aggregate_certificates over the wiring's cert
+    list: 23 trigger names over 25 certs; only the vMF cert's R̄ varies (odom, gyro and preint
+    factor certs score 0, the rest keep the default 1)."""
+    from gcslam.diagnostics import BIN_PATH_CERTS, TAPE_NOT_COMPUTED, cert_summary
+    assert TAPE_NOT_COMPUTED == () and len(BIN_PATH_CERTS) == 25
+    n, d = cert_summary(0.4)
+    assert n == 23 and abs(d - (21.0 + 0.4) / 25.0) < 1e-15
+
+
+@pytest.mark.gpu
+def test_gpu_tape_certificate_summary_fields(ctx):
+    """The four certificate-summary fields on a device scan with the IMU/odom branch computed:
+    directional score from the branch's vMF R̄ (checked against the oracle), the FusionScale
+    sentinels ESS/(excitation + ε) and cond/(support + ε) (fusion.py:121-130)."""
+    from gcslam.diagnostics import tape_from_pipeline
+    from gcslam.pipeline import BatchedScanPipeline, PipelineConfig
+    from oracle import cases
+    case = cases.build(H=2, n_az=256, n_scans=1, io="computed")
+    s = case["scans"][0]
+    pipe = BatchedScanPipeline(2, case["n"], PipelineConfig(n_points_cap=case["n"]), ctx=ctx)
+    hy = case["hyp"]
+    pipe.set_beliefs(hy["X_anchor"], hy["z_lin"], hy["L"], hy["h"], hy["stamp"])
+    pipe.set_weights(hy["weights"])
+    pipe.set_io_mode(True)
+    pipe.set_iw(*case["iw"])
+    pipe.set_map(case["map_record"])
+    pipe.stage_scan(0, s)
+    pipe.run_scan(0, s, 0)
+    ctx.sync()
+    st, comb, res = O.process_scan(case["state"], cases.scan_input(s), None, case["bins"], case["cfg"])
+    d = pipe.hyp_diag()
+    for h in range(2):
+        t = tape_from_pipeline(pipe, 0, s["scan_end"], 0.1, case["n"], case["n"], hyp=h)
+        rbar = res[h]["io_parts"]["imu"]["Rbar"]
+        assert t.cert_n_triggers == 23
+        assert abs(t.mismatch_directional_score - (21.0 + rbar) / 25.0) < 1e-12
+        assert t.overconfidence_ess_to_excitation == d[h, 14] / (d[h, 37] + 1e-12)
+        assert abs(t.overconfidence_cond_to_support - res[h]["cond6"] / (d[h, 36] + 1e-12)) <= 1e-6 * abs(
+            t.overconfidence_cond_to_support)
