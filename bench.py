@@ -29,6 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
+PROFILE_ROUNDS = ("r02", "r01")  # committed rocprofv3 summaries (profiles/<round>/), newest first
 
 
 def parse():
@@ -224,13 +225,13 @@ def measured_traffic(H, n, B):
     """HBM bytes per launch of the contract pair from the committed rocprofv3 PMC summary
     (tools/pmc_traffic.sh; FETCH_SIZE doubled per the gfx950 correction, plus WRITE_SIZE), when it
     was collected at this exact shape; None otherwise."""
-    f = os.path.join(ROOT, "profiles", "r01", "pmc_traffic.json")
-    if not os.path.exists(f):
-        return None
-    t = json.load(open(f))
-    if (t.get("H"), t.get("n"), t.get("B")) != (H, n, B):
-        return None
-    return t
+    for rnd in PROFILE_ROUNDS:  # the newest round's summary first
+        f = os.path.join(ROOT, "profiles", rnd, "pmc_traffic.json")
+        if os.path.exists(f):
+            t = json.load(open(f))
+            if (t.get("H"), t.get("n"), t.get("B")) == (H, n, B):
+                return t
+    return None
 
 
 def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=3):
