@@ -195,16 +195,17 @@ int main() {
   double *p, *t, *w, *bs, *xi, *bins, *part;
   hipMalloc(&p, 8 * 3 * n); hipMalloc(&t, 8 * n); hipMalloc(&w, 8 * n); hipMalloc(&bs, 64);
   hipMalloc(&xi, 8 * 6 * H); hipMalloc(&bins, 8 * 3 * B);
-  const int iters = 8; const int64_t chunks = (n + iters * 256 - 1) / (iters * 256);
+  const int iters = 16; const int64_t chunks = (n + iters * 256 - 1) / (iters * 256);
   const int RL = B * gc::NF_BASE + gc::REC_EXTRA;
   hipMalloc(&part, sizeof(double) * (size_t)H * chunks * RL);
   hipMemcpy(p, hp.data(), 8 * 3 * n, hipMemcpyHostToDevice); hipMemcpy(t, ht.data(), 8 * n, hipMemcpyHostToDevice);
   hipMemcpy(w, hw.data(), 8 * n, hipMemcpyHostToDevice); hipMemcpy(bs, hs.data(), 64, hipMemcpyHostToDevice);
   hipMemcpy(xi, hx.data(), 8 * 6 * H, hipMemcpyHostToDevice); hipMemcpy(bins, hb.data(), 8 * 3 * B, hipMemcpyHostToDevice);
-  const size_t sh = sizeof(double) * std::max<size_t>(4 * gc::kFusedFS * (gc::NF_BASE + 4) + gc::kExpTab + 192, 4 * (size_t)B * gc::NF_BASE + 12);
+  const size_t sh = sizeof(double) * std::max<size_t>(4 * gc::kFusedFS * (gc::NF_BASE + 4) + gc::kExpTab2 + 192, 4 * (size_t)B * gc::NF_BASE + 12);
+  hipFuncSetAttribute((const void*)gc::k_bins_fused<3, true>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh);
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   auto run = [&] { hipLaunchKernelGGL((gc::k_bins_fused<3, true>), dim3(chunks, H), dim3(256), sh, 0, n, B, iters, p, t, w, bs, 100.0, 100.1, xi, bins, 10.0, -0.06, -0.1, 0.1, part); };
-  run(); hipDeviceSynchronize();
+  for (int w = 0; w < 20; ++w) run(); hipDeviceSynchronize();
   hipEventRecord(e0); for (int r = 0; r < 10; ++r) run(); hipEventRecord(e1); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
   printf("k_bins_fused<3> occ=%d nacc=%d: %.3f ms/launch (%s)\n", GC_FUSED_OCC, GC_FUSED_NACC, ms / 10, hipGetErrorString(hipGetLastError()));
