@@ -132,7 +132,7 @@ def main():
         d0 = {k: _abi.DeviceArray.from_host(ctx, s0[k]) for k in ("points", "timestamps", "weights")}
         dbins = _abi.DeviceArray.from_host(ctx, create_fibonacci_atlas(GC_B_BINS).dirs)
         r = roofline_leg(ctx, _abi, s0, d0, xi, dbins, GC_B_BINS, s0["points"].shape[0], H_total,
-                         np.asarray(T_BASE_LIDAR[:3]), reps=args.roofline_reps, warm=2)
+                         np.asarray(T_BASE_LIDAR[:3]), reps=args.roofline_reps)
         print(json.dumps({"roofline": r}), flush=True)
         return
     B = GC_B_BINS
@@ -234,7 +234,7 @@ def measured_traffic(H, n, B):
     return None
 
 
-def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=3):
+def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=8):
     """BinSoftAssign + ScanBinMomentMatch contract kernels over H hypotheses, HBM-bound."""
     from gcslam.constants import GC_TAU_SOFT_ASSIGN
     dxi = _abi.DeviceArray.from_host(ctx, xi)
@@ -249,20 +249,28 @@ def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=3):
     covs = _abi.DeviceArray(ctx, (H, n, 9)); covs.zero()
     lam = _abi.DeviceArray.from_host(ctx, np.ones((H, n)))
     st = _abi.DeviceArray(ctx, (H, B, 38)); ce = _abi.DeviceArray(ctx, (H, 8))
-    ev = [_abi.Event(ctx) for _ in range(3)]
-    t_sa, t_mm = [], []
-    for r in range(reps + warm):
-        ev[0].record()
+    # the pair back to back, reps times after warm untimed pairs (steady-state clocks, no host sync
+    # between launches); one event before each kernel and one after the last, read after one sync
+    def pair(r):
         _abi.call("gc_bin_soft_assign", ctx.handle, H, n, B, dirs.ptr, dbins.ptr, GC_TAU_SOFT_ASSIGN, resp.ptr,
                   idx.ptr, sac.ptr, ctx=ctx)
-        ev[1].record()
+        ev[2 * r + 1].record()
         _abi.call("gc_scan_bin_moment_match", ctx.handle, H, n, B, pts.ptr, covs.ptr, w.ptr, resp.ptr, lam.ptr, op,
                   1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
-        ev[2].record()
-        ctx.sync()
-        if r >= warm:
-            t_sa.append(ev[0].elapsed_ms(ev[1]))
-            t_mm.append(ev[1].elapsed_ms(ev[2]))
+        ev[2 * r + 2].record()
+
+    ev = [_abi.Event(ctx) for _ in range(2 * reps + 1)]
+    for r in range(warm):
+        _abi.call("gc_bin_soft_assign", ctx.handle, H, n, B, dirs.ptr, dbins.ptr, GC_TAU_SOFT_ASSIGN, resp.ptr,
+                  idx.ptr, sac.ptr, ctx=ctx)
+        _abi.call("gc_scan_bin_moment_match", ctx.handle, H, n, B, pts.ptr, covs.ptr, w.ptr, resp.ptr, lam.ptr, op,
+                  1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
+    ev[0].record()
+    for r in range(reps):
+        pair(r)
+    ctx.sync()
+    t_sa = [ev[2 * r].elapsed_ms(ev[2 * r + 1]) for r in range(reps)]
+    t_mm = [ev[2 * r + 1].elapsed_ms(ev[2 * r + 2]) for r in range(reps)]
     ms_sa, ms_mm = float(np.mean(t_sa)), float(np.mean(t_mm))
     b_sa, b_mm = H * bytes_soft_assign(n, B), H * bytes_moment_match(n, B)
     ach = (b_sa + b_mm) / ((ms_sa + ms_mm) * 1e-3) / 1e9
@@ -280,7 +288,7 @@ FP64_PEAK_TFS = 78.6  # MI355X FP64 vector = FP64 matrix peak (16 lanes x FMA pe
 FUSED_FLOP_PER_POINT_BIN = 76  # 5 (dot) + 1 (exp) + 2 (normalise) + 34 x 2 (moment FMAs)
 
 
-def fused_roofline_leg(ctx, _abi, s, B, n, H, bins, origin, reps=10, warm=3):
+def fused_roofline_leg(ctx, _abi, s, B, n, H, bins, origin, reps=10, warm=10):
     """The product's dominant kernel, k_bins_fused (a1->a4->a5->a6 fused, responsibilities in
     registers): FP64-issue-bound, so its roofline is flops against the FP64 peak. Timed with HIP
     events on the library stream around gc_scan_bins_fused (the fused kernel + its ~1 % finalize)."""
@@ -293,18 +301,20 @@ def fused_roofline_leg(ctx, _abi, s, B, n, H, bins, origin, reps=10, warm=3):
     dx, db = _abi.DeviceArray.from_host(ctx, xi), _abi.DeviceArray.from_host(ctx, bins)
     st, ce = _abi.DeviceArray(ctx, (H, B, 38)), _abi.DeviceArray(ctx, (H, 8))
     oa, op = _abi.f64p(origin)
-    ev = [_abi.Event(ctx) for _ in range(2)]
-    ts = []
-    for r in range(reps + warm):
-        ev[0].record()
+    def launch():
         _abi.call("gc_scan_bins_fused", ctx.handle, H, n, n, B, d["points"].ptr, d["timestamps"].ptr,
                   d["weights"].ptr, scal.ptr, s["scan_start"], s["scan_end"], dx.ptr, db.ptr, GC_TAU_SOFT_ASSIGN, op,
                   1e-12, 1e-12, st.ptr, ce.ptr, 0, ctx=ctx)
-        ev[1].record()
-        ctx.sync()
-        if r >= warm:
-            ts.append(ev[0].elapsed_ms(ev[1]))
-    ms = float(np.mean(ts))
+
+    for _ in range(warm):  # back to back (steady-state clocks), then reps launches between two events
+        launch()
+    ev = [_abi.Event(ctx) for _ in range(2)]
+    ev[0].record()
+    for _ in range(reps):
+        launch()
+    ev[1].record()
+    ctx.sync()
+    ms = ev[0].elapsed_ms(ev[1]) / reps
     flop = float(FUSED_FLOP_PER_POINT_BIN) * n * B * H
     ach = flop / (ms * 1e-3) / 1e12
     return {"bound": "fp64", "achieved": ach, "peak": FP64_PEAK_TFS, "unit": "TFLOP/s", "frac": ach / FP64_PEAK_TFS,

@@ -11,6 +11,7 @@ struct gc_ctx {
   std::string err;
   void* scratch = nullptr;  // growable device scratch (per ctx, stream-ordered use only)
   size_t scratch_bytes = 0;
+  int cu_count = 0;  // compute units of the device (queried on first use)
 };
 
 namespace gc {

@@ -54,6 +54,7 @@ struct PipeDev {
   double *budget;                          // 8 budget scalars
   double *budget_part;                     // (64, 3) a1 partials, written by predict's extra workgroups
   unsigned *budget_ticket;                 // arrival counter of those workgroups (reset by the last)
+  unsigned *task_ctr;                      // [task counter, finished pullers] of k_bins_io (reset by the last)
   double *send, *gather;                   // (P), (G, P)
   int G;                                   // ranks
   double *comb;                            // combined belief: L 484, h 22, z 22, X 6, stamp, cert 16
@@ -85,7 +86,6 @@ struct ScanArgs {
 
 // launchers (gc_belief.hip)
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st);
-hipError_t launch_io_branch(const PipeDev& P, const ScanArgs& S, const double* d_odom, hipStream_t st);
 // a1 budget scalars into out (8) with 3 x 64 partials in part (gc_points.hip)
 hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, double* part, double* out,
                                hipStream_t st);
@@ -94,5 +94,13 @@ hipError_t launch_combine_local(const PipeDev& P, hipStream_t st);
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st);
 hipError_t launch_map_derive(const PipeDev& P, hipStream_t st);
 hipError_t launch_iw_Q(const PipeDev& P, hipStream_t st);
+}  // namespace gc
+
+struct gc_ctx;
+namespace gc {
+// a1 -> a6 bins of the local hypotheses (+ the IMU/odom branch's workgroups in the same launch when
+// io) and their finalize into P.stats / P.bincert (gc_points.hip)
+int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
+                           const double* d_pts, const double* d_t, const double* d_w, int64_t n_in);
 
 }  // namespace gc

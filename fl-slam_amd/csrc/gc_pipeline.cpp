@@ -26,12 +26,6 @@ struct gc_pipeline {
   } slots[GC_PIPE_MAX_SLOTS];
   int io_mode = GC_IO_COMPUTED;
   gc_comm* comm = nullptr;
-  double* d_cfg_origin = nullptr;
-  // side stream: the IMU/odom branch runs beside the fused bins kernel (independent inputs and
-  // outputs); events order it into the main stream. The a1 budget statistics need no stream of
-  // their own: they are extra workgroups of the predict grid.
-  hipStream_t side = nullptr;
-  hipEvent_t ev_pred = nullptr, ev_io = nullptr;
   // P.Sig / P.mu_fin were written by the last scan's evidence kernel from the current P.L / P.h
   // (cleared whenever the beliefs are set from the host)
   bool sig_cached = false;
@@ -132,13 +126,10 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   double* ticket = nullptr;
   if (rc == GC_OK) rc = dalloc(p, 1, &ticket);  // zeroed: the predict grid's budget arrival counter
   P.budget_ticket = reinterpret_cast<unsigned*>(ticket);
-  hipError_t e = hipStreamCreateWithFlags(&p->side, hipStreamNonBlocking);
-  for (hipEvent_t* ev : {&p->ev_pred, &p->ev_io})
-    if (e == hipSuccess) e = hipEventCreateWithFlags(ev, hipEventDisableTiming);
-  if (rc == GC_OK && e != hipSuccess) {
-    gc::set_error(p->ctx, std::string("side stream / events: ") + hipGetErrorString(e));
-    rc = GC_ERR_RUNTIME;
-  }
+  double* ctr = nullptr;
+  if (rc == GC_OK) rc = dalloc(p, 1, &ctr);  // zeroed: k_bins_io's task counter + finished pullers
+  P.task_ctr = reinterpret_cast<unsigned*>(ctr);
+  if (rc == GC_OK) GC_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the zero fills land before any launch
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
     return rc;
@@ -150,10 +141,6 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
 int32_t gc_pipeline_destroy(gc_pipeline* p) {
   if (!p) return GC_OK;
   (void)hipStreamSynchronize(p->ctx->stream);
-  if (p->side) (void)hipStreamSynchronize(p->side);
-  for (hipEvent_t ev : {p->ev_pred, p->ev_io})
-    if (ev) (void)hipEventDestroy(ev);
-  if (p->side) (void)hipStreamDestroy(p->side);
   for (void* a : p->allocs) (void)hipFree(a);
   for (auto& s : p->slots) {
     for (double* d : {s.pts, s.t, s.w, s.imu_t, s.imu_g, s.imu_a, s.odom})
@@ -405,19 +392,10 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   // a1 budget scalars (the fused kernel reads the selection / mass scale from them) on extra
   // workgroups of the predict grid; a2 + a3
   GC_HIP(ctx, gc::launch_predict_imu(P, S, ctx->stream));
-  // a9a IMU/odom evidence branch (pipeline.py:595-776): needs the prediction, not the bins, so it
-  // runs on the side stream beside the fused kernel
-  if (io) {
-    GC_HIP(ctx, hipEventRecord(p->ev_pred, ctx->stream));
-    GC_HIP(ctx, hipStreamWaitEvent(p->side, p->ev_pred, 0));
-    GC_HIP(ctx, gc::launch_io_branch(P, S, s.odom, p->side));
-    GC_HIP(ctx, hipEventRecord(p->ev_io, p->side));
-  }
-  // a1 -> a4 -> a5 -> a6 fused over all local hypotheses
-  const double origin[3] = {P.o0, P.o1, P.o2};
-  GC_TRY(gc_scan_bins_fused(ctx, P.Hl, s.n_in, P.n_cap, P.B, s.pts, s.t, s.w, P.budget, scan_start, scan_end,
-                            P.xi, P.bins, P.tau, origin, P.eps_psd, P.eps_mass, P.stats, P.bincert, 0));
-  if (io) GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, p->ev_io, 0));
+  // a1 -> a4 -> a5 -> a6 fused over all local hypotheses, and the a9a IMU/odom evidence branch
+  // (pipeline.py:595-776: it needs the prediction, not the bins) as extra workgroups of the same
+  // launch
+  GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in));
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
   p->sig_cached = true;

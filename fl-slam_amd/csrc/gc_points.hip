@@ -18,6 +18,7 @@
 #include "gc_internal.h"
 #include "gc_wgla.h"
 #include "gc_budget.h"
+#include "gc_iobranch_wg.h"
 
 namespace gc {
 
@@ -832,45 +833,69 @@ constexpr int kFusedFS = 66;
 #ifndef GC_FUSED_NACC
 #define GC_FUSED_NACC 2  // MFMA accumulator sets (even / odd steps)
 #endif
+// Per-launch constants of the fused kernel and its LDS tables (exp table, scaled bins), set up once
+// per workgroup by bins_prologue; a workgroup then runs one (grid form) or many (persistent form)
+// (hypothesis, chunk) tasks with bins_task.
+struct FusedArgs {
+  int64_t n_cap;
+  int B, iters;
+  const double *pts_raw, *t_raw, *w_raw, *bscal;
+  double t0, t1;
+  const double *xi, *bins;
+  double inv_tau, o0, o1, o2;
+  double* partials;  // (H, chunks, RL) records
+};
+constexpr int kFusedNS = NF_BASE + 4;  // feature slab rows: 19 features + d(3) + valid flag
+// dynamic LDS of a fused workgroup (doubles): 4 wave slabs | exp table | scaled bins | epilogue
+// reduction (aliases the slabs)
+__host__ __device__ inline size_t fused_lds_doubles(int B) {
+  const size_t a = 4 * (size_t)kFusedFS * kFusedNS + kExpTab2 + 192, b = 4 * (size_t)B * NF_BASE + 12;
+  return a > b ? a : b;
+}
+
+GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
+  double* Tx = lds + 4 * kFusedFS * kFusedNS;
+  double* Lb = Tx + kExpTab2;  // bin directions pre-scaled by 2048/(τ ln2) (x, y, z rows of 64)
+  exp_table2_init(Tx);
+  const double ysc = A.inv_tau * kTab2OverLn2;
+  if (threadIdx.x < 64) {
+    const int b = threadIdx.x;
+    Lb[b] = b < A.B ? A.bins[3 * b] * ysc : 0.0;
+    Lb[64 + b] = b < A.B ? A.bins[3 * b + 1] * ysc : 0.0;
+    Lb[128 + b] = b < A.B ? A.bins[3 * b + 2] * ysc : 0.0;
+  }
+  __syncthreads();
+}
+
+// One task: hypothesis h, chunk c (points [c·iters·256, (c+1)·iters·256) of the budgeted scan),
+// its partial record written to rec. Ends with the workgroup synchronised (LDS free for the next task).
 template <int BPL, bool FULL>
-__global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap, int B, int iters,
-                                                    const double* __restrict__ pts_raw,
-                                                    const double* __restrict__ t_raw,
-                                                    const double* __restrict__ w_raw,
-                                                    const double* __restrict__ bscal, double t0,
-                                                    double t1, const double* __restrict__ xi,
-                                                    const double* __restrict__ bins, double inv_tau,
-                                                    double o0, double o1, double o2,
-                                                    double* partials) {
+GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec) {
   constexpr int NF = NF_BASE;
   constexpr int NX = NF - 16;  // features on the VALU
-  constexpr int NS = NF + 4;   // + d(3) + valid flag
-  extern __shared__ double lds[];
-  const int h = blockIdx.y;
+  constexpr int NS = kFusedNS;
+  const int64_t n_cap = A.n_cap;
+  const int B = A.B, iters = A.iters;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, bl = lane & 15;
   double* F = lds + wv * (NS * kFusedFS);
-  const double o[3] = {o0, o1, o2};
+  const double o[3] = {A.o0, A.o1, A.o2};
   double xr[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) xr[k] = xi[6 * h + k];
-  const double scale = bscal[2];
-  const int64_t n_sel = (int64_t)bscal[5];
-  const int64_t stride = (int64_t)bscal[6];
+  for (int k = 0; k < 6; ++k) xr[k] = A.xi[6 * h + k];
+  const double* __restrict__ pts_raw = A.pts_raw;
+  const double* __restrict__ t_raw = A.t_raw;
+  const double* __restrict__ w_raw = A.w_raw;
+  const double t0 = A.t0, t1 = A.t1;
+  const double scale = A.bscal[2];
+  const int64_t n_sel = (int64_t)A.bscal[5];
+  const int64_t stride = (int64_t)A.bscal[6];
   const double denom = fmax(t1 - t0, 1e-12);
   const double inv_denom = 1.0 / denom;
   const double inv_sig = 1.0 / fmax(0.1 * denom, 1e-6);
   double* Tx = lds + 4 * kFusedFS * NS;
-  double* Lb = Tx + kExpTab2;  // bin directions pre-scaled by 2048/(τ ln2) (x, y, z rows of 64)
-  exp_table2_init(Tx);
-  const double ysc = inv_tau * kTab2OverLn2;
-  if (threadIdx.x < 64) {
-    const int b = threadIdx.x;
-    Lb[b] = b < B ? bins[3 * b] * ysc : 0.0;
-    Lb[64 + b] = b < B ? bins[3 * b + 1] * ysc : 0.0;
-    Lb[128 + b] = b < B ? bins[3 * b + 2] * ysc : 0.0;
-  }
-  __syncthreads();
+  double* Lb = Tx + kExpTab2;
+  const double ysc = A.inv_tau * kTab2OverLn2;
   constexpr int NACC = GC_FUSED_NACC;
   v4d acc4[NACC][BPL];  // NACC = 2: even / odd steps, 2*BPL independent MFMA accumulation chains
   double accx[BPL][NX];
@@ -892,7 +917,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   const double ymax = ceil(ysc);
   const double Mp = kRoundMagic - ymax;
   const double Beps = (double)B * 1e-12;
-  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
+  const int64_t chunk0 = c * iters * 256;
   // raw point of the next iteration, loaded one iteration ahead (its HBM latency hides behind
   // this iteration's soft assignment)
   double np[3] = {0.0, 0.0, 0.0}, ntt = 0.0, nww = 0.0;
@@ -996,12 +1021,59 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(int64_t n_cap,
   const double logacc = log(zst) + (double)zex * 0.69314718055994530942;
   const double ent = (bl == 0 ? logacc : 0.0) - entq * kExp2C1 +
                      ((lane == 0) ? (ymax * kExp2C1 - Beps) * (double)npts * 0.25 : 0.0);
-  const int RL = B * NF + REC_EXTRA;
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
     if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
-  write_partial_record_mfma<BPL, NX>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds,
-                                     partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL);
+  write_partial_record_mfma<BPL, NX>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec);
+  __syncthreads();  // the epilogue's LDS reads are done before the next task writes the slabs
+}
+
+// Persistent form with the IMU/odom branch (the batched pipeline): workgroups [0, n_io) each run
+// one hypothesis of the branch (io_branch_wg, independent of the bins); the rest stay resident and
+// pull (hypothesis, chunk) tasks from a monotone counter until the H·chunks tasks are taken, so
+// the branch's workgroups are dispatched first and the bin tasks balance over whatever CU slots
+// remain — no stream fork / join and no partial last round of workgroups. Every task writes its
+// own record, so the result does not depend on which workgroup ran it (bit-reproducible). ctr[0]
+// is the task counter, ctr[1] the count of finished pullers; the last one resets both for the next
+// launch (stream order makes the reset visible to it). No workgroup waits on another.
+template <int BPL, bool FULL>
+__global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
+                                                             const double* __restrict__ odom, int n_io, int H,
+                                                             int64_t chunks, unsigned* ctr) {
+  extern __shared__ double lds[];
+  __shared__ unsigned task_s;
+  if ((int)blockIdx.x < n_io) {
+    io_branch_wg(P, S, odom, blockIdx.x, lds);
+    return;
+  }
+  bins_prologue(A, lds);
+  const int RL = A.B * NF_BASE + REC_EXTRA;
+  const unsigned T = (unsigned)(H * chunks);
+  for (;;) {
+    if (threadIdx.x == 0) task_s = atomicAdd(ctr, 1u);
+    __syncthreads();
+    const unsigned t = task_s;
+    __syncthreads();
+    if (t >= T) break;
+    // chunk-major: the workgroups in flight share a chunk's raw points across hypotheses (L2)
+    const int64_t c = t / H;
+    const int h = t % H;
+    bins_task<BPL, FULL>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL);
+  }
+  if (threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == gridDim.x - n_io - 1) {
+    atomicExch(ctr, 0u);
+    atomicExch(ctr + 1, 0u);
+  }
+}
+
+// Grid form (the gc_scan_bins_fused entry): grid (chunks, H), one task per workgroup.
+template <int BPL, bool FULL>
+__global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(FusedArgs A) {
+  extern __shared__ double lds[];
+  bins_prologue(A, lds);
+  const int RL = A.B * NF_BASE + REC_EXTRA;
+  bins_task<BPL, FULL>(A, blockIdx.y, blockIdx.x, lds,
+                       A.partials + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * RL);
 }
 
 // ================================================================ finalize (a6 + certs)
@@ -1399,15 +1471,14 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const int bpl = bpl_for(B);
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
-  const size_t sh = sizeof(double) * std::max<size_t>(4 * kFusedFS * (NF + 4) + kExpTab2 + 192, 4 * (size_t)B * NF + 12);
+  const size_t sh = sizeof(double) * fused_lds_doubles(B);
   dim3 grid((unsigned)chunks, H);
-  const double inv_tau = 1.0 / tau;
+  const FusedArgs FA{n_cap, B, iters, d_points_raw, d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins,
+                     1.0 / tau, h_origin3[0], h_origin3[1], h_origin3[2], (double*)scr};
 #define GC_FUSED(BP, FULL)                                                                                     \
   GC_HIP(ctx, hipFuncSetAttribute((const void*)k_bins_fused<BP, FULL>,                                          \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));                        \
-  hipLaunchKernelGGL((k_bins_fused<BP, FULL>), grid, dim3(256), sh, ctx->stream, n_cap, B, iters, d_points_raw, \
-                     d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins, inv_tau, h_origin3[0],            \
-                     h_origin3[1], h_origin3[2], (double*)scr)
+  hipLaunchKernelGGL((k_bins_fused<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA)
   const bool full = B == 16 * bpl;
   switch (bpl) {
     case 1: if (full) { GC_FUSED(1, true); } else { GC_FUSED(1, false); } break;
@@ -1419,6 +1490,56 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   GC_LAUNCH_CHECK(ctx);
   return launch_finalize(ctx, H, B, NF, chunks, (const double*)scr, eps_psd, eps_mass, d_stats_out, d_cert_out);
 }
+
+}  // extern "C"
+
+namespace gc {
+// The batched pipeline's a1 -> a6 bins for its Hl local hypotheses, with the IMU/odom branch's
+// workgroups in the same launch when io (k_bins_io), then the chunk-order finalize.
+int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
+                           const double* d_pts, const double* d_t, const double* d_w, int64_t n_in) {
+  (void)n_in;
+  if (ctx->cu_count == 0) {
+    int cus = 0;
+    GC_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    ctx->cu_count = cus > 0 ? cus : 1;
+  }
+  const int H = P.Hl, B = P.B;
+  const int pullers = 2 * ctx->cu_count;  // 2 resident bin workgroups per CU (VGPR-bound)
+  // the largest iteration count that still gives every puller >= 4 tasks (tail <= 1/4 task)
+  int iters = 16;
+  while (iters > 1 && H * ((P.n_cap + iters * 256 - 1) / (iters * 256)) < 4 * (int64_t)pullers) iters >>= 1;
+  const int64_t chunks = (P.n_cap + iters * 256 - 1) / (iters * 256);
+  GC_CHECK_ARG(ctx, (int64_t)H * chunks < (int64_t)0xFFFFFFFF, "too many bin tasks");
+  const int NF = NF_BASE;
+  const int RL = B * NF + REC_EXTRA;
+  void* scr;
+  if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
+  const FusedArgs FA{P.n_cap, B, iters, d_pts, d_t, d_w, P.budget, S.t0, S.t1, P.xi, P.bins, 1.0 / P.tau,
+                     P.o0, P.o1, P.o2, (double*)scr};
+  const int n_io = io ? H : 0;
+  const size_t sh = sizeof(double) * std::max<size_t>(fused_lds_doubles(B), io ? (size_t)kIoLdsDoubles : 0);
+  const dim3 grid((unsigned)(n_io + pullers));
+#define GC_BIO(BP, FULL)                                                                                       \
+  GC_HIP(ctx, hipFuncSetAttribute((const void*)k_bins_io<BP, FULL>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                                  (int)sh));                                                                   \
+  hipLaunchKernelGGL((k_bins_io<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA, P, S, d_odom, n_io, H, chunks, \
+                     P.task_ctr)
+  const int bpl = bpl_for(B);
+  const bool full = B == 16 * bpl;
+  switch (bpl) {
+    case 1: if (full) { GC_BIO(1, true); } else { GC_BIO(1, false); } break;
+    case 2: if (full) { GC_BIO(2, true); } else { GC_BIO(2, false); } break;
+    case 3: if (full) { GC_BIO(3, true); } else { GC_BIO(3, false); } break;
+    default: if (full) { GC_BIO(4, true); } else { GC_BIO(4, false); } break;
+  }
+#undef GC_BIO
+  GC_LAUNCH_CHECK(ctx);
+  return launch_finalize(ctx, H, B, NF, chunks, (const double*)scr, P.eps_psd, P.eps_mass, P.stats, P.bincert);
+}
+}  // namespace gc
+
+extern "C" {
 
 int32_t gc_kappa_from_resultant_batch(gc_ctx* ctx, int64_t n, const double* d_R, double eps_r, double d,
                                       double r0, double tau, double* d_kappa_out) {

@@ -49,7 +49,8 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
   const double bytes = (double)H * n * (24 + 72 + 8 + 8 + 8 * B);
   auto timeit = [&](const char* name, auto fn) {
-    fn(); hipDeviceSynchronize();
+    for (int w = 0; w < 15; ++w) fn();  // clocks ramp over the first ~30 ms of sustained load
+    hipDeviceSynchronize();
     hipEventRecord(e0);
     for (int r = 0; r < 5; ++r) fn();
     hipEventRecord(e1); hipEventSynchronize(e1);
