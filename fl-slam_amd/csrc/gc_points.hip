@@ -1049,12 +1049,16 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, Pipe
   bins_prologue(A, lds);
   const int RL = A.B * NF_BASE + REC_EXTRA;
   const unsigned T = (unsigned)(H * chunks);
+  // the next task's ticket is taken at the start of the current one, so the atomic's round trip
+  // overlaps the task (bins_task ends with a barrier: task_s is read by all before it is rewritten)
+  unsigned next = 0;
+  if (threadIdx.x == 0) next = atomicAdd(ctr, 1u);
   for (;;) {
-    if (threadIdx.x == 0) task_s = atomicAdd(ctr, 1u);
+    if (threadIdx.x == 0) task_s = next;
     __syncthreads();
     const unsigned t = task_s;
-    __syncthreads();
     if (t >= T) break;
+    if (threadIdx.x == 0) next = atomicAdd(ctr, 1u);
     // chunk-major: the workgroups in flight share a chunk's raw points across hypotheses (L2)
     const int64_t c = t / H;
     const int h = t % H;
@@ -1088,9 +1092,9 @@ __global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t ch
   const int h = blockIdx.x;
   const int RL = B * NF + REC_EXTRA;
   const double* P = partials + (int64_t)h * chunks * RL;
-  // chunk order fixed per entry; a lane's (up to 4) entries advance together, 8 chunks at a time:
-  // 32 loads in flight per lane (the reduction is L2-latency-bound at small H)
-  constexpr int kE = 4;
+  // chunk order fixed per entry; a lane's (up to 4) entries advance together, 16 chunks at a time:
+  // 64 loads in flight per lane (the reduction is L2-latency-bound at small H)
+  constexpr int kE = 4, kU = 16;
   int ie[kE];
   double v[kE];
 #pragma unroll
@@ -1100,16 +1104,16 @@ __global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t ch
   }
   const int imax = B * NF + 1;  // the max-responsibility entry reduces by fmax
   int64_t c = 0;
-  for (; c + 8 <= chunks; c += 8) {
-    double x[kE][8];
+  for (; c + kU <= chunks; c += kU) {
+    double x[kE][kU];
 #pragma unroll
     for (int e = 0; e < kE; ++e)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) x[e][u] = ie[e] < RL ? P[(c + u) * RL + ie[e]] : 0.0;
+      for (int u = 0; u < kU; ++u) x[e][u] = ie[e] < RL ? P[(c + u) * RL + ie[e]] : 0.0;
 #pragma unroll
     for (int e = 0; e < kE; ++e)
 #pragma unroll
-      for (int u = 0; u < 8; ++u) v[e] = ie[e] == imax ? fmax(v[e], x[e][u]) : v[e] + x[e][u];
+      for (int u = 0; u < kU; ++u) v[e] = ie[e] == imax ? fmax(v[e], x[e][u]) : v[e] + x[e][u];
   }
   for (; c < chunks; ++c)
 #pragma unroll
