@@ -483,10 +483,10 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
   constexpr int RS = 18;
   typedef double dvec2 __attribute__((ext_vector_type(2)));
   __shared__ double red[8];
-  __shared__ double Tx[kExpTab];
+  __shared__ double Tx[kExpTab2];
   __shared__ double Lb[3 * 64];  // bin directions, x / y / z rows of 64 (zero past B)
   __shared__ __attribute__((aligned(16))) double Sl[4][64 * RS];
-  exp_table_init(Tx);
+  exp_table2_init(Tx);
   if (threadIdx.x < 64) {
     const int b = threadIdx.x;
     Lb[b] = b < B ? bins[3 * b] : 0.0;
@@ -503,7 +503,11 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
   // Σ log Z is kept as a product of mantissas and a sum of exponents (frexp), one log at the end
   double zm = 1.0, entq = 0.0, mxr = 0.0;
   int ze = 0;
-  const int64_t chunk0 = (int64_t)blockIdx.x * iters * 256;
+  // iteration it of workgroup b covers points [(it G + b) 256, +256) (G = gridDim.x): the
+  // workgroups in flight write one contiguous window of the responsibility matrix instead of G
+  // chunks spread over the whole hypothesis (DRAM page locality of the 6.4 GB write stream)
+  const int64_t G256 = (int64_t)gridDim.x * 256;
+  const int64_t chunk0 = (int64_t)blockIdx.x * 256;
   // directions of the wave's next 64 points: 192 contiguous doubles, three fully coalesced 512-B
   // loads (8 B per lane, any alignment), handed to lane = point through the LDS slab
   const int64_t nd = 3 * n;
@@ -517,13 +521,13 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
   }
   GC_LOAD_DIRS(chunk0 + wv * 64)
   for (int it = 0; it < iters; ++it) {
-    const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
+    const int64_t wbase = chunk0 + (int64_t)it * G256 + wv * 64;
     if (wbase >= n) break;  // wave-uniform
     S[lane] = nd0; S[64 + lane] = nd1; S[128 + lane] = nd2;
     lds_wave_sync();
     const double d0 = S[3 * lane], d1 = S[3 * lane + 1], d2 = S[3 * lane + 2];
     lds_wave_sync();
-    GC_LOAD_DIRS(wbase + 256)
+    GC_LOAD_DIRS(wbase + G256)
     const int64_t pt = wbase + lane;
     const bool valid = pt < n;
     // pass 1: the exact un-fused similarities (kept in ex[]), their row maximum and the integer bin
@@ -538,27 +542,30 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
       ex[j] = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
       if ((FULL || j < B) && ex[j] > best) { best = ex[j]; bidx = j; }
     }
+    // exponent in units of ln2/2048 (the 2048-entry table exp, exp2s_n); arguments below e^-700
+    // are clamped there (R <= 1e-304 / Z instead of an underflow to 0)
+    const double ysc = inv_tau * kTab2OverLn2;
     double Z = 0.0, sl = 0.0;
 #pragma unroll
     for (int j0 = 0; j0 < NB; j0 += 8) {
-      double x[8];
+      double y[8];
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int j = j0 + jj;
-        // e^-745 underflows to 0 in f64; the clamp keeps the table index in range for tiny τ
-        x[jj] = (FULL || j < B) ? fmax((ex[j] - best) * inv_tau, -1000.0) : 0.0;
+        y[jj] = (FULL || j < B) ? fmax((ex[j] - best) * ysc, -700.0 * kTab2OverLn2) : 0.0;
       }
       double e8[8];
-      exp_neg_n<8, false>(x, Tx, e8);
+      exp2s_n<8>(y, Tx, e8);
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int j = j0 + jj;
         ex[j] = (FULL || j < B) ? e8[jj] : 0.0;
         Z += ex[j];
-        sl = fma(ex[j], x[jj], sl);
+        sl = fma(ex[j], y[jj], sl);
       }
-      asm volatile("" : "+v"(Z), "+v"(sl));  // accumulate now: the x of a group die here
+      asm volatile("" : "+v"(Z), "+v"(sl));  // accumulate now: the y of a group die here
     }
+    sl *= kExp2C1;  // Σ e x in nats
     // the maximal bin has x = 0 and e = 1 exactly: Z >= 1 and max_b R = 1/Z
     const double rZ = recip(Z);
     if (valid) {
