@@ -80,6 +80,17 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
     const int b = h - P.Hl;
     const int64_t stride = budget_stride(S.n_in, P.n_cap);
     budget_partial_block(S.w_raw, S.n_in, stride, b, P.budget_part, sm);
+    // a4's per-point time window (deskew_constant_twist.py:61-68) depends on the point only, not
+    // on the hypothesis: the selected points' w x window once per scan here, read by every
+    // hypothesis's bins task (k_bins_io) in place of the raw weight (the budget's mass scale is
+    // applied there)
+    {
+      const int64_t n_sel = (S.n_in + stride - 1) / stride;
+      const double denom = fmax(S.t1 - S.t0, 1e-12);
+      for (int64_t j = (int64_t)b * kWG + t; j < P.n_cap; j += (int64_t)kBudgetBlocks * kWG)
+        P.w_win[j] = j < n_sel ? S.w_raw[j * stride] * window_weight(S.t_raw[j * stride], S.t0, S.t1, 0.1 * denom)
+                               : 0.0;
+    }
     if (t == 0) {
       const unsigned prev =
           __hip_atomic_fetch_add(P.budget_ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);

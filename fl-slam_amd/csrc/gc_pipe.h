@@ -55,6 +55,8 @@ struct PipeDev {
   double *budget_part;                     // (64, 3) a1 partials, written by predict's extra workgroups
   unsigned *budget_ticket;                 // arrival counter of those workgroups (reset by the last)
   unsigned *task_ctr;                      // [task counter, finished pullers] of k_bins_io (reset by the last)
+  double *w_win;                           // (n_cap) selected points' w x time window, written by predict's
+                                           // budget workgroups (per point, shared by every hypothesis)
   double *send, *gather;                   // (P), (G, P)
   int G;                                   // ranks
   double *comb;                            // combined belief: L 484, h 22, z 22, X 6, stamp, cert 16
@@ -67,6 +69,7 @@ struct ScanArgs {
   double w_process;                        // min(1, scan_count)
   const double* w_raw;                     // (n_in) raw point weights (a1 budget, fused into predict)
   int64_t n_in;                            // raw points of this scan
+  const double* t_raw;                     // (n_in) raw point times (the window of P.w_win)
   int sig_cached;                          // P.Sig / P.mu_fin hold (P.L + εI)⁻¹ and its solve with P.h
 };
 

@@ -129,6 +129,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   double* ctr = nullptr;
   if (rc == GC_OK) rc = dalloc(p, 1, &ctr);  // zeroed: k_bins_io's task counter + finished pullers
   P.task_ctr = reinterpret_cast<unsigned*>(ctr);
+  if (rc == GC_OK) rc = dalloc(p, (size_t)P.n_cap, &P.w_win);
   if (rc == GC_OK) GC_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the zero fills land before any launch
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
@@ -386,7 +387,7 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   gc_ctx* ctx = p->ctx;
   const auto& s = p->slots[slot];
   gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
-                 scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in, p->sig_cached ? 1 : 0};
+                 scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in, s.t, p->sig_cached ? 1 : 0};
   gc::PipeDev& P = p->P;
   const bool io = p->io_mode == GC_IO_COMPUTED;
   // a1 budget scalars (the fused kernel reads the selection / mass scale from them) on extra

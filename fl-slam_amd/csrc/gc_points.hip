@@ -850,7 +850,8 @@ struct FusedArgs {
   double t0, t1;
   const double *xi, *bins;
   double inv_tau, o0, o1, o2;
-  double* partials;  // (H, chunks, RL) records
+  double* partials;      // (H, chunks, RL) records
+  const double* w_win;   // (n_cap) selected w x time window (the pipeline's predict), or NULL: per task
 };
 constexpr int kFusedNS = NF_BASE + 4;  // feature slab rows: 19 features + d(3) + valid flag
 // dynamic LDS of a fused workgroup (doubles): 4 wave slabs | exp table | scaled bins | epilogue
@@ -876,7 +877,7 @@ GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
 
 // One task: hypothesis h, chunk c (points [c·iters·256, (c+1)·iters·256) of the budgeted scan),
 // its partial record written to rec. Ends with the workgroup synchronised (LDS free for the next task).
-template <int BPL, bool FULL>
+template <int BPL, bool FULL, bool PRE>
 GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec) {
   constexpr int NF = NF_BASE;
   constexpr int NX = NF - 16;  // features on the VALU
@@ -935,7 +936,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
       const int64_t i = j * stride;
       np[0] = pts_raw[3 * i]; np[1] = pts_raw[3 * i + 1]; np[2] = pts_raw[3 * i + 2];
       ntt = t_raw[i];
-      nww = w_raw[i];
+      nww = PRE ? A.w_win[j] : w_raw[i];  // PRE: the window is already applied (once per scan)
     }
   };
   fetch(0);
@@ -954,7 +955,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
         if (it + 1 < iters) fetch(it + 1);
         double q[3], d[3], f[NF];
         deskew_point_series(p, (tt - t0) * inv_denom, xr, q);
-        const double wd = inr ? ww * window_weight2(tt, t0, t1, inv_sig, Tx) : 0.0;
+        const double wd = inr ? (PRE ? ww : ww * window_weight2(tt, t0, t1, inv_sig, Tx)) : 0.0;
         direction_fast(q, o, 1e-12, d);
         point_features(q, d, wd, f);
         sumw += wd;
@@ -1069,7 +1070,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, Pipe
     // chunk-major: the workgroups in flight share a chunk's raw points across hypotheses (L2)
     const int64_t c = t / H;
     const int h = t % H;
-    bins_task<BPL, FULL>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL);
+    bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL);
   }
   if (threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == gridDim.x - n_io - 1) {
     atomicExch(ctr, 0u);
@@ -1083,7 +1084,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(FusedArgs A) {
   extern __shared__ double lds[];
   bins_prologue(A, lds);
   const int RL = A.B * NF_BASE + REC_EXTRA;
-  bins_task<BPL, FULL>(A, blockIdx.y, blockIdx.x, lds,
+  bins_task<BPL, FULL, false>(A, blockIdx.y, blockIdx.x, lds,
                        A.partials + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * RL);
 }
 
@@ -1485,7 +1486,7 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const size_t sh = sizeof(double) * fused_lds_doubles(B);
   dim3 grid((unsigned)chunks, H);
   const FusedArgs FA{n_cap, B, iters, d_points_raw, d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins,
-                     1.0 / tau, h_origin3[0], h_origin3[1], h_origin3[2], (double*)scr};
+                     1.0 / tau, h_origin3[0], h_origin3[1], h_origin3[2], (double*)scr, nullptr};
 #define GC_FUSED(BP, FULL)                                                                                     \
   GC_HIP(ctx, hipFuncSetAttribute((const void*)k_bins_fused<BP, FULL>,                                          \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));                        \
@@ -1527,7 +1528,7 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
   const FusedArgs FA{P.n_cap, B, iters, d_pts, d_t, d_w, P.budget, S.t0, S.t1, P.xi, P.bins, 1.0 / P.tau,
-                     P.o0, P.o1, P.o2, (double*)scr};
+                     P.o0, P.o1, P.o2, (double*)scr, P.w_win};
   const int n_io = io ? H : 0;
   const size_t sh = sizeof(double) * std::max<size_t>(fused_lds_doubles(B), io ? (size_t)kIoLdsDoubles : 0);
   const dim3 grid((unsigned)(n_io + pullers));
