@@ -852,6 +852,10 @@ struct FusedArgs {
   double inv_tau, o0, o1, o2;
   double* partials;      // (H, chunks, RL) records
   const double* w_win;   // (n_cap) selected w x time window (the pipeline's predict), or NULL: per task
+  // two chunk tiers: chunks [0, k1) hold iters x 256 points, the rest iters_s x 256 (the persistent
+  // form ends on short tasks, so the pullers finish together); grid form: k1 = chunks, iters_s = iters
+  int64_t k1;
+  int iters_s;
 };
 constexpr int kFusedNS = NF_BASE + 4;  // feature slab rows: 19 features + d(3) + valid flag
 // dynamic LDS of a fused workgroup (doubles): 4 wave slabs | exp table | scaled bins | epilogue
@@ -875,7 +879,7 @@ GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
   __syncthreads();
 }
 
-// One task: hypothesis h, chunk c (points [c·iters·256, (c+1)·iters·256) of the budgeted scan),
+// One task: hypothesis h, chunk c (its points: the tiers of FusedArgs) of the budgeted scan,
 // its partial record written to rec. Ends with the workgroup synchronised (LDS free for the next task).
 template <int BPL, bool FULL, bool PRE>
 GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec) {
@@ -883,7 +887,10 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   constexpr int NX = NF - 16;  // features on the VALU
   constexpr int NS = kFusedNS;
   const int64_t n_cap = A.n_cap;
-  const int B = A.B, iters = A.iters;
+  const int B = A.B;
+  const bool big = c < A.k1;
+  const int iters = big ? A.iters : A.iters_s;
+  const int64_t chunk0 = big ? c * A.iters * 256 : (A.k1 * A.iters + (c - A.k1) * A.iters_s) * 256;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, bl = lane & 15;
   double* F = lds + wv * (NS * kFusedFS);
@@ -925,7 +932,6 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   const double ymax = ceil(ysc);
   const double Mp = kRoundMagic - ymax;
   const double Beps = (double)B * 1e-12;
-  const int64_t chunk0 = c * iters * 256;
   // raw point of the next iteration, loaded one iteration ahead (its HBM latency hides behind
   // this iteration's soft assignment)
   double np[3] = {0.0, 0.0, 0.0}, ntt = 0.0, nww = 0.0;
@@ -1091,50 +1097,53 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(FusedArgs A) {
 // ================================================================ finalize (a6 + certs)
 // One workgroup per hypothesis: chunk records summed in order, per-bin moments -> p̄, Σ_p
 // (PSD-projected), κ; cert reductions in a fixed order.
-__global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t chunks,
-                                                       const double* __restrict__ partials,
-                                                       double eps_psd, double eps_mass,
-                                                       double* stats, double* cert) {
-  extern __shared__ double sm[];  // B*NF + 8 + 4
-  double* red = sm + B * NF + REC_EXTRA;
-  const int h = blockIdx.x;
-  const int RL = B * NF + REC_EXTRA;
-  const double* P = partials + (int64_t)h * chunks * RL;
-  // chunk order fixed per entry; a lane's (up to 4) entries advance together, 16 chunks at a time:
-  // 64 loads in flight per lane (the reduction is L2-latency-bound at small H)
-  constexpr int kE = 4, kU = 16;
-  int ie[kE];
-  double v[kE];
+// one hypothesis h (the whole workgroup); sm: B*NF + REC_EXTRA + 8 doubles
+// Chunk records of one hypothesis summed entry-wise in chunk order (the max entry by fmax), KE
+// entries per thread and KU chunks per batch in flight; a ragged last batch loads zeros past the last
+// chunk (+0 and fmax(·, 0) leave every entry, all >= 0 for the max, unchanged): one L2 round trip per
+// batch. Entries past KE x blockDim go one chunk at a time (none at B <= 48 with the base features).
+template <int KE, int KU>
+GC_DEV void finalize_reduce(const double* __restrict__ P, int RL, int imax, int64_t chunks, double* sm) {
+  const int nt = blockDim.x;
+  int ie[KE];
+  double v[KE];
 #pragma unroll
-  for (int e = 0; e < kE; ++e) {
-    ie[e] = threadIdx.x + e * kWG;
+  for (int e = 0; e < KE; ++e) {
+    ie[e] = threadIdx.x + e * nt;
     v[e] = 0.0;
   }
-  const int imax = B * NF + 1;  // the max-responsibility entry reduces by fmax
-  int64_t c = 0;
-  for (; c + kU <= chunks; c += kU) {
-    double x[kE][kU];
+  for (int64_t c = 0; c < chunks; c += KU) {
+    double x[KE][KU];
 #pragma unroll
-    for (int e = 0; e < kE; ++e)
+    for (int e = 0; e < KE; ++e)
 #pragma unroll
-      for (int u = 0; u < kU; ++u) x[e][u] = ie[e] < RL ? P[(c + u) * RL + ie[e]] : 0.0;
+      for (int u = 0; u < KU; ++u) x[e][u] = (ie[e] < RL && c + u < chunks) ? P[(c + u) * RL + ie[e]] : 0.0;
 #pragma unroll
-    for (int e = 0; e < kE; ++e)
+    for (int e = 0; e < KE; ++e)
 #pragma unroll
-      for (int u = 0; u < kU; ++u) v[e] = ie[e] == imax ? fmax(v[e], x[e][u]) : v[e] + x[e][u];
+      for (int u = 0; u < KU; ++u) v[e] = ie[e] == imax ? fmax(v[e], x[e][u]) : v[e] + x[e][u];
   }
-  for (; c < chunks; ++c)
 #pragma unroll
-    for (int e = 0; e < kE; ++e)
-      if (ie[e] < RL) v[e] = ie[e] == imax ? fmax(v[e], P[c * RL + ie[e]]) : v[e] + P[c * RL + ie[e]];
-#pragma unroll
-  for (int e = 0; e < kE; ++e)
+  for (int e = 0; e < KE; ++e)
     if (ie[e] < RL) sm[ie[e]] = v[e];
-  for (int i = threadIdx.x + kE * kWG; i < RL; i += kWG) {  // B * NF + 4 > 1024 (not at B <= 53)
+  for (int i = threadIdx.x + KE * nt; i < RL; i += nt) {
     double w = 0.0;
     for (int64_t cc = 0; cc < chunks; ++cc) w = i == imax ? fmax(w, P[cc * RL + i]) : w + P[cc * RL + i];
     sm[i] = w;
   }
+}
+// One hypothesis h on a 1024-thread workgroup (kFinWG): the entry sums with 4x the loads in flight of
+// a 256-thread one (the reduction is L2-latency-bound at small H), then per-bin moments -> p̄, Σ_p
+// (PSD-projected), κ on lanes b < B of wave 0 (B <= 64) and the cert reductions on that wave.
+// sm: B*NF + REC_EXTRA doubles.
+constexpr int kFinWG = 1024;
+GC_DEV void finalize_hyp(int h, int B, int NF, int64_t chunks, const double* __restrict__ partials, double eps_psd,
+                         double eps_mass, double* stats, double* cert, double* sm) {
+  const int RL = B * NF + REC_EXTRA;
+  const double* P = partials + (int64_t)h * chunks * RL;
+  const int imax = B * NF + 1;  // the max-responsibility entry reduces by fmax
+  if (RL <= kFinWG) finalize_reduce<1, 32>(P, RL, imax, chunks, sm);
+  else finalize_reduce<2, 16>(P, RL, imax, chunks, sm);
   __syncthreads();
   double Nl = 0.0, N2l = 0.0, psdl = 0.0, epsl = 0.0, sfl = 0.0;
   if ((int)threadIdx.x < B) {
@@ -1186,11 +1195,12 @@ __global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t ch
     for (int k = 0; k < 9; ++k) o[29 + k] = Spp[k];
     Nl = N; N2l = N * N; psdl = c6[0]; epsl = er; sfl = N / (N + eps_mass);
   }
-  const double Nt = wg_sum(Nl, red);
-  const double N2 = wg_sum(N2l, red);
-  const double psd = wg_sum(psdl, red);
-  const double mer = wg_max(epsl, red);
-  const double sf = wg_sum(sfl, red);
+  if (threadIdx.x >= 64) return;  // every bin lives on wave 0 (B <= 64)
+  const double Nt = wave_sum(Nl);
+  const double N2 = wave_sum(N2l);
+  const double psd = wave_sum(psdl);
+  const double mer = wave_max(epsl);
+  const double sf = wave_sum(sfl);
   if (threadIdx.x == 0) {
     const double* ex = sm + B * NF;
     double* c = cert + (int64_t)h * GC_BIN_CERT;
@@ -1203,6 +1213,13 @@ __global__ void __launch_bounds__(256) k_bins_finalize(int B, int NF, int64_t ch
     c[6] = ex[2];
     c[7] = psd + mer;
   }
+}
+__global__ void __launch_bounds__(kFinWG) k_bins_finalize(int B, int NF, int64_t chunks,
+                                                       const double* __restrict__ partials,
+                                                       double eps_psd, double eps_mass,
+                                                       double* stats, double* cert) {
+  extern __shared__ double sm[];  // B*NF + 8 + 4
+  finalize_hyp(blockIdx.x, B, NF, chunks, partials, eps_psd, eps_mass, stats, cert, sm);
 }
 
 __global__ void k_kappa(int64_t n, const double* __restrict__ R, double eps_r, double d, double r0,
@@ -1412,8 +1429,8 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
 
 static int32_t launch_finalize(gc_ctx* ctx, int H, int B, int NF, int64_t chunks, const double* partials,
                                double eps_psd, double eps_mass, double* stats, double* cert) {
-  const size_t sh = sizeof(double) * (B * NF + REC_EXTRA + 8);
-  hipLaunchKernelGGL(k_bins_finalize, dim3(H), dim3(256), sh, ctx->stream, B, NF, chunks, partials, eps_psd,
+  const size_t sh = sizeof(double) * (B * NF + REC_EXTRA);
+  hipLaunchKernelGGL(k_bins_finalize, dim3(H), dim3(kFinWG), sh, ctx->stream, B, NF, chunks, partials, eps_psd,
                      eps_mass, stats, cert);
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
@@ -1486,7 +1503,7 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const size_t sh = sizeof(double) * fused_lds_doubles(B);
   dim3 grid((unsigned)chunks, H);
   const FusedArgs FA{n_cap, B, iters, d_points_raw, d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins,
-                     1.0 / tau, h_origin3[0], h_origin3[1], h_origin3[2], (double*)scr, nullptr};
+                     1.0 / tau, h_origin3[0], h_origin3[1], h_origin3[2], (double*)scr, nullptr, chunks, iters};
 #define GC_FUSED(BP, FULL)                                                                                     \
   GC_HIP(ctx, hipFuncSetAttribute((const void*)k_bins_fused<BP, FULL>,                                          \
                                   hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));                        \
@@ -1519,16 +1536,25 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   const int H = P.Hl, B = P.B;
   const int pullers = 2 * ctx->cu_count;  // 2 resident bin workgroups per CU (VGPR-bound)
   // the largest iteration count that still gives every puller >= 4 tasks (tail <= 1/4 task)
+  // Two tiers of chunks, taken in order: long tasks (iters x 256 points, the prologue / epilogue
+  // amortised) for the bulk, then short ones (2 x 256) that hold about half a long task of work per
+  // puller, so the pullers run out of work together instead of one long task apart.
+  const int64_t U = (P.n_cap + 255) / 256;  // 256-point units per hypothesis
   int iters = 16;
-  while (iters > 1 && H * ((P.n_cap + iters * 256 - 1) / (iters * 256)) < 4 * (int64_t)pullers) iters >>= 1;
-  const int64_t chunks = (P.n_cap + iters * 256 - 1) / (iters * 256);
+  while (iters > 2 && (int64_t)H * U < 3 * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
+  constexpr int kItersShort = 2;
+  int64_t Us = std::max<int64_t>(iters, ((int64_t)pullers * iters + 2 * H - 1) / (2 * H));
+  Us = std::min(Us, U);
+  const int64_t k1 = (U - Us) / iters;  // long chunks; the short tier takes the rest
+  Us = U - k1 * iters;
+  const int64_t chunks = k1 + (Us + kItersShort - 1) / kItersShort;
   GC_CHECK_ARG(ctx, (int64_t)H * chunks < (int64_t)0xFFFFFFFF, "too many bin tasks");
   const int NF = NF_BASE;
   const int RL = B * NF + REC_EXTRA;
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
   const FusedArgs FA{P.n_cap, B, iters, d_pts, d_t, d_w, P.budget, S.t0, S.t1, P.xi, P.bins, 1.0 / P.tau,
-                     P.o0, P.o1, P.o2, (double*)scr, P.w_win};
+                     P.o0, P.o1, P.o2, (double*)scr, P.w_win, k1, kItersShort};
   const int n_io = io ? H : 0;
   const size_t sh = sizeof(double) * std::max<size_t>(fused_lds_doubles(B), io ? (size_t)kIoLdsDoubles : 0);
   const dim3 grid((unsigned)(n_io + pullers));
