@@ -239,33 +239,43 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   for (int i = t; i < NN; i += kWG) P.Sig[(int64_t)hl * NN + i] = W2[i];
   for (int idx = t; idx < 7 * 36; idx += kWG) P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
   GC_PHASE(P, 17);
-  // a13 map increment from hypothesis 0 only (backend_node.py:2081-2083), build-defined pushforward
-  if (P.h_begin + hl == 0) {
+  // a14 anchor drift (anchor_drift.py:93-191) on wave 0 and, beside it on wave 1, the a13 map
+  // increment from hypothesis 0 only (backend_node.py:2081-2083, build-defined pushforward): both
+  // read μ_post, X_new and Σ_post, neither writes what the other reads
+  if (t < 64) {
+    // δz = μ_post of the recomposed belief
     if (t == 0) {
+      const double rho = drift_rho(mupo, nullptr, nullptr);
+      double d6[6];
+      for (int k = 0; k < 6; ++k) d6[k] = rho * mupo[k];
+      compose_exp2(sc + 64, d6, sc + 92);  // X_fin
+      sc[98] = rho;
+    }
+    wave_lds_sync();
+    const double rho = sc[98];
+    if (t < n) zl[t] = (1.0 - rho) * mupo[t];
+    wave_lds_sync();
+    if (t < n) {  // h_fin = L_post z (wg_matvec's row order)
+      double v = 0.0;
+      for (int k = 0; k < n; ++k) v += Lpo[t * n + k] * zl[k];
+      hfin[t] = v;
+    }
+    wave_lds_sync();
+    wave0_chol_solve<kDZ>(Wc, hfin, mufin, n);
+  } else if (t < 128 && P.h_begin + hl == 0) {
+    if (t == 64) {
       double zt[6], R[9];
       compose_exp2(sc + 64, mupo, zt);
       so3_exp(zt + 3, R);
       for (int k = 0; k < 9; ++k) sc[80 + k] = R[k];
       sc[89] = zt[0]; sc[90] = zt[1]; sc[91] = 0.0;  // planar map: t[2] = 0 (CHANGELOG.md:575-578)
     }
-    __syncthreads();
-    if (t < B) pushforward_bin(st + t * 38, sc + 80, sc + 89, W2, n, P.map_inc + t * kMapRec);
-  }
-  GC_PHASE(P, 18);
-  // a14 anchor drift (anchor_drift.py:93-191): δz = μ_post of the recomposed belief
-  if (t == 0) {
-    const double rho = drift_rho(mupo, nullptr, nullptr);
-    double d6[6];
-    for (int k = 0; k < 6; ++k) d6[k] = rho * mupo[k];
-    compose_exp2(sc + 64, d6, sc + 92);  // X_fin
-    sc[98] = rho;
+    wave_lds_sync();
+    for (int b = t - 64; b < B; b += 64) pushforward_bin(st + b * 38, sc + 80, sc + 89, W2, n, P.map_inc + b * kMapRec);
   }
   __syncthreads();
   const double rho = sc[98];
-  if (t < n) zl[t] = (1.0 - rho) * mupo[t];
-  __syncthreads();
-  wg_matvec(Lpo, zl, hfin, n);
-  wg_chol_solve(Wc, hfin, mufin, n);
+  GC_PHASE(P, 18);
   GC_PHASE(P, 19);
   // write the final belief and per-hypothesis outputs
   for (int i = t; i < NN; i += kWG) P.L[(int64_t)hl * NN + i] = Lpo[i];
