@@ -77,6 +77,20 @@ __global__ void __launch_bounds__(256) k_fuse_segments(FuseArgs A, int64_t K, co
   const uint32_t key = keys[i];
   if ((int64_t)key >= A.map.m_slots || (i > 0 && keys[i - 1] == key)) return;  // dropped, or not a segment head
   const int L = A.map.n_lobes;
+  const int64_t s = key;
+  // the slot's current values are loaded first: they do not depend on the rows, so their latency
+  // overlaps the row gathers (one dependent memory round trip fewer per slot)
+  double mL[9], mth[3], met[3 * kMaxLobes], mw, mcam = 0.0, mlid = 0.0, macc[3] = {0, 0, 0}, mden = 0.0;
+  for (int q = 0; q < 9; ++q) mL[q] = A.map.Lambdas[9 * s + q];
+  for (int q = 0; q < 3; ++q) mth[q] = A.map.thetas[3 * s + q];
+  for (int q = 0; q < 3 * L; ++q) met[q] = A.map.etas[(int64_t)3 * L * s + q];
+  mw = A.map.weights[s];
+  if (A.map.cam_mass) {
+    mcam = A.map.cam_mass[s];
+    mlid = A.map.lidar_mass[s];
+    for (int q = 0; q < 3; ++q) macc[q] = A.map.rgb_cam_accum[3 * s + q];
+    mden = A.map.rgb_cam_denom[s];
+  }
   double dL[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, dth[3] = {0, 0, 0}, det[3 * kMaxLobes], dw = 0.0, dr = 0.0;
   double dcam = 0.0, dlid = 0.0, dacc[3] = {0, 0, 0}, dden = 0.0;
   for (int q = 0; q < 3 * L; ++q) det[q] = 0.0;
@@ -104,22 +118,21 @@ __global__ void __launch_bounds__(256) k_fuse_segments(FuseArgs A, int64_t K, co
       }
     }
   }
-  const int64_t s = key;
   double* Ls = A.map.Lambdas + 9 * s;
-  for (int q = 0; q < 9; ++q) Ls[q] += dL[q];
-  for (int q = 0; q < 3; ++q) A.map.thetas[3 * s + q] += dth[q];
-  for (int q = 0; q < 3 * L; ++q) A.map.etas[(int64_t)3 * L * s + q] += det[q];
-  A.map.weights[s] += dw;
+  for (int q = 0; q < 9; ++q) Ls[q] = mL[q] + dL[q];
+  for (int q = 0; q < 3; ++q) A.map.thetas[3 * s + q] = mth[q] + dth[q];
+  for (int q = 0; q < 3 * L; ++q) A.map.etas[(int64_t)3 * L * s + q] = met[q] + det[q];
+  A.map.weights[s] = mw + dw;
   A.map.timestamps[s] = A.timestamp;  // every targeted slot (primitive_map.py:1109)
   if (dr > 0.0) {
     A.map.last_supported_scan_seq[s] = A.scan_seq;
     A.map.last_update_scan_seq[s] = A.scan_seq;
   }
   if (A.map.cam_mass) {
-    A.map.cam_mass[s] += dcam;
-    A.map.lidar_mass[s] += dlid;
-    for (int q = 0; q < 3; ++q) A.map.rgb_cam_accum[3 * s + q] += dacc[q];
-    A.map.rgb_cam_denom[s] += dden;
+    A.map.cam_mass[s] = mcam + dcam;
+    A.map.lidar_mass[s] = mlid + dlid;
+    for (int q = 0; q < 3; ++q) A.map.rgb_cam_accum[3 * s + q] = macc[q] + dacc[q];
+    A.map.rgb_cam_denom[s] = mden + dden;
   }
   atomicAdd(n_unique, 1ull);  // integer count: order-independent
 }
