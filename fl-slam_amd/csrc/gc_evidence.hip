@@ -207,10 +207,17 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   for (int i = t; i < NN; i += kWG) Wc[i] = Lpo[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
   __syncthreads();
   wg_chol(Wc, n);
-  wg_chol_solve(Wc, hpo, dz, n);
-  if (t == 0) {
-    double bch[6];
-    sc[63] = recompose_pose(P.X + (int64_t)hl * 6, zl, dz, sc[61], P.c_frob, sc + 64, sc + 70, bch);  // X_new, δ'
+  // δz and the recompose on wave 0 and, beside them on wave 1, the forward substitution of
+  // Σ_post = (L_post + εI)⁻¹ (its first phase; Sx is free here)
+  if (t < 64) {
+    wave0_chol_solve<kDZ>(Wc, hpo, dz, n);
+    wave_lds_sync();
+    if (t == 0) {
+      double bch[6];
+      sc[63] = recompose_pose(P.X + (int64_t)hl * 6, zl, dz, sc[61], P.c_frob, sc + 64, sc + 70, bch);  // X_new, δ'
+    }
+  } else if (t < 128) {
+    chol_inverse_phase1_lane(Wc, Sx, n, t - 64);
   }
   __syncthreads();
   if (t < n) {
@@ -234,8 +241,11 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     wg_chol(W3, n);
     wg_chol_solve(W3, hps, mups, n);
   }
-  // Σ_post -> W2 (also the next scan's predict Σ, P.Sig); μ_post = (L_post + εI)⁻¹ h_rec on wave 1
-  wg_chol_inverse_and_solve(Wc, W2, Sx, n, hrec, mupo);
+  // Σ_post -> W2 (also the next scan's predict Σ, P.Sig) on waves 1-3 beside μ_post = (L_post + εI)⁻¹
+  // h_rec on wave 0: the same results as wg_chol_inverse_and_solve
+  if (t < 64) wave0_chol_solve<kDZ>(Wc, hrec, mupo, n);
+  else chol_inverse_phase2_part(W2, Sx, n, t - 64, kWG - 64);
+  __syncthreads();
   for (int i = t; i < NN; i += kWG) P.Sig[(int64_t)hl * NN + i] = W2[i];
   for (int idx = t; idx < 7 * 36; idx += kWG) P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
   GC_PHASE(P, 17);

@@ -231,9 +231,8 @@ GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
 // waves): thread (g = t/32, j = t%32) forms Ainv[i][j] = Σ_k W[k][i] W[k][j] for i ≡ g (mod 8),
 // its column j of W in registers and column i broadcast; k ascends over the full range (the
 // entries below the triangles are exact zeros), the order of the reference's product.
-GC_DEV void chol_inverse_phase1(const double* C, double* scratch, int n) {
-  if ((int)threadIdx.x < n) {
-    const int j = threadIdx.x;
+GC_DEV void chol_inverse_phase1_lane(const double* C, double* scratch, int n, int j) {
+  if (j < n) {
     double col[kDZ];
 #pragma unroll
     for (int i = 0; i < kDZ; ++i) {
@@ -253,13 +252,17 @@ GC_DEV void chol_inverse_phase1(const double* C, double* scratch, int n) {
       if (k < n) scratch[j * n + k] = col[k];
   }
 }
-GC_DEV void chol_inverse_phase2(double* Ainv, const double* scratch, int n) {
-  const int j = threadIdx.x & 31, g = threadIdx.x >> 5;
+GC_DEV void chol_inverse_phase1(const double* C, double* scratch, int n) {
+  chol_inverse_phase1_lane(C, scratch, n, threadIdx.x);
+}
+// phase 2 on threads tid in [0, nthr) (a multiple of 32): the same products, rows i = g (mod nthr/32)
+GC_DEV void chol_inverse_phase2_part(double* Ainv, const double* scratch, int n, int tid, int nthr) {
+  const int j = tid & 31, g = tid >> 5;
   if (j < n) {
     double wj[kDZ];
 #pragma unroll
     for (int k = 0; k < kDZ; ++k) wj[k] = k < n ? scratch[j * n + k] : 0.0;
-    for (int i = g; i < n; i += kWG / 32) {
+    for (int i = g; i < n; i += nthr / 32) {
       const double* wi = scratch + i * n;
       double v = 0.0;
 #pragma unroll
@@ -268,6 +271,9 @@ GC_DEV void chol_inverse_phase2(double* Ainv, const double* scratch, int n) {
       Ainv[i * n + j] = v;
     }
   }
+}
+GC_DEV void chol_inverse_phase2(double* Ainv, const double* scratch, int n) {
+  chol_inverse_phase2_part(Ainv, scratch, n, threadIdx.x, kWG);
 }
 GC_DEV void wg_chol_inverse(const double* C, double* Ainv, double* scratch, int n) {
   chol_inverse_phase1(C, scratch, n);
