@@ -464,6 +464,30 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     map_derive_wg(P, red, tab);
     return;
   }
+  if (blockIdx.x == 2) {
+    // ---- the IW applies and the Q rebuild on a third workgroup, beside workgroup 0's barycenter:
+    // they read only the records' IW statistics (reduced here in the same rank order as workgroup
+    // 0's record, 0.0 + Σ_g) and the IW state, and nothing of theirs is read there
+    double* Ri = Lc;  // record entries [kPDPSIP, kPX0)
+    for (int e = kPDPSIP + t; e < kPX0; e += kWG) {
+      double s = 0.0;
+      for (int g = 0; g < P.G; ++g) s += P.gather[(int64_t)g * PLn + e];
+      Ri[e - kPDPSIP] = s;
+    }
+    __syncthreads();
+    GC_PHASE(P, 22);
+    // process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
+    wg_iw_proc_apply(P.nu_proc, P.Psi_proc, Ri, Ri + (kPDNUP - kPDPSIP), S.w_process, P.eps_psd, P.nu_max, P.nu_proc,
+                     P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab);
+    GC_PHASE(P, 23);
+    // measurement-noise IW apply (measurement_noise_iw_jax.py:59-100)
+    wg_iw_meas_apply(P.nu_meas, P.Psi_meas, Ri + (kPDPSIM - kPDPSIP), Ri + (kPDNUM - kPDPSIP), P.eps_psd, P.nu_max,
+                     P.nu_meas, P.Psi_meas, P.iw_cert + 2, tab);
+    GC_PHASE(P, 24);
+    iw_Q_wg(P, Qs, Qp, Sx, red);
+    GC_PHASE(P, 25);
+    return;
+  }
   GC_PHASE(P, 20);
   // fixed rank-order reduction of the gathered partial records
   for (int e = t; e < PLn; e += kWG) {
@@ -501,18 +525,6 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     for (int i = 0; i < n; ++i) mm += R[kPMU + i] * R[kPMU + i];
     cc[10] = R[kPMU2] - mm;  // spread proxy Σ w‖μ_j‖² − ‖Σ w μ_j‖²
   }
-  __syncthreads();
-  GC_PHASE(P, 22);
-  // ---- process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
-  wg_iw_proc_apply(P.nu_proc, P.Psi_proc, R + kPDPSIP, R + kPDNUP, S.w_process, P.eps_psd, P.nu_max, P.nu_proc,
-                   P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab);
-  GC_PHASE(P, 23);
-  // ---- measurement-noise IW apply (measurement_noise_iw_jax.py:59-100)
-  wg_iw_meas_apply(P.nu_meas, P.Psi_meas, R + kPDPSIM, R + kPDNUM, P.eps_psd, P.nu_max, P.nu_meas, P.Psi_meas,
-                   P.iw_cert + 2, tab);
-  GC_PHASE(P, 24);
-  iw_Q_wg(P, Qs, Qp, Sx, red);
-  GC_PHASE(P, 25);
 }
 
 // ------------------------------------------------------------------------------ launchers
@@ -536,8 +548,8 @@ hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
 }
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
   allow_big_lds((const void*)k_combine_final, lds_final());
-  // workgroup 0: record reduction, certificates, IW apply, Q; workgroup 1: map update + derive
-  hipLaunchKernelGGL(k_combine_final, dim3(2), dim3(256), lds_final(), st, P, S);
+  // workgroup 0: record reduction, barycenter, certificates; 1: map update + derive; 2: IW apply, Q
+  hipLaunchKernelGGL(k_combine_final, dim3(3), dim3(256), lds_final(), st, P, S);
   return hipGetLastError();
 }
 hipError_t launch_map_derive(const PipeDev& P, hipStream_t st) {
