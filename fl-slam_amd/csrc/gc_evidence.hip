@@ -28,6 +28,15 @@ GC_DEV void sum_bins(const double* tab, int B, int W, double* out) {
 }
 
 // ==================================================================== a7 .. a15 per hypothesis
+// cond6 = λ_max / λ_min of the pose-6 block, both floored at ε_psd (non-finite -> ε_psd); writes
+// eigmin_pose6 to *eigmin
+GC_DEV double pose6_cond(double lmin, double lmax, double eps_psd, double* eigmin) {
+  const double mn = fmax(isfinite(lmin) ? lmin : eps_psd, eps_psd);
+  const double mx = fmax(isfinite(lmax) ? lmax : eps_psd, eps_psd);
+  *eigmin = mn;
+  return mx / mn;
+}
+
 __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   extern __shared__ double sm[];
   double* Lpr = sm;          // L_pred
@@ -157,6 +166,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   __syncthreads();
   GC_PHASE(P, 13);
   // a10: pose-6 conditioning of L_ev and the fusion scale α
+  const bool alpha_fixed = P.alpha_min == P.alpha_max;
   {
     double* P6 = W3;
     for (int idx = t; idx < 36; idx += kWG) {
@@ -166,20 +176,24 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
       P.lpose[(int64_t)hl * 36 + idx] = Lev[i * n + j];  // L_evidence[pose, pose] for the tape
     }
     __syncthreads();
-    double lmin = 0.0, lmax = 0.0;
-    if (t < 64) wave_extreme_eigvals<6>(P6, lmin, lmax);  // only λ_min / λ_max are consumed
-    if (t == 0) {
-      const double mn = fmax(isfinite(lmin) ? lmin : P.eps_psd, P.eps_psd);
-      const double mx = fmax(isfinite(lmax) ? lmax : P.eps_psd, P.eps_psd);
-      const double cond6 = mx / mn;
-      P.diag[(int64_t)hl * kHypDiag + 39] = mn;  // eigmin_pose6
-      const double ess_ev = sc[53], exc = sc[55];
-      double q = sqrt((P.c0_cond / (cond6 + P.c0_cond)) * (ess_ev / (ess_ev + 1.0)));
-      q *= exp(-sc[56]) * clampd(sc[51], 0.0, 1.0);
-      q *= clampd(sc[52] / (sc[52] + 1.0), 0.0, 1.0) * clampd(exc / (exc + 1.0), 0.0, 1.0);
-      q *= clampd(sc[50], 0.0, 1.0);
-      sc[59] = clampd(P.alpha_min + (P.alpha_max - P.alpha_min) * q, P.alpha_min, P.alpha_max);
-      sc[60] = cond6;
+    if (!alpha_fixed) {
+      double lmin = 0.0, lmax = 0.0;
+      if (t < 64) wave_extreme_eigvals<6>(P6, lmin, lmax);  // only λ_min / λ_max are consumed
+      if (t == 0) {
+        const double cond6 = pose6_cond(lmin, lmax, P.eps_psd, P.diag + (int64_t)hl * kHypDiag + 39);
+        const double ess_ev = sc[53], exc = sc[55];
+        double q = sqrt((P.c0_cond / (cond6 + P.c0_cond)) * (ess_ev / (ess_ev + 1.0)));
+        q *= exp(-sc[56]) * clampd(sc[51], 0.0, 1.0);
+        q *= clampd(sc[52] / (sc[52] + 1.0), 0.0, 1.0) * clampd(exc / (exc + 1.0), 0.0, 1.0);
+        q *= clampd(sc[50], 0.0, 1.0);
+        sc[59] = clampd(P.alpha_min + (P.alpha_max - P.alpha_min) * q, P.alpha_min, P.alpha_max);
+        sc[60] = cond6;
+      }
+    } else if (t == 0) {
+      // α_min = α_max (the reference constants): clamp(α_min + 0·q, α_min, α_min) is α_min for any
+      // q, so the fusion goes ahead and the pose-6 conditioning (diagnostics only) runs on wave 2
+      // beside the fusion's Cholesky
+      sc[59] = P.alpha_min;
     }
     __syncthreads();
   }
@@ -189,7 +203,16 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   for (int i = t; i < NN; i += kWG) W2[i] = Lps[i] + alpha * Lev[i];
   if (t < n) hpo[t] = hps[t] + alpha * hev[t];
   __syncthreads();
-  wg_psd_project_fast(W2, Lpo, P.eps_psd, n, Sx, red, c6);
+  {
+    // the pose-6 conditioning of L_ev (P6 = W3, untouched by the projection) on wave 2 when α did not need it
+    const auto cond_side = [&]() {
+      if (!alpha_fixed) return;
+      double lmin = 0.0, lmax = 0.0;
+      wave_extreme_eigvals<6>(W3, lmin, lmax);
+      if (t == 128) sc[60] = pose6_cond(lmin, lmax, P.eps_psd, P.diag + (int64_t)hl * kHypDiag + 39);
+    };
+    wg_psd_project_fast(W2, Lpo, P.eps_psd, n, Sx, red, c6, cond_side);
+  }
   GC_PHASE(P, 15);
   // a12 recompose: T from every operator's trigger magnitude (pipeline.py:1211)
   if (t == 0) {

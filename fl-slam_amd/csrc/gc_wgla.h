@@ -457,8 +457,13 @@ GC_DEV void wg_psd_project(const double* M, double* Mp, double eps, int n, doubl
 // the projection is M_sym itself (the reference's V diag(λ) Vᵀ reconstructs M_sym up to
 // rounding, ~1e-15 ||M||). projection_delta is then 0 and the eigen fields of cert6 are NaN
 // (not computed). Otherwise the full Jacobi projection runs. scratch: 2n*n + 4n doubles.
+struct NoSideWork {
+  GC_DEV void operator()() const {}
+};
+// side(): optional wave-level work for wave 2, run beside the Cholesky (no barrier inside)
+template <typename Side = NoSideWork>
 GC_DEV void wg_psd_project_fast(const double* M, double* Mp, double eps, int n, double* scratch,
-                                double* red, double* cert6) {
+                                double* red, double* cert6, const Side& side = Side()) {
   for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
     const int i = idx / n, j = idx % n;
     scratch[idx] = 0.5 * (M[i * n + j] + M[j * n + i]) - ((i == j) ? eps : 0.0);
@@ -477,6 +482,8 @@ GC_DEV void wg_psd_project_fast(const double* M, double* Mp, double eps, int n, 
     }
     symloc = wave_sum(symloc);
     if (threadIdx.x == 64) red[5] = symloc;
+  } else if (threadIdx.x < 192) {
+    side();
   }
   __syncthreads();
   const bool spd = red[4] == 0.0;
