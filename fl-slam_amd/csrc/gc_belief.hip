@@ -110,8 +110,10 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   // this thread's IMU slots, loaded beside the belief (one exposed latency for both) and parked in
   // the preintegration scratch (Bm..V2, 15 doubles per thread, not live before the IMU section)
   imu_pair_store(load_imu_pair(P.M, S.imu_t, S.imu_g, S.imu_a), Bm + 15 * t);
-  for (int i = t; i < N2; i += kWG) Lp[i] = P.L[(int64_t)h * N2 + i];
-  if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
+  if (!S.sig_cached) {  // with the cached Σ / μ of the previous scan's evidence, L and h are not read
+    for (int i = t; i < N2; i += kWG) Lp[i] = P.L[(int64_t)h * N2 + i];
+    if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
+  }
   __syncthreads();
   // --- a2 predict (predict.py:43-98): L_pred -> W1, h_pred, mu_prev, cert
   wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,

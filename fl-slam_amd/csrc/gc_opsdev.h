@@ -226,20 +226,21 @@ GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, d
                        bool full_cert = false, const double* Sig_cached = nullptr,
                        const double* mu_cached = nullptr) {
   const int t = threadIdx.x, n = kDZ;
+  const double ef = exp(-2.0 * lambda_ou * dt);
+  const double dc = (1.0 - ef) / (2.0 * lambda_ou + kF64Eps);
   if (Sig_cached) {
     // The batched pipeline's evidence kernel already factorised this very (L + εI) with the same
-    // routines (Σ_post and μ_fin of the previous scan): bit-identical, so reuse them.
-    for (int i = t; i < kNN; i += kWG) W2[i] = Sig_cached[i];
+    // routines (Σ_post and μ_fin of the previous scan): bit-identical, so reuse them; Σ and Q
+    // arrive in one round trip
+    for (int i = t; i < kNN; i += kWG) W2[i] = ef * Sig_cached[i] + dc * Q[i];
     if (t < n) mu[t] = mu_cached[t];
     __syncthreads();
   } else {
     wg_solve_lifted(Lp, hprev, mu, eps_lift, n, W1);  // W1 = chol(L + εI)
     wg_chol_inverse(W1, W2, W3, n);                    // W2 = Σ
+    for (int i = t; i < kNN; i += kWG) W2[i] = ef * W2[i] + dc * Q[i];
+    __syncthreads();
   }
-  const double ef = exp(-2.0 * lambda_ou * dt);
-  const double dc = (1.0 - ef) / (2.0 * lambda_ou + kF64Eps);
-  for (int i = t; i < kNN; i += kWG) W2[i] = ef * W2[i] + dc * Q[i];
-  __syncthreads();
   if (full_cert) wg_psd_project(W2, W3, eps_psd, n, Sx, red, c1);  // Σ'_psd -> W3
   else wg_psd_project_fast(W2, W3, eps_psd, n, Sx, red, c1);
   double trl = (t < n) ? W3[t * n + t] : 0.0;
