@@ -242,8 +242,9 @@ static size_t lds_predict() {
 }
 
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  (void)hipFuncSetAttribute((const void*)k_predict_imu, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)lds_predict());
+  if (hipError_t e = hipFuncSetAttribute((const void*)k_predict_imu, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                         (int)lds_predict()))
+    return e;
   // P.Hl hypothesis workgroups + kBudgetBlocks a1 budget workgroups (S.w_raw, S.n_in)
   hipLaunchKernelGGL(k_predict_imu, dim3(P.Hl + kBudgetBlocks), dim3(256), lds_predict(), st, P, S);
   return hipGetLastError();

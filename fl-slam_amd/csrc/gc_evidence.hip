@@ -557,11 +557,11 @@ static size_t lds_final() { return sizeof(double) * (2 * NN + 2 * NN + 4 * kDZ +
 }  // namespace gc
 
 namespace gc {
-static void allow_big_lds(const void* fn, size_t bytes) {
-  if (bytes > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+static hipError_t allow_big_lds(const void* fn, size_t bytes) {
+  return bytes > 65536 ? hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) : hipSuccess;
 }
 hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  allow_big_lds((const void*)k_evidence, lds_evidence());
+  if (hipError_t e = allow_big_lds((const void*)k_evidence, lds_evidence())) return e;
   hipLaunchKernelGGL(k_evidence, dim3(P.Hl), dim3(256), lds_evidence(), st, P, S);
   return hipGetLastError();
 }
@@ -570,7 +570,7 @@ hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
   return hipGetLastError();
 }
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  allow_big_lds((const void*)k_combine_final, lds_final());
+  if (hipError_t e = allow_big_lds((const void*)k_combine_final, lds_final())) return e;
   // workgroup 0: record reduction, barycenter, certificates; 1: map update + derive; 2: IW apply, Q
   hipLaunchKernelGGL(k_combine_final, dim3(3), dim3(256), lds_final(), st, P, S);
   return hipGetLastError();

@@ -568,8 +568,8 @@ __global__ void __launch_bounds__(256) k_op_barycenter(int H, const double* L, c
 }
 
 size_t lds_bytes(int doubles) { return sizeof(double) * (size_t)doubles; }
-void allow_lds(const void* fn, size_t bytes) {
-  if (bytes > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+hipError_t allow_lds(const void* fn, size_t bytes) {
+  return bytes > 65536 ? hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) : hipSuccess;
 }
 
 }  // namespace
@@ -599,7 +599,7 @@ int32_t gc_predict_diffusion_batch(gc_ctx* ctx, int32_t H, const double* d_L, co
   GC_CHECK_ARG(ctx, H > 0 && d_L && d_h && d_Q && d_L_out && d_h_out && d_cert_out, "bad arguments");
   GC_CHECK_ARG(ctx, lambda_ou >= 0.0, "lambda_ou must be >= 0");
   const size_t sh = lds_bytes(5 * kNN + 2 * kNN + 4 * kDZ + 3 * kDZ + 32);
-  allow_lds((const void*)k_op_predict, sh);
+  GC_HIP(ctx, allow_lds((const void*)k_op_predict, sh));
   hipLaunchKernelGGL(k_op_predict, dim3(H), dim3(256), sh, ctx->stream, d_L, d_h, d_Q, dt_sec, eps_psd, eps_lift,
                      lambda_ou, d_L_out, d_h_out, d_cert_out);
   GC_LAUNCH_CHECK(ctx);
@@ -629,7 +629,7 @@ int32_t gc_preintegrate_imu_batch(gc_ctx* ctx, int32_t H, int32_t M, const doubl
   const double g0 = h_gravity3 ? h_gravity3[0] : kGravity[0], g1 = h_gravity3 ? h_gravity3[1] : kGravity[1],
                g2 = h_gravity3 ? h_gravity3[2] : kGravity[2];
   const size_t sh = lds_bytes(256 * 24 + 16 + kPreint + 9);
-  allow_lds((const void*)k_op_preintegrate, sh);
+  GC_HIP(ctx, allow_lds((const void*)k_op_preintegrate, sh));
   hipLaunchKernelGGL(k_op_preintegrate, dim3(H), dim3(256), sh, ctx->stream, M, d_stamps, d_gyro, d_accel, d_weights,
                      weights_stride, d_rotvec0, d_gyro_bias, d_accel_bias, g0, g1, g2, d_out);
   GC_LAUNCH_CHECK(ctx);
@@ -746,7 +746,7 @@ int32_t gc_iw_process_suffstats_batch(gc_ctx* ctx, int32_t H, const double* d_L_
   GC_OP_CTX(ctx);
   GC_CHECK_ARG(ctx, H > 0 && d_L_pred && d_h_pred && d_L_post && d_h_post && d_dPsi_out && d_dnu_out, "bad arguments");
   const size_t sh = lds_bytes(6 * kNN + 4 * kDZ);
-  allow_lds((const void*)k_op_iw_proc_stats, sh);
+  GC_HIP(ctx, allow_lds((const void*)k_op_iw_proc_stats, sh));
   hipLaunchKernelGGL(k_op_iw_proc_stats, dim3(H), dim3(256), sh, ctx->stream, d_L_pred, d_h_pred, d_L_post, d_h_post,
                      eps_lift, d_dPsi_out, d_dnu_out);
   GC_LAUNCH_CHECK(ctx);

@@ -315,6 +315,52 @@ GC_DEV void deskew_point_series(const double* p, double alpha, const double* xi,
   q[0] = p[0] - t[0]; q[1] = p[1] - t[1]; q[2] = p[2] - t[2];
   mat3_tvec(R, q, out);
 }
+// Fused-kernel deskew in cross-product form: V ρ = ρ + B φ×ρ + C φ×(φ×ρ) and Rᵀ q = q − a φ×q + B φ×(φ×q)
+// (the same Rodrigues matrices applied as vectors: 4 cross products instead of two 3x3 forms and two
+// matrix-vector products). SHORT: the series for θ² <= kDeskewShortTs (six terms, first omitted term
+// < 1e-18 relative), chosen wave-uniformly by the caller; otherwise ten terms (θ² <= 1), and the
+// sincos form beyond.
+constexpr double kDeskewShortTs = 0.04;
+template <bool SHORT>
+GC_DEV void deskew_point_cross(const double* p, double alpha, const double* xi, double* out) {
+  const double phi[3] = {alpha * xi[3], alpha * xi[4], alpha * xi[5]};
+  const double ts = dot3(phi, phi);
+  if (!SHORT && ts > 1.0) {
+    deskew_point_fast(p, alpha, xi, out);
+    return;
+  }
+  const double rho[3] = {alpha * xi[0], alpha * xi[1], alpha * xi[2]};
+  const double u = -ts;
+  constexpr int K = SHORT ? 5 : 9;  // highest power of θ² kept
+  double a = kInvFact[2 * K + 1], Bv = kInvFact[2 * K + 2], Cv = kInvFact[2 * K + 3];
+#pragma unroll
+  for (int k = K - 1; k >= 0; --k) {
+    a = fma(a, u, kInvFact[2 * k + 1]);
+    Bv = fma(Bv, u, kInvFact[2 * k + 2]);
+    Cv = fma(Cv, u, kInvFact[2 * k + 3]);
+  }
+  double c1[3], c2[3], q[3];
+  cross3(phi, rho, c1);
+  cross3(phi, c1, c2);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) q[k] = p[k] - fma(Cv, c2[k], fma(Bv, c1[k], rho[k]));
+  cross3(phi, q, c1);
+  cross3(phi, c1, c2);
+#pragma unroll
+  for (int k = 0; k < 3; ++k) out[k] = fma(Bv, c2[k], fma(-a, c1[k], q[k]));
+}
+// point_features with w folded into the first factor of each product (w d_i d_j as (w d_i) d_j)
+GC_DEV void point_features_w(const double* p, const double* d, double w, double* f) {
+  const double wd[3] = {w * d[0], w * d[1], w * d[2]};
+  const double wp[3] = {w * p[0], w * p[1], w * p[2]};
+  f[0] = w;
+  f[1] = wd[0]; f[2] = wd[1]; f[3] = wd[2];
+  f[4] = wd[0] * d[0]; f[5] = wd[0] * d[1]; f[6] = wd[0] * d[2];
+  f[7] = wd[1] * d[1]; f[8] = wd[1] * d[2]; f[9] = wd[2] * d[2];
+  f[10] = wp[0]; f[11] = wp[1]; f[12] = wp[2];
+  f[13] = wp[0] * p[0]; f[14] = wp[0] * p[1]; f[15] = wp[0] * p[2];
+  f[16] = wp[1] * p[1]; f[17] = wp[1] * p[2]; f[18] = wp[2] * p[2];
+}
 GC_DEV void direction_fast(const double* p, const double* o, double eps, double* d) {
   const double r0 = p[0] - o[0], r1 = p[1] - o[1], r2 = p[2] - o[2];
   const double inv = recip(sqrt(r0 * r0 + r1 * r1 + r2 * r2) + eps);
@@ -439,11 +485,13 @@ __global__ void k_point_dirs(int64_t rows, const double* __restrict__ pts, doubl
 // ============================================================================ a5 soft assign
 // grid (chunks, H), chunk = iters*256 points; each wave owns 64 points per iteration with
 // lane = point: the 16*BPL similarities, exps and the softmax sum of a point stay in one lane
-// (no cross-lane reductions), the bin directions are wave-uniform (scalar loads), and the
-// argmax is a running compare in bin order (lowest index on ties). The lane's normalised row
-// is transposed through a wave-private LDS slab one 16-bin block at a time (row stride 18
-// doubles: the 8 lanes of a ds_write_b128 group hit disjoint banks) and leaves as contiguous
-// 128-B row segments, 16 B per lane (FULL: B == 16*BPL) or 8 B per lane (ragged B).
+// (no cross-lane reductions) and the bin directions are wave-uniform LDS reads.
+// The bin index is a running argmax in bin order (lowest index on ties).
+// FULL (B == 16 BPL <= 48): the normalised rows leave through a wave-private LDS slab one half-wave at a
+// time: 32 rows of B doubles (row stride B + 2: the 8 lanes of a ds_write_b128 group hit disjoint
+// banks) go out as the contiguous 32·B·8-byte block they form in HBM, 16 B per lane, 1 KiB per store
+// instruction. Ragged B and B = 64: the rows are transposed one 16-bin block at a time (row stride 18) and leave
+// as 128-B row segments, 8 B per lane.
 // One 16-bin block of a wave's 64 normalised rows, from the LDS transpose slab (row stride 18) to
 // HBM as 128-B row segments: 16 B per lane (FULL, B == 16 BPL) or 8 B per lane (ragged B).
 template <int BPL, bool FULL>
@@ -475,17 +523,23 @@ GC_DEV void sa_store_block(const double* S, double* Rh, int64_t wbase, int64_t n
 // 0.9 GB of extra writes per C3 launch, tools/probe/probe_sa3.hip; 1.74 -> 1.32 ms)
 #define GC_SA_OCC 2
 #endif
+// dynamic LDS of a soft-assign workgroup (doubles): exp table | bins (x, y, z rows of 64) | reduction |
+// 4 wave slabs (FULL: 32 rows of 16 BPL + 2; ragged: 64 rows of 18)
+__host__ __device__ constexpr bool sa_linear(int BPL, bool full) { return full && BPL <= 3; }  // B = 64: 16-bin blocks (register budget)
+__host__ __device__ constexpr int sa_slab_doubles(int BPL, bool full) { return sa_linear(BPL, full) ? 32 * (16 * BPL + 2) : 64 * 18; }
+__host__ __device__ constexpr int sa_lds_doubles(int BPL, bool full) { return kExpTab2 + 192 + 8 + 4 * sa_slab_doubles(BPL, full); }
 template <int BPL, bool FULL>
 __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
                                                      const double* __restrict__ bins, double inv_tau,
                                                      double* resp, int32_t* bin_idx, double* partial) {
   constexpr int NB = 16 * BPL;
-  constexpr int RS = 18;
+  constexpr int RS = 18;       // ragged slab row stride
+  constexpr int RS2 = NB + 2;  // FULL slab row stride
   typedef double dvec2 __attribute__((ext_vector_type(2)));
-  __shared__ double red[8];
-  __shared__ double Tx[kExpTab2];
-  __shared__ double Lb[3 * 64];  // bin directions, x / y / z rows of 64 (zero past B)
-  __shared__ __attribute__((aligned(16))) double Sl[4][64 * RS];
+  extern __shared__ __attribute__((aligned(16))) double sa_lds[];
+  double* Tx = sa_lds;
+  double* Lb = Tx + kExpTab2;  // bin directions, x / y / z rows of 64 (zero past B)
+  double* red = Lb + 192;
   exp_table2_init(Tx);
   if (threadIdx.x < 64) {
     const int b = threadIdx.x;
@@ -498,7 +552,7 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double* Rh = resp + (int64_t)h * n * B;
   const double* Dh = dirs + (int64_t)h * n * 3;
-  double* S = Sl[wv];
+  double* S = red + 8 + wv * sa_slab_doubles(BPL, FULL);
   const double Beps = (double)B * 1e-12;
   // Σ log Z is kept as a product of mantissas and a sum of exponents (frexp), one log at the end
   double zm = 1.0, entq = 0.0, mxr = 0.0;
@@ -542,9 +596,11 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
       ex[j] = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
       if ((FULL || j < B) && ex[j] > best) { best = ex[j]; bidx = j; }
     }
-    // exponent in units of ln2/2048 (the 2048-entry table exp, exp2s_n); arguments below e^-700
-    // are clamped there (R <= 1e-304 / Z instead of an underflow to 0)
+    // exponent in units of ln2/2048 (the 2048-entry table exp, exp2s_n): y = S ysc - S_max ysc by one
+    // fma (the maximal bin gets y = the rounding error of S_max ysc, |y| < 1e-11, e = 1 within an ulp);
+    // arguments below e^-700 are clamped there (R <= 1e-304 / Z instead of an underflow to 0)
     const double ysc = inv_tau * kTab2OverLn2;
+    const double nbs = -(best * ysc);
     double Z = 0.0, sl = 0.0;
 #pragma unroll
     for (int j0 = 0; j0 < NB; j0 += 8) {
@@ -552,7 +608,7 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
 #pragma unroll
       for (int jj = 0; jj < 8; ++jj) {
         const int j = j0 + jj;
-        y[jj] = (FULL || j < B) ? fmax((ex[j] - best) * ysc, -700.0 * kTab2OverLn2) : 0.0;
+        y[jj] = (FULL || j < B) ? fmax(fma(ex[j], ysc, nbs), -700.0 * kTab2OverLn2) : 0.0;
       }
       double e8[8];
       exp2s_n<8>(y, Tx, e8);
@@ -566,7 +622,7 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
       asm volatile("" : "+v"(Z), "+v"(sl));  // accumulate now: the y of a group die here
     }
     sl *= kExp2C1;  // Σ e x in nats
-    // the maximal bin has x = 0 and e = 1 exactly: Z >= 1 and max_b R = 1/Z
+    // the maximal bin has e = 1 (within an ulp): Z >= 1 and max_b R = 1/Z
     const double rZ = recip(Z);
     if (valid) {
       // entropy of the point: log Z - S/Z - B ε   (-Σ R log(R+ε) up to ≤ B·ε)
@@ -577,15 +633,42 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
       mxr = fmax(mxr, rZ);
       if (bin_idx) bin_idx[(int64_t)h * n + pt] = bidx;
     }
+    if constexpr (sa_linear(BPL, FULL)) {
 #pragma unroll
-    for (int blk = 0; blk < BPL; ++blk) {
+      for (int j = 0; j < NB; ++j) ex[j] *= rZ;
 #pragma unroll
-      for (int q = 0; q < 8; ++q)
-        *reinterpret_cast<dvec2*>(&S[lane * RS + 2 * q]) =
-            dvec2{ex[16 * blk + 2 * q] * rZ, ex[16 * blk + 2 * q + 1] * rZ};
-      lds_wave_sync();
-      sa_store_block<BPL, FULL>(S, Rh, wbase, n, B, blk, lane);
-      lds_wave_sync();
+      for (int hf = 0; hf < 2; ++hf) {
+        if ((lane >> 5) == hf) {
+          const int i = lane & 31;
+#pragma unroll
+          for (int q = 0; q < NB / 2; ++q)
+            *reinterpret_cast<dvec2*>(&S[i * RS2 + 2 * q]) = dvec2{ex[2 * q], ex[2 * q + 1]};
+        }
+        lds_wave_sync();
+        // the half's 32 rows are one contiguous block of 32 NB doubles in HBM: 1 KiB per instruction
+        const int64_t pbase = wbase + 32 * hf;
+        double* dst = Rh + pbase * NB;
+        const int64_t lim = (n - pbase) * NB;  // doubles of the block that belong to points < n
+#pragma unroll
+        for (int m = 0; m < NB / 4; ++m) {
+          const int o = m * 128 + 2 * lane;
+          const int row = o / NB, col = o - row * NB;
+          const dvec2 v = *reinterpret_cast<const dvec2*>(&S[row * RS2 + col]);
+          if (o < lim) *reinterpret_cast<dvec2*>(dst + o) = v;
+        }
+        lds_wave_sync();
+      }
+    } else {
+#pragma unroll
+      for (int blk = 0; blk < BPL; ++blk) {
+#pragma unroll
+        for (int q = 0; q < 8; ++q)
+          *reinterpret_cast<dvec2*>(&S[lane * RS + 2 * q]) =
+              dvec2{ex[16 * blk + 2 * q] * rZ, ex[16 * blk + 2 * q + 1] * rZ};
+        lds_wave_sync();
+        sa_store_block<BPL, FULL>(S, Rh, wbase, n, B, blk, lane);
+        lds_wave_sync();
+      }
     }
     int e;
     zm = frexp(zm, &e);  // renormalise once per 64 points: |log2 zm| stays below ~64
@@ -628,7 +711,10 @@ __global__ void k_soft_assign_finalize(const double* __restrict__ partial, int64
 // NACC = 2: even and odd steps accumulate into separate tiles (2*BPL*NT independent MFMA chains)
 // added in the epilogue. The 4 waves are reduced in a fixed order into one record per chunk.
 constexpr int kMomFS = 34;
-template <int BPL, bool COV, bool LAM, int NACC>
+// PAIR (B >= 32, 16-B aligned rows): bins 0..31 arrive as one 16-B load per lane (bins 2l, 2l+1 of its
+// point: four 256-B row segments per load instead of two loads of four 128-B segments); tile 0 holds
+// the even bins, tile 1 the odd ones (row i of tile j < 2 is bin 2i + j), tiles >= 2 bins 16j + l.
+template <int BPL, bool COV, bool LAM, int NACC, bool PAIR>
 __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, int groups,
                                                            const double* __restrict__ pts,
                                                            const double* __restrict__ covs,
@@ -670,7 +756,13 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
       int64_t p_ = (BASE) + 4 * s_ + g;                                         \
       p_ = p_ < wend ? p_ : wend - 1; /* prefetch past the range re-reads a line */ \
       const double* row_ = Rh + p_ * B;                                         \
-      _Pragma("unroll") for (int j_ = 0; j_ < BPL; ++j_) RR[s_][j_] = GC_RESP_LOAD(row_ + cb[j_]); \
+      if constexpr (PAIR) {                                                     \
+        typedef double dv2_ __attribute__((ext_vector_type(2)));                \
+        const dv2_ v_ = *reinterpret_cast<const dv2_*>(row_ + 2 * bl);         \
+        RR[s_][0] = v_.x;                                                       \
+        RR[s_][1] = v_.y;                                                       \
+      }                                                                         \
+      _Pragma("unroll") for (int j_ = PAIR ? 2 : 0; j_ < BPL; ++j_) RR[s_][j_] = GC_RESP_LOAD(row_ + cb[j_]); \
     }                                                                           \
   }
   // raw inputs of one 32-point group (point = lane & 31), loaded by every lane into registers and
@@ -761,7 +853,7 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
     for (int t = 0; t < NT; ++t)
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const int b = 16 * j + g + 4 * r, k = 16 * t + bl;  // D[row g + 4r][col l]
+        const int b = (PAIR && j < 2) ? 2 * (g + 4 * r) + j : 16 * j + g + 4 * r, k = 16 * t + bl;  // D[row g + 4r][col l]
         if (b < B && k < NF) red[(wv * B + b) * NF + k] = NACC == 2 ? acc[0][j][t][r] + acc[NACC - 1][j][t][r] : acc[0][j][t][r];
       }
   __syncthreads();
@@ -960,10 +1052,15 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
         const double tt = ntt, ww = nww * scale;
         if (it + 1 < iters) fetch(it + 1);
         double q[3], d[3], f[NF];
-        deskew_point_series(p, (tt - t0) * inv_denom, xr, q);
+        const double al = (tt - t0) * inv_denom;
+        {  // six series terms when every lane of the wave has θ² <= kDeskewShortTs (wave-uniform branch)
+          const double ph[3] = {al * xr[3], al * xr[4], al * xr[5]};
+          if (__all(dot3(ph, ph) <= kDeskewShortTs)) deskew_point_cross<true>(p, al, xr, q);
+          else deskew_point_cross<false>(p, al, xr, q);
+        }
         const double wd = inr ? (PRE ? ww : ww * window_weight2(tt, t0, t1, inv_sig, Tx)) : 0.0;
         direction_fast(q, o, 1e-12, d);
-        point_features(q, d, wd, f);
+        point_features_w(q, d, wd, f);
         sumw += wd;
   #pragma unroll
         for (int k = 0; k < NF; ++k) F[k * kFusedFS + lane] = f[k];
@@ -1411,12 +1508,18 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
   const bool full = (B % 16) == 0 && ((uintptr_t)d_resp_out & 15) == 0;
 #define GC_SA(BP)                                                                                        \
   do {                                                                                                   \
-    if (full)                                                                                            \
-      hipLaunchKernelGGL((k_soft_assign<BP, true>), grid, dim3(256), 0, ctx->stream, n, B, iters, d_dirs, d_bins, \
-                         inv_tau, d_resp_out, d_bin_index_out, (double*)scr);                            \
-    else                                                                                                 \
-      hipLaunchKernelGGL((k_soft_assign<BP, false>), grid, dim3(256), 0, ctx->stream, n, B, iters, d_dirs, d_bins, \
-                         inv_tau, d_resp_out, d_bin_index_out, (double*)scr);                            \
+    const size_t sh = sizeof(double) * (size_t)sa_lds_doubles(BP, full);                                 \
+    if (full) {                                                                                          \
+      GC_HIP(ctx, hipFuncSetAttribute((const void*)k_soft_assign<BP, true>,                              \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));            \
+      hipLaunchKernelGGL((k_soft_assign<BP, true>), grid, dim3(256), sh, ctx->stream, n, B, iters, d_dirs, \
+                         d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr);                    \
+    } else {                                                                                             \
+      GC_HIP(ctx, hipFuncSetAttribute((const void*)k_soft_assign<BP, false>,                             \
+                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));            \
+      hipLaunchKernelGGL((k_soft_assign<BP, false>), grid, dim3(256), sh, ctx->stream, n, B, iters, d_dirs, \
+                         d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr);                    \
+    }                                                                                                    \
   } while (0)
   switch (bpl_for(B)) { case 1: GC_SA(1); break; case 2: GC_SA(2); break; case 3: GC_SA(3); break; default: GC_SA(4); }
 #undef GC_SA
@@ -1459,14 +1562,20 @@ int32_t gc_scan_bin_moment_match(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, c
   const int bpl = bpl_for(B);
   const int NT = (NF + 15) / 16;
   const size_t sh = sizeof(double) * std::max<size_t>((size_t)4 * 16 * NT * kMomFS, (size_t)4 * B * NF);
+#ifndef GC_MOM_PAIR
+#define GC_MOM_PAIR 1
+#endif
+  const bool pair = GC_MOM_PAIR && B >= 32 && ((uintptr_t)d_resp & 15) == 0;
+#define GC_MOM_L(BP, CV, LM, PR)                                                                                 \
+  hipLaunchKernelGGL((k_moment_partials<BP, CV, LM, 1, PR>), grid, dim3(256), sh, ctx->stream, n, B, groups,    \
+                     d_points, d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr)
 #define GC_MOM(BP, CV)                                                                                          \
   do {                                                                                                          \
-    if (d_lambda)                                                                                               \
-      hipLaunchKernelGGL((k_moment_partials<BP, CV, true, 1>), grid, dim3(256), sh, ctx->stream, n, B, groups,  \
-                         d_points, d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr);             \
-    else                                                                                                        \
-      hipLaunchKernelGGL((k_moment_partials<BP, CV, false, 1>), grid, dim3(256), sh, ctx->stream, n, B, groups, \
-                         d_points, d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr);             \
+    if (d_lambda) {                                                                                             \
+      if (pair && BP >= 2) GC_MOM_L(BP, CV, true, (BP >= 2)); else GC_MOM_L(BP, CV, true, false);              \
+    } else {                                                                                                    \
+      if (pair && BP >= 2) GC_MOM_L(BP, CV, false, (BP >= 2)); else GC_MOM_L(BP, CV, false, false);            \
+    }                                                                                                           \
   } while (0)
   if (cov) {
     switch (bpl) { case 1: GC_MOM(1, true); break; case 2: GC_MOM(2, true); break; case 3: GC_MOM(3, true); break; default: GC_MOM(4, true); }
@@ -1474,6 +1583,7 @@ int32_t gc_scan_bin_moment_match(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, c
     switch (bpl) { case 1: GC_MOM(1, false); break; case 2: GC_MOM(2, false); break; case 3: GC_MOM(3, false); break; default: GC_MOM(4, false); }
   }
 #undef GC_MOM
+#undef GC_MOM_L
   GC_LAUNCH_CHECK(ctx);
   return launch_finalize(ctx, H, B, NF, chunks, (const double*)scr, eps_psd, eps_mass, d_stats_out, d_cert_out);
 }

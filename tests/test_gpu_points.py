@@ -61,7 +61,7 @@ def test_deskew_matches_oracle(ctx):
     assert cert.exact and cert.support.ess_total == 3.0
 
 
-@pytest.mark.parametrize("B,n", [(48, 4096), (20, 1000), (64, 777), (7, 300), (48, 65536)])
+@pytest.mark.parametrize("B,n", [(48, 4096), (20, 1000), (64, 777), (7, 300), (48, 65536), (48, 1000), (32, 333), (16, 97)])
 def test_soft_assign_matches_oracle(ctx, B, n):
     from gcslam.ops.binning import bin_soft_assign_batch
     rng = np.random.default_rng(3 + B)
