@@ -1147,17 +1147,33 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
 // own record, so the result does not depend on which workgroup ran it (bit-reproducible). ctr[0]
 // is the task counter, ctr[1] the count of finished pullers; the last one resets both for the next
 // launch (stream order makes the reset visible to it). No workgroup waits on another.
+#ifdef GC_BINS_TIMING  // dev: per-workgroup [start, first task, end, tasks, iterations] cycle counters
+__device__ double g_bins_dbg[8192 * 5];
+#endif
 template <int BPL, bool FULL>
 __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
                                                              const double* __restrict__ odom, int n_io, int H,
                                                              int64_t chunks, unsigned* ctr) {
   extern __shared__ double lds[];
   __shared__ unsigned task_s;
+#ifdef GC_BINS_TIMING
+  const double tb0 = (double)__builtin_readcyclecounter();
+  double tb1 = 0.0, ntask = 0.0, nit = 0.0;
+#endif
   if ((int)blockIdx.x < n_io) {
     io_branch_wg(P, S, odom, blockIdx.x, lds);
+#ifdef GC_BINS_TIMING
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {
+      double* d = g_bins_dbg + 5 * blockIdx.x;
+      d[0] = tb0; d[1] = tb0; d[2] = (double)__builtin_readcyclecounter(); d[3] = -1.0; d[4] = 0.0;
+    }
+#endif
     return;
   }
   bins_prologue(A, lds);
+#ifdef GC_BINS_TIMING
+  tb1 = (double)__builtin_readcyclecounter();
+#endif
   const int RL = A.B * NF_BASE + REC_EXTRA;
   const unsigned T = (unsigned)(H * chunks);
   // the next task's ticket is taken at the start of the current one, so the atomic's round trip
@@ -1174,7 +1190,17 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, Pipe
     const int64_t c = t / H;
     const int h = t % H;
     bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL);
+#ifdef GC_BINS_TIMING
+    ntask += 1.0;
+    nit += (c < A.k1) ? A.iters : A.iters_s;
+#endif
   }
+#ifdef GC_BINS_TIMING
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    double* d = g_bins_dbg + 5 * blockIdx.x;
+    d[0] = tb0; d[1] = tb1; d[2] = (double)__builtin_readcyclecounter(); d[3] = ntask; d[4] = nit;
+  }
+#endif
   if (threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == gridDim.x - n_io - 1) {
     atomicExch(ctr, 0u);
     atomicExch(ctr + 1, 0u);
@@ -1436,6 +1462,12 @@ hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, d
 }  // namespace gc
 
 extern "C" {
+
+#ifdef GC_BINS_TIMING
+int32_t gc_debug_bins_timing(double* host, int64_t n) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gc::g_bins_dbg), sizeof(double) * (size_t)n) == hipSuccess ? 0 : 1;
+}
+#endif
 
 int32_t gc_budget_stats(gc_ctx* ctx, const double* d_w, int64_t n_in, int64_t n_cap, double* d_out) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
