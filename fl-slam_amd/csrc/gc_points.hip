@@ -28,7 +28,10 @@ constexpr int NF_BASE = 19;   // [1, d(3), dd(6: 00 01 02 11 12 22), p(3), pp(6)
 constexpr int NF_COV = 9;     // full 3x3 point covariance x w
 constexpr int REC_EXTRA = 4;  // [entropy_sum, max_resp, sum_w, n_points]
 #ifndef GC_NT_RESP
-#define GC_NT_RESP 0  // non-temporal responsibility stream (tuning knob, probes)
+// the moment kernel reads the responsibility stream exactly once: non-temporal loads for the 8-B
+// per-lane tiles (A/B on one box, C3 contract launch: 1.548 -> 1.49 ms; the paired 16-B loads of bins
+// 0-31 stay temporal: non-temporal there too measured 1.52, profiles/r02/ab_contract_pair_nt.txt)
+#define GC_NT_RESP 1
 #endif
 #if GC_NT_RESP
 #define GC_RESP_LOAD(ptr) __builtin_nontemporal_load(ptr)
