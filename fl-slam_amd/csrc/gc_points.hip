@@ -1533,7 +1533,10 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
   GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
   GC_CHECK_ARG(ctx, tau > 0.0, "tau must be positive");
   GC_CHECK_ARG(ctx, d_dirs && d_bins && d_resp_out && d_cert_out, "NULL buffer");
-  int iters = 8;
+#ifndef GC_SA_ITERS
+#define GC_SA_ITERS 8
+#endif
+  int iters = GC_SA_ITERS;
   while (iters > 1 && ((n + iters * 256 - 1) / (iters * 256)) * (int64_t)H < 4096) iters >>= 1;
   const int64_t blocks = (n + iters * 256 - 1) / (iters * 256);
   void* scr;
