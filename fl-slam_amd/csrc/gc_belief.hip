@@ -148,10 +148,6 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   }
   __syncthreads();
   GC_PHASE(P, 4);
-  if (t == 0) {
-    compose_exp(P.X + (int64_t)h * 6, mu_inc, misc + 8);  // pose_pred (for MF / planar)
-    for (int k = 0; k < 6; ++k) P.pose_pred[(int64_t)h * 6 + k] = misc[8 + k];
-  }
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + 22 + t] = mu_inc[t];
   // ------------------------------------------------------------------ IMU (a3)
   const ImuPair q = imu_pair_load(Bm + 15 * t);  // own slots: no barrier needed
@@ -213,6 +209,13 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   GC_PHASE(P, 7);
   wg_sum_n<12>(rr, A);
   GC_PHASE(P, 8);
+  if (t == 128) {
+    // pose_pred = X ⊕ μ_inc (for MF / planar in the later kernels; nothing here reads it) on wave 2
+    // beside the ξ_body and IW-statistics lanes
+    double pp[6];
+    compose_exp(P.X + (int64_t)h * 6, mu_inc, pp);
+    for (int k = 0; k < 6; ++k) P.pose_pred[(int64_t)h * 6 + k] = pp[k];
+  }
   if (t == 64) {  // ξ_body = se3_log(R0ᵀ Δpose) on wave 1 beside thread 0's IW statistics
     double dR[9], dpose[6], xi[6];
     mat3_mul_tn(R0, pre, dR);

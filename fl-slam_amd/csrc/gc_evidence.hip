@@ -85,14 +85,12 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     const double* s = st + t * 38;
     const double* m = P.map + t * kMapRec;
     mf_bin_row(s[0], s + 1, m[12], m, eps, tab + t * 10);
+  } else if (t == 64) {  // R_pred on wave 1 beside the per-bin rows (B <= 64)
+    so3_exp(P.pose_pred + (int64_t)hl * 6 + 3, sc + 100);
   }
   __syncthreads();
   sum_bins(tab, B, 10, acc);
-  if (t == 0) {
-    double Rp[9];
-    so3_exp(P.pose_pred + (int64_t)hl * 6 + 3, Rp);
-    mf_finalize(acc, Rp, eps, P.eps_psd, mf);
-  }
+  if (t == 0) mf_finalize(acc, sc + 100, eps, P.eps_psd, mf);
   __syncthreads();
   GC_PHASE(P, 11);
   // ---------------------------------------------- a8 planar translation WLS (R_hat = R_mf)
