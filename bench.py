@@ -38,6 +38,9 @@ def parse():
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=50,
                     help="untimed steps first: the clocks ramp over the first ~30 ms of sustained f64 load")
+    ap.add_argument("--prewarm-s", type=float, default=0.25,
+                    help="untimed steps run for this many seconds before the --warmup steps, so a small W "
+                         "still times the steady-state clocks (reported as prewarm_steps)")
     ap.add_argument("--hyps", type=int, default=256, help="total hypotheses per scan (strong scaling)")
     ap.add_argument("--n-az", type=int, default=4096, help="azimuth steps (x16 rings = points)")
     ap.add_argument("--scans", type=int, default=4, help="distinct resident scans cycled through")
@@ -168,6 +171,19 @@ def main():
         pipe.run_scan(k, scans[k], count[0])
         count[0] += 1
 
+    # clock ramp: untimed steps for prewarm_s of sustained load (a 5-step W is ~7 ms, less than the
+    # ~30 ms the clocks take to ramp under this f64 load), then the W warmup steps
+    # (blocks of 10; every rank takes the same decision from the max over ranks, since each step
+    # runs a collective when N > 1)
+    t_pw = time.perf_counter()
+    prewarm_steps = 0
+    while args.prewarm_s > 0.0:
+        for _ in range(10):
+            step()
+        prewarm_steps += 10
+        ctx.sync()
+        if dist.max(time.perf_counter() - t_pw) >= args.prewarm_s:
+            break
     for _ in range(args.warmup):
         step()
     ctx.sync()
@@ -189,6 +205,7 @@ def main():
         "n_gpus": dist.world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "prewarm_steps": prewarm_steps,
         "ms_per_step": 1e3 * elapsed / args.steps,
         "higher_is_better": True,
         "scaling": "strong",
