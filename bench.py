@@ -53,7 +53,52 @@ def parse():
                     help="run only the contract-pair roofline leg (PMC traffic passes, tools/pmc_traffic.sh)")
     ap.add_argument("--io-given", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--roofline-reps", type=int, default=10)
+    ap.add_argument("--no-ingest", action="store_true",
+                    help="stage the scans once before the timed region (round-2 methodology) instead of every step")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch the ranks and exchange the communicator id, then exit (no GPU work)")
     return ap.parse_args()
+
+
+def launch_ranks(n: int) -> int:
+    """`bench.py --gpus N` without a torch.distributed.run environment: re-launch this script under
+    torch.distributed.run with N ranks (one process per GPU) as a child process and return its exit
+    code. Nothing in this parent process touches the GPU."""
+    import socket
+    import subprocess
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__), *sys.argv[1:]]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(dist):
+    """The rank launch and the communicator-id exchange without GPU work: rank 0 makes the RCCL
+    unique id (a random token of the same size when no GPU is visible) and broadcasts it; rank 0
+    prints every rank's view of (rank, world, id digest)."""
+    import hashlib
+    uid = None
+    if dist.rank == 0:
+        from gcslam import _abi
+        try:
+            from gcslam.pipeline import BatchedScanPipeline
+            uid = BatchedScanPipeline.comm_unique_id() if _abi.device_count() > 0 else None
+        except RuntimeError:
+            uid = None
+        uid = uid if uid is not None else os.urandom(128)
+    if dist.world > 1:
+        box = [uid]
+        dist.td.broadcast_object_list(box, src=0)
+        uid = box[0]
+        views = [None] * dist.world
+        dist.td.all_gather_object(views, (dist.rank, dist.world, hashlib.sha256(uid).hexdigest()))
+    else:
+        views = [(0, 1, hashlib.sha256(uid).hexdigest())]
+    if dist.rank == 0:
+        print(json.dumps({"dry_run": True, "n_ranks": dist.world, "ranks": views}), flush=True)
 
 
 class Dist:
@@ -81,6 +126,11 @@ class Dist:
         t = torch.tensor([x], dtype=torch.float64)
         self.td.all_reduce(t, op=self.td.ReduceOp.MAX)
         return float(t.item())
+
+
+def pipe_partial_len(pipe):
+    from gcslam.pipeline import partial_len
+    return partial_len(pipe.B)
 
 
 def bytes_soft_assign(n, B):
@@ -115,7 +165,14 @@ def warmup_map_record(ctx, _abi, scan, n, B, bins, origin):
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if world_env != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world_env}")
     dist = Dist(args.gpus)
+    if args.dry_run:
+        return dry_run(dist)
     from gcslam import _abi
     from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
     from gcslam.ops.binning import create_fibonacci_atlas
@@ -161,14 +218,23 @@ def main():
         uid = [pipe.comm_unique_id() if dist.rank == 0 else None]
         dist.td.broadcast_object_list(uid, src=0)
         pipe.attach_comm(uid[0])
-    for k, s in enumerate(scans):
-        pipe.stage_scan(k, s)
+    ingest = not args.no_ingest
+    if not ingest:
+        for k, s in enumerate(scans):
+            pipe.stage_scan(k, s)
 
     count = [0]
 
     def step():
-        k = count[0] % len(scans)
-        pipe.run_scan(k, scans[k], count[0])
+        # with ingest, every step stages its scan from host memory (pinned mirror + DMA on the copy
+        # stream) into one of two slots, so the copy of scan k+1 overlaps scan k's compute
+        k = count[0]
+        sc = scans[k % len(scans)]
+        if ingest:
+            pipe.stage_scan(k % 2, sc)
+            pipe.run_scan(k % 2, sc, k)
+        else:
+            pipe.run_scan(k % len(scans), sc, k)
         count[0] += 1
 
     # clock ramp: untimed steps for prewarm_s of sustained load (a 5-step W is ~7 ms, less than the
@@ -197,12 +263,23 @@ def main():
     t1 = time.perf_counter()
     elapsed = dist.max(t1 - t0)
     scans_per_s = args.steps / elapsed
+    n_gpus = pipe.comm_size() if dist.world > 1 else 1  # the RCCL communicator's size
+    exchange = None
+    if dist.world > 1:
+        # the per-scan all-gather's device time (HIP events around ncclAllGather on the pipeline
+        # stream), untimed scans after the timed region: median over 20, max over ranks
+        xs = []
+        for _ in range(20):
+            step()
+            xs.append(pipe.exchange_ms())
+        exchange = {"ms_median": dist.max(float(np.median(xs))), "record_bytes": 8 * pipe_partial_len(pipe),
+                    "scans": len(xs), "op": "ncclAllGather (RCCL) of each rank's partial record"}
 
     out = {
         "metric": "LiDAR scans/sec (64k pts, 256 hypotheses) at 1/2/4/8 MI355X",
         "value": scans_per_s,
         "unit": "scans/s",
-        "n_gpus": dist.world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "prewarm_steps": prewarm_steps,
@@ -217,8 +294,13 @@ def main():
                                "(a1-a16: budget, predict, IMU preint, deskew, soft-assign, moment-match, "
                                "Matrix-Fisher, planar, tempering, fusion, recompose, IW, map, anchor drift, "
                                "barycenter combine)" % H_total,
-                   "points": n, "hypotheses": H_total, "bins": B, "parallelism": "hypotheses/%d" % dist.world},
+                   "points": n, "hypotheses": H_total, "bins": B, "parallelism": "hypotheses/%d" % dist.world,
+                   "ingest": ("every step stages its scan host -> HBM (pinned mirror + DMA on a copy stream, "
+                              "overlapped with the previous scan's compute)") if ingest else
+                             "scans pre-staged in HBM before the timed region"},
     }
+    if exchange is not None:
+        out["exchange"] = exchange
 
     if dist.rank == 0 and not args.no_roofline:
         rng = np.random.default_rng(5)

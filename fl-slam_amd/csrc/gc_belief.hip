@@ -78,6 +78,8 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
     // second stream. The last workgroup to arrive (agent-scope acq_rel ticket) sums the partials
     // in block order — the same fixed order as k_budget_final — and re-arms the ticket.
     const int b = h - P.Hl;
+    // re-arm k_bins_io's task counter for this scan's bins launch (next on the stream)
+    if (b == 0 && t == 0) P.task_ctr[0] = 0u;
     const int64_t stride = budget_stride(S.n_in, P.n_cap);
     budget_partial_block(S.w_raw, S.n_in, stride, b, P.budget_part, sm);
     // a4's per-point time window (deskew_constant_twist.py:61-68) depends on the point only, not

@@ -92,11 +92,12 @@ __global__ void k_cloud_parse(const uint8_t* __restrict__ data, int64_t n, int32
 
 }  // namespace gc
 
-extern "C" int32_t gc_pointcloud2_parse(gc_ctx* ctx, const uint8_t* d_data, int64_t n_points, int32_t point_step,
-                                        const int32_t* h_fields, double header_stamp, const double* h_R9,
-                                        const double* h_t3, double* d_points_out, double* d_t_out,
-                                        double* d_w_out, uint8_t* d_ring_out, uint8_t* d_tag_out) {
-  GC_CHECK_ARG(nullptr, ctx, "NULL ctx");
+namespace gc {
+// the parse on stream st with a caller-owned device flag word (the pipeline's copy stream and slot)
+int32_t cloud_parse_on(gc_ctx* ctx, hipStream_t st, int32_t* flag, const uint8_t* d_data, int64_t n_points,
+                       int32_t point_step, const int32_t* h_fields, double header_stamp, const double* h_R9,
+                       const double* h_t3, double* d_points_out, double* d_t_out, double* d_w_out,
+                       uint8_t* d_ring_out, uint8_t* d_tag_out) {
   GC_CHECK_ARG(ctx, n_points >= 0 && h_fields && h_R9 && h_t3, "bad arguments");
   if (n_points == 0) return GC_OK;
   GC_CHECK_ARG(ctx, d_data && d_points_out && d_t_out && d_w_out && d_ring_out && d_tag_out, "NULL buffer");
@@ -110,21 +111,30 @@ extern "C" int32_t gc_pointcloud2_parse(gc_ctx* ctx, const uint8_t* d_data, int6
   const int toff = h_fields[8], ttype = h_fields[9];
   GC_CHECK_ARG(ctx, toff < 0 || (ttype >= 1 && ttype <= 8 && toff + size_of(ttype) <= point_step),
                "bad time field");
-  void* scr;
-  if (int rc = gc::scratch(ctx, sizeof(int32_t) * 4, &scr)) return rc;
-  int32_t* flag = (int32_t*)scr;
-  GC_HIP(ctx, hipMemsetAsync(flag, 0, sizeof(int32_t), ctx->stream));
+  GC_HIP(ctx, hipMemsetAsync(flag, 0, sizeof(int32_t), st));
   const unsigned blocks = (unsigned)((n_points + 255) / 256);
   if (toff >= 0)
-    hipLaunchKernelGGL(gc::k_cloud_time_flag, dim3(blocks), dim3(256), 0, ctx->stream, d_data, n_points, point_step,
-                       toff, ttype, flag);
+    hipLaunchKernelGGL(k_cloud_time_flag, dim3(blocks), dim3(256), 0, st, d_data, n_points, point_step, toff, ttype,
+                       flag);
   GcExtrinsic ex;
   for (int k = 0; k < 9; ++k) ex.R[k] = h_R9[k];
   for (int k = 0; k < 3; ++k) ex.t[k] = h_t3[k];
-  hipLaunchKernelGGL(gc::k_cloud_parse, dim3(blocks), dim3(256), 0, ctx->stream, d_data, n_points, point_step,
+  hipLaunchKernelGGL(k_cloud_parse, dim3(blocks), dim3(256), 0, st, d_data, n_points, point_step,
                      make_int4(h_fields[0], h_fields[1], 0, 0), make_int4(h_fields[2], h_fields[3], 0, 0),
                      make_int4(h_fields[4], h_fields[5], h_fields[6], h_fields[7]), make_int2(toff, ttype), flag,
                      header_stamp, ex, d_points_out, d_t_out, d_w_out, d_ring_out, d_tag_out);
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
+}
+}  // namespace gc
+
+extern "C" int32_t gc_pointcloud2_parse(gc_ctx* ctx, const uint8_t* d_data, int64_t n_points, int32_t point_step,
+                                        const int32_t* h_fields, double header_stamp, const double* h_R9,
+                                        const double* h_t3, double* d_points_out, double* d_t_out,
+                                        double* d_w_out, uint8_t* d_ring_out, uint8_t* d_tag_out) {
+  GC_CHECK_ARG(nullptr, ctx, "NULL ctx");
+  void* scr;
+  if (int rc = gc::scratch(ctx, sizeof(int32_t) * 4, &scr)) return rc;
+  return gc::cloud_parse_on(ctx, ctx->stream, (int32_t*)scr, d_data, n_points, point_step, h_fields, header_stamp,
+                            h_R9, h_t3, d_points_out, d_t_out, d_w_out, d_ring_out, d_tag_out);
 }

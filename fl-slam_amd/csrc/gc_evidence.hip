@@ -496,17 +496,17 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
       Ri[e - kPDPSIP] = s;
     }
     __syncthreads();
-    GC_PHASE(P, 22);
+    GC_PHASE_WG(P, 22, 2);
     // process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
     wg_iw_proc_apply(P.nu_proc, P.Psi_proc, Ri, Ri + (kPDNUP - kPDPSIP), S.w_process, P.eps_psd, P.nu_max, P.nu_proc,
                      P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab);
-    GC_PHASE(P, 23);
+    GC_PHASE_WG(P, 23, 2);
     // measurement-noise IW apply (measurement_noise_iw_jax.py:59-100)
     wg_iw_meas_apply(P.nu_meas, P.Psi_meas, Ri + (kPDPSIM - kPDPSIP), Ri + (kPDNUM - kPDPSIP), P.eps_psd, P.nu_max,
                      P.nu_meas, P.Psi_meas, P.iw_cert + 2, tab);
-    GC_PHASE(P, 24);
+    GC_PHASE_WG(P, 24, 2);
     iw_Q_wg(P, Qs, Qp, Sx, red);
-    GC_PHASE(P, 25);
+    GC_PHASE_WG(P, 25, 2);
     return;
   }
   GC_PHASE(P, 20);

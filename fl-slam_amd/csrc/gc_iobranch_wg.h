@@ -31,14 +31,6 @@ GC_DEV void io_branch_wg(const PipeDev& P, const ScanArgs& S, const double* __re
   double* misc = red + 8;                   // 64
   double* EX = misc + 64;                   // 9 x 16
   const int t = threadIdx.x;
-#ifdef GC_IO_TIMING  // dev: cycle counter at the phase boundaries of every hypothesis (io_parts[30..34])
-  double tc[5];
-#define GC_IOT(i) \
-  if (t == 0) tc[i] = (double)__builtin_readcyclecounter()
-#else
-#define GC_IOT(i)
-#endif
-  GC_IOT(0);
   const double* aux = P.mu_aux + (int64_t)hl * kMuAux;  // [mu_prev 22, mu_inc 22, pose0 6]
   const double* mu_prev = aux;
   const double* mu_inc = aux + 22;
@@ -72,7 +64,6 @@ GC_DEV void io_branch_wg(const PipeDev& P, const ScanArgs& S, const double* __re
   double* pre = misc + 16;  // kPreint = 25
   const ImuPair q = load_imu_pair(M, S.imu_t, S.imu_g, S.imu_a);
   wg_preintegrate(M, q, wa, wb, misc, bg, ba, g, A, Bm, V1, V2, pre);
-  GC_IOT(1);
   // time-resolved vMF gravity (imu_evidence.py:402-559): all threads; w = w_imu_int per slot
   {
     double* w = A;  // preint scratch is free again
@@ -92,7 +83,6 @@ GC_DEV void io_branch_wg(const PipeDev& P, const ScanArgs& S, const double* __re
         F[kIoN2 + 3 + i] = hr[i];
       }
   }
-  GC_IOT(2);
   // Σ_g, Σ_a = measurement-IW modes (measurement_noise_iw_jax.py:38-56, backend_node.py:2021-2023)
   auto iw_mode = [&](int idx, double* out) {
     double Sg[9];
@@ -167,7 +157,6 @@ GC_DEV void io_branch_wg(const PipeDev& P, const ScanArgs& S, const double* __re
     }
   }
   __syncthreads();
-  GC_IOT(3);
   // dependence scalings, sum in the reference's order (pipeline.py:728-750)
   const double* ex_im = EX + 1 * kIofExtra;
   const double* ex_kc = EX + 8 * kIofExtra;
@@ -209,12 +198,7 @@ GC_DEV void io_branch_wg(const PipeDev& P, const ScanArgs& S, const double* __re
     for (int k = 0; k < 6; ++k) q[28 + k] = ex_kc[k];
     q[34] = so;
     q[35] = ex_od[6]; q[36] = ex_im[6]; q[37] = ex_gy[3]; q[38] = dt_int; q[39] = trig;
-#ifdef GC_IO_TIMING
-    GC_IOT(4);
-    for (int k = 0; k < 5; ++k) q[30 + k] = tc[k];
-#endif
   }
-#undef GC_IOT
 }
 
 }  // namespace gc

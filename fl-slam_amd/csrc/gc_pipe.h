@@ -29,6 +29,7 @@ struct PipeDev {
   int h_begin;   // global index of local hypothesis 0
   int B;         // bins
   int M;         // IMU slots (<= 512)
+  int geom_H;    // bins chunk geometry as for this many hypotheses (0: Hl)
   int64_t n_in, n_cap;
   double tau, o0, o1, o2;
   double eps_psd, eps_lift, eps_mass, lambda_ou, c_frob, forgetting, weight_floor;
@@ -54,7 +55,7 @@ struct PipeDev {
   double *budget;                          // 8 budget scalars
   double *budget_part;                     // (64, 3) a1 partials, written by predict's extra workgroups
   unsigned *budget_ticket;                 // arrival counter of those workgroups (reset by the last)
-  unsigned *task_ctr;                      // [task counter, finished pullers] of k_bins_io (reset by the last)
+  unsigned *task_ctr;                      // k_bins_io task counter (zeroed by the predict launch)
   double *w_win;                           // (n_cap) selected points' w x time window, written by predict's
                                            // budget workgroups (per point, shared by every hypothesis)
   double *send, *gather;                   // (P), (G, P)
@@ -73,19 +74,21 @@ struct ScanArgs {
   int sig_cached;                          // P.Sig / P.mu_fin hold (P.L + εI)⁻¹ and its solve with P.h
 };
 
-// dev instrumentation: -DGC_PHASE_TIMING records s_memtime at phase boundaries of hypothesis 0
-// into io_parts[slot] (read with the pipeline in GC_IO_GIVEN mode); compiled out otherwise
+// dev instrumentation: -DGC_PHASE_TIMING records s_memtime at phase boundaries of workgroup wg
+// (hypothesis 0's, or combine_final's IW workgroup) into io_parts[slot] (read with the pipeline in
+// GC_IO_GIVEN mode; tools/phase_timing.py); compiled out otherwise
 #ifdef GC_PHASE_TIMING
-#define GC_PHASE(P, i)                                                                   \
+#define GC_PHASE_WG(P, i, wg)                                                             \
   do {                                                                                   \
     __syncthreads();                                                                     \
-    if (blockIdx.x == 0 && threadIdx.x == 0) (P).io_parts[i] = (double)__builtin_readcyclecounter(); \
+    if (blockIdx.x == (wg) && threadIdx.x == 0) (P).io_parts[i] = (double)__builtin_readcyclecounter(); \
   } while (0)
 #else
-#define GC_PHASE(P, i) \
-  do {                 \
+#define GC_PHASE_WG(P, i, wg) \
+  do {                        \
   } while (0)
 #endif
+#define GC_PHASE(P, i) GC_PHASE_WG(P, i, 0)
 
 // launchers (gc_belief.hip)
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st);

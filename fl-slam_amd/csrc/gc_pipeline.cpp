@@ -11,19 +11,36 @@ struct gc_comm;
 namespace gc {
 int comm_allgather(gc_comm* comm, gc_ctx* ctx, const double* d_send, double* d_recv, int64_t count);
 int comm_size(const gc_comm* comm);
+int32_t cloud_parse_on(gc_ctx* ctx, hipStream_t st, int32_t* flag, const uint8_t* d_data, int64_t n_points,
+                       int32_t point_step, const int32_t* h_fields, double header_stamp, const double* h_R9,
+                       const double* h_t3, double* d_points_out, double* d_t_out, double* d_w_out,
+                       uint8_t* d_ring_out, uint8_t* d_tag_out);
 }
 
 struct gc_pipeline {
   gc_ctx* ctx = nullptr;
   gc::PipeDev P{};
   std::vector<void*> allocs;
+  // Scan slots. Ingest runs on a copy stream of its own: the host arrays are copied into the slot's
+  // pinned mirror, then one DMA per field moves them into the slot's device block, ordered after the
+  // last kernel of the previous scan that read the slot (`consumed`); scan_local waits on `ready`.
+  // So staging scan k+1 overlaps scan k's compute, and the caller's arrays are free on return.
   struct Slot {
+    double* dev = nullptr;   // [pts 3n | t n | w n | imu_t M | imu_g 3M | imu_a 3M | odom kOdomLen]
+    double* host = nullptr;  // pinned mirror of dev (same layout)
     double *pts = nullptr, *t = nullptr, *w = nullptr, *imu_t = nullptr, *imu_g = nullptr, *imu_a = nullptr;
-    double* odom = nullptr;  // kOdomLen doubles (device), staged by gc_pipeline_stage_odom
-    uint8_t *bytes = nullptr, *ring = nullptr, *tag = nullptr;  // PointCloud2 staging
+    double* odom = nullptr;
+    bool has_odom = false;
+    uint8_t *bytes = nullptr, *hbytes = nullptr, *ring = nullptr, *tag = nullptr;  // PointCloud2 staging
+    int32_t* flag = nullptr;  // device word of the parse's seconds / nanoseconds test
     size_t bytes_cap = 0;
     int64_t n_in = 0;
+    hipEvent_t ready = nullptr;      // copy stream: the slot's device block holds the staged scan
+    hipEvent_t odom_done = nullptr;  // copy stream: the odometry DMA has read its pinned area
+    hipEvent_t consumed = nullptr;   // compute stream: the last scan that read the slot is past it
+    bool ready_rec = false, odom_rec = false, consumed_rec = false;
   } slots[GC_PIPE_MAX_SLOTS];
+  hipStream_t cstream = nullptr;  // ingest (copy) stream
   int io_mode = GC_IO_COMPUTED;
   gc_comm* comm = nullptr;
   // P.Sig / P.mu_fin were written by the last scan's evidence kernel from the current P.L / P.h
@@ -34,6 +51,8 @@ struct gc_pipeline {
   bool pending = false;
   gc::ScanArgs pending_S{};
   double* own_gather = nullptr;  // separate gather buffer of a single-rank pipeline with a communicator
+  hipEvent_t x0 = nullptr, x1 = nullptr;  // around the last scan's all-gather (gc_pipeline_exchange_ms)
+  bool x_rec = false;
 };
 
 namespace {
@@ -61,11 +80,52 @@ int down(gc_pipeline* p, double* h, const double* d, size_t count) {
   return GC_OK;
 }
 
+// slot block layout (doubles): pts 3n | t n | w n | imu_t M | imu_g 3M | imu_a 3M | odom
+struct SlotLayout {
+  size_t t, w, imu, odom, len;
+  explicit SlotLayout(const gc::PipeDev& P) {
+    const size_t n = (size_t)P.n_in, M = (size_t)P.M;
+    t = 3 * n; w = 4 * n; imu = 5 * n; odom = imu + 7 * M; len = odom + gc::kOdomLen;
+  }
+};
+
+int slot_alloc(gc_pipeline* p, gc_pipeline::Slot& s) {
+  if (s.dev) return GC_OK;
+  const SlotLayout Ly(p->P);
+  GC_HIP(p->ctx, hipMalloc((void**)&s.dev, Ly.len * sizeof(double)));
+  GC_HIP(p->ctx, hipHostMalloc((void**)&s.host, Ly.len * sizeof(double), hipHostMallocDefault));
+  for (hipEvent_t* e : {&s.ready, &s.odom_done, &s.consumed})
+    GC_HIP(p->ctx, hipEventCreateWithFlags(e, hipEventDisableTiming));
+  s.pts = s.dev; s.t = s.dev + Ly.t; s.w = s.dev + Ly.w;
+  s.imu_t = s.dev + Ly.imu; s.imu_g = s.imu_t + p->P.M; s.imu_a = s.imu_g + 3 * p->P.M;
+  s.odom = s.dev + Ly.odom;
+  return GC_OK;
+}
+
 #define GC_TRY(expr)             \
   do {                           \
     int _rc = (expr);            \
     if (_rc != GC_OK) return _rc; \
   } while (0)
+
+// the copy stream may overwrite the slot's device block only after the last scan that read it
+int slot_wait_consumed(gc_pipeline* p, gc_pipeline::Slot& s) {
+  if (s.consumed_rec) GC_HIP(p->ctx, hipStreamWaitEvent(p->cstream, s.consumed, 0));
+  return GC_OK;
+}
+
+// host arrays -> the slot's pinned mirror (the previous DMA out of it has finished) -> device, on the
+// copy stream; imu block = [imu_t M | imu_g 3M | imu_a 3M]
+int slot_stage_imu_host(gc_pipeline* p, gc_pipeline::Slot& s, const double* h_imu_t, const double* h_imu_g,
+                        const double* h_imu_a) {
+  const SlotLayout Ly(p->P);
+  const size_t M = (size_t)p->P.M;
+  double* h = s.host + Ly.imu;
+  std::memcpy(h, h_imu_t, M * sizeof(double));
+  std::memcpy(h + M, h_imu_g, 3 * M * sizeof(double));
+  std::memcpy(h + 4 * M, h_imu_a, 3 * M * sizeof(double));
+  return GC_OK;
+}
 
 }  // namespace
 
@@ -80,6 +140,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   GC_CHECK_ARG(ctx, dims->M >= 2 && dims->M <= 512, "IMU slots M must be in [2, 512]");
   GC_CHECK_ARG(ctx, dims->n_in_max > 0 && dims->n_cap > 0, "point counts must be positive");
   GC_CHECK_ARG(ctx, dims->world_size >= 1 && dims->rank >= 0 && dims->rank < dims->world_size, "bad rank");
+  GC_CHECK_ARG(ctx, dims->geom_hyps >= 0 && dims->geom_hyps <= 65536, "geom_hyps must be in [0, 65536]");
   GC_CHECK_ARG(ctx, cfg[GC_PCFG_TAU] >= GC_FUSED_TAU_MIN, "tau must be >= GC_FUSED_TAU_MIN (3e-3)");
   GC_HIP(ctx, hipSetDevice(ctx->device));
   gc_pipeline* p = new gc_pipeline();
@@ -87,6 +148,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   gc::PipeDev& P = p->P;
   P.Hl = dims->h_count; P.H = dims->H_total; P.h_begin = dims->h_begin; P.B = dims->B; P.M = dims->M;
   P.n_in = dims->n_in_max; P.n_cap = dims->n_cap; P.G = dims->world_size;
+  P.geom_H = dims->geom_hyps;
   P.tau = cfg[GC_PCFG_TAU]; P.o0 = cfg[GC_PCFG_ORIGIN]; P.o1 = cfg[GC_PCFG_ORIGIN + 1]; P.o2 = cfg[GC_PCFG_ORIGIN + 2];
   P.eps_psd = cfg[GC_PCFG_EPS_PSD]; P.eps_lift = cfg[GC_PCFG_EPS_LIFT]; P.eps_mass = cfg[GC_PCFG_EPS_MASS];
   P.lambda_ou = cfg[GC_PCFG_LAMBDA_OU]; P.c_frob = cfg[GC_PCFG_C_FROB]; P.forgetting = cfg[GC_PCFG_FORGETTING];
@@ -130,6 +192,10 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   if (rc == GC_OK) rc = dalloc(p, 1, &ctr);  // zeroed: k_bins_io's task counter + finished pullers
   P.task_ctr = reinterpret_cast<unsigned*>(ctr);
   if (rc == GC_OK) rc = dalloc(p, (size_t)P.n_cap, &P.w_win);
+  if (rc == GC_OK && hipStreamCreateWithFlags(&p->cstream, hipStreamNonBlocking) != hipSuccess) {
+    gc::set_error(ctx, "hipStreamCreateWithFlags failed for the ingest stream");
+    rc = GC_ERR_RUNTIME;
+  }
   if (rc == GC_OK) GC_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the zero fills land before any launch
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
@@ -142,25 +208,33 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
 int32_t gc_pipeline_destroy(gc_pipeline* p) {
   if (!p) return GC_OK;
   (void)hipStreamSynchronize(p->ctx->stream);
+  if (p->cstream) (void)hipStreamSynchronize(p->cstream);
   for (void* a : p->allocs) (void)hipFree(a);
   for (auto& s : p->slots) {
-    for (double* d : {s.pts, s.t, s.w, s.imu_t, s.imu_g, s.imu_a, s.odom})
+    for (void* d : {(void*)s.dev, (void*)s.bytes, (void*)s.ring, (void*)s.tag, (void*)s.flag})
       if (d) (void)hipFree(d);
-    for (uint8_t* d : {s.bytes, s.ring, s.tag})
-      if (d) (void)hipFree(d);
+    for (void* h : {(void*)s.host, (void*)s.hbytes})
+      if (h) (void)hipHostFree(h);
+    for (hipEvent_t e : {s.ready, s.odom_done, s.consumed})
+      if (e) (void)hipEventDestroy(e);
   }
+  for (hipEvent_t e : {p->x0, p->x1})
+    if (e) (void)hipEventDestroy(e);
+  if (p->cstream) (void)hipStreamDestroy(p->cstream);
   delete p;
   return GC_OK;
 }
 
 int32_t gc_pipeline_set_bins(gc_pipeline* p, const double* h_bins) {
   GC_CHECK_ARG(nullptr, p && h_bins, "NULL argument");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   return up(p, p->P.bins, h_bins, (size_t)p->P.B * 3);
 }
 
 int32_t gc_pipeline_set_beliefs(gc_pipeline* p, const double* h_X, const double* h_z, const double* h_L,
                                 const double* h_h, const double* h_stamp) {
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   const size_t Hl = p->P.Hl;
   p->sig_cached = false;
   GC_TRY(up(p, p->P.X, h_X, Hl * 6));
@@ -183,11 +257,13 @@ int32_t gc_pipeline_get_beliefs(gc_pipeline* p, double* h_X, double* h_z, double
 
 int32_t gc_pipeline_set_weights(gc_pipeline* p, const double* h_w) {
   GC_CHECK_ARG(nullptr, p && h_w, "NULL argument");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   return up(p, p->P.weights, h_w, p->P.H);
 }
 
 int32_t gc_pipeline_set_io_evidence(gc_pipeline* p, const double* h_L, const double* h_h, const double* h_cert) {
   GC_CHECK_ARG(nullptr, p && h_L && h_h && h_cert, "NULL argument");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   const size_t Hl = p->P.Hl;
   GC_TRY(up(p, p->P.io_L, h_L, Hl * 484));
   GC_TRY(up(p, p->P.io_h, h_h, Hl * 22));
@@ -197,6 +273,7 @@ int32_t gc_pipeline_set_io_evidence(gc_pipeline* p, const double* h_L, const dou
 
 int32_t gc_pipeline_set_io_mode(gc_pipeline* p, int32_t mode) {
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   GC_CHECK_ARG(p->ctx, mode == GC_IO_GIVEN || mode == GC_IO_COMPUTED, "io mode must be GC_IO_GIVEN or GC_IO_COMPUTED");
   p->io_mode = mode;
   return GC_OK;
@@ -208,13 +285,20 @@ int32_t gc_pipeline_stage_odom(gc_pipeline* p, int32_t slot, const double* h_pos
   GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS, "slot out of range");
   GC_CHECK_ARG(p->ctx, h_pose6 && h_cov36 && h_twist6 && h_twist_cov36, "NULL odometry array");
   auto& s = p->slots[slot];
-  if (!s.odom) GC_HIP(p->ctx, hipMalloc((void**)&s.odom, gc::kOdomLen * sizeof(double)));
-  double buf[gc::kOdomLen];
+  GC_TRY(slot_alloc(p, s));
+  if (s.odom_rec) GC_HIP(p->ctx, hipEventSynchronize(s.odom_done));  // the last odometry DMA read its area
+  double* buf = s.host + SlotLayout(p->P).odom;
   std::memcpy(buf, h_pose6, 6 * sizeof(double));
   std::memcpy(buf + 6, h_cov36, 36 * sizeof(double));
   std::memcpy(buf + 42, h_twist6, 6 * sizeof(double));
   std::memcpy(buf + 48, h_twist_cov36, 36 * sizeof(double));
-  return up(p, s.odom, buf, gc::kOdomLen);
+  GC_TRY(slot_wait_consumed(p, s));
+  GC_HIP(p->ctx, hipMemcpyAsync(s.odom, buf, gc::kOdomLen * sizeof(double), hipMemcpyHostToDevice, p->cstream));
+  GC_HIP(p->ctx, hipEventRecord(s.odom_done, p->cstream));
+  GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));  // scan_local's wait covers the odometry too
+  s.odom_rec = s.ready_rec = true;
+  s.has_odom = true;
+  return GC_OK;
 }
 
 int32_t gc_pipeline_get_io_parts(gc_pipeline* p, double* h_parts) {
@@ -233,6 +317,7 @@ int32_t gc_pipeline_get_io_evidence(gc_pipeline* p, double* h_L, double* h_h, do
 int32_t gc_pipeline_set_iw(gc_pipeline* p, const double* nu_proc, const double* Psi_proc, const double* nu_meas,
                            const double* Psi_meas) {
   GC_CHECK_ARG(nullptr, p && nu_proc && Psi_proc && nu_meas && Psi_meas, "NULL argument");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   GC_TRY(up(p, p->P.nu_proc, nu_proc, 7));
   GC_TRY(up(p, p->P.Psi_proc, Psi_proc, 252));
   GC_TRY(up(p, p->P.nu_meas, nu_meas, 3));
@@ -244,6 +329,7 @@ int32_t gc_pipeline_set_iw(gc_pipeline* p, const double* nu_proc, const double* 
 int32_t gc_pipeline_get_iw(gc_pipeline* p, double* nu_proc, double* Psi_proc, double* nu_meas, double* Psi_meas,
                            double* Q, double* cert4) {
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   GC_TRY(down(p, nu_proc, p->P.nu_proc, 7));
   GC_TRY(down(p, Psi_proc, p->P.Psi_proc, 252));
   GC_TRY(down(p, nu_meas, p->P.nu_meas, 3));
@@ -254,6 +340,7 @@ int32_t gc_pipeline_get_iw(gc_pipeline* p, double* nu_proc, double* Psi_proc, do
 
 int32_t gc_pipeline_set_map(gc_pipeline* p, const double* h_map) {
   GC_CHECK_ARG(nullptr, p && h_map, "NULL argument");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   GC_TRY(up(p, p->P.map, h_map, (size_t)p->P.B * gc::kMapRec));
   GC_HIP(p->ctx, gc::launch_map_derive(p->P, p->ctx->stream));
   return GC_OK;
@@ -261,6 +348,7 @@ int32_t gc_pipeline_set_map(gc_pipeline* p, const double* h_map) {
 
 int32_t gc_pipeline_get_map(gc_pipeline* p, double* h_map, double* h_map_der, double* h_misc2) {
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   GC_TRY(down(p, h_map, p->P.map, (size_t)p->P.B * gc::kMapRec));
   GC_TRY(down(p, h_map_der, p->P.map_der, (size_t)p->P.B * gc::kMapDer));
   return down(p, h_misc2, p->P.map_misc, 2);
@@ -274,19 +362,24 @@ int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_pts
   GC_CHECK_ARG(p->ctx, n_in > 0 && n_in <= p->P.n_in, "n_in must be in [1, n_in_max]");
   GC_CHECK_ARG(p->ctx, h_pts && h_t && h_w && h_imu_t && h_imu_g && h_imu_a, "NULL scan array");
   auto& s = p->slots[slot];
-  if (!s.pts) {
-    const size_t n = (size_t)p->P.n_in, M = (size_t)p->P.M;
-    double** bufs[] = {&s.pts, &s.t, &s.w, &s.imu_t, &s.imu_g, &s.imu_a};
-    const size_t cnt[] = {3 * n, n, n, M, 3 * M, 3 * M};
-    for (int i = 0; i < 6; ++i) GC_HIP(p->ctx, hipMalloc((void**)bufs[i], cnt[i] * sizeof(double)));
-  }
+  GC_TRY(slot_alloc(p, s));
+  if (s.ready_rec) GC_HIP(p->ctx, hipEventSynchronize(s.ready));  // the last DMA out of the mirror is done
+  const SlotLayout Ly(p->P);
+  const size_t n = (size_t)n_in, M = (size_t)p->P.M;
+  std::memcpy(s.host, h_pts, 3 * n * sizeof(double));
+  std::memcpy(s.host + Ly.t, h_t, n * sizeof(double));
+  std::memcpy(s.host + Ly.w, h_w, n * sizeof(double));
+  GC_TRY(slot_stage_imu_host(p, s, h_imu_t, h_imu_g, h_imu_a));
+  GC_TRY(slot_wait_consumed(p, s));
+  const hipMemcpyKind k = hipMemcpyHostToDevice;
+  GC_HIP(p->ctx, hipMemcpyAsync(s.pts, s.host, 3 * n * sizeof(double), k, p->cstream));
+  GC_HIP(p->ctx, hipMemcpyAsync(s.t, s.host + Ly.t, n * sizeof(double), k, p->cstream));
+  GC_HIP(p->ctx, hipMemcpyAsync(s.w, s.host + Ly.w, n * sizeof(double), k, p->cstream));
+  GC_HIP(p->ctx, hipMemcpyAsync(s.imu_t, s.host + Ly.imu, 7 * M * sizeof(double), k, p->cstream));
+  GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));
+  s.ready_rec = true;
   s.n_in = n_in;
-  GC_TRY(up(p, s.pts, h_pts, 3 * (size_t)n_in));
-  GC_TRY(up(p, s.t, h_t, (size_t)n_in));
-  GC_TRY(up(p, s.w, h_w, (size_t)n_in));
-  GC_TRY(up(p, s.imu_t, h_imu_t, (size_t)p->P.M));
-  GC_TRY(up(p, s.imu_g, h_imu_g, 3 * (size_t)p->P.M));
-  return up(p, s.imu_a, h_imu_a, 3 * (size_t)p->P.M);
+  return GC_OK;
 }
 
 int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_t* h_data, int64_t n_points,
@@ -303,30 +396,35 @@ int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_
     return gc_pipeline_stage_scan(p, slot, z3, &z1, &z1, 1, h_imu_t, h_imu_g, h_imu_a);
   }
   auto& s = p->slots[slot];
-  if (!s.pts) {
-    const size_t n = (size_t)p->P.n_in, M = (size_t)p->P.M;
-    double** bufs[] = {&s.pts, &s.t, &s.w, &s.imu_t, &s.imu_g, &s.imu_a};
-    const size_t cnt[] = {3 * n, n, n, M, 3 * M, 3 * M};
-    for (int i = 0; i < 6; ++i) GC_HIP(p->ctx, hipMalloc((void**)bufs[i], cnt[i] * sizeof(double)));
-  }
+  GC_TRY(slot_alloc(p, s));
   if (!s.ring) {
     GC_HIP(p->ctx, hipMalloc((void**)&s.ring, (size_t)p->P.n_in));
     GC_HIP(p->ctx, hipMalloc((void**)&s.tag, (size_t)p->P.n_in));
+    GC_HIP(p->ctx, hipMalloc((void**)&s.flag, 4 * sizeof(int32_t)));
   }
+  if (s.ready_rec) GC_HIP(p->ctx, hipEventSynchronize(s.ready));  // the last DMA / parse from this slot is done
   const size_t nb = (size_t)n_points * (size_t)point_step;
   if (s.bytes_cap < nb) {
     if (s.bytes) GC_HIP(p->ctx, hipFree(s.bytes));
+    if (s.hbytes) GC_HIP(p->ctx, hipHostFree(s.hbytes));
+    s.bytes = s.hbytes = nullptr;
+    s.bytes_cap = 0;
     GC_HIP(p->ctx, hipMalloc((void**)&s.bytes, nb));
+    GC_HIP(p->ctx, hipHostMalloc((void**)&s.hbytes, nb, hipHostMallocDefault));
     s.bytes_cap = nb;
   }
-  GC_HIP(p->ctx, hipMemcpyAsync(s.bytes, h_data, nb, hipMemcpyHostToDevice, p->ctx->stream));
-  GC_TRY(gc_pointcloud2_parse(p->ctx, s.bytes, n_points, point_step, h_fields, header_stamp, h_R9, h_t3, s.pts,
-                              s.t, s.w, s.ring, s.tag));
-  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
+  std::memcpy(s.hbytes, h_data, nb);
+  GC_TRY(slot_stage_imu_host(p, s, h_imu_t, h_imu_g, h_imu_a));
+  GC_TRY(slot_wait_consumed(p, s));
+  GC_HIP(p->ctx, hipMemcpyAsync(s.bytes, s.hbytes, nb, hipMemcpyHostToDevice, p->cstream));
+  GC_TRY(gc::cloud_parse_on(p->ctx, p->cstream, s.flag, s.bytes, n_points, point_step, h_fields, header_stamp, h_R9,
+                            h_t3, s.pts, s.t, s.w, s.ring, s.tag));
+  GC_HIP(p->ctx, hipMemcpyAsync(s.imu_t, s.host + SlotLayout(p->P).imu, 7 * (size_t)p->P.M * sizeof(double),
+                                hipMemcpyHostToDevice, p->cstream));
+  GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));
+  s.ready_rec = true;
   s.n_in = n_points;
-  GC_TRY(up(p, s.imu_t, h_imu_t, (size_t)p->P.M));
-  GC_TRY(up(p, s.imu_g, h_imu_g, 3 * (size_t)p->P.M));
-  return up(p, s.imu_a, h_imu_a, 3 * (size_t)p->P.M);
+  return GC_OK;
 }
 
 int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm) {
@@ -367,10 +465,19 @@ int32_t gc_pipeline_scan_finish(gc_pipeline* p, const double* h_gather) {
   gc_ctx* ctx = p->ctx;
   gc::PipeDev& P = p->P;
   const int64_t PL = gc::partial_len(P.B);
-  if (h_gather) {  // the G records of this scan, gathered by the caller (rank order)
-    GC_TRY(up(p, P.gather, h_gather, (size_t)PL * P.G));
-  } else if (p->comm) {
-    GC_TRY(gc::comm_allgather(p->comm, ctx, P.send, P.gather, PL));
+  if (h_gather || p->comm) {
+    if (!p->x0) {
+      GC_HIP(ctx, hipEventCreate(&p->x0));
+      GC_HIP(ctx, hipEventCreate(&p->x1));
+    }
+    GC_HIP(ctx, hipEventRecord(p->x0, ctx->stream));
+    if (h_gather) {  // the G records of this scan, gathered by the caller (rank order)
+      GC_TRY(up(p, P.gather, h_gather, (size_t)PL * P.G));
+    } else {
+      GC_TRY(gc::comm_allgather(p->comm, ctx, P.send, P.gather, PL));
+    }
+    GC_HIP(ctx, hipEventRecord(p->x1, ctx->stream));
+    p->x_rec = true;
   }
   p->pending = false;
   GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream));
@@ -381,11 +488,12 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
                                double t_scan, double dt_sec, int64_t scan_count) {
   GC_CHECK_ARG(nullptr, p, "NULL pipeline");
   GC_CHECK_ARG(p->ctx, !p->pending, "the previous scan's exchange is pending (gc_pipeline_scan_finish)");
-  GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS && p->slots[slot].pts, "scan slot not staged");
-  GC_CHECK_ARG(p->ctx, p->io_mode == GC_IO_GIVEN || p->slots[slot].odom,
+  GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS && p->slots[slot].n_in > 0, "scan slot not staged");
+  GC_CHECK_ARG(p->ctx, p->io_mode == GC_IO_GIVEN || p->slots[slot].has_odom,
                "GC_IO_COMPUTED needs the slot's odometry (gc_pipeline_stage_odom)");
   gc_ctx* ctx = p->ctx;
-  const auto& s = p->slots[slot];
+  auto& s = p->slots[slot];
+  GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, s.ready, 0));  // the slot's staged scan has landed
   gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
                  scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in, s.t, p->sig_cached ? 1 : 0};
   gc::PipeDev& P = p->P;
@@ -397,6 +505,9 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   // (pipeline.py:595-776: it needs the prediction, not the bins) as extra workgroups of the same
   // launch
   GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in));
+  // nothing after the bins reads the slot: the next staging into it may proceed from here
+  GC_HIP(ctx, hipEventRecord(s.consumed, ctx->stream));
+  s.consumed_rec = true;
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
   p->sig_cached = true;
@@ -409,6 +520,7 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
 
 int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out) {
   GC_CHECK_ARG(nullptr, p && h_out, "NULL argument");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   GC_TRY(down(p, h_out, p->P.comb, GC_COMB_LEN));
   double* cc = h_out + 484 + 22 + 22 + 6;
   if (cc[2] != cc[2]) {
@@ -427,6 +539,16 @@ int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out) {
   }
   return GC_OK;
 }
+
+int32_t gc_pipeline_exchange_ms(gc_pipeline* p, float* ms) {
+  GC_CHECK_ARG(nullptr, p && ms, "NULL argument");
+  GC_CHECK_ARG(p->ctx, p->x_rec, "no exchange has run (single rank without a communicator)");
+  GC_HIP(p->ctx, hipEventSynchronize(p->x1));
+  GC_HIP(p->ctx, hipEventElapsedTime(ms, p->x0, p->x1));
+  return GC_OK;
+}
+
+int32_t gc_pipeline_comm_size(const gc_pipeline* p) { return p ? (p->comm ? gc::comm_size(p->comm) : 0) : 0; }
 
 int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag) {
   GC_CHECK_ARG(nullptr, p && h_diag, "NULL argument");

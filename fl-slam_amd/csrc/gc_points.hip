@@ -1147,36 +1147,21 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
 // pull (hypothesis, chunk) tasks from a monotone counter until the H·chunks tasks are taken, so
 // the branch's workgroups are dispatched first and the bin tasks balance over whatever CU slots
 // remain — no stream fork / join and no partial last round of workgroups. Every task writes its
-// own record, so the result does not depend on which workgroup ran it (bit-reproducible). ctr[0]
-// is the task counter, ctr[1] the count of finished pullers; the last one resets both for the next
-// launch (stream order makes the reset visible to it). No workgroup waits on another.
-#ifdef GC_BINS_TIMING  // dev: per-workgroup [start, first task, end, tasks, iterations] cycle counters
-__device__ double g_bins_dbg[8192 * 5];
-#endif
+// own record, so the result does not depend on which workgroup ran it (bit-reproducible for a fixed
+// device and shard size: the chunk geometry follows the CU count and H_l). ctr[0] is the task
+// counter; the predict launch that precedes every k_bins_io on the stream zeroes it, so a launch
+// never depends on how the previous one ended. No workgroup waits on another.
 template <int BPL, bool FULL>
 __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
                                                              const double* __restrict__ odom, int n_io, int H,
                                                              int64_t chunks, unsigned* ctr) {
   extern __shared__ double lds[];
   __shared__ unsigned task_s;
-#ifdef GC_BINS_TIMING
-  const double tb0 = (double)__builtin_readcyclecounter();
-  double tb1 = 0.0, ntask = 0.0, nit = 0.0;
-#endif
   if ((int)blockIdx.x < n_io) {
     io_branch_wg(P, S, odom, blockIdx.x, lds);
-#ifdef GC_BINS_TIMING
-    if (threadIdx.x == 0 && blockIdx.x < 8192) {
-      double* d = g_bins_dbg + 5 * blockIdx.x;
-      d[0] = tb0; d[1] = tb0; d[2] = (double)__builtin_readcyclecounter(); d[3] = -1.0; d[4] = 0.0;
-    }
-#endif
     return;
   }
   bins_prologue(A, lds);
-#ifdef GC_BINS_TIMING
-  tb1 = (double)__builtin_readcyclecounter();
-#endif
   const int RL = A.B * NF_BASE + REC_EXTRA;
   const unsigned T = (unsigned)(H * chunks);
   // the next task's ticket is taken at the start of the current one, so the atomic's round trip
@@ -1193,20 +1178,6 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, Pipe
     const int64_t c = t / H;
     const int h = t % H;
     bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL);
-#ifdef GC_BINS_TIMING
-    ntask += 1.0;
-    nit += (c < A.k1) ? A.iters : A.iters_s;
-#endif
-  }
-#ifdef GC_BINS_TIMING
-  if (threadIdx.x == 0 && blockIdx.x < 8192) {
-    double* d = g_bins_dbg + 5 * blockIdx.x;
-    d[0] = tb0; d[1] = tb1; d[2] = (double)__builtin_readcyclecounter(); d[3] = ntask; d[4] = nit;
-  }
-#endif
-  if (threadIdx.x == 0 && atomicAdd(ctr + 1, 1u) == gridDim.x - n_io - 1) {
-    atomicExch(ctr, 0u);
-    atomicExch(ctr + 1, 0u);
   }
 }
 
@@ -1466,11 +1437,6 @@ hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, d
 
 extern "C" {
 
-#ifdef GC_BINS_TIMING
-int32_t gc_debug_bins_timing(double* host, int64_t n) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(gc::g_bins_dbg), sizeof(double) * (size_t)n) == hipSuccess ? 0 : 1;
-}
-#endif
 
 int32_t gc_budget_stats(gc_ctx* ctx, const double* d_w, int64_t n_in, int64_t n_cap, double* d_out) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
@@ -1688,11 +1654,14 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   // amortised) for the bulk, then short ones (2 x 256) that hold one long task of work per puller,
   // so the pullers run out of work together instead of one long task apart (A/B on one box against
   // half a long task: 1.2998/1.2984/1.2981 vs 1.3004/1.2997/1.2990 ms at H = 256, 0.342 vs 0.345 at 32)
+  // (P.geom_H > 0: sized as for a shard of that many hypotheses, the summation order then being the
+  // same for every shard size)
   const int64_t U = (P.n_cap + 255) / 256;  // 256-point units per hypothesis
+  const int Hg = P.geom_H > 0 ? P.geom_H : H;
   int iters = 16;
-  while (iters > 2 && (int64_t)H * U < 3 * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
+  while (iters > 2 && (int64_t)Hg * U < 3 * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
   constexpr int kItersShort = 2;
-  int64_t Us = std::max<int64_t>(iters, ((int64_t)pullers * iters + H - 1) / H);
+  int64_t Us = std::max<int64_t>(iters, ((int64_t)pullers * iters + Hg - 1) / Hg);
   Us = std::min(Us, U);
   const int64_t k1 = (U - Us) / iters;  // long chunks; the short tier takes the rest
   Us = U - k1 * iters;

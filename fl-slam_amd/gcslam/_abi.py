@@ -82,6 +82,8 @@ SIGNATURES = {
     "gc_pipeline_get_bin_stats": [_vp, _vp, _vp, _vp],
     "gc_pipeline_get_hyp_stats": [_vp, _vp, _vp, _vp],
     "gc_pipeline_attach_comm": [_vp, _vp],
+    "gc_pipeline_comm_size": [_vp],
+    "gc_pipeline_exchange_ms": [_vp, C.POINTER(C.c_float)],
     "gc_comm_unique_id": [_vp],
     "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],
     "gc_comm_destroy": [_vp],
@@ -143,7 +145,7 @@ GC_BARY_CERT = 16
 
 class PipelineDims(C.Structure):
     _fields_ = [("H_total", C.c_int32), ("h_begin", C.c_int32), ("h_count", C.c_int32), ("B", C.c_int32),
-                ("M", C.c_int32), ("world_size", C.c_int32), ("rank", C.c_int32), ("pad_", C.c_int32),
+                ("M", C.c_int32), ("world_size", C.c_int32), ("rank", C.c_int32), ("geom_hyps", C.c_int32),
                 ("n_in_max", C.c_int64), ("n_cap", C.c_int64)]
 
 _lib = None

@@ -78,7 +78,9 @@ class BatchedScanPipeline:
     """One rank's device-resident hypothesis shard."""
 
     def __init__(self, H_total: int, n_in_max: int, cfg: PipelineConfig = None, rank: int = 0,
-                 world_size: int = 1, ctx: _abi.Context = None):
+                 world_size: int = 1, ctx: _abi.Context = None, geometry_hyps: int = 0):
+        """geometry_hyps > 0 sizes the bins launch's chunks as for a shard of that many hypotheses
+        (e.g. H_total on every rank: per-hypothesis results then do not depend on world_size)."""
         self.cfg = cfg or PipelineConfig()
         self.ctx = ctx or _abi.default_context()
         self.H = H_total
@@ -87,7 +89,7 @@ class BatchedScanPipeline:
         self.B = self.cfg.n_bins
         self.M = self.cfg.imu_len
         self.rank, self.world = rank, world_size
-        d = _abi.PipelineDims(H_total, self.h0, self.Hl, self.B, self.M, world_size, rank, 0,
+        d = _abi.PipelineDims(H_total, self.h0, self.Hl, self.B, self.M, world_size, rank, int(geometry_hyps),
                               int(n_in_max), int(self.cfg.n_points_cap))
         cfgv = self.cfg.as_array(H_total)
         h = C.c_void_p()
@@ -254,6 +256,16 @@ class BatchedScanPipeline:
         _abi.call("gc_comm_init", self.ctx.handle, self.world, self.rank, C.addressof(buf), C.byref(h), ctx=self.ctx)
         self._comm = h.value
         self._call("gc_pipeline_attach_comm", self._comm)
+
+    def comm_size(self) -> int:
+        """Size of the attached RCCL communicator (0 without one)."""
+        return int(_abi.lib().gc_pipeline_comm_size(self.handle))
+
+    def exchange_ms(self) -> float:
+        """Device time of the last scan's exchange (all-gather or host-record upload), in ms."""
+        ms = C.c_float(0.0)
+        self._call("gc_pipeline_exchange_ms", C.byref(ms))
+        return float(ms.value)
 
     def close(self):
         if getattr(self, "handle", None):

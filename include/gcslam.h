@@ -171,7 +171,10 @@ typedef struct {
   int32_t M;         /* IMU slots (GC_MAX_IMU_PREINT_LEN = 512) */
   int32_t world_size;
   int32_t rank;
-  int32_t pad_;
+  int32_t geom_hyps; /* 0: the bins launch's chunk geometry follows h_count (and the CU count);
+                        k > 0: as for a shard of k hypotheses, so shards of different sizes sum each
+                        hypothesis's points in the same order (cross-world-size bit-reproducibility
+                        of the per-hypothesis results) */
   int64_t n_in_max;  /* raw points per scan (max) */
   int64_t n_cap;     /* N_POINTS_CAP */
 } gc_pipeline_dims;
@@ -256,6 +259,12 @@ int32_t gc_pipeline_get_iw(gc_pipeline* p, double* h_nu_proc7, double* h_Psi_pro
                            double* h_Psi_meas3x9, double* h_Q22x22, double* h_cert4);
 int32_t gc_pipeline_set_map(gc_pipeline* p, const double* h_map);
 int32_t gc_pipeline_get_map(gc_pipeline* p, double* h_map, double* h_map_der, double* h_misc2);
+/* Staging (stage_scan / stage_pointcloud2 / stage_odom) is the per-scan ingest
+ * (backend_node.py:1679-1690): the host arrays are copied into the slot's pinned mirror before the
+ * call returns (the caller may reuse them at once), then DMA'd into HBM on the pipeline's copy
+ * stream, ordered after the last scan that read the slot; scan_local waits for the slot's copy. So
+ * staging scan k+1 into a second slot overlaps scan k's compute. The call blocks only while the
+ * slot's previous DMA is still reading its pinned mirror. */
 int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_points, const double* h_t,
                                const double* h_w, int64_t n_in, const double* h_imu_t, const double* h_imu_gyro,
                                const double* h_imu_accel);
@@ -280,7 +289,12 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
  *               with NULL the pipeline all-gathers over its RCCL communicator (world_size > 1, or a
  *               single rank with one attached) or reads its own record (one rank, none attached).
  *               Then the fixed rank-order reduction, barycenter, IW apply, Q and map update.
- * Every rank ends the scan with a bit-identical combined belief, IW state and map. */
+ * Every rank ends the scan with a bit-identical combined belief, IW state and map.
+ * Between the two halves the state the combine reads or writes is locked: set_bins / set_beliefs /
+ * set_weights / set_io_evidence / set_io_mode / set_iw / set_map, get_combined / get_iw / get_map,
+ * attach_comm and a second scan_local return GC_ERR_ARG. Allowed: get_partial, the per-hypothesis
+ * getters (beliefs, diag, bin stats, hyp stats, io evidence: final after scan_local) and staging
+ * the next scan into any slot (ordered after the pending scan's reads of it). */
 int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
                                double t_scan, double dt_sec, int64_t scan_count);
 int32_t gc_pipeline_partial_len(const gc_pipeline* p);
@@ -298,6 +312,12 @@ int32_t gc_pipeline_get_bin_stats(gc_pipeline* p, double* h_stats, double* h_cer
  * (Hl,22,22) (BeliefGaussianInfo covariance, belief.py:373-386). */
 int32_t gc_pipeline_get_hyp_stats(gc_pipeline* p, double* h_dPsi_proc, double* h_dPsi_meas, double* h_Sigma);
 int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm);
+/* Size of the attached RCCL communicator (0 when none is attached). */
+int32_t gc_pipeline_comm_size(const gc_pipeline* p);
+/* Device time (ms, HIP events on the pipeline stream) of the last scan's exchange: the RCCL
+ * all-gather of the partial records, or the upload of the host-gathered records. Synchronises on
+ * it. GC_ERR_ARG when no exchange has run (one rank without a communicator). */
+int32_t gc_pipeline_exchange_ms(gc_pipeline* p, float* ms);
 
 /* ------------------------------------------------------------------ RCCL communicator */
 #define GC_COMM_ID_BYTES 128

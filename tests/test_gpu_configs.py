@@ -60,26 +60,30 @@ def _record_to_map(rec):
                       rec[:, 13].copy(), rec[:, 14:17].copy(), rec[:, 17:26].reshape(B, 3, 3).copy())
 
 
-def _pipeline(case, ctx, H, cap, io_computed):
+def _pipeline(case, ctx, H, cap, io_computed, rank=0, world=1, geometry_hyps=0):
     from gcslam.pipeline import BatchedScanPipeline, PipelineConfig
     n_in = case["scans"][0]["points"].shape[0]
-    pipe = BatchedScanPipeline(H, n_in, PipelineConfig(n_points_cap=cap), ctx=ctx)
+    pipe = BatchedScanPipeline(H, n_in, PipelineConfig(n_points_cap=cap), rank=rank, world_size=world, ctx=ctx,
+                               geometry_hyps=geometry_hyps)
     hy = case["hyp"]
-    pipe.set_beliefs(hy["X_anchor"], hy["z_lin"], hy["L"], hy["h"], hy["stamp"])
+    sl = slice(pipe.h0, pipe.h1)
+    pipe.set_beliefs(hy["X_anchor"][sl], hy["z_lin"][sl], hy["L"][sl], hy["h"][sl], hy["stamp"][sl])
     pipe.set_weights(hy["weights"])
     if io_computed:
         pipe.set_io_mode(True)
     else:
-        pipe.set_io_evidence(*case["io"])
+        pipe.set_io_evidence(*(a[sl] for a in case["io"]))
     pipe.set_iw(*case["iw"])
     pipe.set_map(case["map_record"])
     return pipe
 
 
-def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed):
+def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None):
+    """pipe: a BatchedScanPipeline, or any object with its scan / getter surface (the sharded
+    view of test_gpu_shards.py); default: one unsharded pipeline."""
     cfg = O.PipeConfig(n_points_cap=cap)
     bins = case["bins"]
-    pipe = _pipeline(case, ctx, H, cap, io_computed)
+    pipe = pipe if pipe is not None else _pipeline(case, ctx, H, cap, io_computed)
     weights = case["hyp"]["weights"]
     floor = 0.01 / H
     for k, s in enumerate(case["scans"][:n_scans]):

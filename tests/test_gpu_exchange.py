@@ -75,6 +75,7 @@ def test_host_gathered_shards_match_unsharded(ctx):
         for p in shards:
             p.finish_scan(recs)
         ctx.sync()
+        assert all(p.exchange_ms() >= 0.0 for p in shards)  # the record upload, timed on the stream
         ref = _state(full)
         st = [_state(p) for p in shards]
         for key in SHARED:

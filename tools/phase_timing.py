@@ -40,9 +40,12 @@ names = {1: "predict: wg_predict", 2: "predict: compose", 3: "predict: chol", 4:
          11: "evidence: start..MF", 12: "evidence: MF..planar", 13: "evidence: L_raw,beta,excitation",
          14: "evidence: pose6 cond+alpha", 15: "evidence: fusion PSD", 16: "evidence: recompose+IW stats",
          17: "evidence: IW solves/inverse", 18: "evidence: map increment", 19: "evidence: drift+final solves",
-         21: "combine: reduce + 22x22 PSD", 22: "combine: weight certs", 23: "combine: process IW apply",
-         24: "combine: meas IW apply", 25: "combine: Q rebuild"}
+         21: "combine wg0: reduce + 22x22 PSD", 23: "combine wg2: process IW apply",
+         24: "combine wg2: meas IW apply", 25: "combine wg2: Q rebuild"}
 for i in sorted(names):
     if t[i] and t[i - 1]:
         print(f"{names[i]:36s} {t[i] - t[i - 1]:10.0f} cycles")
-print("predict total", t[8] - t[0], "evidence 10..19", t[19] - t[10], "combine 20..25", t[25] - t[20])
+# combine_final's workgroups 0 (slots 20-21) and 2 (22-25) run side by side: their counters are
+# compared only within a workgroup
+print("predict total", t[8] - t[0], "evidence 10..19", t[19] - t[10], "combine wg0 20..21", t[21] - t[20],
+      "combine wg2 22..25", t[25] - t[22])
