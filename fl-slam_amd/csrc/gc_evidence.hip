@@ -300,7 +300,11 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
       so3_exp(zt + 3, R);
       for (int k = 0; k < 9; ++k) sc[80 + k] = R[k];
       sc[89] = zt[0]; sc[90] = zt[1]; sc[91] = 0.0;  // planar map: t[2] = 0 (CHANGELOG.md:575-578)
+      for (int k = 0; k < 6; ++k) P.h0rec[k] = zt[k];
     }
+    // hypothesis 0's pose covariance and deskew twist for the in-scan PrimitiveMap update
+    if (t - 64 < 36) P.h0rec[6 + (t - 64)] = W2[((t - 64) / 6) * n + (t - 64) % 6];
+    else if (t - 64 < 42) P.h0rec[42 + (t - 100)] = P.xi[(int64_t)hl * 6 + (t - 100)];
     wave_lds_sync();
     for (int b = t - 64; b < B; b += 64) pushforward_bin(st + b * 38, sc + 80, sc + 89, W2, n, P.map_inc + b * kMapRec);
   }
@@ -398,6 +402,7 @@ __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
     double r = (q[0] + q[1]) + (q[2] + q[3]);
     if (e >= kPX0 && e < kPX0 + 6) r = (P.h_begin == 0) ? P.X[e - kPX0] : 0.0;
     else if (e == kPSTAMP0) r = (P.h_begin == 0) ? P.stamp[0] : 0.0;
+    else if (e >= rec_h0(P.B)) r = (P.h_begin == 0) ? P.h0rec[e - rec_h0(P.B)] : 0.0;
     else if (e >= kPMAP) r = (P.h_begin == 0) ? P.map_inc[e - kPMAP] : 0.0;
     P.send[e] = r;
   }

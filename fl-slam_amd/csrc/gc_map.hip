@@ -152,6 +152,12 @@ __global__ void k_fuse_colors(gc_primitive_map map, double eps_mass) {
 }
 
 }  // namespace
+
+// the all-slot colour estimate (rgb, colors) of primitive_map_fuse, for the in-scan update
+hipError_t launch_fuse_colors(const gc_primitive_map& map, double eps_mass, hipStream_t st) {
+  hipLaunchKernelGGL(k_fuse_colors, dim3((unsigned)((map.m_slots + 255) / 256)), dim3(256), 0, st, map, eps_mass);
+  return hipGetLastError();
+}
 }  // namespace gc
 
 using namespace gc;

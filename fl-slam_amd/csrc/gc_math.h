@@ -448,4 +448,40 @@ GC_DEV void solve3(const double* A, const double* b, double* x) {
   mat3_vec(Ai, b, x);
 }
 
+// p0 = Exp(α ξ)^{-1} p  (deskew_constant_twist.py:50-58: se3_exp then so3_exp of the rotvec)
+GC_DEV void deskew_point(const double* p, double alpha, const double* xi, double* out) {
+  const double rho[3] = {alpha * xi[0], alpha * xi[1], alpha * xi[2]};
+  const double phi[3] = {alpha * xi[3], alpha * xi[4], alpha * xi[5]};
+  const double ts = dot3(phi, phi);
+  const double th = sqrt(ts);
+  double Bv, Cv, a, b;
+  if (th < kSmallAngle) {
+    Bv = 0.5 - ts / 24.0;
+    Cv = 1.0 / 6.0 - ts / 120.0;
+    a = 1.0;
+    b = 0.5;
+  } else {
+    double s, c;
+    sincos(th, &s, &c);
+    const double sts = (ts < kSmallAngle * kSmallAngle) ? 1.0 : ts;
+    Bv = (1.0 - c) / sts;
+    Cv = (th - s) / (sts * th);
+    a = s / th;
+    b = Bv;
+  }
+  double V[9], R[9], t[3], q[3];
+  rodrigues_form(phi, Bv, Cv, V);
+  mat3_vec(V, rho, t);
+  rodrigues_form(phi, a, b, R);
+  q[0] = p[0] - t[0]; q[1] = p[1] - t[1]; q[2] = p[2] - t[2];
+  mat3_tvec(R, q, out);
+}
+
+// unit ray direction from the LiDAR origin (pipeline.py:589-593)
+GC_DEV void direction(const double* p, const double* o, double eps, double* d) {
+  const double r0 = p[0] - o[0], r1 = p[1] - o[1], r2 = p[2] - o[2];
+  const double den = sqrt(r0 * r0 + r1 * r1 + r2 * r2) + eps;
+  d[0] = r0 / den; d[1] = r1 / den; d[2] = r2 / den;
+}
+
 }  // namespace gc

@@ -21,7 +21,11 @@ constexpr int kBudgetBlocks = 64;  // a1 budget partial workgroups (gc_budget.h)
 // Partial-sum record exchanged between ranks once per scan (doubles).
 constexpr int kPL = 0, kPH = 484, kPZ = 506, kPMU = 528, kPMU2 = 550, kPDPSIP = 551, kPDNUP = 803,
               kPDPSIM = 810, kPDNUM = 837, kPX0 = 841, kPSTAMP0 = 847, kPMAP = 848;
-__host__ __device__ inline int partial_len(int B) { return kPMAP + B * kMapRec; }
+// after the map increments: hypothesis 0's [z_t 6 (recomposed world pose), Σ_post pose block 36,
+// ξ_body 6] for the in-scan PrimitiveMap update every rank runs (gc_scanmap.hip)
+constexpr int kH0Len = 48;
+__host__ __device__ inline int rec_h0(int B) { return kPMAP + B * kMapRec; }
+__host__ __device__ inline int partial_len(int B) { return rec_h0(B) + kH0Len; }
 
 struct PipeDev {
   int Hl;        // local hypotheses
@@ -51,6 +55,7 @@ struct PipeDev {
   double *bins;                            // (B, 3)
   double *map, *map_der, *map_misc;        // (B, 26), (B, 17), [z_scale, N_dir_total, ...]
   double *map_inc;                         // (B, 26) written by hypothesis 0's owner
+  double *h0rec;                           // (kH0Len) hypothesis 0's pose block (its owner's k_evidence)
   double *nu_proc, *Psi_proc, *nu_meas, *Psi_meas;  // (7), (7,36), (3), (3,9)
   double *budget;                          // 8 budget scalars
   double *budget_part;                     // (64, 3) a1 partials, written by predict's extra workgroups

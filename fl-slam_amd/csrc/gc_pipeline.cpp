@@ -6,6 +6,7 @@
 #include <vector>
 #include "gc_internal.h"
 #include "gc_pipe.h"
+#include "gc_scanmap.h"
 
 struct gc_comm;
 namespace gc {
@@ -53,6 +54,14 @@ struct gc_pipeline {
   double* own_gather = nullptr;  // separate gather buffer of a single-rank pipeline with a communicator
   hipEvent_t x0 = nullptr, x1 = nullptr;  // around the last scan's all-gather (gc_pipeline_exchange_ms)
   bool x_rec = false;
+  // the in-scan PrimitiveMap update (gc_scanmap.hip), run by scan_finish after the combine
+  bool smap_on = false;
+  gc_primitive_map smap{};
+  double smap_voxel = 0.0;
+  bool smap_colors = false;  // the colour pass is due (first update after attaching a map with colours)
+  gc::ScanMapWork smapW;
+  int pending_slot = -1;
+  int64_t pending_seq = 0;
 };
 
 namespace {
@@ -172,10 +181,11 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
                           (size_t)Hl * gc::kIoParts, (size_t)Hl * 36, (size_t)Hl * NN};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
-                       &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert};
+                       &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert,
+                       &P.h0rec};
   const size_t ssz[] = {(size_t)P.H, (size_t)NN, (size_t)B * 3, (size_t)B * gc::kMapRec, (size_t)B * gc::kMapDer, 8,
                         (size_t)B * gc::kMapRec, 7, 7 * 36, 3, 27, 8, (size_t)PL, (size_t)PL * P.G,
-                        GC_COMB_LEN, 4};
+                        GC_COMB_LEN, 4, gc::kH0Len};
   for (size_t i = 0; i < sizeof(ssz) / sizeof(ssz[0]) && rc == GC_OK; ++i) rc = dalloc(p, ssz[i], shared[i]);
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
@@ -220,6 +230,7 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
   }
   for (hipEvent_t e : {p->x0, p->x1})
     if (e) (void)hipEventDestroy(e);
+  if (p->smapW.buf) (void)hipFree(p->smapW.buf);
   if (p->cstream) (void)hipStreamDestroy(p->cstream);
   delete p;
   return GC_OK;
@@ -481,6 +492,61 @@ int32_t gc_pipeline_scan_finish(gc_pipeline* p, const double* h_gather) {
   }
   p->pending = false;
   GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream));
+  if (p->smap_on) {
+    auto& s = p->slots[p->pending_slot];
+    const gc::ScanArgs& S = p->pending_S;
+    const gc::ScanMapInput in{s.pts, s.t, S.t0, S.t1, p->smap_voxel, S.t1, p->pending_seq};
+    GC_TRY(gc::scan_map_update(ctx, ctx->stream, &p->smapW, p->smap, P, in));
+    if (p->smap_colors) {
+      // primitive_map_fuse ends with colors = rgb = the estimate from the camera accumulators on
+      // every slot (primitive_map.py:1090-1098); LiDAR rows leave those inputs unchanged, so after
+      // the first pass the assignment is idempotent and later updates skip it
+      GC_HIP(ctx, gc::launch_fuse_colors(p->smap, P.eps_mass, ctx->stream));
+      p->smap_colors = false;
+    }
+    GC_HIP(ctx, hipEventRecord(s.consumed, ctx->stream));  // the map update was the slot's last reader
+    s.consumed_rec = true;
+  }
+  return GC_OK;
+}
+
+int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const gc_primitive_map* map, double voxel_m) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  if (!map) {
+    p->smap_on = false;
+    return GC_OK;
+  }
+  GC_CHECK_ARG(p->ctx, map->m_slots > 0 && map->m_slots < (int64_t)0xFFFFFFFF, "m_slots out of range");
+  GC_CHECK_ARG(p->ctx, map->n_lobes >= 1 && map->n_lobes <= 8, "n_lobes must be in [1, 8]");
+  GC_CHECK_ARG(p->ctx, map->Lambdas && map->thetas && map->etas && map->weights && map->timestamps &&
+                           map->last_supported_scan_seq && map->last_update_scan_seq,
+               "NULL map field");
+  GC_CHECK_ARG(p->ctx, voxel_m > 0.0, "voxel_m must be positive");
+  GC_TRY(gc::scan_map_prepare(p->ctx, &p->smapW, p->P.n_cap, map->m_slots));
+  p->smap = *map;
+  p->smap_voxel = voxel_m;
+  p->smap_colors = map->cam_mass != nullptr;
+  GC_CHECK_ARG(p->ctx, !p->smap_colors || (map->rgb_cam_accum && map->rgb_cam_denom && map->rgb),
+               "colour fields must be all set or all NULL");
+  p->smap_on = true;
+  return GC_OK;
+}
+
+int32_t gc_pipeline_get_scan_map_pose(gc_pipeline* p, double* h_out) {
+  GC_CHECK_ARG(nullptr, p && h_out, "NULL argument");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  return down(p, h_out, p->P.send + gc::rec_h0(p->P.B), gc::kH0Len);
+}
+
+int32_t gc_pipeline_get_scan_map_count(gc_pipeline* p, int64_t* n_slots) {
+  GC_CHECK_ARG(nullptr, p && n_slots, "NULL argument");
+  GC_CHECK_ARG(p->ctx, p->smap_on, "no PrimitiveMap attached");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  unsigned long long n = 0;
+  GC_HIP(p->ctx, hipMemcpyAsync(&n, p->smapW.count, sizeof(n), hipMemcpyDeviceToHost, p->ctx->stream));
+  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
+  *n_slots = (int64_t)n;
   return GC_OK;
 }
 
@@ -505,15 +571,20 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   // (pipeline.py:595-776: it needs the prediction, not the bins) as extra workgroups of the same
   // launch
   GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in));
-  // nothing after the bins reads the slot: the next staging into it may proceed from here
-  GC_HIP(ctx, hipEventRecord(s.consumed, ctx->stream));
-  s.consumed_rec = true;
+  // nothing after the bins reads the slot (but the in-scan map update in scan_finish, when a map
+  // is attached): the next staging into it may proceed from here
+  if (!p->smap_on) {
+    GC_HIP(ctx, hipEventRecord(s.consumed, ctx->stream));
+    s.consumed_rec = true;
+  }
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
   p->sig_cached = true;
   // a16 local part: this rank's partial record (weighted sums, IW statistics, map increment)
   GC_HIP(ctx, gc::launch_combine_local(P, ctx->stream));
   p->pending_S = S;
+  p->pending_slot = slot;
+  p->pending_seq = scan_count;
   p->pending = true;
   return GC_OK;
 }

@@ -229,35 +229,6 @@ GC_DEV double sim_nofma(double d0, double d1, double d2, double b0, double b1, d
   return s;
 }
 
-// p0 = Exp(α ξ)^{-1} p  (deskew_constant_twist.py:50-58: se3_exp then so3_exp of the rotvec)
-GC_DEV void deskew_point(const double* p, double alpha, const double* xi, double* out) {
-  const double rho[3] = {alpha * xi[0], alpha * xi[1], alpha * xi[2]};
-  const double phi[3] = {alpha * xi[3], alpha * xi[4], alpha * xi[5]};
-  const double ts = dot3(phi, phi);
-  const double th = sqrt(ts);
-  double Bv, Cv, a, b;
-  if (th < kSmallAngle) {
-    Bv = 0.5 - ts / 24.0;
-    Cv = 1.0 / 6.0 - ts / 120.0;
-    a = 1.0;
-    b = 0.5;
-  } else {
-    double s, c;
-    sincos(th, &s, &c);
-    const double sts = (ts < kSmallAngle * kSmallAngle) ? 1.0 : ts;
-    Bv = (1.0 - c) / sts;
-    Cv = (th - s) / (sts * th);
-    a = s / th;
-    b = Bv;
-  }
-  double V[9], R[9], t[3], q[3];
-  rodrigues_form(phi, Bv, Cv, V);
-  mat3_vec(V, rho, t);
-  rodrigues_form(phi, a, b, R);
-  q[0] = p[0] - t[0]; q[1] = p[1] - t[1]; q[2] = p[2] - t[2];
-  mat3_tvec(R, q, out);
-}
-
 // Fused-kernel variants of the three per-point helpers: reciprocals (hardware rcp + 2 Newton
 // steps, <= 1 ulp) instead of IEEE divisions and the LDS-table exp in the window sigmoid.
 // Results agree with the exact forms to a few ulps; they feed only floating-point moments
@@ -396,11 +367,6 @@ GC_DEV void point_features(const double* p, const double* d, double w, double* f
   f[16] = w * (p[1] * p[1]); f[17] = w * (p[1] * p[2]); f[18] = w * (p[2] * p[2]);
 }
 
-GC_DEV void direction(const double* p, const double* o, double eps, double* d) {
-  const double r0 = p[0] - o[0], r1 = p[1] - o[1], r2 = p[2] - o[2];
-  const double den = sqrt(r0 * r0 + r1 * r1 + r2 * r2) + eps;
-  d[0] = r0 / den; d[1] = r1 / den; d[2] = r2 / den;
-}
 
 // =============================================================================== a1 budget
 // Two-level deterministic reduction: 64 workgroups write [Σw_in, Σw_sel, Σw_sel²] partials, one

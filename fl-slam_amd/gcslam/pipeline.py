@@ -243,6 +243,28 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_get_hyp_stats", _p(a), _p(b), _p(c))
         return a, b, c
 
+    # ---------------------------------------------------------------- C5 in-scan map update
+    def attach_primitive_map(self, dmap, voxel_m: float = 0.1):
+        """Fuse every scan into a device-resident PrimitiveMap (gcslam.primitive_map.DevicePrimitiveMap)
+        in scan_finish: the budgeted points deskewed with hypothesis 0's twist, pushed to the world
+        frame by its recomposed pose with pose-covariance inflation, one row per point into the slot
+        of its voxel (build-defined, include/gcslam.h). dmap=None detaches."""
+        self._call("gc_pipeline_attach_primitive_map", None if dmap is None else C.addressof(dmap._struct),
+                   float(voxel_m))
+        self._smap = dmap  # the device arrays must outlive the attachment
+
+    def scan_map_pose(self):
+        """(z_t (6), Σ_pose (6,6), ξ_body (6)) of hypothesis 0 that the last scan's map update used."""
+        o = np.empty(H0_LEN)
+        self._call("gc_pipeline_get_scan_map_pose", _p(o))
+        return o[0:6], o[6:42].reshape(6, 6), o[42:48]
+
+    def scan_map_count(self) -> int:
+        """Distinct map slots the last in-scan update touched."""
+        n = C.c_int64(0)
+        self._call("gc_pipeline_get_scan_map_count", C.byref(n))
+        return int(n.value)
+
     # ---------------------------------------------------------------- multi-GPU
     @staticmethod
     def comm_unique_id() -> bytes:
@@ -309,7 +331,14 @@ def iw_meas_prior(lidar_sigma: float = 0.01):
 # Layout of the per-rank partial record exchanged once per scan (csrc/gc_pipe.h kP*).
 RECORD = dict(L=(0, 484), h=(484, 506), z=(506, 528), mu=(528, 550), mu2=(550, 551), dPsiP=(551, 803),
               dnuP=(803, 810), dPsiM=(810, 837), dnuM=(837, 840), X0=(841, 847), stamp0=(847, 848))
+MAP_INC0 = 848  # (B, 26) hypothesis 0's map increments, then its pose block (H0_LEN)
+H0_LEN = 48     # [z_t 6, Σ_post pose block 36, ξ_body 6] of hypothesis 0 (in-scan PrimitiveMap update)
+
+
+def record_h0(B: int) -> int:
+    """Offset of hypothesis 0's pose block in the partial record."""
+    return MAP_INC0 + 26 * B
 
 
 def partial_len(B: int) -> int:
-    return 848 + 26 * B
+    return record_h0(B) + H0_LEN

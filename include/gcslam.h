@@ -319,6 +319,23 @@ int32_t gc_pipeline_comm_size(const gc_pipeline* p);
  * it. GC_ERR_ARG when no exchange has run (one rank without a communicator). */
 int32_t gc_pipeline_exchange_ms(gc_pipeline* p, float* ms);
 
+/* The C5 in-scan PrimitiveMap update (config C5; the reference's step 12b, pipeline.py:1236-1327,
+ * transform_gaussian_to_world :1248-1256 + primitive_map_fuse, primitive_map.py:992-1163).
+ * BUILD-DEFINED, parity unpinned (csrc/gc_scanmap.hip): with a map attached,
+ * scan_finish fuses every budgeted point of the scan, deskewed with hypothesis 0's twist, as one
+ * world-frame Gaussian row (pose z_t of hypothesis 0 with t_z = 0, covariance Σ_lidar inflated by
+ * J Σ_pose Jᵀ) into the slot hashed from its voxel (edge voxel_m), responsibility 1, source
+ * LiDAR, timestamp scan_end, scan_seq = scan_count. Every rank runs it from the reduced record,
+ * so replicated maps stay bit-identical. The map's device arrays must outlive the attachment;
+ * map == NULL detaches. */
+struct gc_primitive_map; /* defined with the PrimitiveMap entries below */
+int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const struct gc_primitive_map* map, double voxel_m);
+/* Hypothesis 0's [z_t 6, Σ_post pose block 36 (row-major 6x6), ξ_body 6] that the last scan's
+ * update used (from the reduced record). */
+int32_t gc_pipeline_get_scan_map_pose(gc_pipeline* p, double* h_out48);
+/* Distinct map slots the last in-scan update touched (synchronises the stream). */
+int32_t gc_pipeline_get_scan_map_count(gc_pipeline* p, int64_t* n_slots);
+
 /* ------------------------------------------------------------------ RCCL communicator */
 #define GC_COMM_ID_BYTES 128
 int32_t gc_comm_unique_id(uint8_t* h_id_out);

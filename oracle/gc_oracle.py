@@ -1347,6 +1347,54 @@ def primitive_map_fuse(tile: dict, slots, Lambdas, thetas, etas, weights, resp, 
     return out, int(np.unique(idx).shape[0])
 
 
+def scan_map_slot(mu_w, voxel, M):
+    """Spatial hash of the world voxel of each row (uint64 arithmetic, mod M)."""
+    v = np.floor(mu_w / voxel).astype(np.int64).view(np.uint64)
+    h = (v[:, 0] * np.uint64(73856093)) ^ (v[:, 1] * np.uint64(19349663)) ^ (v[:, 2] * np.uint64(83492791))
+    return (h % np.uint64(M)).astype(np.int64)
+
+
+def scan_map_rows(scan_points, scan_t, scan_w, n_points_cap, t0, t1, h0, nu_meas, Psi_meas, origin, voxel, M,
+                  n_lobes=3, eps_mass=EPS_MASS):
+    """The C5 in-scan PrimitiveMap update's rows (csrc/gc_scanmap.hip). BUILD-DEFINED, parity
+    unpinned: the reference's step 12b (pipeline.py:1236-1327) fuses a measurement batch built
+    upstream of the OT association (outside this path) through transform_gaussian_to_world
+    (:1248-1256). Here every budgeted point (a1), deskewed with hypothesis 0's twist h0[42:48] (a4),
+    is one Gaussian row pushed to the world frame by z_t = h0[0:6] with t_z = 0, its covariance
+    Σ_lidar = Ψ_2 / (ν_2 + 4) (measurement_noise_mean_jax's LiDAR block; the IW apply keeps Ψ PSD)
+    inflated by J Σ_pose Jᵀ, J = [R | −R[p]×] (a13's inflation, Σ_pose = h0[6:42]); η lobe 0 = R d.
+    Returns (slots with -1 for dropped rows, Λ_w, θ_w, η_w, w)."""
+    bud = point_budget_resample(scan_points, scan_t, scan_w, None, None, n_points_cap)
+    p0, wd, _ = deskew_constant_twist(bud["points"], bud["timestamps"], bud["weights"], t0, t1, h0[42:48])
+    valid = (np.arange(n_points_cap) < bud["n_output"]) & (wd > 0.0)
+    R = so3_exp(h0[3:6])
+    t = np.array([h0[0], h0[1], 0.0])
+    mu = np.stack([((R[i, 0] * p0[:, 0] + R[i, 1] * p0[:, 1]) + R[i, 2] * p0[:, 2]) + t[i] for i in range(3)], axis=1)
+    Sl = Psi_meas[2] / (nu_meas[2] + 3.0 + 1.0)
+    Sp = np.asarray(h0[6:42]).reshape(6, 6)
+    K = p0.shape[0]
+    J = np.zeros((K, 3, 6))
+    J[:, :, 0:3] = R[None]
+    J[:, :, 3:6] = -np.einsum("ij,kjl->kil", R, np.stack([skew(p) for p in p0]))
+    Sw = (R @ Sl @ R.T)[None] + np.einsum("kia,ab,kjb->kij", J, Sp, J)
+    Sw = 0.5 * (Sw + np.swapaxes(Sw, 1, 2))
+    Lw = np.linalg.inv(Sw)
+    th = np.einsum("kij,kj->ki", Lw, mu)
+    eta = np.zeros((K, n_lobes, 3))
+    eta[:, 0] = point_directions(p0, np.asarray(origin), eps_mass) @ R.T
+    slots = np.where(valid, scan_map_slot(mu, voxel, M), -1)
+    return slots, Lw, th, eta, wd
+
+
+def scan_map_update(tile, rows, timestamp, scan_seq):
+    """Fuse the rows of scan_map_rows: responsibility 1, source LiDAR, no colours (primitive_map_fuse
+    restated; LiDAR rows leave the colour estimate unchanged)."""
+    slots, Lw, th, eta, wd = rows
+    K = slots.shape[0]
+    return primitive_map_fuse(tile, slots, Lw, th, eta, wd, np.ones(K), timestamp, scan_seq, None, None,
+                              np.ones(K, np.int64))
+
+
 # ---------------------------------------------------------------------------------------
 # PrimitiveMap maintenance (structures/primitive_map.py), SURVEY §8f rank 3. A tile is a dict of
 # the create_empty_tile fields (valid_mask bool); each function returns a new tile dict.

@@ -42,7 +42,7 @@ def _pack(case, res, h0, h1):
     if h0 == 0:
         rec[slice(*RECORD["X0"])] = res[0]["belief"].X_anchor
         from oracle import cases
-        rec[848:] = cases.map_to_record(res[0]["map_inc"]).reshape(-1)
+        rec[848:848 + 26 * B] = cases.map_to_record(res[0]["map_inc"]).reshape(-1)
     return rec
 
 
@@ -105,4 +105,5 @@ def test_sharded_exchange_equals_unsharded_combine(world):
     aP = sum(case["state"].weights[i] * res[i]["dPsi_proc"] for i in range(6))
     np.testing.assert_allclose(red[slice(*RECORD["dPsiP"])].reshape(7, 6, 6), aP, rtol=1e-12, atol=1e-30)
     # map increments come from hypothesis 0's owner only
-    np.testing.assert_allclose(red[848:].reshape(48, 26), cases.map_to_record(res[0]["map_inc"]), rtol=0, atol=0)
+    np.testing.assert_allclose(red[848:848 + 26 * 48].reshape(48, 26), cases.map_to_record(res[0]["map_inc"]),
+                               rtol=0, atol=0)

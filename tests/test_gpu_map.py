@@ -31,7 +31,7 @@ def _tile(rng, M, L=3):
 
 
 @pytest.mark.parametrize("K,M,world", [(5000, 1 << 12, False), (20000, 1 << 16, False), (3000, 2000, True),
-                                       (1, 10, False)])
+                                       (1, 10, False), (131072, 1 << 20, False), (131072, 1 << 20, True)])
 def test_primitive_map_fuse_matches_oracle(ctx, K, M, world):
     from gcslam.primitive_map import DevicePrimitiveMap, fuse_rows
     rng = np.random.default_rng(K + M)

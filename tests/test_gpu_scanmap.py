@@ -1,0 +1,130 @@
+"""The C5 in-scan PrimitiveMap update (csrc/gc_scanmap.hip; build-defined, parity unpinned — the
+reference's step 12b, pipeline.py:1236-1327, fuses a measurement batch built outside this path).
+
+Every budgeted point, deskewed with hypothesis 0's twist, is one world-frame Gaussian row (pose
+z_t of hypothesis 0, t_z = 0, Σ_lidar inflated by J Σ_pose Jᵀ) fused into the slot hashed from its
+voxel. The oracle rebuilds the rows from the raw scan and the pose block the GPU used
+(gc_pipeline_get_scan_map_pose), fuses them with its np.add.at restatement of primitive_map_fuse
+and must agree: slot keys, touched-slot count, timestamps, scan sequences, camera mass and colours
+exactly; Λ, θ, η, w and LiDAR mass within 1e-12 of each field's largest entry (the rows' 3x3
+inverse and products round differently in NumPy). The pose block itself is the pipeline's own
+hypothesis-0 result (ξ and Σ_post bit-identical to the per-hypothesis getters), which the config
+tests compare with the oracle at the north-star bars.
+"""
+
+import numpy as np
+import pytest
+
+from oracle import cases
+from oracle import gc_oracle as O
+from test_gpu_configs import _pipeline
+
+pytestmark = pytest.mark.gpu
+
+FIELDS_CLOSE = ("Lambdas", "thetas", "etas", "weights", "lidar_mass")
+FIELDS_EXACT = ("timestamps", "last_supported_scan_seq", "last_update_scan_seq", "cam_mass", "rgb", "colors",
+                "rgb_cam_accum", "rgb_cam_denom")
+
+
+def _map(ctx, M, seed):
+    from gcslam.primitive_map import DevicePrimitiveMap
+    rng = np.random.default_rng(seed)
+    B = rng.normal(size=(M, 3, 3))
+    dm = DevicePrimitiveMap(1, M, ctx=ctx)
+    dm.upload(Lambdas=B @ np.swapaxes(B, 1, 2) + np.eye(3), thetas=rng.normal(size=(M, 3)),
+              etas=rng.normal(size=(M, 3, 3)), weights=rng.uniform(0, 2, M), timestamps=rng.uniform(0, 5, M),
+              lidar_mass=rng.uniform(0, 1, M))
+    return dm
+
+
+def _check_scan(pipe, dm, tile0, s, k, cap, M, voxel):
+    zt, Sp, xi = pipe.scan_map_pose()
+    _, _, xi_all = pipe.bin_stats()
+    _, _, Sig = pipe.hyp_stats()
+    assert np.array_equal(xi, xi_all[0]), "pose block: ξ is not hypothesis 0's"
+    assert np.array_equal(Sp, Sig[0][0:6, 0:6]), "pose block: Σ_pose is not hypothesis 0's Σ_post"
+    iw = pipe.get_iw()
+    h0 = np.concatenate([zt, Sp.reshape(-1), xi])
+    rows = O.scan_map_rows(s["points"], s["timestamps"], s["weights"], cap, s["scan_start"], s["scan_end"], h0,
+                           iw["nu_meas"], iw["Psi_meas"], np.asarray(pipe.cfg.lidar_origin), voxel, M)
+    ref, nref = O.scan_map_update(tile0, rows, s["scan_end"], k)
+    got = dm.download()
+    assert pipe.scan_map_count() == nref, f"scan{k}: touched slots {pipe.scan_map_count()} vs {nref}"
+    for f in FIELDS_EXACT:
+        assert np.array_equal(got[f], ref[f]), f"scan{k} {f}"
+    for f in FIELDS_CLOSE:
+        scale = np.max(np.abs(ref[f]))
+        err = np.max(np.abs(got[f] - ref[f]))
+        assert err <= 1e-12 * scale, f"scan{k} {f}: {err:.3e} vs scale {scale:.3e}"
+    return nref
+
+
+@pytest.mark.parametrize("n_az,cap,M", [(1024, 16384, 1 << 14), (8192, 65536, 1 << 20)])
+def test_scan_map_update_matches_oracle(ctx, n_az, cap, M):
+    """Small map, and the C5 geometry: 131,072-point scans budgeted to 65,536 rows into 1,048,576 slots."""
+    voxel = 0.1
+    case = cases.build(H=8, n_az=n_az, n_scans=2, io="computed", cap=cap)
+    pipe = _pipeline(case, ctx, 8, cap, True)
+    dm = _map(ctx, M, n_az)
+    pipe.attach_primitive_map(dm, voxel)
+    touched = []
+    for k, s in enumerate(case["scans"]):
+        tile0 = dm.download()
+        pipe.stage_scan(0, s)
+        pipe.run_scan(0, s, k)
+        touched.append(_check_scan(pipe, dm, tile0, s, k, cap, M, voxel))
+    assert all(t > 1000 for t in touched), touched
+    pipe.close()
+
+
+def test_scan_map_update_replicated_across_shards(ctx):
+    """Two shards (4 + 4 of 8, chunk geometry as for 8) each with its own copy of the map and
+    host-gathered records: both maps end bit-identical to the unsharded pipeline's."""
+    case = cases.build(H=8, n_az=1024, n_scans=2, io="computed")
+    cap = case["n"]
+    full = _pipeline(case, ctx, 8, cap, True)
+    shards = [_pipeline(case, ctx, 8, cap, True, rank=r, world=2, geometry_hyps=8) for r in range(2)]
+    maps = [_map(ctx, 1 << 14, 3) for _ in range(3)]
+    full.attach_primitive_map(maps[0], 0.1)
+    for p, m in zip(shards, maps[1:]):
+        p.attach_primitive_map(m, 0.1)
+    for k, s in enumerate(case["scans"]):
+        full.stage_scan(0, s)
+        full.run_scan(0, s, k)
+        for p in shards:
+            p.stage_scan(0, s)
+            p.run_scan_local(0, s, k)
+        recs = np.stack([p.partial() for p in shards])
+        for p in shards:
+            p.finish_scan(recs)
+        ctx.sync()
+        ref = maps[0].download()
+        for m in maps[1:]:
+            got = m.download()
+            for f in ref:
+                assert np.array_equal(got[f], ref[f]), f"scan{k} {f}"
+
+
+def test_scan_map_attach_rules(ctx):
+    from gcslam.primitive_map import DevicePrimitiveMap
+    case = cases.build(H=2, n_az=256, n_scans=1, io="computed")
+    pipe = _pipeline(case, ctx, 2, case["n"], True)
+    dm = DevicePrimitiveMap(1, 1024, ctx=ctx)
+    with pytest.raises(ValueError, match="voxel"):
+        pipe.attach_primitive_map(dm, 0.0)
+    with pytest.raises(ValueError, match="no PrimitiveMap"):
+        pipe.scan_map_count()
+    s = case["scans"][0]
+    pipe.attach_primitive_map(dm, 0.2)
+    pipe.stage_scan(0, s)
+    pipe.run_scan_local(0, s, 0)
+    with pytest.raises(ValueError, match="pending"):
+        pipe.attach_primitive_map(None)
+    pipe.finish_scan()
+    assert pipe.scan_map_count() > 0
+    pipe.attach_primitive_map(None)
+    w0 = dm.download("weights")["weights"]
+    pipe.stage_scan(0, s)
+    pipe.run_scan(0, s, 1)
+    ctx.sync()
+    assert np.array_equal(dm.download("weights")["weights"], w0)  # detached: no update
