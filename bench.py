@@ -421,11 +421,11 @@ def fused_roofline_leg(ctx, _abi, s, B, n, H, bins, origin, reps=10, warm=10):
             "kernel": "k_bins_fused + k_bins_finalize (gc_scan_bins_fused)", "hypotheses": H, "points": n, "bins": B}
 
 
-def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5):
+def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5, m_slots=1 << 20, voxel=0.1):
     """C5 on one GPU: 131,072-point scans budgeted to 65,536 (stride 2) x 1024
-    hypotheses through the full batched pipeline, plus the 1M-slot PrimitiveMap fuse of
-    map_fuse_leg timed separately. BASELINE.json quotes C5 on 8 GPUs; this is one GPU's
-    whole-job throughput at the full 1024 hypotheses."""
+    hypotheses through the full batched pipeline, each scan staged from host memory and fused into
+    a resident 1M-slot PrimitiveMap by the in-scan map update (csrc/gc_scanmap.hip). BASELINE.json
+    quotes C5 on 8 GPUs; this is one GPU's whole-job throughput at the full 1024 hypotheses."""
     from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
     from gcslam.ops.binning import create_fibonacci_atlas
     from gcslam.pipeline import BatchedScanPipeline, PipelineConfig, iw_meas_prior, iw_process_prior
@@ -441,20 +441,39 @@ def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5):
     pipe.set_iw(*iw_process_prior(), *iw_meas_prior())
     pipe.set_map(warmup_map_record(ctx, _abi, make_scan(0, n_az=n_az), n_in, B, create_fibonacci_atlas(B).dirs,
                                    np.asarray(T_BASE_LIDAR[:3])))
-    for k, sc in enumerate(scans):
-        pipe.stage_scan(k, sc)
-    for i in range(warmup):
+    dm = primitive_map_1m(ctx, m_slots)
+    pipe.attach_primitive_map(dm, voxel)  # the in-scan map update runs inside every timed scan
+
+    def step(i):
+        pipe.stage_scan(i % 2, scans[i % 2])
         pipe.run_scan(i % 2, scans[i % 2], i)
+
+    for i in range(warmup):
+        step(i)
     ctx.sync()
     t0 = time.perf_counter()
     for i in range(steps):
-        pipe.run_scan(i % 2, scans[i % 2], warmup + i)
+        step(warmup + i)
     ctx.sync()
     dt = (time.perf_counter() - t0) / steps
+    touched = pipe.scan_map_count()
     pipe.close()
-    return {"workload": "C5 shape on 1 GPU: %d-point scans, budget cap %d (stride 2), %d hypotheses, full pipeline"
-                        % (n_in, cap, H), "ms_per_scan": 1e3 * dt, "scans_per_s": 1.0 / dt, "steps": steps,
-            "warmup": warmup}
+    return {"workload": "C5 shape on 1 GPU: %d-point scans (staged every step), budget cap %d (stride 2), %d "
+                        "hypotheses, full pipeline + the in-scan PrimitiveMap update (%d rows into a %d-slot map, "
+                        "voxel %.2f m)" % (n_in, cap, H, cap, m_slots, voxel),
+            "ms_per_scan": 1e3 * dt, "scans_per_s": 1.0 / dt, "steps": steps, "warmup": warmup,
+            "map_slots_touched_last_scan": touched}
+
+
+def primitive_map_1m(ctx, M, seed=20261015):
+    """A resident M-slot PrimitiveMap (random SPD Λ with eigenvalues 10..1e4, θ, 3-lobe η, w in (0, 1])."""
+    from gcslam.primitive_map import DevicePrimitiveMap
+    rng = np.random.default_rng(seed)
+    Q, _ = np.linalg.qr(rng.normal(size=(M, 3, 3)))
+    dm = DevicePrimitiveMap(1, M, ctx=ctx)
+    dm.upload(Lambdas=np.einsum("nij,nj,nkj->nik", Q, 10.0 ** rng.uniform(1, 4, (M, 3)), Q),
+              thetas=rng.normal(size=(M, 3)), etas=rng.normal(size=(M, 3, 3)), weights=rng.uniform(1e-3, 1.0, M))
+    return dm
 
 
 def map_fuse_leg(ctx, _abi, m_slots=1 << 20, rows=1 << 17, reps=5):
