@@ -10,8 +10,9 @@ G = 8 rank-ordered reduction of k_combine_final that the RCCL all-gather feeds o
 Bars:
   * the combined belief, IW state, Q and map are bit-identical on all 8 shards;
   * against the unsharded pipeline run beside them: with the shards' chunk geometry sized as
-    for the full hypothesis count (geometry_hyps = H) every per-hypothesis result is bit-identical
-    and the shared state within 1e-12 relative (the 8 shard sums associate differently from one);
+    for the full hypothesis count (geometry_hyps = H) every per-hypothesis result of the first scan
+    is bit-identical, the shared state within 1e-12 relative (the 8 shard sums associate
+    differently from one) and so, through it, every later scan's per-hypothesis results;
     at the production geometry (each shard sized for its own 32 / 128 hypotheses, as the bench
     runs) the per-hypothesis sums run in another order, so the bars are the oracle's;
   * sampled hypotheses on both sides of every shard boundary tested (0, 31, 32, 255 for C4;
@@ -77,6 +78,7 @@ class ShardSet:
         if self.full is not None:
             self.full.run_scan(slot, s, k)
         self._check(k)
+        self.k += 1
 
     def _check(self, k):
         st = [self._shared(p) for p in self.shards]
@@ -93,13 +95,17 @@ class ShardSet:
             if self.exact and not e <= 1e-12:
                 _FAILS.append(f"scan{k} {key} vs unsharded: {e:.3e} relative (bar 1e-12)")
         b, bf = self.get_beliefs(), self.full.get_beliefs()
+        # bit-identical per hypothesis on the first scan; from the second on, the shared state the
+        # scan starts from (Q from the IW state, the map) carries the 1e-16 of the cross-shard sums
+        first = self.k == 0
         for key in ("X_anchor", "z_lin", "L", "h"):
-            if self.exact:
-                if not np.array_equal(b[key], bf[key]):
-                    _FAILS.append(f"scan{k} per-hypothesis {key} not bit-identical to the unsharded pipeline")
-            else:
-                self.report.append((k, key, _rel(b[key], bf[key])))
-        if self.exact:
+            e = _rel(b[key], bf[key])
+            self.report.append((k, key, e))
+            if self.exact and first and not np.array_equal(b[key], bf[key]):
+                _FAILS.append(f"scan{k} per-hypothesis {key} not bit-identical to the unsharded pipeline")
+            elif self.exact and not e <= 1e-12:
+                _FAILS.append(f"scan{k} per-hypothesis {key} vs unsharded: {e:.3e} relative (bar 1e-12)")
+        if self.exact and first:
             for a, c in zip(self.bin_stats(), self.full.bin_stats()):
                 if not np.array_equal(a, c):
                     _FAILS.append(f"scan{k} bin statistics not bit-identical to the unsharded pipeline")
