@@ -224,14 +224,19 @@ def main():
             pipe.stage_scan(k, s)
 
     count = [0]
+    stage_s = [0.0, 0]  # host wall time inside stage_scan over the timed steps, and their count
 
-    def step():
+    def step(timed=False):
         # with ingest, every step stages its scan from host memory (pinned mirror + DMA on the copy
         # stream) into one of two slots, so the copy of scan k+1 overlaps scan k's compute
         k = count[0]
         sc = scans[k % len(scans)]
         if ingest:
+            ts = time.perf_counter()
             pipe.stage_scan(k % 2, sc)
+            if timed:
+                stage_s[0] += time.perf_counter() - ts
+                stage_s[1] += 1
             pipe.run_scan(k % 2, sc, k)
         else:
             pipe.run_scan(k % len(scans), sc, k)
@@ -257,7 +262,7 @@ def main():
     ctx.sync()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        step()
+        step(timed=True)
     ctx.sync()
     dist.barrier()
     t1 = time.perf_counter()
@@ -301,6 +306,8 @@ def main():
     }
     if exchange is not None:
         out["exchange"] = exchange
+    if ingest:
+        out["ingest_host_ms_per_scan"] = 1e3 * stage_s[0] / max(stage_s[1], 1)
 
     if dist.rank == 0 and not args.no_roofline:
         rng = np.random.default_rng(5)

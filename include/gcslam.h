@@ -294,7 +294,8 @@ int32_t gc_pipeline_run_scan(gc_pipeline* p, int32_t slot, double scan_start, do
  * set_weights / set_io_evidence / set_io_mode / set_iw / set_map, get_combined / get_iw / get_map,
  * attach_comm and a second scan_local return GC_ERR_ARG. Allowed: get_partial, the per-hypothesis
  * getters (beliefs, diag, bin stats, hyp stats, io evidence: final after scan_local) and staging
- * the next scan into any slot (ordered after the pending scan's reads of it). */
+ * the next scan into any slot (ordered after the pending scan's reads of it) except, with a
+ * PrimitiveMap attached, the pending scan's own slot (its map update reads it in scan_finish). */
 int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
                                double t_scan, double dt_sec, int64_t scan_count);
 int32_t gc_pipeline_partial_len(const gc_pipeline* p);

@@ -120,6 +120,9 @@ def test_scan_map_attach_rules(ctx):
     pipe.run_scan_local(0, s, 0)
     with pytest.raises(ValueError, match="pending"):
         pipe.attach_primitive_map(None)
+    with pytest.raises(ValueError, match="map update"):  # its slot is still to be read by scan_finish
+        pipe.stage_scan(0, s)
+    pipe.stage_scan(1, s)
     pipe.finish_scan()
     assert pipe.scan_map_count() > 0
     pipe.attach_primitive_map(None)
