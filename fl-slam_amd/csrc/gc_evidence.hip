@@ -79,6 +79,27 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     zl[t] = P.z[(int64_t)hl * n + t];
   }
   const double* st = P.stats + (int64_t)hl * B * 38;
+  // a6 certificate of the bins (binning.py:285-324): the cross-bin reductions of the split finalize's
+  // per-bin terms, on wave 0 in k_bins_finalize's wave_sum order (lane b = bin b, B <= 64); thread 0
+  // reads them back below (its own writes)
+  if (t < 64) {
+    double Nl = 0.0, N2l = 0.0, psdl = 0.0, epsl = 0.0, sfl = 0.0;
+    if (t < B) {
+      const double N = st[t * 38];
+      const double* ax = P.binaux + ((int64_t)hl * B + t) * 2;
+      Nl = N; N2l = N * N; psdl = ax[0]; epsl = ax[1]; sfl = N / (N + eps);
+    }
+    const double Nt = wave_sum(Nl), N2 = wave_sum(N2l), psd = wave_sum(psdl), mer = wave_max(epsl),
+                 sf = wave_sum(sfl);
+    if (t == 0) {
+      double* c = P.bincert + (int64_t)hl * 8;
+      c[0] = Nt * Nt / (N2 + eps);
+      c[1] = sf / (double)B;
+      c[2] = psd;
+      c[3] = mer;
+      c[7] = psd + mer;
+    }
+  }
   GC_PHASE(P, 10);
   // ---------------------------------------------- a7 MatrixFisher: per-bin cross-covariance
   if (t < B) {

@@ -44,6 +44,7 @@ struct PipeDev {
   double *X, *z, *L, *h, *stamp;           // belief (in/out)
   double *Lpred, *hpred, *pred_cert, *pose_pred, *xi, *imu_out, *dPsiM;
   double *stats, *bincert;                 // (Hl, B, 38), (Hl, 8)
+  double *binaux;                          // (Hl, B, 2) per-bin [projection delta, mass-eps ratio]
   double *io_L, *io_h, *io_cert;           // IMU/odom-branch evidence (computed or given)
   double *mu_aux, *io_parts;               // (Hl, kMuAux), (Hl, kIoParts)
   double *dPsiP, *mu_fin, *diag;

@@ -89,6 +89,19 @@ int down(gc_pipeline* p, double* h, const double* d, size_t count) {
   return GC_OK;
 }
 
+// Host wait for a copy-stream event by polling: hipEventSynchronize may sleep on an interrupt and
+// take tens to hundreds of microseconds to wake, enough to make the host, not the device, the
+// bottleneck of a 0.3 ms scan. Falls back to the blocking wait after ~10^5 polls.
+int wait_event(gc_ctx* ctx, hipEvent_t e) {
+  for (int spin = 0; spin < 100000; ++spin) {
+    const hipError_t q = hipEventQuery(e);
+    if (q == hipSuccess) return GC_OK;
+    if (q != hipErrorNotReady) GC_HIP(ctx, q);
+  }
+  GC_HIP(ctx, hipEventSynchronize(e));
+  return GC_OK;
+}
+
 // slot block layout (doubles): pts 3n | t n | w n | imu_t M | imu_g 3M | imu_a 3M | odom
 struct SlotLayout {
   size_t t, w, imu, odom, len;
@@ -184,13 +197,13 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   int rc = GC_OK;
   double** fields[] = {&P.X, &P.z, &P.L, &P.h, &P.stamp, &P.Lpred, &P.hpred, &P.pred_cert, &P.pose_pred, &P.xi,
                        &P.imu_out, &P.dPsiM, &P.stats, &P.bincert, &P.io_L, &P.io_h, &P.io_cert, &P.dPsiP,
-                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose, &P.Sig};
+                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose, &P.Sig, &P.binaux};
   const size_t sizes[] = {(size_t)Hl * 6, (size_t)Hl * 22, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl,
                           (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kPredCert, (size_t)Hl * 6,
                           (size_t)Hl * 6, (size_t)Hl * gc::kImuOut, (size_t)Hl * 27, (size_t)Hl * B * 38,
                           (size_t)Hl * 8, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kIoCert,
                           (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag, (size_t)Hl * gc::kMuAux,
-                          (size_t)Hl * gc::kIoParts, (size_t)Hl * 36, (size_t)Hl * NN};
+                          (size_t)Hl * gc::kIoParts, (size_t)Hl * 36, (size_t)Hl * NN, (size_t)Hl * B * 2};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert,
@@ -310,7 +323,7 @@ int32_t gc_pipeline_stage_odom(gc_pipeline* p, int32_t slot, const double* h_pos
   GC_CHECK_ARG(p->ctx, h_pose6 && h_cov36 && h_twist6 && h_twist_cov36, "NULL odometry array");
   auto& s = p->slots[slot];
   GC_TRY(slot_alloc(p, s));
-  if (s.odom_rec) GC_HIP(p->ctx, hipEventSynchronize(s.odom_done));  // the last odometry DMA read its area
+  if (s.odom_rec) GC_TRY(wait_event(p->ctx, s.odom_done));  // the last odometry DMA read its area
   double* buf = s.host + SlotLayout(p->P).odom;
   std::memcpy(buf, h_pose6, 6 * sizeof(double));
   std::memcpy(buf + 6, h_cov36, 36 * sizeof(double));
@@ -388,7 +401,7 @@ int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_pts
   GC_CHECK_ARG(p->ctx, h_pts && h_t && h_w && h_imu_t && h_imu_g && h_imu_a, "NULL scan array");
   auto& s = p->slots[slot];
   GC_TRY(slot_alloc(p, s));
-  if (s.ready_rec) GC_HIP(p->ctx, hipEventSynchronize(s.ready));  // the last DMA out of the mirror is done
+  if (s.ready_rec) GC_TRY(wait_event(p->ctx, s.ready));  // the last DMA out of the mirror is done
   const SlotLayout Ly(p->P);
   const size_t n = (size_t)n_in, M = (size_t)p->P.M;
   std::memcpy(s.host, h_pts, 3 * n * sizeof(double));
@@ -428,7 +441,7 @@ int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_
     GC_HIP(p->ctx, hipMalloc((void**)&s.tag, (size_t)p->P.n_in));
     GC_HIP(p->ctx, hipMalloc((void**)&s.flag, 4 * sizeof(int32_t)));
   }
-  if (s.ready_rec) GC_HIP(p->ctx, hipEventSynchronize(s.ready));  // the last DMA / parse from this slot is done
+  if (s.ready_rec) GC_TRY(wait_event(p->ctx, s.ready));  // the last DMA / parse from this slot is done
   const size_t nb = (size_t)n_points * (size_t)point_step;
   if (s.bytes_cap < nb) {
     if (s.bytes) GC_HIP(p->ctx, hipFree(s.bytes));
@@ -577,11 +590,7 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   // the slot's staged scan must have landed. The host waits for the copy rather than the compute
   // stream: a cross-queue barrier costs ~6 us of device time per scan, while the host is normally a
   // scan or more ahead of the device and the copy (ordered after an earlier scan's bins) long done
-  if (s.ready_rec) {
-    const hipError_t q = hipEventQuery(s.ready);
-    if (q == hipErrorNotReady) GC_HIP(ctx, hipEventSynchronize(s.ready));
-    else GC_HIP(ctx, q);
-  }
+  if (s.ready_rec) GC_TRY(wait_event(ctx, s.ready));
   gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
                  scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in, s.t, p->sig_cached ? 1 : 0};
   gc::PipeDev& P = p->P;

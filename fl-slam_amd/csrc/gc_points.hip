@@ -1195,6 +1195,58 @@ GC_DEV void finalize_reduce(const double* __restrict__ P, int RL, int imax, int6
     sm[i] = w;
   }
 }
+// One bin's finalize (binning.py:139-209): its NF summed moments a -> the GC_BIN_STATS row o
+// (p̄, Σ_p PSD-projected, κ; N, s_dir, scatter and the raw sums), its projection delta and
+// mass-epsilon ratio.
+GC_DEV void finalize_bin(const double* a, int NF, double eps_psd, double eps_mass, double* o, double* psd_out,
+                         double* er_out) {
+  const double N = a[0];
+  const double denom = N + eps_mass + kF64Eps;
+  const double invN = 1.0 / denom, er = eps_mass / denom;
+  const double sd[3] = {a[1], a[2], a[3]};
+  const double Ssc[9] = {a[4], a[5], a[6], a[5], a[7], a[8], a[6], a[8], a[9]};
+  const double sp[3] = {a[10], a[11], a[12]};
+  const double Spp[9] = {a[13], a[14], a[15], a[14], a[16], a[17], a[15], a[17], a[18]};
+  double pb[3] = {sp[0] * invN, sp[1] * invN, sp[2] * invN};
+  double Sr[9], Sp[9], c6[6];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double v = Spp[3 * i + j] * invN - pb[i] * pb[j];
+      if (NF > NF_BASE) v += a[NF_BASE + 3 * i + j] * invN;
+      Sr[3 * i + j] = v;
+    }
+  // certified shortcut (as wg_psd_project_fast): Cholesky of Σ_sym - εI succeeds => the clamp
+  // is inactive and the projection is Σ_sym itself (projection delta 0 up to rounding)
+  {
+    double S[9];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 0; j < 3; ++j) S[3 * i + j] = 0.5 * (Sr[3 * i + j] + Sr[3 * j + i]);
+    const double a00 = S[0] - eps_psd;
+    const double l10 = S[3] / sqrt(fmax(a00, 1e-300)), l20 = S[6] / sqrt(fmax(a00, 1e-300));
+    const double a11 = S[4] - eps_psd - l10 * l10;
+    const double l21 = (S[7] - l20 * l10) / sqrt(fmax(a11, 1e-300));
+    const double a22 = S[8] - eps_psd - l20 * l20 - l21 * l21;
+    if (a00 > 0.0 && a11 > 0.0 && a22 > 0.0) {
+      for (int k = 0; k < 9; ++k) Sp[k] = S[k];
+      c6[0] = 0.0;
+    } else {
+      psd_project3(Sr, eps_psd, Sp, c6);
+    }
+  }
+  const double Rbar = sqrt(sd[0] * sd[0] + sd[1] * sd[1] + sd[2] * sd[2]) * invN;
+  const double kap = kappa_blend(Rbar, 1e-6, 3.0, 0.8, 0.03);
+  o[0] = N;
+  for (int k = 0; k < 3; ++k) o[1 + k] = sd[k];
+  for (int k = 0; k < 9; ++k) o[4 + k] = Ssc[k];
+  for (int k = 0; k < 3; ++k) o[13 + k] = pb[k];
+  for (int k = 0; k < 9; ++k) o[16 + k] = Sp[k];
+  o[25] = kap;
+  for (int k = 0; k < 3; ++k) o[26 + k] = sp[k];
+  for (int k = 0; k < 9; ++k) o[29 + k] = Spp[k];
+  *psd_out = c6[0];
+  *er_out = er;
+}
+
 // One hypothesis h on a 1024-thread workgroup (kFinWG): the entry sums with 4x the loads in flight of
 // a 256-thread one (the reduction is L2-latency-bound at small H), then per-bin moments -> p̄, Σ_p
 // (PSD-projected), κ on lanes b < B of wave 0 (B <= 64) and the cert reductions on that wave.
@@ -1211,52 +1263,9 @@ GC_DEV void finalize_hyp(int h, int B, int NF, int64_t chunks, const double* __r
   double Nl = 0.0, N2l = 0.0, psdl = 0.0, epsl = 0.0, sfl = 0.0;
   if ((int)threadIdx.x < B) {
     const int b = threadIdx.x;
-    const double* a = sm + b * NF;
-    const double N = a[0];
-    const double denom = N + eps_mass + kF64Eps;
-    const double invN = 1.0 / denom, er = eps_mass / denom;
-    const double sd[3] = {a[1], a[2], a[3]};
-    const double Ssc[9] = {a[4], a[5], a[6], a[5], a[7], a[8], a[6], a[8], a[9]};
-    const double sp[3] = {a[10], a[11], a[12]};
-    const double Spp[9] = {a[13], a[14], a[15], a[14], a[16], a[17], a[15], a[17], a[18]};
-    double pb[3] = {sp[0] * invN, sp[1] * invN, sp[2] * invN};
-    double Sr[9], Sp[9], c6[6];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) {
-        double v = Spp[3 * i + j] * invN - pb[i] * pb[j];
-        if (NF > NF_BASE) v += a[NF_BASE + 3 * i + j] * invN;
-        Sr[3 * i + j] = v;
-      }
-    // certified shortcut (as wg_psd_project_fast): Cholesky of Σ_sym - εI succeeds => the clamp
-    // is inactive and the projection is Σ_sym itself (projection delta 0 up to rounding)
-    {
-      double S[9];
-      for (int i = 0; i < 3; ++i)
-        for (int j = 0; j < 3; ++j) S[3 * i + j] = 0.5 * (Sr[3 * i + j] + Sr[3 * j + i]);
-      const double a00 = S[0] - eps_psd;
-      const double l10 = S[3] / sqrt(fmax(a00, 1e-300)), l20 = S[6] / sqrt(fmax(a00, 1e-300));
-      const double a11 = S[4] - eps_psd - l10 * l10;
-      const double l21 = (S[7] - l20 * l10) / sqrt(fmax(a11, 1e-300));
-      const double a22 = S[8] - eps_psd - l20 * l20 - l21 * l21;
-      if (a00 > 0.0 && a11 > 0.0 && a22 > 0.0) {
-        for (int k = 0; k < 9; ++k) Sp[k] = S[k];
-        c6[0] = 0.0;
-      } else {
-        psd_project3(Sr, eps_psd, Sp, c6);
-      }
-    }
-    const double Rbar = sqrt(sd[0] * sd[0] + sd[1] * sd[1] + sd[2] * sd[2]) * invN;
-    const double kap = kappa_blend(Rbar, 1e-6, 3.0, 0.8, 0.03);
-    double* o = stats + ((int64_t)h * B + b) * GC_BIN_STATS;
-    o[0] = N;
-    for (int k = 0; k < 3; ++k) o[1 + k] = sd[k];
-    for (int k = 0; k < 9; ++k) o[4 + k] = Ssc[k];
-    for (int k = 0; k < 3; ++k) o[13 + k] = pb[k];
-    for (int k = 0; k < 9; ++k) o[16 + k] = Sp[k];
-    o[25] = kap;
-    for (int k = 0; k < 3; ++k) o[26 + k] = sp[k];
-    for (int k = 0; k < 9; ++k) o[29 + k] = Spp[k];
-    Nl = N; N2l = N * N; psdl = c6[0]; epsl = er; sfl = N / (N + eps_mass);
+    const double N = sm[b * NF];
+    finalize_bin(sm + b * NF, NF, eps_psd, eps_mass, stats + ((int64_t)h * B + b) * GC_BIN_STATS, &psdl, &epsl);
+    Nl = N; N2l = N * N; sfl = N / (N + eps_mass);
   }
   if (threadIdx.x >= 64) return;  // every bin lives on wave 0 (B <= 64)
   const double Nt = wave_sum(Nl);
@@ -1283,6 +1292,56 @@ __global__ void __launch_bounds__(kFinWG) k_bins_finalize(int B, int NF, int64_t
                                                        double* stats, double* cert) {
   extern __shared__ double sm[];  // B*NF + 8 + 4
   finalize_hyp(blockIdx.x, B, NF, chunks, partials, eps_psd, eps_mass, stats, cert, sm);
+}
+
+// The batched pipeline's finalize, split over bins: grid (S, H), workgroup s of hypothesis h owns
+// bins [s kFinBins, (s+1) kFinBins) (and, the last one, the record's extra entries). One lane per
+// record entry sums the chunk records in chunk order (finalize_reduce's order and batching, so
+// every sum is bit-identical to k_bins_finalize's), then one lane per bin runs finalize_bin. At
+// small H this spreads a hypothesis's ~0.6 MB of records over S CUs instead of one (k_bins_finalize
+// is bound by one CU's load rate there). The cross-bin certificate reductions need every bin: the
+// per-bin projection delta and mass-epsilon ratio go to aux (H, B, 2) and k_evidence reduces them
+// (finalize_cert), in k_bins_finalize's wave_sum order.
+constexpr int kFinBins = 6;
+constexpr int kFinSplitWG = 128;
+static_assert(kFinBins * NF_BASE + REC_EXTRA <= kFinSplitWG, "one lane per record entry");
+__global__ void __launch_bounds__(kFinSplitWG) k_bins_finalize_split(int B, int NF, int64_t chunks,
+                                                                     const double* __restrict__ partials,
+                                                                     double eps_psd, double eps_mass, double* stats,
+                                                                     double* cert, double* aux) {
+  __shared__ double sm[kFinBins * NF_BASE + REC_EXTRA];
+  const int h = blockIdx.y, s = blockIdx.x;
+  const int RL = B * NF + REC_EXTRA;
+  const int b0 = s * kFinBins, nb = min(kFinBins, B - b0);
+  const bool last = s == (int)gridDim.x - 1;
+  const int ne = nb * NF + (last ? REC_EXTRA : 0);
+  const int e0 = b0 * NF, imax = B * NF + 1;
+  const double* P = partials + (int64_t)h * chunks * RL;
+  const int t = threadIdx.x;
+  if (t < ne) {
+    const int e = e0 + t;
+    constexpr int KU = 16;
+    double v = 0.0;
+    for (int64_t c = 0; c < chunks; c += KU) {
+      double x[KU];
+#pragma unroll
+      for (int u = 0; u < KU; ++u) x[u] = c + u < chunks ? P[(c + u) * RL + e] : 0.0;
+#pragma unroll
+      for (int u = 0; u < KU; ++u) v = e == imax ? fmax(v, x[u]) : v + x[u];
+    }
+    sm[t] = v;
+  }
+  __syncthreads();
+  if (t < nb) {
+    double* ax = aux + ((int64_t)h * B + b0 + t) * 2;
+    finalize_bin(sm + t * NF, NF, eps_psd, eps_mass, stats + ((int64_t)h * B + b0 + t) * GC_BIN_STATS, ax, ax + 1);
+  } else if (last && t == 64) {
+    const double* ex = sm + nb * NF;
+    double* c = cert + (int64_t)h * GC_BIN_CERT;
+    c[4] = ex[0] / (ex[3] + eps_mass);
+    c[5] = ex[1];
+    c[6] = ex[2];
+  }
 }
 
 __global__ void k_kappa(int64_t n, const double* __restrict__ R, double eps_r, double d, double r0,
@@ -1657,7 +1716,11 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   }
 #undef GC_BIO
   GC_LAUNCH_CHECK(ctx);
-  return launch_finalize(ctx, H, B, NF, chunks, (const double*)scr, P.eps_psd, P.eps_mass, P.stats, P.bincert);
+  const dim3 fgrid((unsigned)((B + kFinBins - 1) / kFinBins), (unsigned)H);
+  hipLaunchKernelGGL(k_bins_finalize_split, fgrid, dim3(kFinSplitWG), 0, ctx->stream, B, NF, chunks,
+                     (const double*)scr, P.eps_psd, P.eps_mass, P.stats, P.bincert, P.binaux);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
 }
 }  // namespace gc
 
