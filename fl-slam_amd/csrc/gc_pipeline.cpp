@@ -652,6 +652,33 @@ int32_t gc_pipeline_exchange_ms(gc_pipeline* p, float* ms) {
 
 int32_t gc_pipeline_comm_size(const gc_pipeline* p) { return p ? (p->comm ? gc::comm_size(p->comm) : 0) : 0; }
 
+int32_t gc_pipeline_get_hyp_conditioning(gc_pipeline* p, double* h_out) {
+  GC_CHECK_ARG(nullptr, p && h_out, "NULL argument");
+  GC_CHECK_ARG(p->ctx, p->sig_cached, "no scan has run since the beliefs were set");
+  // The batched scan certifies these projections by Cholesky (their eigen-decompositions are skipped
+  // on the scan path); the reference's ConditioningCert of each is the clamped spectrum of the same
+  // stored matrix, computed here on demand by the Jacobi projection (off the scan path, as
+  // gc_pipeline_get_combined does for the combined belief)
+  const int Hl = p->P.Hl, NN = 484;
+  double* ws = nullptr;
+  const size_t len = (size_t)Hl * (NN + 6);
+  GC_HIP(p->ctx, hipMalloc((void**)&ws, sizeof(double) * 2 * len));
+  const double* mats[2] = {p->P.Lpred, p->P.L};
+  int32_t rc = GC_OK;
+  for (int m = 0; m < 2 && rc == GC_OK; ++m)
+    rc = gc_domain_projection_psd_batch(p->ctx, Hl, 22, mats[m], p->P.eps_psd, ws + m * len,
+                                        ws + m * len + (size_t)Hl * NN);
+  std::vector<double> c6((size_t)2 * Hl * 6);
+  if (rc == GC_OK) rc = down(p, c6.data(), ws + (size_t)Hl * NN, (size_t)Hl * 6);
+  if (rc == GC_OK) rc = down(p, c6.data() + (size_t)Hl * 6, ws + len + (size_t)Hl * NN, (size_t)Hl * 6);
+  (void)hipFree(ws);
+  if (rc != GC_OK) return rc;
+  for (int h = 0; h < Hl; ++h)
+    for (int m = 0; m < 2; ++m)
+      for (int k = 0; k < 4; ++k) h_out[((size_t)h * 2 + m) * 4 + k] = c6[((size_t)m * Hl + h) * 6 + 2 + k];
+  return GC_OK;
+}
+
 int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag) {
   GC_CHECK_ARG(nullptr, p && h_diag, "NULL argument");
   return down(p, h_diag, p->P.diag, (size_t)p->P.Hl * gc::kHypDiag);

@@ -78,6 +78,7 @@ SIGNATURES = {
     "gc_pipeline_scan_finish": [_vp, _vp],
     "gc_pipeline_get_combined": [_vp, _vp],
     "gc_pipeline_get_hyp_diag": [_vp, _vp],
+    "gc_pipeline_get_hyp_conditioning": [_vp, _vp],
     "gc_pipeline_get_lpose6": [_vp, _vp],
     "gc_pipeline_get_bin_stats": [_vp, _vp, _vp, _vp],
     "gc_pipeline_get_hyp_stats": [_vp, _vp, _vp, _vp],

@@ -225,6 +225,14 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_get_hyp_diag", _p(o))
         return o
 
+    def hyp_conditioning(self):
+        """(Hl, 2, 4): the ConditioningCert [eig_min, eig_max, cond, near_null_count] of each
+        hypothesis's predict (L_pred, predict.py:183-188) and fusion (L_post, fusion.py:150-230)
+        PSD projections of the last scan (computed on demand, off the scan path)."""
+        o = np.empty((self.Hl, 2, 4))
+        self._call("gc_pipeline_get_hyp_conditioning", _p(o))
+        return o
+
     def lpose6(self):
         """L_evidence[pose, pose] per hypothesis of the last scan (Hl, 6, 6)."""
         o = np.empty((self.Hl, 6, 6))

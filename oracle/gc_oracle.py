@@ -1248,7 +1248,8 @@ def scan_hypothesis(b_prev: Belief, scan: ScanInput, Q, io: IOEvidence, mapst: M
                 map_inc=inc, T=T, beta=beta, alpha=alpha, s_dt=s_dt, s_ex=s_ex, xi_body=xi,
                 moments=mm, assign=sa, mf=mf, planar=tr, rho=dr["rho"], frob=rc["frobenius_strength"],
                 budget=bud, retained=retained, pose=world_pose(b_fin), L_post=L_post, h_post=h_post,
-                io=io, io_parts=io_parts, L_ev=L_ev, cond6=cond6, eigmin6=pose6_eigs(L_ev)[0])
+                io=io, io_parts=io_parts, L_ev=L_ev, cond6=cond6, eigmin6=pose6_eigs(L_ev)[0],
+                pred_cond=pc["cond"], fusion_cond=np.asarray(fc[2:6]))
 
 
 @dataclass

@@ -98,6 +98,7 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None)
         pipe.run_scan(0, s, k)
         ctx.sync()
         diag = pipe.hyp_diag()
+        hcond = pipe.hyp_conditioning()
         stats, bcert, xi = pipe.bin_stats()
         bel = pipe.get_beliefs()
         dPp, dPm, Sig = pipe.hyp_stats()
@@ -142,6 +143,13 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None)
             S_ref = _cov(b.L)
             _close(Sig[i][0:6, 0:6], S_ref[0:6, 0:6], 0.0, 1e-6, f"{tag} pose covariance")  # north-star bar
             _close(Sig[i], S_ref, 1e-8, 0.0, f"{tag} covariance")
+            # per-hypothesis ConditioningCert of the predict and fusion PSD projections: eigenvalue
+            # extremes at the absolute accuracy of eigh (~1e-12 of the largest), near-null count exact
+            for m, (name, ref) in enumerate((("predict", r["pred_cond"]), ("fusion", r["fusion_cond"]))):
+                _close(hcond[i, m, 1], ref[1], 1e-10, 0.0, f"{tag} {name} eig_max")
+                _close(hcond[i, m, 0], ref[0], 0.0, 1e-12 * ref[1], f"{tag} {name} eig_min")
+                _close(hcond[i, m, 2], hcond[i, m, 1] / hcond[i, m, 0], 1e-15, 0.0, f"{tag} {name} cond")
+                _close(hcond[i, m, 3], ref[3], 0.0, 0.0, f"{tag} {name} near-null count")
             _close(dPp[i], r["dPsi_proc"], 1e-8, 1e-18, f"{tag} dPsi_proc")
             _close(dPm[i], r["dPsi_meas"], 1e-8, 1e-18, f"{tag} dPsi_meas")
         # every hypothesis: the device covariance is the inverse of the device information matrix

@@ -124,6 +124,9 @@ class ShardSet:
     def hyp_diag(self):
         return self._cat(lambda p: p.hyp_diag())
 
+    def hyp_conditioning(self):
+        return self._cat(lambda p: p.hyp_conditioning())
+
     def bin_stats(self):
         return self._cat(lambda p: p.bin_stats())
 
