@@ -486,6 +486,9 @@ GC_DEV void sa_store_block(const double* S, double* Rh, int64_t wbase, int64_t n
     }
   }
 }
+#ifndef GC_SA_NT
+#define GC_SA_NT 1
+#endif
 #ifndef GC_SA_OCC
 // 2 waves per SIMD: the 48 similarities / exps of a lane's point stay in registers with no spill
 // (at 3, the 168-VGPR budget spilled ~12-27 VGPRs per point to scratch: 0.6 GB of extra HBM reads and
@@ -623,7 +626,13 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
           const int o = m * 128 + 2 * lane;
           const int row = o / NB, col = o - row * NB;
           const dvec2 v = *reinterpret_cast<const dvec2*>(&S[row * RS2 + col]);
-          if (o < lim) *reinterpret_cast<dvec2*>(dst + o) = v;
+          if (o < lim) {
+#if GC_SA_NT
+            __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(dst + o));
+#else
+            *reinterpret_cast<dvec2*>(dst + o) = v;
+#endif
+          }
         }
         lds_wave_sync();
       }
