@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-PROFILE_ROUNDS = ("r02", "r01")  # committed rocprofv3 summaries (profiles/<round>/), newest first
+PROFILE_ROUNDS = ("r03", "r02", "r01")  # committed rocprofv3 summaries (profiles/<round>/), newest first
 
 
 def parse():
@@ -51,6 +51,9 @@ def parse():
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 single-GPU pipeline leg")
     ap.add_argument("--roofline-only", action="store_true",
                     help="run only the contract-pair roofline leg (PMC traffic passes, tools/pmc_traffic.sh)")
+    ap.add_argument("--map-only", action="store_true",
+                    help="run only the C5 PrimitiveMap fuse leg (PMC passes, tools/pmc_fuse.sh)")
+    ap.add_argument("--c5-only", action="store_true", help="run only the C5 pipeline leg (PMC passes)")
     ap.add_argument("--io-given", action="store_true", help=argparse.SUPPRESS)
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-ingest", action="store_true",
@@ -181,6 +184,12 @@ def main():
 
     ctx = _abi.Context(dist.local_rank)
     H_total = args.hyps
+    if args.map_only:
+        print(json.dumps({"c5_map_fuse": map_fuse_leg(ctx, _abi)}), flush=True)
+        return
+    if args.c5_only:
+        print(json.dumps({"c5": c5_leg(ctx, _abi, args)}), flush=True)
+        return
     if args.roofline_only:
         from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
         from gcslam.ops.binning import create_fibonacci_atlas

@@ -1,0 +1,40 @@
+"""Summarise tools/pmc_fuse.sh: per C5 map kernel, HBM bytes per dispatch (2 x FETCH_SIZE, the gfx950
+correction of MI355X_MICROARCH.md 'HBM', + WRITE_SIZE) and the average duration from the kernel
+trace of the same command; the leg's algorithmic bytes from its bench JSON line."""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+src, dst = sys.argv[1], sys.argv[2]
+out = {}
+for leg in ("map-only", "c5-only"):
+    acc = collections.defaultdict(lambda: collections.defaultdict(list))
+    for f in glob.glob(os.path.join(src, leg, "**", "*counter_collection.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    dur = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(src, leg, "kt", "**", "*kernel_trace.csv"), recursive=True):
+        for r in csv.DictReader(open(f)):
+            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    per = {}
+    for k, cs in acc.items():
+        if not any(t in k for t in ("fuse", "smap", "Radix", "radix", "Onesweep", "onesweep")):
+            continue
+        m = {c: sum(v) / len(v) for c, v in cs.items()}
+        rd, wr = 2.0 * m.get("FETCH_SIZE", 0.0) * 1024, m.get("WRITE_SIZE", 0.0) * 1024
+        us = sum(dur[k]) / len(dur[k]) if dur.get(k) else None
+        per[k[:90]] = {"read_bytes": rd, "write_bytes": wr, "avg_us": us,
+                       "GB/s": (rd + wr) / (us * 1e-6) / 1e9 if us else None}
+    line = [l for l in open(os.path.join(src, leg + ".kt.log")) if l.startswith("{")]
+    out[leg] = {"kernels": per, "bench": json.loads(line[-1]) if line else None}
+json.dump(out, open(dst, "w"), indent=1)
+for leg, v in out.items():
+    print(leg)
+    for k, d in v["kernels"].items():
+        print("  %-60s rd %8.1f MB wr %8.1f MB %8s us" % (k[:60], d["read_bytes"] / 1e6, d["write_bytes"] / 1e6,
+                                                          "%.1f" % d["avg_us"] if d["avg_us"] else "-"))

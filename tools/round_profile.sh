@@ -11,7 +11,11 @@ timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout
 tail -2 $out/gpu_tests.log
 timeout -k 10 300 python3 bench.py > $out/bench.json 2> $out/bench.err
 tail -c 400 $out/bench.json
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- python3 bench.py --no-cpu --no-c5 > $out/bench_rocprof.json 2> $out/bench_rocprof.err
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- python3 bench.py --no-cpu > $out/bench_rocprof.json 2> $out/bench_rocprof.err
 cp "$(find $out/kt -name '*kernel_stats.csv' | head -1)" $out/kernel_stats.csv
 bash tools/pmc_traffic.sh $round
 cp gpurun_out/pmc_traffic_$round.json $out/pmc_traffic.json
+bash tools/pmc_fuse.sh $round
+cp gpurun_out/pmc_fuse_$round.json $out/pmc_fuse.json
+bash tools/trace_scan.sh 32 h32 > /dev/null && cp gpurun_out/trace_h32/timeline.txt $out/timeline_h32.txt
+bash tools/trace_scan.sh 256 h256 > /dev/null && cp gpurun_out/trace_h256/timeline.txt $out/timeline_h256.txt
