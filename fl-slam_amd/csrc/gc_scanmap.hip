@@ -12,17 +12,20 @@
 //   Λ_w = Σ_w⁻¹,     θ_w = Λ_w μ_w,   η_w = [R d, 0, ..] (d = the unit ray direction),
 // with Σ_lidar the measurement-IW LiDAR block's mode Ψ_2 / (ν_2 + 4) and the row's weight the
 // deskewed point weight (a4). Its slot is the spatial hash of the world voxel of μ_w. The rows are
-// fused with responsibility 1 and source LiDAR by the same reduce-by-key as gc_map.hip: a stable
-// radix sort of (slot, row) and one thread per distinct slot summing its rows in row order, so the
-// result is np.add.at's and bit-reproducible. LiDAR rows leave the camera accumulators unchanged,
+// fused with responsibility 1 and source LiDAR by a reduce-by-key: a stable radix sort of (slot,
+// row), the rows gathered into that order, rocprim's deterministic reduce_by_key (a fixed
+// association per run, so bit-reproducible run to run; within 1e-12 of np.add.at's sequential
+// order) and one thread per distinct slot applying its sum. A scan's points crowd into few voxels
+// (~65k rows into ~5k slots, runs of thousands near the sensor), so rows are computed one per
+// thread and the runs reduced in parallel: one thread per run summing its rows serially took
+// ~1 ms per scan. LiDAR rows leave the camera accumulators unchanged,
 // so the all-slot colour recompute (colors = rgb) runs only on the first update after the map is
 // attached (gc_pipeline.cpp), when it may change colours an empty tile holds.
 //
-// Rows are never materialised: the key pass computes μ_w only, and the segment pass recomputes the
-// row from the point index (40 B of point data per row instead of a 176 B row written and re-read).
 // Every rank runs the update from the reduced record, so the maps stay bit-identical across ranks.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_reduce_by_key.hpp>
 #include "gc_internal.h"
 #include "gc_math.h"
 #include "gc_pipe.h"
@@ -41,6 +44,19 @@ struct ScanMapArgs {
   int64_t n_cap;
   double t0, t1, o0, o1, o2, voxel, timestamp, eps_mass;
   int64_t scan_seq;
+};
+
+constexpr int kSmapRow = 16;  // [Λ_w 9, θ_w 3, η_w lobe 0 3, w]
+struct SmapRow {
+  double v[kSmapRow];
+};
+struct SmapRowSum {
+  __host__ __device__ SmapRow operator()(const SmapRow& a, const SmapRow& b) const {
+    SmapRow c;
+#pragma unroll
+    for (int q = 0; q < kSmapRow; ++q) c.v[q] = a.v[q] + b.v[q];
+    return c;
+  }
 };
 
 // the row's deskewed body point and weight (false: padding or zero weight -> dropped)
@@ -71,20 +87,6 @@ GC_DEV uint32_t smap_slot(const double* mw, double voxel, int64_t M) {
 GC_DEV void smap_pose(const ScanMapArgs& A, double* R, double* tt) {
   so3_exp(A.h0 + 3, R);
   tt[0] = A.h0[0]; tt[1] = A.h0[1]; tt[2] = 0.0;  // planar map: t_z = 0 (CHANGELOG.md:575-578)
-}
-
-__global__ void k_smap_keys(ScanMapArgs A, uint32_t* keys, uint32_t* vals) {
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= A.n_cap) return;
-  double R[9], tt[3], p0[3], mw[3], w;
-  smap_pose(A, R, tt);
-  uint32_t key = (uint32_t)A.map.m_slots;  // dropped rows sort after every slot
-  if (smap_point(A, j, p0, &w)) {
-    smap_world_mean(R, tt, p0, mw);
-    key = smap_slot(mw, A.voxel, A.map.m_slots);
-  }
-  keys[j] = key;
-  vals[j] = (uint32_t)j;
 }
 
 // One world row (the comment at the top): Λ_w (9), θ_w (3), η_w lobe 0 (3).
@@ -129,53 +131,59 @@ GC_DEV void smap_row(const ScanMapArgs& A, const double* R, const double* tt, co
   mat3_vec(R, d, e0);
 }
 
-__global__ void __launch_bounds__(256) k_smap_segments(ScanMapArgs A, const uint32_t* __restrict__ keys,
-                                                       const uint32_t* __restrict__ vals,
-                                                       unsigned long long* n_unique) {
-#pragma clang fp contract(off)  // r·X then add, as the fuse and np.add.at
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t K = A.n_cap;
-  if (i >= K) return;
-  const uint32_t key = keys[i];
-  if ((int64_t)key >= A.map.m_slots || (i > 0 && keys[i - 1] == key)) return;  // dropped / not a segment head
-  const int L = A.map.n_lobes;
-  const int64_t s = key;
-  // the slot's current values first (their latency overlaps the row work)
-  double mL[9], mth[3], met[3 * kSmapMaxLobes], mw, mlid = 0.0;
-  for (int q = 0; q < 9; ++q) mL[q] = A.map.Lambdas[9 * s + q];
-  for (int q = 0; q < 3; ++q) mth[q] = A.map.thetas[3 * s + q];
-  for (int q = 0; q < 3 * L; ++q) met[q] = A.map.etas[(int64_t)3 * L * s + q];
-  mw = A.map.weights[s];
-  if (A.map.lidar_mass) mlid = A.map.lidar_mass[s];
-  double R[9], tt[3], Sl[9];
+// one thread per row: its slot key (m_slots for a dropped row, sorted after every slot) and its
+// world row [Λ_w 9, θ_w 3, η_w lobe 0 3, w] (zeros when dropped)
+__global__ void k_smap_rows(ScanMapArgs A, uint32_t* keys, uint32_t* vals, SmapRow* rows) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= A.n_cap) return;
+  double R[9], tt[3], p0[3], w, mw[3], Sl[9];
   smap_pose(A, R, tt);
-  {
+  SmapRow row;
+  for (int q = 0; q < kSmapRow; ++q) row.v[q] = 0.0;
+  uint32_t key = (uint32_t)A.map.m_slots;
+  if (smap_point(A, j, p0, &w)) {
+    smap_world_mean(R, tt, p0, mw);
+    key = smap_slot(mw, A.voxel, A.map.m_slots);
     const double den = A.nu_meas[2] + 3.0 + 1.0;  // measurement_noise_mean_jax, LiDAR block
     for (int q = 0; q < 9; ++q) Sl[q] = A.Psi_meas[18 + q] / den;
+    smap_row(A, R, tt, Sl, p0, row.v, row.v + 9, row.v + 12);
+    row.v[15] = w;
   }
-  double dL[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, dth[3] = {0, 0, 0}, de0[3] = {0, 0, 0}, dw = 0.0, dlid = 0.0;
-  for (int64_t j = i; j < K && keys[j] == key; ++j) {
-    const int64_t row = vals[j];
-    double p0[3], w, Lw[9], th[3], e0[3];
-    smap_point(A, row, p0, &w);  // a row with a key is valid
-    smap_row(A, R, tt, Sl, p0, Lw, th, e0);
-    const double r = 1.0;
-    for (int q = 0; q < 9; ++q) dL[q] += r * Lw[q];
-    for (int q = 0; q < 3; ++q) dth[q] += r * th[q];
-    for (int q = 0; q < 3; ++q) de0[q] += r * e0[q];
-    dw += r * w;
-    dlid += r * w;
-  }
-  for (int q = 0; q < 9; ++q) A.map.Lambdas[9 * s + q] = mL[q] + dL[q];
-  for (int q = 0; q < 3; ++q) A.map.thetas[3 * s + q] = mth[q] + dth[q];
-  // lobes > 0 receive 0.0 per row: x + 0.0 = x for every x but -0.0, written as the fuse does
-  for (int q = 0; q < 3; ++q) A.map.etas[(int64_t)3 * L * s + q] = met[q] + de0[q];
-  for (int q = 3; q < 3 * L; ++q) A.map.etas[(int64_t)3 * L * s + q] = met[q] + 0.0;
-  A.map.weights[s] = mw + dw;
+  keys[j] = key;
+  vals[j] = (uint32_t)j;
+  rows[j] = row;
+}
+
+// the rows in sorted (slot, row) order, one double per thread (coalesced)
+__global__ void k_smap_gather(int64_t n, const uint32_t* __restrict__ vals, const double* __restrict__ rows,
+                              double* srows) {
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n * kSmapRow) return;
+  const int64_t i = e / kSmapRow, q = e % kSmapRow;
+  srows[e] = rows[(int64_t)vals[i] * kSmapRow + q];
+}
+
+// one thread per run of the sorted keys: slot += its row sum (the fuse's read-modify-write)
+__global__ void k_smap_apply(ScanMapArgs A, const uint32_t* __restrict__ unique, const SmapRow* __restrict__ agg,
+                             const uint32_t* __restrict__ n_runs, unsigned long long* n_unique) {
+#pragma clang fp contract(off)
+  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= (int64_t)*n_runs) return;
+  const uint32_t key = unique[u];
+  if ((int64_t)key >= A.map.m_slots) return;  // the dropped rows' run
+  const int64_t s = key;
+  const int L = A.map.n_lobes;
+  const SmapRow d = agg[u];
+  for (int q = 0; q < 9; ++q) A.map.Lambdas[9 * s + q] = A.map.Lambdas[9 * s + q] + d.v[q];
+  for (int q = 0; q < 3; ++q) A.map.thetas[3 * s + q] = A.map.thetas[3 * s + q] + d.v[9 + q];
+  // lobes > 0 receive 0.0 per row: x + 0.0 (as the fuse writes them)
+  for (int q = 0; q < 3 * L; ++q)
+    A.map.etas[(int64_t)3 * L * s + q] = A.map.etas[(int64_t)3 * L * s + q] + (q < 3 ? d.v[12 + q] : 0.0);
+  A.map.weights[s] = A.map.weights[s] + d.v[15];
   A.map.timestamps[s] = A.timestamp;
   A.map.last_supported_scan_seq[s] = A.scan_seq;
   A.map.last_update_scan_seq[s] = A.scan_seq;
-  if (A.map.lidar_mass) A.map.lidar_mass[s] = mlid + dlid;
+  if (A.map.lidar_mass) A.map.lidar_mass[s] = A.map.lidar_mass[s] + d.v[15];
   atomicAdd(n_unique, 1ull);  // integer count: order-independent
 }
 
@@ -190,15 +198,19 @@ inline int key_bits(int64_t M) {
 int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_slots) {
   W->n_cap = n_cap;
   W->bits = key_bits(m_slots);
-  size_t temp = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const uint32_t*)nullptr, (uint32_t*)nullptr,
+  size_t t_sort = 0, t_red = 0;
+  if (hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                          (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n_cap, 0, W->bits,
-                                         ctx->stream) != hipSuccess) {
-    set_error(ctx, "radix sort sizing failed");
+                                         ctx->stream) != hipSuccess ||
+      rocprim::deterministic_reduce_by_key(nullptr, t_red, (const uint32_t*)nullptr, (const SmapRow*)nullptr,
+                                           (size_t)n_cap, (uint32_t*)nullptr, (SmapRow*)nullptr, (uint32_t*)nullptr,
+                                           SmapRowSum(), rocprim::equal_to<uint32_t>(), ctx->stream) != hipSuccess) {
+    set_error(ctx, "sort / reduce-by-key sizing failed");
     return GC_ERR_RUNTIME;
   }
-  const size_t kv = ((size_t)n_cap * sizeof(uint32_t) + 255) / 256 * 256;
-  const size_t bytes = 4 * kv + 256 + temp;
+  auto up = [](size_t b) { return (b + 255) / 256 * 256; };
+  const size_t kv = up((size_t)n_cap * sizeof(uint32_t)), rv = up((size_t)n_cap * sizeof(SmapRow));
+  const size_t bytes = 5 * kv + 3 * rv + 512 + up(t_sort) + up(t_red);
   if (bytes > W->bytes) {
     if (W->buf) GC_HIP(ctx, hipFree(W->buf));
     W->buf = nullptr;
@@ -211,9 +223,16 @@ int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_s
   W->vals_in = (uint32_t*)(base + kv);
   W->keys = (uint32_t*)(base + 2 * kv);
   W->vals = (uint32_t*)(base + 3 * kv);
-  W->count = (unsigned long long*)(base + 4 * kv);
-  W->temp = base + 4 * kv + 256;
-  W->temp_bytes = temp;
+  W->unique = (uint32_t*)(base + 4 * kv);
+  W->rows = (double*)(base + 5 * kv);
+  W->srows = (double*)(base + 5 * kv + rv);
+  W->agg = (double*)(base + 5 * kv + 2 * rv);
+  W->count = (unsigned long long*)(base + 5 * kv + 3 * rv);
+  W->n_runs = (uint32_t*)(base + 5 * kv + 3 * rv + 256);
+  W->temp = base + 5 * kv + 3 * rv + 512;
+  W->temp_bytes = up(t_sort);
+  W->temp2 = (char*)W->temp + up(t_sort);
+  W->temp2_bytes = up(t_red);
   return GC_OK;
 }
 
@@ -229,18 +248,28 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
   A.o0 = P.o0; A.o1 = P.o1; A.o2 = P.o2;
   A.voxel = in.voxel; A.timestamp = in.timestamp; A.eps_mass = P.eps_mass;
   A.scan_seq = in.scan_seq;
-  const unsigned grid = (unsigned)((P.n_cap + 255) / 256);
+  const int64_t n = P.n_cap;
+  const unsigned grid = (unsigned)((n + 255) / 256);
   GC_HIP(ctx, hipMemsetAsync(W->count, 0, sizeof(unsigned long long), st));
-  hipLaunchKernelGGL(k_smap_keys, dim3(grid), dim3(256), 0, st, A, W->keys_in, W->vals_in);
+  hipLaunchKernelGGL(k_smap_rows, dim3(grid), dim3(256), 0, st, A, W->keys_in, W->vals_in, (SmapRow*)W->rows);
   GC_LAUNCH_CHECK(ctx);
-  size_t temp = W->temp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(W->temp, temp, W->keys_in, W->keys, W->vals_in, W->vals, (int)P.n_cap, 0,
-                                         W->bits, st) != hipSuccess) {
+  size_t t1 = W->temp_bytes, t2 = W->temp2_bytes;
+  if (hipcub::DeviceRadixSort::SortPairs(W->temp, t1, W->keys_in, W->keys, W->vals_in, W->vals, (int)n, 0, W->bits,
+                                         st) != hipSuccess) {
     set_error(ctx, "radix sort failed");
     return GC_ERR_RUNTIME;
   }
-  hipLaunchKernelGGL(k_smap_segments, dim3(grid), dim3(256), 0, st, A, (const uint32_t*)W->keys,
-                     (const uint32_t*)W->vals, W->count);
+  hipLaunchKernelGGL(k_smap_gather, dim3((unsigned)((n * kSmapRow + 255) / 256)), dim3(256), 0, st, n,
+                     (const uint32_t*)W->vals, (const double*)W->rows, W->srows);
+  GC_LAUNCH_CHECK(ctx);
+  if (rocprim::deterministic_reduce_by_key(W->temp2, t2, (const uint32_t*)W->keys, (const SmapRow*)W->srows,
+                                           (size_t)n, W->unique, (SmapRow*)W->agg, W->n_runs, SmapRowSum(),
+                                           rocprim::equal_to<uint32_t>(), st) != hipSuccess) {
+    set_error(ctx, "reduce-by-key failed");
+    return GC_ERR_RUNTIME;
+  }
+  hipLaunchKernelGGL(k_smap_apply, dim3(grid), dim3(256), 0, st, A, (const uint32_t*)W->unique,
+                     (const SmapRow*)W->agg, (const uint32_t*)W->n_runs, W->count);
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
 }

@@ -6,7 +6,17 @@ import csv
 import glob
 import json
 import os
+import re
 import sys
+
+
+def kname(full):
+    """k_* kernel name (anonymous namespaces included), or the rocprim kernel's short name."""
+    m = re.search(r"(k_\w+)", full)
+    if m:
+        return m.group(1)
+    m = re.search(r"(\w*(?:sort|Sort|onesweep|histogram|scan)\w*)", full)
+    return ("rocprim:" + m.group(1)) if m else full[:60]
 
 src, dst = sys.argv[1], sys.argv[2]
 out = {}
@@ -14,16 +24,16 @@ for leg in ("map-only", "c5-only"):
     acc = collections.defaultdict(lambda: collections.defaultdict(list))
     for f in glob.glob(os.path.join(src, leg, "**", "*counter_collection.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            k = kname(r["Kernel_Name"])
             acc[k][r["Counter_Name"]].append(float(r["Counter_Value"]))
     dur = collections.defaultdict(list)
     for f in glob.glob(os.path.join(src, leg, "kt", "**", "*kernel_trace.csv"), recursive=True):
         for r in csv.DictReader(open(f)):
-            k = r["Kernel_Name"].split("(")[0].replace("void ", "")
+            k = kname(r["Kernel_Name"])
             dur[k].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     per = {}
     for k, cs in acc.items():
-        if not any(t in k for t in ("fuse", "smap", "Radix", "radix", "Onesweep", "onesweep")):
+        if not (k.startswith("k_fuse") or k.startswith("k_smap") or k.startswith("rocprim:")):
             continue
         m = {c: sum(v) / len(v) for c, v in cs.items()}
         rd, wr = 2.0 * m.get("FETCH_SIZE", 0.0) * 1024, m.get("WRITE_SIZE", 0.0) * 1024
