@@ -9,18 +9,17 @@ struct gc_ctx;
 
 namespace gc {
 
-// device work buffers of one pipeline's update: keys / row indices in and sorted, the rows, the run
-// keys and sums, the touched-slot counter and the sort / reduce temporaries (sized for n_cap rows
+// device work buffers of one pipeline's update: keys / row indices in and sorted, the rows, the
+// run-piece sums, the touched-slot counter and the sort's temporary storage (sized for n_cap rows
 // and the map's key width)
 struct ScanMapWork {
   void* buf = nullptr;
   size_t bytes = 0;
-  uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys = nullptr, *vals = nullptr, *unique = nullptr;
-  uint32_t* n_runs = nullptr;
-  double *rows = nullptr, *srows = nullptr, *agg = nullptr;  // (n_cap, 16) rows, in sorted order, run sums
+  uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys = nullptr, *vals = nullptr;
+  double *rows = nullptr, *pieces = nullptr;  // (n_cap, 16) rows by row index; run-piece sums by sorted index
   unsigned long long* count = nullptr;
-  void *temp = nullptr, *temp2 = nullptr;  // radix sort / reduce-by-key temporary storage
-  size_t temp_bytes = 0, temp2_bytes = 0;
+  void* temp = nullptr;  // radix sort temporary storage
+  size_t temp_bytes = 0;
   int64_t n_cap = 0;
   int bits = 0;
 };

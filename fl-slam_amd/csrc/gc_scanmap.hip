@@ -13,9 +13,9 @@
 // with Σ_lidar the measurement-IW LiDAR block's mode Ψ_2 / (ν_2 + 4) and the row's weight the
 // deskewed point weight (a4). Its slot is the spatial hash of the world voxel of μ_w. The rows are
 // fused with responsibility 1 and source LiDAR by a reduce-by-key: a stable radix sort of (slot,
-// row), the rows gathered into that order, rocprim's deterministic reduce_by_key (a fixed
-// association per run, so bit-reproducible run to run; within 1e-12 of np.add.at's sequential
-// order) and one thread per distinct slot applying its sum. A scan's points crowd into few voxels
+// row) and a two-pass segmented reduction in a fixed order (k_smap_pieces / k_smap_apply:
+// bit-reproducible, within 1e-12 of np.add.at's sequential order), one thread per distinct slot
+// applying its sum. A scan's points crowd into few voxels
 // (~65k rows into ~5k slots, runs of thousands near the sensor), so rows are computed one per
 // thread and the runs reduced in parallel: one thread per run summing its rows serially took
 // ~1 ms per scan. LiDAR rows leave the camera accumulators unchanged,
@@ -25,7 +25,6 @@
 // Every rank runs the update from the reduced record, so the maps stay bit-identical across ranks.
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
-#include <rocprim/device/device_reduce_by_key.hpp>
 #include "gc_internal.h"
 #include "gc_math.h"
 #include "gc_pipe.h"
@@ -49,14 +48,6 @@ struct ScanMapArgs {
 constexpr int kSmapRow = 16;  // [Λ_w 9, θ_w 3, η_w lobe 0 3, w]
 struct SmapRow {
   double v[kSmapRow];
-};
-struct SmapRowSum {
-  __host__ __device__ SmapRow operator()(const SmapRow& a, const SmapRow& b) const {
-    SmapRow c;
-#pragma unroll
-    for (int q = 0; q < kSmapRow; ++q) c.v[q] = a.v[q] + b.v[q];
-    return c;
-  }
 };
 
 // the row's deskewed body point and weight (false: padding or zero weight -> dropped)
@@ -89,64 +80,88 @@ GC_DEV void smap_pose(const ScanMapArgs& A, double* R, double* tt) {
   tt[0] = A.h0[0]; tt[1] = A.h0[1]; tt[2] = 0.0;  // planar map: t_z = 0 (CHANGELOG.md:575-578)
 }
 
-// One world row (the comment at the top): Λ_w (9), θ_w (3), η_w lobe 0 (3).
-GC_DEV void smap_row(const ScanMapArgs& A, const double* R, const double* tt, const double* Sl, const double* p0,
-                     double* Lw, double* th, double* e0) {
-  double mw[3];
-  smap_world_mean(R, tt, p0, mw);
-  // Σ_w = R Σ_l Rᵀ + J Σ_pose Jᵀ, J = [R | −R K], K = [p0]×
-  double M3[9], Sw[9];
-  mat3_mul(R, Sl, M3);
-  mat3_mul_nt(M3, R, Sw);
-  const double K[9] = {0.0, -p0[2], p0[1], p0[2], 0.0, -p0[0], -p0[1], p0[0], 0.0};
-  double RK[9], J[18];
-  mat3_mul(R, K, RK);
+// One world row (the comment at the top), in the body frame first: with K = [p]× and the pose
+// covariance blocks A = [[A_tt, A_tr], [A_rt, A_rr]], J Σ_pose Jᵀ = R M Rᵀ with
+// M = A_tt + A_tr K − K A_rt − K A_rr K (J = R [I | −K], Kᵀ = −K), so Σ_w = R (Σ_lidar + M) Rᵀ,
+// Λ_w = R (Σ_lidar + M)⁻¹ Rᵀ and θ_w = Λ_w μ_w = R (Σ_lidar + M)⁻¹ (p + Rᵀ t): one symmetric 3x3
+// inverse and sparse skew products instead of the 3x6 Jacobian algebra. C: [R 9, Rᵀt 3, Σ_lidar 9,
+// A 36] of the scan (LDS). Writes Λ_w (9), θ_w (3), η_w lobe 0 (3).
+constexpr int kSmapC = 57;
+GC_DEV void smap_row(const double* C, const double* o, double eps_mass, const double* p, double* Lw, double* th,
+                     double* e0) {
+  const double* R = C;
+  const double* Rtt = C + 9;
+  const double* Sl = C + 12;
+  const double* A = C + 21;  // 6 x 6 row-major
+  const double K[9] = {0.0, -p[2], p[1], p[2], 0.0, -p[0], -p[1], p[0], 0.0};
+  double X[9], Y[9], Sb[9];
+  // X = A_tr K, Y = K A_rt, then K A_rr K
   for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) { J[i * 6 + j] = R[3 * i + j]; J[i * 6 + 3 + j] = -RK[3 * i + j]; }
-  const double* Sp = A.h0 + 6;
-  double JS[18];  // J Σ_pose (3 x 6)
-  for (int i = 0; i < 3; ++i)
-    for (int c = 0; c < 6; ++c) {
-      double v = 0.0;
-      for (int a = 0; a < 6; ++a) v += J[i * 6 + a] * Sp[a * 6 + c];
-      JS[i * 6 + c] = v;
+    for (int j = 0; j < 3; ++j) {
+      double x = 0.0, y = 0.0;
+      for (int k = 0; k < 3; ++k) {
+        x += A[i * 6 + 3 + k] * K[3 * k + j];
+        y += K[3 * i + k] * A[(3 + k) * 6 + j];
+      }
+      X[3 * i + j] = x;
+      Y[3 * i + j] = y;
     }
+  double KA[9];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) {
       double v = 0.0;
-      for (int c = 0; c < 6; ++c) v += JS[i * 6 + c] * J[j * 6 + c];
-      Sw[3 * i + j] += v;
+      for (int k = 0; k < 3; ++k) v += K[3 * i + k] * A[(3 + k) * 6 + 3 + j];
+      KA[3 * i + j] = v;
+    }
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) {
+      double kak = 0.0;
+      for (int k = 0; k < 3; ++k) kak += KA[3 * i + k] * K[3 * k + j];
+      Sb[3 * i + j] = Sl[3 * i + j] + A[i * 6 + j] + X[3 * i + j] - Y[3 * i + j] - kak;
     }
   for (int i = 0; i < 3; ++i)  // symmetric by construction up to rounding: symmetrise before inverting
     for (int j = i + 1; j < 3; ++j) {
-      const double v = 0.5 * (Sw[3 * i + j] + Sw[3 * j + i]);
-      Sw[3 * i + j] = v;
-      Sw[3 * j + i] = v;
+      const double v = 0.5 * (Sb[3 * i + j] + Sb[3 * j + i]);
+      Sb[3 * i + j] = v;
+      Sb[3 * j + i] = v;
     }
-  inv3(Sw, Lw);
-  mat3_vec(Lw, mw, th);
-  const double o[3] = {A.o0, A.o1, A.o2};
+  double Ib[9], T[9];
+  inv3(Sb, Ib);
+  mat3_mul(R, Ib, T);
+  mat3_mul_nt(T, R, Lw);
+  const double q[3] = {p[0] + Rtt[0], p[1] + Rtt[1], p[2] + Rtt[2]};
+  mat3_vec(T, q, th);
   double d[3];
-  direction(p0, o, A.eps_mass, d);
+  direction(p, o, eps_mass, d);
   mat3_vec(R, d, e0);
 }
 
 // one thread per row: its slot key (m_slots for a dropped row, sorted after every slot) and its
 // world row [Λ_w 9, θ_w 3, η_w lobe 0 3, w] (zeros when dropped)
 __global__ void k_smap_rows(ScanMapArgs A, uint32_t* keys, uint32_t* vals, SmapRow* rows) {
+  __shared__ double C[kSmapC + 3];
+  if (threadIdx.x == 0) {  // the scan's constants: R, tt, Rᵀ t, Σ_lidar, Σ_pose
+    double R[9], tt[3];
+    smap_pose(A, R, tt);
+    for (int q = 0; q < 9; ++q) C[q] = R[q];
+    mat3_tvec(R, tt, C + 9);
+    const double den = A.nu_meas[2] + 3.0 + 1.0;  // measurement_noise_mean_jax, LiDAR block
+    for (int q = 0; q < 9; ++q) C[12 + q] = A.Psi_meas[18 + q] / den;
+    for (int q = 0; q < 36; ++q) C[21 + q] = A.h0[6 + q];
+    for (int q = 0; q < 3; ++q) C[kSmapC + q] = tt[q];
+  }
+  __syncthreads();
   const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= A.n_cap) return;
-  double R[9], tt[3], p0[3], w, mw[3], Sl[9];
-  smap_pose(A, R, tt);
+  double p0[3], w, mw[3];
   SmapRow row;
   for (int q = 0; q < kSmapRow; ++q) row.v[q] = 0.0;
   uint32_t key = (uint32_t)A.map.m_slots;
   if (smap_point(A, j, p0, &w)) {
-    smap_world_mean(R, tt, p0, mw);
+    smap_world_mean(C, C + kSmapC, p0, mw);
     key = smap_slot(mw, A.voxel, A.map.m_slots);
-    const double den = A.nu_meas[2] + 3.0 + 1.0;  // measurement_noise_mean_jax, LiDAR block
-    for (int q = 0; q < 9; ++q) Sl[q] = A.Psi_meas[18 + q] / den;
-    smap_row(A, R, tt, Sl, p0, row.v, row.v + 9, row.v + 12);
+    const double o[3] = {A.o0, A.o1, A.o2};
+    smap_row(C, o, A.eps_mass, p0, row.v, row.v + 9, row.v + 12);
     row.v[15] = w;
   }
   keys[j] = key;
@@ -154,26 +169,66 @@ __global__ void k_smap_rows(ScanMapArgs A, uint32_t* keys, uint32_t* vals, SmapR
   rows[j] = row;
 }
 
-// the rows in sorted (slot, row) order, one double per thread (coalesced)
-__global__ void k_smap_gather(int64_t n, const uint32_t* __restrict__ vals, const double* __restrict__ rows,
-                              double* srows) {
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n * kSmapRow) return;
-  const int64_t i = e / kSmapRow, q = e % kSmapRow;
-  srows[e] = rows[(int64_t)vals[i] * kSmapRow + q];
+// Runs of the sorted keys summed in a fixed order, in two passes. Pass 1: one workgroup per 256
+// sorted rows gathers them into LDS and runs a segmented inclusive scan (Hillis-Steele, a step
+// adds the entry d back when it has the same key: sorted keys make that the same run); the last
+// entry of each run piece in the block writes the piece's sum. Pass 2: one thread per run head
+// adds its pieces block by block in ascending order and applies the total to the slot. The order
+// depends on the row positions only: bit-reproducible.
+constexpr int kSmapBlk = 256;
+__global__ void __launch_bounds__(kSmapBlk) k_smap_pieces(int64_t n, const uint32_t* __restrict__ keys,
+                                                          const uint32_t* __restrict__ vals,
+                                                          const SmapRow* __restrict__ rows, SmapRow* pieces) {
+  __shared__ double v[kSmapRow][kSmapBlk];
+  __shared__ uint32_t k[kSmapBlk];
+  const int t = threadIdx.x;
+  const int64_t i = (int64_t)blockIdx.x * kSmapBlk + t;
+  const bool in = i < n;
+  k[t] = in ? keys[i] : 0xFFFFFFFFu;
+  SmapRow r;
+  if (in) r = rows[vals[i]];
+  else
+    for (int q = 0; q < kSmapRow; ++q) r.v[q] = 0.0;
+  for (int q = 0; q < kSmapRow; ++q) v[q][t] = r.v[q];
+  __syncthreads();
+  for (int d = 1; d < kSmapBlk; d <<= 1) {
+    const bool take = t >= d && k[t - d] == k[t];
+    double a[kSmapRow];
+    for (int q = 0; q < kSmapRow; ++q) a[q] = take ? v[q][t - d] : 0.0;
+    __syncthreads();
+    if (take)
+      for (int q = 0; q < kSmapRow; ++q) v[q][t] = a[q] + v[q][t];
+    __syncthreads();
+  }
+  if (in && (t == kSmapBlk - 1 || i == n - 1 || k[t + 1] != k[t])) {
+    SmapRow o;
+    for (int q = 0; q < kSmapRow; ++q) o.v[q] = v[q][t];
+    pieces[i] = o;
+  }
 }
 
-// one thread per run of the sorted keys: slot += its row sum (the fuse's read-modify-write)
-__global__ void k_smap_apply(ScanMapArgs A, const uint32_t* __restrict__ unique, const SmapRow* __restrict__ agg,
-                             const uint32_t* __restrict__ n_runs, unsigned long long* n_unique) {
+// one thread per run tail: the run's pieces are at the ends of the blocks it covers and at the tail
+// itself; the head's block is found by stepping back over block boundaries (one load per block of
+// the run), then the pieces are added in ascending block order and the total applied to the slot
+// (the fuse's read-modify-write)
+__global__ void k_smap_apply(ScanMapArgs A, int64_t n, const uint32_t* __restrict__ keys,
+                             const SmapRow* __restrict__ pieces, unsigned long long* n_unique) {
 #pragma clang fp contract(off)
-  const int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= (int64_t)*n_runs) return;
-  const uint32_t key = unique[u];
-  if ((int64_t)key >= A.map.m_slots) return;  // the dropped rows' run
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const uint32_t key = keys[e];
+  if ((int64_t)key >= A.map.m_slots || (e + 1 < n && keys[e + 1] == key)) return;  // dropped / not a run tail
+  const int64_t bt = e / kSmapBlk;
+  int64_t bh = bt;
+  while (bh > 0 && keys[bh * kSmapBlk - 1] == key) --bh;
+  SmapRow d;
+  for (int q = 0; q < kSmapRow; ++q) d.v[q] = 0.0;
+  for (int64_t b = bh; b <= bt; ++b) {
+    const SmapRow p = pieces[b < bt ? (b + 1) * kSmapBlk - 1 : e];
+    for (int q = 0; q < kSmapRow; ++q) d.v[q] = d.v[q] + p.v[q];
+  }
   const int64_t s = key;
   const int L = A.map.n_lobes;
-  const SmapRow d = agg[u];
   for (int q = 0; q < 9; ++q) A.map.Lambdas[9 * s + q] = A.map.Lambdas[9 * s + q] + d.v[q];
   for (int q = 0; q < 3; ++q) A.map.thetas[3 * s + q] = A.map.thetas[3 * s + q] + d.v[9 + q];
   // lobes > 0 receive 0.0 per row: x + 0.0 (as the fuse writes them)
@@ -198,19 +253,16 @@ inline int key_bits(int64_t M) {
 int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_slots) {
   W->n_cap = n_cap;
   W->bits = key_bits(m_slots);
-  size_t t_sort = 0, t_red = 0;
+  size_t t_sort = 0;
   if (hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, (const uint32_t*)nullptr, (uint32_t*)nullptr,
                                          (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n_cap, 0, W->bits,
-                                         ctx->stream) != hipSuccess ||
-      rocprim::deterministic_reduce_by_key(nullptr, t_red, (const uint32_t*)nullptr, (const SmapRow*)nullptr,
-                                           (size_t)n_cap, (uint32_t*)nullptr, (SmapRow*)nullptr, (uint32_t*)nullptr,
-                                           SmapRowSum(), rocprim::equal_to<uint32_t>(), ctx->stream) != hipSuccess) {
-    set_error(ctx, "sort / reduce-by-key sizing failed");
+                                         ctx->stream) != hipSuccess) {
+    set_error(ctx, "radix sort sizing failed");
     return GC_ERR_RUNTIME;
   }
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t kv = up((size_t)n_cap * sizeof(uint32_t)), rv = up((size_t)n_cap * sizeof(SmapRow));
-  const size_t bytes = 5 * kv + 3 * rv + 512 + up(t_sort) + up(t_red);
+  const size_t bytes = 4 * kv + 2 * rv + 256 + up(t_sort);
   if (bytes > W->bytes) {
     if (W->buf) GC_HIP(ctx, hipFree(W->buf));
     W->buf = nullptr;
@@ -223,16 +275,11 @@ int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_s
   W->vals_in = (uint32_t*)(base + kv);
   W->keys = (uint32_t*)(base + 2 * kv);
   W->vals = (uint32_t*)(base + 3 * kv);
-  W->unique = (uint32_t*)(base + 4 * kv);
-  W->rows = (double*)(base + 5 * kv);
-  W->srows = (double*)(base + 5 * kv + rv);
-  W->agg = (double*)(base + 5 * kv + 2 * rv);
-  W->count = (unsigned long long*)(base + 5 * kv + 3 * rv);
-  W->n_runs = (uint32_t*)(base + 5 * kv + 3 * rv + 256);
-  W->temp = base + 5 * kv + 3 * rv + 512;
+  W->rows = (double*)(base + 4 * kv);
+  W->pieces = (double*)(base + 4 * kv + rv);
+  W->count = (unsigned long long*)(base + 4 * kv + 2 * rv);
+  W->temp = base + 4 * kv + 2 * rv + 256;
   W->temp_bytes = up(t_sort);
-  W->temp2 = (char*)W->temp + up(t_sort);
-  W->temp2_bytes = up(t_red);
   return GC_OK;
 }
 
@@ -253,23 +300,18 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
   GC_HIP(ctx, hipMemsetAsync(W->count, 0, sizeof(unsigned long long), st));
   hipLaunchKernelGGL(k_smap_rows, dim3(grid), dim3(256), 0, st, A, W->keys_in, W->vals_in, (SmapRow*)W->rows);
   GC_LAUNCH_CHECK(ctx);
-  size_t t1 = W->temp_bytes, t2 = W->temp2_bytes;
+  size_t t1 = W->temp_bytes;
   if (hipcub::DeviceRadixSort::SortPairs(W->temp, t1, W->keys_in, W->keys, W->vals_in, W->vals, (int)n, 0, W->bits,
                                          st) != hipSuccess) {
     set_error(ctx, "radix sort failed");
     return GC_ERR_RUNTIME;
   }
-  hipLaunchKernelGGL(k_smap_gather, dim3((unsigned)((n * kSmapRow + 255) / 256)), dim3(256), 0, st, n,
-                     (const uint32_t*)W->vals, (const double*)W->rows, W->srows);
+  hipLaunchKernelGGL(k_smap_pieces, dim3((unsigned)((n + kSmapBlk - 1) / kSmapBlk)), dim3(kSmapBlk), 0, st, n,
+                     (const uint32_t*)W->keys, (const uint32_t*)W->vals, (const SmapRow*)W->rows,
+                     (SmapRow*)W->pieces);
   GC_LAUNCH_CHECK(ctx);
-  if (rocprim::deterministic_reduce_by_key(W->temp2, t2, (const uint32_t*)W->keys, (const SmapRow*)W->srows,
-                                           (size_t)n, W->unique, (SmapRow*)W->agg, W->n_runs, SmapRowSum(),
-                                           rocprim::equal_to<uint32_t>(), st) != hipSuccess) {
-    set_error(ctx, "reduce-by-key failed");
-    return GC_ERR_RUNTIME;
-  }
-  hipLaunchKernelGGL(k_smap_apply, dim3(grid), dim3(256), 0, st, A, (const uint32_t*)W->unique,
-                     (const SmapRow*)W->agg, (const uint32_t*)W->n_runs, W->count);
+  hipLaunchKernelGGL(k_smap_apply, dim3(grid), dim3(256), 0, st, A, n, (const uint32_t*)W->keys,
+                     (const SmapRow*)W->pieces, W->count);
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
 }

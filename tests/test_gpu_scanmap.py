@@ -7,7 +7,8 @@ voxel. The oracle rebuilds the rows from the raw scan and the pose block the GPU
 (gc_pipeline_get_scan_map_pose), fuses them with its np.add.at restatement of primitive_map_fuse
 and must agree: slot keys, touched-slot count, timestamps, scan sequences, camera mass and colours
 exactly; Λ, θ, η, w and LiDAR mass within 1e-12 of each field's largest entry (the rows' 3x3
-inverse and products round differently in NumPy). The pose block itself is the pipeline's own
+inverse and products round differently in NumPy, and the device sums each slot's rows in a fixed
+tree order where np.add.at adds them one by one). The pose block itself is the pipeline's own
 hypothesis-0 result (ξ and Σ_post bit-identical to the per-hypothesis getters), which the config
 tests compare with the oracle at the north-star bars.
 """
