@@ -6,7 +6,9 @@ process_scan_single_hypothesis (backend/pipeline.py:1527-1570), RuntimeManifest
 The tape fields come from the batched pipeline's device diagnostics of one hypothesis (hyp_diag,
 lpose6, bin cert); the file formats (JSONL, npz) match the reference's so its tools read them.
 Every field of the reference tape is filled (TAPE_NOT_COMPUTED is empty); the certificate-summary
-fields follow the static cert list of the bin-path wiring (BIN_PATH_CERTS)."""
+fields follow the static cert list of the bin-path wiring (BIN_PATH_CERTS), a reconstruction: the
+two fields it determines are listed in TAPE_DERIVED_FROM_RESTATEMENT (derived, not computed; parity
+unpinned)."""
 
 from __future__ import annotations
 
@@ -101,6 +103,12 @@ _NPZ_NAME = dict(scan_number="scan_numbers", timestamp="timestamps", dt_sec="dt_
 
 # reference tape fields the device pipeline does not evaluate (defaults kept): none
 TAPE_NOT_COMPUTED = ()
+# tape fields DERIVED from the bin-path restatement rather than computed by the device: the
+# reference's pipeline.py no longer wires the legacy bin operators into all_certs, so the
+# certificate list below is the build's reconstruction of that wiring. cert_n_triggers is then a
+# constant of the list and mismatch_directional_score depends only on the device's vMF R̄ (parity
+# unpinned: the reference holds no value for either).
+TAPE_DERIVED_FROM_RESTATEMENT = ("cert_n_triggers", "mismatch_directional_score")
 
 # The per-hypothesis certificate list of the bin-path wiring, in pipeline.py's all_certs order
 # (:379-1502 with the legacy bin operators in the map-branch slot): (operator, approximation trigger
