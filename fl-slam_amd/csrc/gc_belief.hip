@@ -117,23 +117,22 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
     if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
   }
   __syncthreads();
-  // --- a2 predict (predict.py:43-98): L_pred -> W1, h_pred, mu_prev, cert
+  // --- a2 predict (predict.py:43-98): L_pred -> W1, h_pred, mu_prev, cert; and chol(L_pred + εI)
+  // -> W4 for the predicted moments (pipeline.py:436-453), factored on wave 1 beside L_pred's PSD
+  // certificate on wave 0, with pose0 = world pose of belief_prev on wave 3 (one lane; read after
+  // the barrier)
+  const auto pose0_side = [&]() {
+    if (t == 192) compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);
+  };
   wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,
              P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2, false,
-             S.sig_cached ? P.Sig + (int64_t)h * N2 : nullptr, S.sig_cached ? P.mu_fin + (int64_t)h * n : nullptr);
+             S.sig_cached ? P.Sig + (int64_t)h * N2 : nullptr, S.sig_cached ? P.mu_fin + (int64_t)h * n : nullptr,
+             W4, pose0_side);
   GC_PHASE(P, 1);
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + t] = mu_prev[t];
   for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
   if (t < n) P.hpred[(int64_t)h * n + t] = hpred[t];
-  // --- predicted moments: Σ_pred[15,15] and mu_inc (pipeline.py:436-453) from chol(L_pred+εI)
-  for (int i = t; i < N2; i += kWG) W4[i] = W1[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
-  __syncthreads();
   GC_PHASE(P, 2);
-  // the factorisation on wave 0 (wg_chol's body) and, beside it on wave 1, pose0 = world pose of
-  // belief_prev (one lane; read after the barrier)
-  if (t < 64) (void)wave0_chol<kDZ, false>(W4, n);
-  else if (t == 64) compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);
-  __syncthreads();
   GC_PHASE(P, 3);
   // μ_inc on wave 0; beside it, one lane each of waves 1 and 2: σ_warp from (L_pred+εI)⁻¹[15,15]
   // and R0 = Exp(rotvec of pose0) (pose0 from phase 1)

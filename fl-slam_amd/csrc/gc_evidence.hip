@@ -223,14 +223,16 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   if (t < n) hpo[t] = hps[t] + alpha * hev[t];
   __syncthreads();
   {
-    // the pose-6 conditioning of L_ev (P6 = W3, untouched by the projection) on wave 2 when α did not need it
+    // the PSD projection of the fusion (Cholesky-certified) on wave 0 and, at the same time on wave 1,
+    // the factorization of L_post + εI the recompose and the solves below need (Wc); the pose-6
+    // conditioning of L_ev (P6 = W3, untouched by the projection) on wave 3 when α did not need it
     const auto cond_side = [&]() {
       if (!alpha_fixed) return;
       double lmin = 0.0, lmax = 0.0;
       wave_extreme_eigvals<6>(W3, lmin, lmax);
-      if (t == 128) sc[60] = pose6_cond(lmin, lmax, P.eps_psd, P.diag + (int64_t)hl * kHypDiag + 39);
+      if ((t & 63) == 0) sc[60] = pose6_cond(lmin, lmax, P.eps_psd, P.diag + (int64_t)hl * kHypDiag + 39);
     };
-    wg_psd_project_fast(W2, Lpo, P.eps_psd, n, Sx, red, c6, cond_side);
+    wg_psd_fast_lifted_chol(W2, Lpo, P.eps_psd, P.eps_lift, n, Sx, Wc, red, c6, cond_side);
   }
   GC_PHASE(P, 15);
   // a12 recompose: T from every operator's trigger magnitude (pipeline.py:1211)
@@ -246,9 +248,6 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     sc[61] = T;
     sc[62] = c6[0];
   }
-  for (int i = t; i < NN; i += kWG) Wc[i] = Lpo[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
-  __syncthreads();
-  wg_chol(Wc, n);
   // δz and the recompose on wave 0 and, beside them on wave 1, the forward substitution of
   // Σ_post = (L_post + εI)⁻¹ (its first phase; Sx is free here)
   if (t < 64) {

@@ -220,11 +220,14 @@ constexpr int kPredCertLen = 8;  // [lift, psd Δ, eig_min, eig_max, cond, nnc, 
 // Scratch: W1..W3 (n x n each), Sx (2 n² + 4 n), red (>= 8), c1/c2 (6 each).
 // full_cert: exact eigen certificate (per-operator entry); otherwise the Cholesky-certified
 // fast projection (pipeline: only the projection delta is consumed, eigen fields NaN).
+// Llift (batched pipeline, fast path): also returns chol(L_pred + ε_lift I) there (n x n; may alias
+// W3), factored beside L_pred's certificate, with side() on wave 3 meanwhile (mu is final by then).
+template <typename Side = NoSideWork>
 GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, double dt, double eps_psd,
                        double eps_lift, double lambda_ou, double* Lout, double* hout, double* mu, double* cert,
                        double* W1, double* W2, double* W3, double* Sx, double* red, double* c1, double* c2,
                        bool full_cert = false, const double* Sig_cached = nullptr,
-                       const double* mu_cached = nullptr) {
+                       const double* mu_cached = nullptr, double* Llift = nullptr, const Side& side = Side()) {
   const int t = threadIdx.x, n = kDZ;
   const double ef = exp(-2.0 * lambda_ou * dt);
   const double dc = (1.0 - ef) / (2.0 * lambda_ou + kF64Eps);
@@ -241,13 +244,23 @@ GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, d
     for (int i = t; i < kNN; i += kWG) W2[i] = ef * W2[i] + dc * Q[i];
     __syncthreads();
   }
-  if (full_cert) wg_psd_project(W2, W3, eps_psd, n, Sx, red, c1);  // Σ'_psd -> W3
-  else wg_psd_project_fast(W2, W3, eps_psd, n, Sx, red, c1);
+  if (full_cert) {
+    wg_psd_project(W2, W3, eps_psd, n, Sx, red, c1);  // Σ'_psd -> W3
+  } else {
+    // Σ'_psd -> W3, certified on wave 0 while wave 1 factors Σ'_psd + εI into W1 (wg_inverse_lifted's
+    // factorization)
+    wg_psd_fast_lifted_chol(W2, W3, eps_psd, eps_lift, n, Sx, W1, red, c1);
+  }
   double trl = (t < n) ? W3[t * n + t] : 0.0;
   const double trace_cov = wg_sum(trl, red);
-  wg_inverse_lifted(W3, W2, eps_lift, n, W1, Lout);      // L' raw -> W2 (Lout as work)
-  if (full_cert) wg_psd_project(W2, Lout, eps_psd, n, Sx, red, c2);
-  else wg_psd_project_fast(W2, Lout, eps_psd, n, Sx, red, c2);
+  if (full_cert) {
+    wg_inverse_lifted(W3, W2, eps_lift, n, W1, Lout);  // L' raw -> W2 (Lout as work)
+    wg_psd_project(W2, Lout, eps_psd, n, Sx, red, c2);
+  } else {
+    wg_chol_inverse(W1, W2, Lout, n);  // L' raw -> W2 (Lout as work)
+    if (Llift) wg_psd_fast_lifted_chol(W2, Lout, eps_psd, eps_lift, n, Sx, Llift, red, c2, side);
+    else wg_psd_project_fast(W2, Lout, eps_psd, n, Sx, red, c2);
+  }
   wg_matvec(Lout, mu, hout, n);
   if (t == 0 && cert) {
     const double lift = 2.0 * eps_lift * n;

@@ -106,12 +106,14 @@ GC_DEV double readlane_f64(double v, int lane) {
 // (or NaN) clears ok and is replaced by 1 so the rest stays finite (wg_chol_checked semantics).
 // The pivot scale is one v_rsq_f64 + a Goldschmidt step (d = √p and 1/d to ~1 ulp) instead of a
 // correctly rounded sqrt and a per-lane division. Column k is broadcast as: L[k+1][k] by
-// readlane (it feeds the next pivot), L[k+2..][k] through a 22-double LDS row (one ds_write per
-// lane, then same-address broadcast reads, no readlane hazard NOPs). Wave 0 only, in program
-// order, so the LDS row needs no barrier.
+// readlane (it feeds the next pivot), L[k+2..][k] through a 22-double LDS row of the calling wave
+// (one ds_write per lane, then same-address broadcast reads, no readlane hazard NOPs). One wave, in
+// program order, so the LDS row needs no barrier.
 template <int NM, bool CHECKED>
 GC_DEV void lane_chol(double (&a)[NM], int lane, bool& ok) {
-  __shared__ __attribute__((aligned(16))) double colbuf[NM + 2];
+  // one broadcast row per wave: two waves may factor two matrices at once
+  __shared__ __attribute__((aligned(16))) double colbufs[4][NM + 2];
+  double* colbuf = colbufs[threadIdx.x >> 6];
 #pragma unroll
   for (int k = 0; k < NM; ++k) {
     double piv = readlane_f64(a[k], k);
@@ -154,7 +156,7 @@ GC_DEV void lane_store_lower(double* A, int n, int lane, const double (&a)[NM]) 
 // the padded identity costs full columns, so small blocks take the short form
 template <int NM, bool CHECKED>
 GC_DEV bool wave0_chol(double* A, int n) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & 63;  // any single wave (wave 0, or wave 1 beside a wave-0 factorization)
   double a[NM];
   lane_load_rows<NM>(A, n, lane, a);
   bool ok = true;
@@ -502,6 +504,63 @@ GC_DEV void wg_psd_project_fast(const double* M, double* Mp, double eps, int n, 
     return;
   }
   wg_psd_project(M, Mp, eps, n, scratch, red, cert6);
+}
+
+// wg_psd_project_fast of M and the lifted factorization of its result, the two Cholesky
+// factorizations at once: wave 0 certifies M_sym − εI (as wg_psd_project_fast), wave 1 factors
+// M_sym + ε_lift I into Cl, which is chol(Mp + ε_lift I) whenever the certificate holds (Mp =
+// M_sym then, the same values the separate calls would factor: bit-identical), wave 2 the symmetry
+// deviation, wave 3 side(). If the certificate fails, the Jacobi projection runs and Cl is
+// refactored from Mp. On return Mp is the projection and Cl its lifted factor (lower, upper zeroed).
+// scratch: 2n*n + 4n doubles; Cl: n*n.
+template <typename Side = NoSideWork>
+GC_DEV void wg_psd_fast_lifted_chol(const double* M, double* Mp, double eps, double eps_lift, int n, double* scratch,
+                                    double* Cl, double* red, double* cert6, const Side& side = Side()) {
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    const double sym = 0.5 * (M[i * n + j] + M[j * n + i]);
+    scratch[idx] = sym - ((i == j) ? eps : 0.0);
+    Cl[idx] = sym + ((i == j) ? eps_lift : 0.0);
+  }
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    const bool okc = n <= 8 ? wave0_chol<8, true>(scratch, n) : wave0_chol<kDZ, true>(scratch, n);
+    if (threadIdx.x == 0) red[4] = okc ? 0.0 : 1.0;
+  } else if (threadIdx.x < 128) {
+    if (n <= 8) (void)wave0_chol<8, false>(Cl, n);
+    else (void)wave0_chol<kDZ, false>(Cl, n);
+  } else if (threadIdx.x < 192) {
+    double symloc = 0.0;
+    for (int idx = threadIdx.x - 128; idx < n * n; idx += 64) {
+      const int i = idx / n, j = idx % n;
+      const double d = 0.5 * (M[i * n + j] + M[j * n + i]) - M[idx];
+      symloc += d * d;
+    }
+    symloc = wave_sum(symloc);
+    if (threadIdx.x == 128) red[5] = symloc;
+  } else {
+    side();
+  }
+  __syncthreads();
+  const bool spd = red[4] == 0.0;
+  const double symd = red[5];
+  __syncthreads();
+  if (spd) {
+    for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
+      const int i = idx / n, j = idx % n;
+      Mp[idx] = 0.5 * (M[i * n + j] + M[j * n + i]);
+    }
+    if (cert6 && threadIdx.x == 0) {
+      const double nan = __builtin_nan("");
+      cert6[0] = 0.0; cert6[1] = sqrt(symd); cert6[2] = nan; cert6[3] = nan; cert6[4] = nan; cert6[5] = nan;
+    }
+    __syncthreads();
+    return;
+  }
+  wg_psd_project(M, Mp, eps, n, scratch, red, cert6);
+  for (int idx = threadIdx.x; idx < n * n; idx += kWG) Cl[idx] = Mp[idx] + ((idx / n == idx % n) ? eps_lift : 0.0);
+  __syncthreads();
+  wg_chol(Cl, n);
 }
 
 GC_DEV void wave_lds_sync() {

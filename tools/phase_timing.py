@@ -1,6 +1,7 @@
 """Dev helper: per-phase cycle counts of hypothesis 0's workgroup in k_predict_imu (slots 0-8) and
-k_evidence (10-19), from a library built with -DGC_PHASE_TIMING (tools/probe/libgcslam_timing.so):
-    make -C fl-slam_amd BUILD=build_timing OUT=../tools/probe/libgcslam_timing.so \
+k_evidence (10-19) and k_combine_final (20-25), from a library built with -DGC_PHASE_TIMING
+(fl-slam_amd/build_var/timing/libgcslam.so, or $GC_TIMING_LIB):
+    make -C fl-slam_amd BUILD=build_timing OUT=build_var/timing/libgcslam.so \
         CXXFLAGS="-O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -I../include -DGC_PHASE_TIMING"
 Runs the bench workload (64k points x 256 hypotheses) with the IMU/odom branch given (GC_IO_GIVEN
 leaves io_parts to the instrumentation)."""
@@ -12,7 +13,7 @@ sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
 sys.path.insert(0, ROOT)
 from gcslam import _abi  # noqa: E402
 
-_abi.LIB_PATH = os.path.join(ROOT, "tools", "probe", "libgcslam_timing.so")
+_abi.LIB_PATH = os.environ.get("GC_TIMING_LIB", os.path.join(ROOT, "fl-slam_amd", "build_var", "timing", "libgcslam.so"))
 import numpy as np  # noqa: E402
 from gcslam.pipeline import BatchedScanPipeline, PipelineConfig, iw_meas_prior, iw_process_prior  # noqa: E402
 from gcslam.synth import make_hypotheses, make_io_evidence, make_scan  # noqa: E402
