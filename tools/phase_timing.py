@@ -26,7 +26,13 @@ n = scans[0]["points"].shape[0]
 pipe = BatchedScanPipeline(H, n, PipelineConfig(n_points_cap=n), ctx=ctx)
 hy = make_hypotheses(H)
 pipe.set_beliefs(hy["X_anchor"], hy["z_lin"], hy["L"], hy["h"], hy["stamp"])
-pipe.set_io_evidence(*make_io_evidence(H))
+# the given evidence without dt / extrinsic information, as the computed branch's (the excitation
+# scales are then 0 and k_evidence takes the bench's path: μ_pred from predict, no extra factorization)
+Lio, hio, cio = make_io_evidence(H)
+Lio[:, 15:, :] = 0.0
+Lio[:, :, 15:] = 0.0
+hio[:, 15:] = 0.0
+pipe.set_io_evidence(Lio, hio, cio)
 pipe.set_iw(*iw_process_prior(), *iw_meas_prior())
 m0 = cases.warmup_map(make_scan(0), n, np.asarray(pipe.cfg.lidar_origin), cases.O.fibonacci_atlas(48))
 pipe.set_map(cases.map_to_record(m0))
