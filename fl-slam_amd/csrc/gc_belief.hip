@@ -111,8 +111,14 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   GC_PHASE(P, 0);
   // this thread's IMU slots, loaded beside the belief (one exposed latency for both) and parked in
   // the preintegration scratch (Bm..V2, 15 doubles per thread, not live before the IMU section)
-  imu_pair_store(load_imu_pair(P.M, S.imu_t, S.imu_g, S.imu_a), Bm + 15 * t);
-  if (!S.sig_cached) {  // with the cached Σ / μ of the previous scan's evidence, L and h are not read
+  if (S.sig_cached) {
+    // the cached Σ / μ of the previous scan's evidence (L and h are not read): e^{-2λdt}Σ + dc Q formed
+    // here in W3 (wg_predict's second work matrix), its loads in flight with the IMU slots'
+    const PredictPrefill pf = predict_prefill_load(P.Sig + (int64_t)h * N2, P.Q, P.mu_fin + (int64_t)h * n);
+    imu_pair_store(load_imu_pair(P.M, S.imu_t, S.imu_g, S.imu_a), Bm + 15 * t);
+    predict_prefill_store(pf, S.dt, P.lambda_ou, W3, mu_prev);
+  } else {
+    imu_pair_store(load_imu_pair(P.M, S.imu_t, S.imu_g, S.imu_a), Bm + 15 * t);
     for (int i = t; i < N2; i += kWG) Lp[i] = P.L[(int64_t)h * N2 + i];
     if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
   }
@@ -126,8 +132,8 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   };
   wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,
              P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2, false,
-             S.sig_cached ? P.Sig + (int64_t)h * N2 : nullptr, S.sig_cached ? P.mu_fin + (int64_t)h * n : nullptr,
-             W4, pose0_side);
+             S.sig_cached ? W3 : nullptr, nullptr,
+             W4, pose0_side, P.io_parts);
   GC_PHASE(P, 1);
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + t] = mu_prev[t];
   for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
@@ -174,7 +180,7 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   double* pre = misc + 32;  // kPreint
   const double kG[3] = {0.0, 0.0, -9.81 * P.gravity_scale};  // GC_GRAVITY_W · imu_gravity_scale
   GC_PHASE(P, 5);
-  wg_preintegrate(M, q, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, pre);
+  wg_preintegrate(M, q, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, pre, P.io_parts);
   GC_PHASE(P, 6);
   const double *ga = q.ga, *gb = q.gb, *aa = q.aa, *ab = q.ab;
   // --- scan-to-scan window: omega_avg and measurement-noise IW statistics

@@ -17,12 +17,19 @@ GC_DEV void compose_exp2(const double* X, const double* d6, double* out) {
   se3_compose(X, e, out);
 }
 
-// Sum a per-bin table [B][W] over bins (fixed order) into out[W] (threads < W).
+// Sum a per-bin table [B][W] (W <= 16) over bins into out[W] on wave 0: lane (q, c) = (lane / 16,
+// lane % 16) sums column c over bins q, q + 4, ... in ascending order, then the four quarters are
+// combined as (q0 + q1) + (q2 + q3) by two xor-shuffles (a fixed order: deterministic).
 GC_DEV void sum_bins(const double* tab, int B, int W, double* out) {
-  if ((int)threadIdx.x < W) {
+  const int t = threadIdx.x;
+  if (t < 64) {
+    const int c = t & 15, q = t >> 4;
     double s = 0.0;
-    for (int b = 0; b < B; ++b) s += tab[b * W + threadIdx.x];
-    out[threadIdx.x] = s;
+    if (c < W)
+      for (int b = q; b < B; b += 4) s += tab[b * W + c];
+    s += __shfl_xor(s, 16);
+    s += __shfl_xor(s, 32);
+    if (t < W) out[t] = s;
   }
   __syncthreads();
 }
@@ -110,7 +117,9 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     so3_exp(P.pose_pred + (int64_t)hl * 6 + 3, sc + 100);
   }
   __syncthreads();
+  GC_PHASE(P, 30);
   sum_bins(tab, B, 10, acc);
+  GC_PHASE(P, 31);
   if (t == 0) mf_finalize(acc, sc + 100, eps, P.eps_psd, mf);
   __syncthreads();
   GC_PHASE(P, 11);
@@ -122,7 +131,9 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     planar_bin_row(mf, s[0], s + 13, s + 16, m[13], md + 4, md + 7, eps, tab + t * 13);
   }
   __syncthreads();
+  GC_PHASE(P, 32);
   sum_bins(tab, B, 13, acc);
+  GC_PHASE(P, 33);
   if (t == 0) planar_finalize(acc, P.map_misc[0], P.pose_pred + (int64_t)hl * 6, eps, P.eps_psd, pt);
   __syncthreads();
   GC_PHASE(P, 12);
@@ -301,6 +312,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
       for (int k = 0; k < 6; ++k) d6[k] = rho * mupo[k];
       compose_exp2(sc + 64, d6, sc + 92);  // X_fin
       sc[98] = rho;
+      GC_STAMP(P.io_parts, 36);
     }
     wave_lds_sync();
     const double rho = sc[98];
@@ -313,6 +325,7 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     }
     wave_lds_sync();
     wave0_chol_solve<kDZ>(Wc, hfin, mufin, n);
+    if (t == 0) GC_STAMP(P.io_parts, 37);
   } else if (t < 128 && P.h_begin + hl == 0) {
     if (t == 64) {
       double zt[6], R[9];
@@ -321,12 +334,14 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
       for (int k = 0; k < 9; ++k) sc[80 + k] = R[k];
       sc[89] = zt[0]; sc[90] = zt[1]; sc[91] = 0.0;  // planar map: t[2] = 0 (CHANGELOG.md:575-578)
       for (int k = 0; k < 6; ++k) P.h0rec[k] = zt[k];
+      GC_STAMP(P.io_parts, 34);
     }
     // hypothesis 0's pose covariance and deskew twist for the in-scan PrimitiveMap update
     if (t - 64 < 36) P.h0rec[6 + (t - 64)] = W2[((t - 64) / 6) * n + (t - 64) % 6];
     else if (t - 64 < 42) P.h0rec[42 + (t - 100)] = P.xi[(int64_t)hl * 6 + (t - 100)];
     wave_lds_sync();
     for (int b = t - 64; b < B; b += 64) pushforward_bin(st + b * 38, sc + 80, sc + 89, W2, n, P.map_inc + b * kMapRec);
+    if (t == 64) GC_STAMP(P.io_parts, 35);
   }
   __syncthreads();
   const double rho = sc[98];

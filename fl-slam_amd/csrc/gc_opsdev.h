@@ -162,6 +162,9 @@ GC_DEV double drift_rho(const double* mu, double* drift_m, double* drift_r) {
 // Push one scan bin into the world frame (build-defined PoseCovInflationPushforward):
 // s_dir → R s, S → R S Rᵀ, N_dir = N_pos = N, sum_p = N p_w, sum_ppT = N (Σ_w + p_w p_wᵀ) with
 // Σ_w = R Σ_p Rᵀ + J Σ_pose Jᵀ, J = [R | −R[p̄]×], p_w = R p̄ + t. Σ_pose: 6x6 (row stride ld).
+// With Σ_pose = [[A, B], [Bᵀ, C]] and K = [p̄]× (Kᵀ = −K), J Σ_pose Jᵀ = R (A + BK + (BK)ᵀ − KCK) Rᵀ:
+// the inflation is added in the body frame and rotated once with Σ_p (the same Σ_w as the oracle's
+// J Σ Jᵀ up to rounding, a third of its products).
 // s: bin stats record (GC_BIN_STATS layout); o: map record (kMapRec).
 GC_DEV void pushforward_bin(const double* s, const double* R, const double* tt, const double* Sp, int ld,
                             double* o) {
@@ -176,24 +179,24 @@ GC_DEV void pushforward_bin(const double* s, const double* R, const double* tt, 
   double pw[3];
   mat3_vec(R, s + 13, pw);
   for (int k = 0; k < 3; ++k) pw[k] += tt[k];
-  mat3_mul(R, s + 16, M3);
-  mat3_mul_nt(M3, R, M4);
   const double* pb = s + 13;
   const double K[9] = {0.0, -pb[2], pb[1], pb[2], 0.0, -pb[0], -pb[1], pb[0], 0.0};
-  double RK[9], J[18];
-  mat3_mul(R, K, RK);
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) { J[i * 6 + j] = R[3 * i + j]; J[i * 6 + 3 + j] = -RK[3 * i + j]; }
+  double A[9], Bm[9], C[9];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) {
-      double v = 0.0;
-      for (int a = 0; a < 6; ++a) {
-        double ja = 0.0;
-        for (int c = 0; c < 6; ++c) ja += Sp[a * ld + c] * J[j * 6 + c];
-        v += J[i * 6 + a] * ja;
-      }
-      M4[3 * i + j] += v;
+      A[3 * i + j] = Sp[i * ld + j];
+      Bm[3 * i + j] = Sp[i * ld + 3 + j];
+      C[3 * i + j] = Sp[(3 + i) * ld + 3 + j];
     }
+  double BK[9], CK[9], KCK[9], Mb[9];
+  mat3_mul(Bm, K, BK);
+  mat3_mul(C, K, CK);
+  mat3_mul(K, CK, KCK);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      Mb[3 * i + j] = s[16 + 3 * i + j] + ((A[3 * i + j] + (BK[3 * i + j] + BK[3 * j + i])) - KCK[3 * i + j]);
+  mat3_mul(R, Mb, M3);
+  mat3_mul_nt(M3, R, M4);
   for (int k = 0; k < 3; ++k) o[14 + k] = N * pw[k];
   for (int i = 0; i < 3; ++i)
     for (int j = 0; j < 3; ++j) o[17 + 3 * i + j] = N * (M4[3 * i + j] + pw[i] * pw[j]);
@@ -222,16 +225,51 @@ constexpr int kPredCertLen = 8;  // [lift, psd Δ, eig_min, eig_max, cond, nnc, 
 // fast projection (pipeline: only the projection delta is consumed, eigen fields NaN).
 // Llift (batched pipeline, fast path): also returns chol(L_pred + ε_lift I) there (n x n; may alias
 // W3), factored beside L_pred's certificate, with side() on wave 3 meanwhile (mu is final by then).
+// The Sig_cached form of wg_predict's first step in two halves, so the caller can put the global loads
+// of Σ, Q and μ in flight beside its own (one exposed latency): predict_prefill_load() then, after the
+// caller's loads, predict_prefill_store() writes W2 and μ (a barrier must follow before wg_predict is
+// called with Sig_cached = W2).
+struct PredictPrefill {
+  double s[2], q[2], m;
+};
+GC_DEV PredictPrefill predict_prefill_load(const double* Sig, const double* Q, const double* mu_cached) {
+  const int t = threadIdx.x;
+  PredictPrefill f;
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int i = t + r * kWG;
+    f.s[r] = i < kNN ? Sig[i] : 0.0;
+    f.q[r] = i < kNN ? Q[i] : 0.0;
+  }
+  f.m = t < kDZ ? mu_cached[t] : 0.0;
+  return f;
+}
+GC_DEV void predict_prefill_store(const PredictPrefill& f, double dt, double lambda_ou, double* W2, double* mu) {
+  const int t = threadIdx.x;
+  const double ef = exp(-2.0 * lambda_ou * dt);
+  const double dc = (1.0 - ef) / (2.0 * lambda_ou + kF64Eps);
+#pragma unroll
+  for (int r = 0; r < 2; ++r) {
+    const int i = t + r * kWG;
+    if (i < kNN) W2[i] = ef * f.s[r] + dc * f.q[r];
+  }
+  if (t < kDZ) mu[t] = f.m;
+}
+
 template <typename Side = NoSideWork>
 GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, double dt, double eps_psd,
                        double eps_lift, double lambda_ou, double* Lout, double* hout, double* mu, double* cert,
                        double* W1, double* W2, double* W3, double* Sx, double* red, double* c1, double* c2,
                        bool full_cert = false, const double* Sig_cached = nullptr,
-                       const double* mu_cached = nullptr, double* Llift = nullptr, const Side& side = Side()) {
+                       const double* mu_cached = nullptr, double* Llift = nullptr, const Side& side = Side(),
+                       double* sink = nullptr) {
   const int t = threadIdx.x, n = kDZ;
+  (void)sink;
   const double ef = exp(-2.0 * lambda_ou * dt);
   const double dc = (1.0 - ef) / (2.0 * lambda_ou + kF64Eps);
-  if (Sig_cached) {
+  if (Sig_cached == W2) {
+    // the caller has already formed W2 = e^{-2λdt} Σ + dc Q and μ (predict_prefill) and synchronised
+  } else if (Sig_cached) {
     // The batched pipeline's evidence kernel already factorised this very (L + εI) with the same
     // routines (Σ_post and μ_fin of the previous scan): bit-identical, so reuse them; Σ and Q
     // arrive in one round trip
@@ -249,8 +287,10 @@ GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, d
   } else {
     // Σ'_psd -> W3, certified on wave 0 while wave 1 factors Σ'_psd + εI into W1 (wg_inverse_lifted's
     // factorization)
+    GC_MARK(sink, 26);
     wg_psd_fast_lifted_chol(W2, W3, eps_psd, eps_lift, n, Sx, W1, red, c1);
   }
+  GC_MARK(sink, 27);
   double trl = (t < n) ? W3[t * n + t] : 0.0;
   const double trace_cov = wg_sum(trl, red);
   if (full_cert) {
@@ -258,9 +298,11 @@ GC_DEV void wg_predict(const double* Lp, const double* hprev, const double* Q, d
     wg_psd_project(W2, Lout, eps_psd, n, Sx, red, c2);
   } else {
     wg_chol_inverse(W1, W2, Lout, n);  // L' raw -> W2 (Lout as work)
+    GC_MARK(sink, 28);
     if (Llift) wg_psd_fast_lifted_chol(W2, Lout, eps_psd, eps_lift, n, Sx, Llift, red, c2, side);
     else wg_psd_project_fast(W2, Lout, eps_psd, n, Sx, red, c2);
   }
+  GC_MARK(sink, 29);
   wg_matvec(Lout, mu, hout, n);
   if (t == 0 && cert) {
     const double lift = 2.0 * eps_lift * n;
@@ -312,8 +354,9 @@ GC_DEV ImuPair imu_pair_load(const double* d) {
 }
 GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const double* R0, const double* bg,
                             const double* ba, const double* g, double* A, double* Bm, double* V1, double* V2,
-                            double* out) {
+                            double* out, double* sink = nullptr) {
   const int t = threadIdx.x;
+  (void)sink;
   const int ia = 2 * t, ib = 2 * t + 1;
   const double ta = q.ta, tb = q.tb;
   // dt_i = max(t_{i+1} - t_i, 0), last slot 0 (imu_preintegration.py:84-85)
@@ -329,6 +372,7 @@ GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const
     so3_exp(wv2, dRb);
     mat3_mul(dRa, dRb, Pl);
   }
+  GC_MARK(sink, 40);
   // inclusive scan of 3x3 products X_t = Pl_0 ... Pl_t: 6 shuffle levels inside each wave, then the
   // wave totals (left to right) applied on the left; result rows in A for the reads below
   double* src = A;
@@ -363,6 +407,7 @@ GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const
     for (int k = 0; k < 9; ++k) A[t * 9 + k] = X[k];
     __syncthreads();
   }
+  GC_MARK(sink, 41);
   double Ea[9], Rb[9];
   if (t == 0) {
     for (int k = 0; k < 9; ++k) Ea[k] = R0[k];
@@ -399,6 +444,7 @@ GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const
     for (int k = 0; k < 3; ++k) V1[t * 3 + k] = v[k];
     __syncthreads();
   }
+  GC_MARK(sink, 42);
   double pc[3];
   for (int k = 0; k < 3; ++k) {
     const double va = (t > 0) ? vs[(t - 1) * 3 + k] : 0.0;
@@ -413,6 +459,7 @@ GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const
     sums[9 + k] = awa[k] * dea + awb[k] * deb;
   }
   sums[12] = dea + deb;
+  GC_MARK(sink, 43);
   wg_sum_n<13>(sums, Bm);  // 13 sums in wg_sum's order with two barriers (Bm: free again)
   if (t == 0) {
     mat3_mul(R0, src + (kWG - 1) * 9, out);  // R_end
@@ -439,29 +486,6 @@ GC_DEV double nu_project(double nu_raw, double dim, double nu_max) {
   return nu_max - softplus(nu_max - nf);
 }
 
-// Projection of one padded 6x6 IW block whose active part is the leading d x d (d in {1,3}):
-// the padded block is [A, 0; 0, 0], so its PSD projection is [PSD(A), 0; 0, eps I] and the
-// projection delta picks up (6-d) eps^2 (the reference projects the padded 6x6 as a whole).
-GC_DEV double psd_padded_small(const double* A6, int d, double eps, double* out6) {
-  for (int k = 0; k < 36; ++k) out6[k] = 0.0;
-  double d2 = (6 - d) * eps * eps;
-  if (d == 1) {
-    const double a = A6[0], p = fmax(a, eps);
-    out6[0] = p;
-    d2 += (p - a) * (p - a);
-  } else {
-    double A[9], Pp[9], c[6];
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) A[3 * i + j] = A6[6 * i + j];
-    psd_project3_fast(A, eps, Pp, c);
-    for (int i = 0; i < 3; ++i)
-      for (int j = 0; j < 3; ++j) out6[6 * i + j] = Pp[3 * i + j];
-    d2 += c[0] * c[0];
-  }
-  for (int k = d; k < 6; ++k) out6[7 * k] = eps;
-  return sqrt(d2);
-}
-
 // Process-noise IW apply (inverse_wishart_jax.py:126-185), one workgroup:
 // Ψ_b' = PSD((ρ_b Ψ_b + w dΨ_b) ⊙ mask_b), ν_b' = proj(ρ_b ν_b + w dν_b).
 // Outputs may alias the inputs (all reads precede the writes). cert (thread 0) =
@@ -478,15 +502,31 @@ GC_DEV void wg_iw_proc_apply(const double* nu, const double* Psi, const double* 
     tab[16 + t] = fabs(nn - nr);
     tab[24 + t] = nn;
   }
-  if (t < 6) {  // 3x3 and 1x1 blocks in registers
-    double A6[36], O6[36];
+  if (t < 6) {
+    // 3x3 blocks (t < 5) and the 1x1 block (t = 5) in registers. The reference projects each masked
+    // block padded to 6x6, [A, 0; 0, 0] -> [PSD(A), 0; 0, εI], so P = PSD(leading 3x3) or
+    // diag(max(a, ε), ε, ε), and the projection delta picks up (6 - d) ε²; written out entry by
+    // entry (no run-time indexed array)
+    const double rho = kIwRhoProc[t];
+    const double* Ps = Psi + t * 36;
+    const double* dP = dPsi + t * 36;
+    double Pp[9], d2;
+    if (t == 5) {
+      const double a = rho * Ps[0] + w * dP[0], pv = fmax(a, eps_psd);
+      for (int k = 0; k < 9; ++k) Pp[k] = (k == 0) ? pv : ((k % 4 == 0) ? eps_psd : 0.0);
+      d2 = 5.0 * eps_psd * eps_psd + (pv - a) * (pv - a);
+    } else {
+      double A[9], c[6];
+      for (int i = 0; i < 3; ++i)
+        for (int j = 0; j < 3; ++j) A[3 * i + j] = rho * Ps[6 * i + j] + w * dP[6 * i + j];
+      psd_project3_fast(A, eps_psd, Pp, c);
+      d2 = 3.0 * eps_psd * eps_psd + c[0] * c[0];
+    }
+    tab[8 + t] = sqrt(d2);
     for (int k = 0; k < 36; ++k) {
       const int i = k / 6, j = k % 6;
-      const double m = (i < kIwBlockDim[t] && j < kIwBlockDim[t]) ? 1.0 : 0.0;
-      A6[k] = (kIwRhoProc[t] * Psi[t * 36 + k] + w * dPsi[t * 36 + k]) * m;
+      Qs[t * 36 + k] = (i < 3 && j < 3) ? Pp[3 * i + j] : ((i == j) ? eps_psd : 0.0);
     }
-    tab[8 + t] = psd_padded_small(A6, kIwBlockDim[t], eps_psd, O6);
-    for (int k = 0; k < 36; ++k) Qs[t * 36 + k] = O6[k];
   }
   if (t < 36) blk[t] = kIwRhoProc[6] * Psi[6 * 36 + t] + w * dPsi[6 * 36 + t];
   __syncthreads();

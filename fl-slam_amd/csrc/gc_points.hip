@@ -620,18 +620,28 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
         // the half's 32 rows are one contiguous block of 32 NB doubles in HBM: 1 KiB per instruction
         const int64_t pbase = wbase + 32 * hf;
         double* dst = Rh + pbase * NB;
-        const int64_t lim = (n - pbase) * NB;  // doubles of the block that belong to points < n
-#pragma unroll
-        for (int m = 0; m < NB / 4; ++m) {
-          const int o = m * 128 + 2 * lane;
-          const int row = o / NB, col = o - row * NB;
-          const dvec2 v = *reinterpret_cast<const dvec2*>(&S[row * RS2 + col]);
-          if (o < lim) {
+        const auto put = [&](int o, const dvec2& v) {
 #if GC_SA_NT
-            __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(dst + o));
+          __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(dst + o));
 #else
-            *reinterpret_cast<dvec2*>(dst + o) = v;
+          *reinterpret_cast<dvec2*>(dst + o) = v;
 #endif
+        };
+        if (pbase + 32 <= n) {  // wave-uniform: the whole block is in range (every block but the tail's)
+#pragma unroll
+          for (int m = 0; m < NB / 4; ++m) {
+            const int o = m * 128 + 2 * lane;
+            const int row = o / NB, col = o - row * NB;
+            put(o, *reinterpret_cast<const dvec2*>(&S[row * RS2 + col]));
+          }
+        } else {
+          const int64_t lim = (n - pbase) * NB;  // doubles of the block that belong to points < n
+#pragma unroll
+          for (int m = 0; m < NB / 4; ++m) {
+            const int o = m * 128 + 2 * lane;
+            const int row = o / NB, col = o - row * NB;
+            const dvec2 v = *reinterpret_cast<const dvec2*>(&S[row * RS2 + col]);
+            if (o < lim) put(o, v);
           }
         }
         lds_wave_sync();
@@ -1692,13 +1702,18 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   // same for every shard size)
   const int64_t U = (P.n_cap + 255) / 256;  // 256-point units per hypothesis
   const int Hg = P.geom_H > 0 ? P.geom_H : H;
-  int iters = 16;
-  while (iters > 2 && (int64_t)Hg * U < 3 * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
-#ifndef GC_SHORT_DIV
-#define GC_SHORT_DIV 4
+#ifndef GC_BINS_MIN_TASKS
+#define GC_BINS_MIN_TASKS 3
 #endif
-  // short tasks of a quarter of a long one, at least 2 iterations (H = 256: 4-iteration short tasks,
-  // 1.2628 -> 1.2532 ms/scan A/B; H = 32: 2, which stays best there)
+  int iters = 16;
+  while (iters > 2 && (int64_t)Hg * U < GC_BINS_MIN_TASKS * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
+#ifndef GC_SHORT_DIV
+#define GC_SHORT_DIV 2
+#endif
+  // short tasks of half a long one, at least 2 iterations: H = 256 8-iteration short tasks (interleaved
+  // A/B on one box, 1.2499/1.2463 ms/scan with 4 -> 1.2377/1.2391 with 8); H = 32 (4-iteration long
+  // tasks) 2, which stays best there (0.3013/0.3004/0.3003 ms against 0.305-0.313 for 8-iteration long
+  // tasks with 2- or 4-iteration short ones and for 4-iteration tasks only; tools/ab32.sh)
   const int kItersShort = std::max(2, iters / GC_SHORT_DIV);
   int64_t Us = std::max<int64_t>(iters, ((int64_t)pullers * iters + Hg - 1) / Hg);
   Us = std::min(Us, U);

@@ -17,21 +17,65 @@ namespace gc {
 constexpr int kWG = 256;
 constexpr int kDZ = 22;
 
+// dev instrumentation (gc_pipe.h GC_PHASE) inside device helpers: sink = P.io_parts (or nullptr)
+#ifdef GC_PHASE_TIMING
+#define GC_MARK(sink, i)                                                                        \
+  do {                                                                                          \
+    __syncthreads();                                                                            \
+    if ((sink) && blockIdx.x == 0 && threadIdx.x == 0) (sink)[i] = (double)__builtin_readcyclecounter(); \
+  } while (0)
+// one thread's own stamp, no barrier (workgroup 0)
+#define GC_STAMP(sink, i)                                                               \
+  do {                                                                                  \
+    if ((sink) && blockIdx.x == 0) (sink)[i] = (double)__builtin_readcyclecounter();    \
+  } while (0)
+#else
+#define GC_MARK(sink, i) \
+  do {                   \
+  } while (0)
+#define GC_STAMP(sink, i) \
+  do {                    \
+  } while (0)
+#endif
+
 GC_DEV int tid() { return threadIdx.x; }
 
-// Deterministic workgroup sum (fixed shuffle tree + fixed wave order). red: >= 4 doubles of LDS.
+GC_DEV double readlane_f64(double v, int lane) {
+  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
+  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
+  return __hiloint2double(hi, lo);
+}
+
+// Wave reductions (every lane active): within each 16-lane row a DPP butterfly (quad_perm
+// [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror: each step pairs a lane with a partner holding a
+// disjoint partial, so the row ends with one bit-identical total), then the four row totals by
+// v_readlane as ((r0 + r1) + (r2 + r3)): VALU and SALU only, where the xor butterfly of
+// __shfl_xor was six dependent ds_bpermute round trips through the LDS pipe. The result is wave-
+// uniform; the order is fixed (deterministic).
+template <int CTRL>
+GC_DEV double wdpp_f64(double v) {
+  const int lo = __builtin_amdgcn_mov_dpp(__double2loint(v), CTRL, 0xF, 0xF, false);
+  const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
+template <typename Op>
+GC_DEV double wave_reduce(double v, const Op& op) {
+  v = op(v, wdpp_f64<0xB1>(v));   // quad_perm [1,0,3,2]
+  v = op(v, wdpp_f64<0x4E>(v));   // quad_perm [2,3,0,1]
+  v = op(v, wdpp_f64<0x141>(v));  // row_half_mirror
+  v = op(v, wdpp_f64<0x140>(v));  // row_mirror
+  return op(op(readlane_f64(v, 0), readlane_f64(v, 16)), op(readlane_f64(v, 32), readlane_f64(v, 48)));
+}
 GC_DEV double wave_sum(double v) {
-  for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off, 64);
-  return v;
+  return wave_reduce(v, [](double a, double b) { return a + b; });
 }
 GC_DEV double wave_max(double v) {
-  for (int off = 32; off >= 1; off >>= 1) v = fmax(v, __shfl_xor(v, off, 64));
-  return v;
+  return wave_reduce(v, [](double a, double b) { return fmax(a, b); });
 }
 GC_DEV double wave_min(double v) {
-  for (int off = 32; off >= 1; off >>= 1) v = fmin(v, __shfl_xor(v, off, 64));
-  return v;
+  return wave_reduce(v, [](double a, double b) { return fmin(a, b); });
 }
+// Deterministic workgroup sum (fixed wave tree + fixed wave order). red: >= 4 doubles of LDS.
 GC_DEV double wg_sum(double v, double* red) {
   v = wave_sum(v);
   __syncthreads();
@@ -96,12 +140,7 @@ GC_DEV void wg_copy(double* dst, const double* src, int count) {
 // unchanged); column broadcasts are v_readlane (compile-time lane, loops fully unrolled). No LDS
 // traffic or workgroup barriers inside the factorization: ~5x shorter latency than the
 // LDS/barrier-per-column form on the 22x22 information matrices of the per-hypothesis kernels.
-GC_DEV double readlane_f64(double v, int lane) {
-  const int lo = __builtin_amdgcn_readlane(__double2loint(v), lane);
-  const int hi = __builtin_amdgcn_readlane(__double2hiint(v), lane);
-  return __hiloint2double(hi, lo);
-}
-
+//
 // Right-looking Cholesky of the lane rows a (lower triangle significant). CHECKED: a pivot <= 0
 // (or NaN) clears ok and is replaced by 1 so the rest stays finite (wg_chol_checked semantics).
 // The pivot scale is one v_rsq_f64 + a Goldschmidt step (d = √p and 1/d to ~1 ulp) instead of a

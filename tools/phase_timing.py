@@ -41,7 +41,7 @@ for k, s in enumerate(scans):
 for r in range(6):
     pipe.run_scan(r % 3, scans[r % 3], r)
 ctx.sync()
-t = pipe.io_parts()[0]
+t = pipe.io_parts().reshape(-1)  # hypothesis 0's slots, then hypothesis 1's (40+: preint marks)
 names = {1: "predict: wg_predict", 2: "predict: compose", 3: "predict: chol", 4: "predict: chol_solve",
          5: "predict: moments+dt_imu", 6: "predict: preintegrate", 7: "predict: xi+omega", 8: "predict: meas IW",
          11: "evidence: start..MF", 12: "evidence: MF..planar", 13: "evidence: L_raw,beta,excitation",
@@ -49,6 +49,25 @@ names = {1: "predict: wg_predict", 2: "predict: compose", 3: "predict: chol", 4:
          17: "evidence: IW solves/inverse", 18: "evidence: map increment", 19: "evidence: drift+final solves",
          21: "combine wg0: reduce + 22x22 PSD", 23: "combine wg2: process IW apply",
          24: "combine wg2: meas IW apply", 25: "combine wg2: Q rebuild"}
+inner = {26: "predict: load Sig/Q, W2", 27: "predict: PSD Σ' + chol", 28: "predict: chol inverse",
+         29: "predict: PSD L' + lifted chol"}
+for i in sorted(inner):
+    if t[i] and t[i - 1 if i > 26 else 0]:
+        print(f"{inner[i]:36s} {t[i] - t[i - 1 if i > 26 else 0]:10.0f} cycles")
+for a, b, nm in ((10, 30, "evidence: MF rows"), (30, 31, "evidence: MF sum_bins"), (31, 11, "evidence: mf_finalize"),
+                 (11, 32, "evidence: planar rows"), (32, 33, "evidence: planar sum_bins"),
+                 (33, 12, "evidence: planar_finalize")):
+    if t[a] and t[b]:
+        print(f"{nm:36s} {t[b] - t[a]:10.0f} cycles")
+for a, b, nm in ((5, 40, "predict: preint: 2 x so3_exp"), (40, 41, "predict: preint: rotation scan"),
+                 (41, 42, "predict: preint: velocity scan"), (42, 43, "predict: preint: position terms"),
+                 (43, 6, "predict: preint: sums")):
+    if t[a] and t[b]:
+        print(f"{nm:36s} {t[b] - t[a]:10.0f} cycles")
+for a, b, nm in ((17, 34, "evidence: map inc: zt, R (lane 64)"), (34, 35, "evidence: map inc: pushforward"),
+                 (17, 36, "evidence: drift: X_fin (lane 0)"), (36, 37, "evidence: drift: h_fin, μ_fin")):
+    if t[a] and t[b]:
+        print(f"{nm:36s} {t[b] - t[a]:10.0f} cycles")
 for i in sorted(names):
     if t[i] and t[i - 1]:
         print(f"{names[i]:36s} {t[i] - t[i - 1]:10.0f} cycles")
