@@ -17,6 +17,7 @@
 #include <hipcub/hipcub.hpp>
 #include "gc_internal.h"
 #include "gc_math.h"
+#include "gc_mapslot.h"
 
 namespace gc {
 namespace {
@@ -44,7 +45,7 @@ __global__ void k_view_keys(gc_primitive_map map, int64_t m_tile, const int64_t*
   double key = 1e30;  // -score of an invalid slot (score -1e30)
   if (d >= 0) {
     const int64_t g = d * m_tile + s;
-    if (map.valid_mask[g]) key = -map.weights[g];
+    if (mValid(map, g)) key = -mW(map, g);
   }
   keys[i] = key;
   vals[i] = (int32_t)s;
@@ -66,21 +67,21 @@ __global__ void k_view_gather(gc_primitive_map map, int64_t m_tile, const int64_
   uint8_t valid = 0;
   if (d >= 0) {
     const int64_t g = d * m_tile + slot;
-    for (int q = 0; q < 9; ++q) Lr[q] = map.Lambdas[9 * g + q];
-    for (int q = 0; q < 3; ++q) th[q] = map.thetas[3 * g + q];
+    for (int q = 0; q < 9; ++q) Lr[q] = mLam(map, g)[q];
+    for (int q = 0; q < 3; ++q) th[q] = mTh(map, g)[q];
     for (int l = 0; l < L; ++l) {
       for (int q = 0; q < 3; ++q) {
-        const double e = map.etas[((int64_t)L * g + l) * 3 + q];
+        const double e = mEta(map, g)[3 * l + q];
         V.etas[(v * L + l) * 3 + q] = e;
         es[q] += e;
       }
     }
-    w = map.weights[g];
-    pid = map.primitive_ids ? map.primitive_ids[g] : 0;
-    last = map.last_supported_scan_seq[g];
-    valid = map.valid_mask[g];
+    w = mW(map, g);
+    pid = map.primitive_ids ? mPid(map, g) : 0;
+    last = mSup(map, g);
+    valid = mValid(map, g);
     if (map.rgb)
-      for (int q = 0; q < 3; ++q) rgb[q] = map.rgb[3 * g + q];
+      for (int q = 0; q < 3; ++q) rgb[q] = mRgb(map, g)[q];
   } else {
     for (int q = 0; q < 3 * L; ++q) V.etas[v * 3 * L + q] = 0.0;
   }

@@ -18,6 +18,7 @@
 #include <hipcub/hipcub.hpp>
 #include "gc_internal.h"
 #include "gc_math.h"
+#include "gc_mapslot.h"
 
 namespace gc {
 namespace {
@@ -56,7 +57,7 @@ __global__ void k_sum_parts(const double* __restrict__ part, int blocks, double*
 
 __global__ void k_forget(Tile T, double gamma) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < T.n) T.m.weights[T.s0 + s] = gamma * T.m.weights[T.s0 + s];
+  if (s < T.n) mW(T.m, T.s0 + s) = gamma * mW(T.m, T.s0 + s);
 }
 
 GC_DEV double recency_decay(int64_t seq, int64_t last, double lam) {
@@ -69,14 +70,14 @@ __global__ void __launch_bounds__(256) k_recency(Tile T, int64_t seq, double lam
   double acc[3] = {0.0, 0.0, 0.0};
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < T.n; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t g = T.s0 + s;
-    const bool valid = T.m.valid_mask[g] != 0;
-    double decay = fmin(fmax(recency_decay(seq, T.m.last_supported_scan_seq[g], lam), min_scale), 1.0);
+    const bool valid = mValid(T.m, g) != 0;
+    double decay = fmin(fmax(recency_decay(seq, mSup(T.m, g), lam), min_scale), 1.0);
     if (!valid) decay = 1.0;
-    double* L = T.m.Lambdas + 9 * g;
+    double* L = mLam(T.m, g);
 #pragma unroll
     for (int q = 0; q < 9; ++q) L[q] = L[q] * decay;
 #pragma unroll
-    for (int q = 0; q < 3; ++q) T.m.thetas[3 * g + q] = T.m.thetas[3 * g + q] * decay;
+    for (int q = 0; q < 3; ++q) mTh(T.m, g)[q] = mTh(T.m, g)[q] * decay;
     if (valid) {
       acc[0] += 1.0;
       acc[1] += 1.0 - decay;
@@ -91,8 +92,8 @@ __global__ void __launch_bounds__(256) k_cull_count(Tile T, double thr, double* 
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < T.n; s += (int64_t)gridDim.x * blockDim.x) {
     const int64_t g = T.s0 + s;
-    const double w = T.m.weights[g];
-    const bool valid = T.m.valid_mask[g] != 0;
+    const double w = mW(T.m, g);
+    const bool valid = mValid(T.m, g) != 0;
     const bool below = valid && w < thr;
     acc[0] += valid ? 1.0 : 0.0;
     acc[1] += below ? 1.0 : 0.0;
@@ -104,20 +105,20 @@ __global__ void __launch_bounds__(256) k_cull_count(Tile T, double thr, double* 
 
 __global__ void k_cull_keys(Tile T, double* keys) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (s < T.n) keys[s] = T.m.weights[T.s0 + s] * (T.m.valid_mask[T.s0 + s] ? 1.0 : 0.0);
+  if (s < T.n) keys[s] = mW(T.m, T.s0 + s) * (mValid(T.m, T.s0 + s) ? 1.0 : 0.0);
 }
 
 __global__ void k_cull_apply(Tile T, double thr) {
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= T.n) return;
   const int64_t g = T.s0 + s;
-  if (T.m.valid_mask[g] && T.m.weights[g] < thr) T.m.valid_mask[g] = 0;
+  if (mValid(T.m, g) && mW(T.m, g) < thr) mValid(T.m, g) = 0;
 }
 
 __global__ void __launch_bounds__(256) k_count_valid(Tile T, double* part) {
   double acc[1] = {0.0};
   for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < T.n; s += (int64_t)gridDim.x * blockDim.x)
-    acc[0] += T.m.valid_mask[T.s0 + s] ? 1.0 : 0.0;
+    acc[0] += mValid(T.m, T.s0 + s) ? 1.0 : 0.0;
   block_partials<1>(acc, part);
 }
 
@@ -127,8 +128,8 @@ __global__ void k_insert_keys(Tile T, int64_t seq, double lam, double* keys, int
   const int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= T.n) return;
   const int64_t g = T.s0 + s;
-  const double ret = T.m.weights[g] * recency_decay(seq, T.m.last_supported_scan_seq[g], lam);
-  keys[s] = T.m.valid_mask[g] ? ret : -INFINITY;
+  const double ret = mW(T.m, g) * recency_decay(seq, mSup(T.m, g), lam);
+  keys[s] = mValid(T.m, g) ? ret : -INFINITY;
   vals[s] = (int32_t)s;
 }
 
@@ -161,29 +162,29 @@ __global__ void __launch_bounds__(256) k_insert_apply(Tile T, gc_insert_batch B,
     if (ids_out) ids_out[k] = ins ? next_id + run : -1;
     if (!ins) continue;
     const int64_t g = T.s0 + slot;
-    for (int q = 0; q < 9; ++q) T.m.Lambdas[9 * g + q] = B.Lambdas[9 * k + q];
-    for (int q = 0; q < 3; ++q) T.m.thetas[3 * g + q] = B.thetas[3 * k + q];
-    for (int q = 0; q < 3 * L; ++q) T.m.etas[(int64_t)3 * L * g + q] = B.etas[(int64_t)3 * L * k + q];
+    for (int q = 0; q < 9; ++q) mLam(T.m, g)[q] = B.Lambdas[9 * k + q];
+    for (int q = 0; q < 3; ++q) mTh(T.m, g)[q] = B.thetas[3 * k + q];
+    for (int q = 0; q < 3 * L; ++q) mEta(T.m, g)[q] = B.etas[(int64_t)3 * L * k + q];
     const double w = B.weights[k];
-    T.m.weights[g] = w;
-    T.m.timestamps[g] = ts;
-    if (T.m.created_timestamps) T.m.created_timestamps[g] = ts;
-    T.m.last_supported_scan_seq[g] = seq;
-    T.m.last_update_scan_seq[g] = seq;
-    if (T.m.primitive_ids) T.m.primitive_ids[g] = next_id + run;
-    T.m.valid_mask[g] = 1;
+    mW(T.m, g) = w;
+    mTs(T.m, g) = ts;
+    if (T.m.created_timestamps) mCreated(T.m, g) = ts;
+    mSup(T.m, g) = seq;
+    mUpd(T.m, g) = seq;
+    if (T.m.primitive_ids) mPid(T.m, g) = next_id + run;
+    mValid(T.m, g) = 1;
     if (color) {
       const int src = B.sources ? B.sources[k] : 1;
       const double cam = w * (src == 0 ? 1.0 : 0.0), lid = w * (src == 1 ? 1.0 : 0.0);
-      T.m.cam_mass[g] = cam;
-      T.m.lidar_mass[g] = lid;
-      T.m.rgb_cam_denom[g] = cam;
+      mCam(T.m, g) = cam;
+      mLid(T.m, g) = lid;
+      mDen(T.m, g) = cam;
       for (int q = 0; q < 3; ++q) {
         const double c = B.colors ? B.colors[3 * k + q] : 0.0;
         const double rgb = cam > 0.0 ? clampd(c, 0.0, 1.0) : 0.5;
-        T.m.rgb_cam_accum[3 * g + q] = c * cam;
-        T.m.rgb[3 * g + q] = rgb;
-        if (T.m.colors) T.m.colors[3 * g + q] = rgb;
+        mAcc(T.m, g)[q] = c * cam;
+        mRgb(T.m, g)[q] = rgb;
+        if (T.m.colors) mCol(T.m, g)[q] = rgb;
       }
     }
     ++run;
@@ -198,8 +199,8 @@ __global__ void k_merge_prep(Tile T, double eps_lift, double* mu, double* Sig, d
   if (s >= T.n) return;
   const int64_t g = T.s0 + s;
   double Lr[9];
-  for (int q = 0; q < 9; ++q) Lr[q] = T.m.Lambdas[9 * g + q] + ((q % 4 == 0) ? eps_lift : 0.0);
-  solve3(Lr, T.m.thetas + 3 * g, mu + 3 * s);
+  for (int q = 0; q < 9; ++q) Lr[q] = mLam(T.m, g)[q] + ((q % 4 == 0) ? eps_lift : 0.0);
+  solve3(Lr, mTh(T.m, g), mu + 3 * s);
   inv3(Lr, Sig + 9 * s);
   dets[s] = det3(Sig + 9 * s);
 }
@@ -233,7 +234,7 @@ __global__ void k_merge_dist(Tile T, int64_t P, const double* __restrict__ mu, c
   mat3_tvec(Si, dm, rv);  // dmuᵀ S⁻¹
   const double quad = 0.125 * dot3(rv, dm);
   const double logt = 0.5 * log(detS / sqrt(dets[i] * dets[j] + 1e-24));
-  const bool pv = T.m.valid_mask[T.s0 + i] && T.m.valid_mask[T.s0 + j];
+  const bool pv = mValid(T.m, T.s0 + i) && mValid(T.m, T.s0 + j);
   keys[p] = pv ? quad + logt : INFINITY;
   vals[p] = (uint32_t)p;
 }
@@ -268,7 +269,7 @@ __global__ void k_merge_apply(Tile T, const double* __restrict__ mu, const doubl
   if (k >= max_pairs || k >= *n_sel) return;
   const int64_t i = sel[2 * k], j = sel[2 * k + 1];
   const int64_t gi = T.s0 + i, gj = T.s0 + j;
-  const double w1 = T.m.weights[gi], w2 = T.m.weights[gj], ws = w1 + w2;
+  const double w1 = mW(T.m, gi), w2 = mW(T.m, gj), ws = w1 + w2;
   if (!(ws > 0.0)) return;
   const double* m1 = mu + 3 * i;
   const double* m2 = mu + 3 * j;
@@ -283,34 +284,34 @@ __global__ void k_merge_apply(Tile T, const double* __restrict__ mu, const doubl
     }
   inv3(Sm, Lm);
   mat3_vec(Lm, mm, th);
-  for (int q = 0; q < 9; ++q) T.m.Lambdas[9 * gi + q] = Lm[q];
-  for (int q = 0; q < 3; ++q) T.m.thetas[3 * gi + q] = th[q];
+  for (int q = 0; q < 9; ++q) mLam(T.m, gi)[q] = Lm[q];
+  for (int q = 0; q < 3; ++q) mTh(T.m, gi)[q] = th[q];
   const int L = T.m.n_lobes;
-  double* ei = T.m.etas + (int64_t)3 * L * gi;
-  const double* ej = T.m.etas + (int64_t)3 * L * gj;
+  double* ei = mEta(T.m, gi);
+  const double* ej = mEta(T.m, gj);
   for (int q = 0; q < 3 * L; ++q) ei[q] = (w1 * ei[q] + w2 * ej[q]) / ws;
-  T.m.weights[gi] = ws;
+  mW(T.m, gi) = ws;
   if (T.m.cam_mass) {
-    const double cm = T.m.cam_mass[gi] + T.m.cam_mass[gj];
-    const double den = T.m.rgb_cam_denom[gi] + T.m.rgb_cam_denom[gj];
-    T.m.cam_mass[gi] = cm;
-    T.m.lidar_mass[gi] = T.m.lidar_mass[gi] + T.m.lidar_mass[gj];
-    T.m.rgb_cam_denom[gi] = den;
+    const double cm = mCam(T.m, gi) + mCam(T.m, gj);
+    const double den = mDen(T.m, gi) + mDen(T.m, gj);
+    mCam(T.m, gi) = cm;
+    mLid(T.m, gi) = mLid(T.m, gi) + mLid(T.m, gj);
+    mDen(T.m, gi) = den;
     for (int q = 0; q < 3; ++q) {
-      const double acc = T.m.rgb_cam_accum[3 * gi + q] + T.m.rgb_cam_accum[3 * gj + q];
+      const double acc = mAcc(T.m, gi)[q] + mAcc(T.m, gj)[q];
       const double rgb = cm > 0.0 ? clampd(acc / fmax(den, eps_psd), 0.0, 1.0) : 0.5;
-      T.m.rgb_cam_accum[3 * gi + q] = acc;
-      T.m.rgb[3 * gi + q] = rgb;
-      if (T.m.colors) T.m.colors[3 * gi + q] = rgb;
+      mAcc(T.m, gi)[q] = acc;
+      mRgb(T.m, gi)[q] = rgb;
+      if (T.m.colors) mCol(T.m, gi)[q] = rgb;
     }
   }
-  T.m.timestamps[gi] = fmax(T.m.timestamps[gi], T.m.timestamps[gj]);
-  if (T.m.created_timestamps) T.m.created_timestamps[gi] = fmin(T.m.created_timestamps[gi], T.m.created_timestamps[gj]);
-  const int64_t ls = T.m.last_supported_scan_seq[gj], lu = T.m.last_update_scan_seq[gj];
-  if (ls > T.m.last_supported_scan_seq[gi]) T.m.last_supported_scan_seq[gi] = ls;
-  if (lu > T.m.last_update_scan_seq[gi]) T.m.last_update_scan_seq[gi] = lu;
-  T.m.weights[gj] = 0.0;
-  T.m.valid_mask[gj] = 0;
+  mTs(T.m, gi) = fmax(mTs(T.m, gi), mTs(T.m, gj));
+  if (T.m.created_timestamps) mCreated(T.m, gi) = fmin(mCreated(T.m, gi), mCreated(T.m, gj));
+  const int64_t ls = mSup(T.m, gj), lu = mUpd(T.m, gj);
+  if (ls > mSup(T.m, gi)) mSup(T.m, gi) = ls;
+  if (lu > mUpd(T.m, gi)) mUpd(T.m, gi) = lu;
+  mW(T.m, gj) = 0.0;
+  mValid(T.m, gj) = 0;
 }
 
 unsigned blocks_for(int64_t n) { return (unsigned)((n + 255) / 256); }

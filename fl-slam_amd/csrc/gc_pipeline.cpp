@@ -58,7 +58,7 @@ struct gc_pipeline {
   bool smap_on = false;
   gc_primitive_map smap{};
   double smap_voxel = 0.0;
-  bool smap_colors = false;  // the colour pass is due (first update after attaching a map with colours)
+  bool smap_colors = false;  // the colour pass is due (first update after attaching a map with colours not current)
   gc::ScanMapWork smapW;
   int pending_slot = -1;
   int64_t pending_seq = 0;
@@ -554,7 +554,7 @@ int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const gc_primitive_map*
   GC_TRY(gc::scan_map_prepare(p->ctx, &p->smapW, p->P.n_cap, map->m_slots));
   p->smap = *map;
   p->smap_voxel = voxel_m;
-  p->smap_colors = map->cam_mass != nullptr;
+  p->smap_colors = map->cam_mass != nullptr && !map->colors_current;
   GC_CHECK_ARG(p->ctx, !p->smap_colors || (map->rgb_cam_accum && map->rgb_cam_denom && map->rgb),
                "colour fields must be all set or all NULL");
   p->smap_on = true;

@@ -27,6 +27,7 @@
 #include <hipcub/hipcub.hpp>
 #include "gc_internal.h"
 #include "gc_math.h"
+#include "gc_mapslot.h"
 #include "gc_pipe.h"
 #include "gc_scanmap.h"
 
@@ -229,16 +230,16 @@ __global__ void k_smap_apply(ScanMapArgs A, int64_t n, const uint32_t* __restric
   }
   const int64_t s = key;
   const int L = A.map.n_lobes;
-  for (int q = 0; q < 9; ++q) A.map.Lambdas[9 * s + q] = A.map.Lambdas[9 * s + q] + d.v[q];
-  for (int q = 0; q < 3; ++q) A.map.thetas[3 * s + q] = A.map.thetas[3 * s + q] + d.v[9 + q];
+  for (int q = 0; q < 9; ++q) mLam(A.map, s)[q] = mLam(A.map, s)[q] + d.v[q];
+  for (int q = 0; q < 3; ++q) mTh(A.map, s)[q] = mTh(A.map, s)[q] + d.v[9 + q];
   // lobes > 0 receive 0.0 per row: x + 0.0 (as the fuse writes them)
   for (int q = 0; q < 3 * L; ++q)
-    A.map.etas[(int64_t)3 * L * s + q] = A.map.etas[(int64_t)3 * L * s + q] + (q < 3 ? d.v[12 + q] : 0.0);
-  A.map.weights[s] = A.map.weights[s] + d.v[15];
-  A.map.timestamps[s] = A.timestamp;
-  A.map.last_supported_scan_seq[s] = A.scan_seq;
-  A.map.last_update_scan_seq[s] = A.scan_seq;
-  if (A.map.lidar_mass) A.map.lidar_mass[s] = A.map.lidar_mass[s] + d.v[15];
+    mEta(A.map, s)[q] = mEta(A.map, s)[q] + (q < 3 ? d.v[12 + q] : 0.0);
+  mW(A.map, s) = mW(A.map, s) + d.v[15];
+  mTs(A.map, s) = A.timestamp;
+  mSup(A.map, s) = A.scan_seq;
+  mUpd(A.map, s) = A.scan_seq;
+  if (A.map.lidar_mass) mLid(A.map, s) = mLid(A.map, s) + d.v[15];
   atomicAdd(n_unique, 1ull);  // integer count: order-independent
 }
 

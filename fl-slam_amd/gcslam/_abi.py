@@ -111,6 +111,8 @@ SIGNATURES = {
     "gc_iw_meas_apply": [_vp, _vp, _vp, _vp, _vp, _f64, _f64, _vp, _vp, _vp],
     "gc_hypothesis_barycenter": [_vp, _i32, _vp, _vp, _vp, _vp, _f64, _f64, _f64, _vp, _vp, _vp, _vp],
     "gc_primitive_map_fuse": [_vp, _vp, _vp, _vp, _f64, _f64, _f64, _i64, _vp],
+    "gc_primitive_map_record_layout": [_i32, _vp, _vp],
+    "gc_copy_strided": [_vp, _vp, _i64, _vp, _i64, _i64, _i64],
     "gc_primitive_map_forget": [_vp, _vp, _i64, _i64, _f64],
     "gc_primitive_map_recency_inflate": [_vp, _vp, _i64, _i64, _i64, _f64, _f64, _vp],
     "gc_primitive_map_cull": [_vp, _vp, _i64, _i64, _f64, _i64, _vp],

@@ -119,7 +119,7 @@ def extract_atlas_map_view(atlas_map: DevicePrimitiveMap, tile_ids: List[int], m
         raise ValueError(f"extract_atlas_map_view: m_tile_view must be > 0, got {m_tile_view}")
     view = DeviceMapView(atlas_map.ctx, tile_ids, m_tile_view, atlas_map.n_lobes)
     dense = np.array([atlas_map.dense_tile(int(t)) for t in view.tile_ids], np.int64)
-    _abi.call("gc_extract_map_view", atlas_map.ctx.handle, C.byref(atlas_map._struct), int(atlas_map.m_tile),
+    _abi.call("gc_extract_map_view", atlas_map.ctx.handle, C.byref(atlas_map.struct()), int(atlas_map.m_tile),
               dense.ctypes.data, view.tile_ids.ctypes.data, float(eps_lift), float(eps_mass), C.byref(view.struct),
               ctx=atlas_map.ctx)
     return view

@@ -257,7 +257,7 @@ class BatchedScanPipeline:
         in scan_finish: the budgeted points deskewed with hypothesis 0's twist, pushed to the world
         frame by its recomposed pose with pose-covariance inflation, one row per point into the slot
         of its voxel (build-defined, include/gcslam.h). dmap=None detaches."""
-        self._call("gc_pipeline_attach_primitive_map", None if dmap is None else C.addressof(dmap._struct),
+        self._call("gc_pipeline_attach_primitive_map", None if dmap is None else C.addressof(dmap.struct()),
                    float(voxel_m))
         self._smap = dmap  # the device arrays must outlive the attachment
 

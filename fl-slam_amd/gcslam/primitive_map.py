@@ -31,8 +31,8 @@ _MAINT = ("valid_mask", "created_timestamps", "primitive_ids")
 
 
 class _MapStruct(C.Structure):
-    _fields_ = [("m_slots", C.c_int64), ("n_lobes", C.c_int32), ("pad_", C.c_int32)] + \
-               [(k, C.c_void_p) for k in _F64 + _I64 + _COL + _MAINT]
+    _fields_ = [("m_slots", C.c_int64), ("n_lobes", C.c_int32), ("colors_current", C.c_int32)] + \
+               [(k, C.c_void_p) for k in _F64 + _I64 + _COL + _MAINT] + [("slot_bytes", C.c_int64)]
 
 
 class _InsertStruct(C.Structure):
@@ -47,35 +47,85 @@ class _FuseStruct(C.Structure):
 
 
 class DevicePrimitiveMap:
-    """n_tiles x m_tile slots of PrimitiveMapTile fields (create_empty_tile, primitive_map.py:148-175)."""
+    """n_tiles x m_tile slots of PrimitiveMapTile fields (create_empty_tile, primitive_map.py:148-175).
+
+    packed=True (default) keeps one record per slot in HBM (gc_primitive_map_record_layout: the
+    fuse's read-modify-write fields in the record's first two 128-B lines); upload / download
+    transpose to and from the reference's per-field arrays on the device (gc_copy_strided).
+    packed=False keeps the per-field arrays themselves."""
 
     def __init__(self, n_tiles: int, m_tile: int, n_lobes: int = GC_VMF_N_LOBES, track_colors: bool = True,
-                 ctx=None):
+                 ctx=None, packed: bool = True):
         self.ctx = ctx or _abi.default_context()
         self.n_tiles, self.m_tile, self.n_lobes = int(n_tiles), int(m_tile), int(n_lobes)
         M = self.M = self.n_tiles * self.m_tile
-        shapes = dict(Lambdas=(M, 3, 3), thetas=(M, 3), etas=(M, n_lobes, 3), weights=(M,), timestamps=(M,),
-                      last_supported_scan_seq=(M,), last_update_scan_seq=(M,), cam_mass=(M,), lidar_mass=(M,),
-                      rgb_cam_accum=(M, 3), rgb_cam_denom=(M,), rgb=(M, 3), colors=(M, 3),
-                      valid_mask=(M,), created_timestamps=(M,), primitive_ids=(M,))
-        dtypes = dict(last_supported_scan_seq=np.int64, last_update_scan_seq=np.int64, primitive_ids=np.int64,
-                      valid_mask=np.uint8)
-        self.fields: Dict[str, _abi.DeviceArray] = {}
-        for k, shp in shapes.items():
-            if k in _COL and not track_colors:
-                continue
-            self.fields[k] = _abi.DeviceArray(self.ctx, shp, dtypes.get(k, np.float64))
-            self.fields[k].zero()
+        self.shapes = dict(Lambdas=(M, 3, 3), thetas=(M, 3), etas=(M, n_lobes, 3), weights=(M,), timestamps=(M,),
+                           last_supported_scan_seq=(M,), last_update_scan_seq=(M,), cam_mass=(M,), lidar_mass=(M,),
+                           rgb_cam_accum=(M, 3), rgb_cam_denom=(M,), rgb=(M, 3), colors=(M, 3),
+                           valid_mask=(M,), created_timestamps=(M,), primitive_ids=(M,))
+        self.dtypes = {k: np.dtype(np.float64) for k in self.shapes}
+        self.dtypes.update(last_supported_scan_seq=np.dtype(np.int64), last_update_scan_seq=np.dtype(np.int64),
+                           primitive_ids=np.dtype(np.int64), valid_mask=np.dtype(np.uint8))
+        names = [k for k in _F64 + _I64 + _COL + _MAINT if track_colors or k not in _COL]
+        self.packed = bool(packed)
+        self.ptrs: Dict[str, int] = {}
+        self.fields: Dict[str, _abi.DeviceArray] = {}  # per-field arrays (packed=False)
+        if self.packed:
+            off = np.zeros(16, np.int64)
+            sb = C.c_int64(0)
+            _abi.call("gc_primitive_map_record_layout", self.n_lobes, off.ctypes.data, C.byref(sb))
+            self.slot_bytes = int(sb.value)
+            self.records = _abi.DeviceArray(self.ctx, M * self.slot_bytes, np.uint8)
+            self.records.zero()
+            order = _F64 + _I64 + _COL + _MAINT
+            for k in names:
+                self.ptrs[k] = self.records.ptr + int(off[order.index(k)])
+        else:
+            self.slot_bytes = 0
+            for k in names:
+                self.fields[k] = _abi.DeviceArray(self.ctx, self.shapes[k], self.dtypes[k])
+                self.fields[k].zero()
+                self.ptrs[k] = self.fields[k].ptr
+        self._struct = _MapStruct(M, self.n_lobes, 0, *[self.ptrs.get(k) for k in _F64 + _I64 + _COL + _MAINT],
+                                  self.slot_bytes)
         if track_colors:
-            self.fields["rgb"].upload(np.full((M, 3), 0.5))
-        self._struct = _MapStruct(M, self.n_lobes, 0, *[self.fields[k].ptr if k in self.fields else None
-                                                        for k in _F64 + _I64 + _COL + _MAINT])
+            self.upload(rgb=np.full((M, 3), 0.5))
+        # per tile: every slot's rgb and colors = the fuse's estimate of its camera accumulators. Not so
+        # for an empty tile (create_empty_tile: rgb gray, colors 0); a fuse leaves its tile current,
+        # insert / merge / a colour upload do not
+        self._tile_cc = [False] * self.n_tiles
         # AtlasMap bookkeeping (primitive_map.py:183-201): host integers, as in the reference
         self.next_global_id = 0
         self.total_count = 0
         self.tile_count: Dict[int, int] = {}
         # tile keys of the dense tiles (the reference's packed MA-hex tile ids); default 0..n-1
         self.tile_keys: List[int] = list(range(self.n_tiles))
+
+    @property
+    def colors_current(self) -> bool:
+        """True while every slot's rgb / colors equal the fuse's estimate of its camera accumulators
+        (a fuse then recomputes only the slots it touches, as gc_primitive_map.colors_current)."""
+        return all(self._tile_cc)
+
+    @colors_current.setter
+    def colors_current(self, v: bool) -> None:
+        self._tile_cc = [bool(v)] * self.n_tiles
+
+    def struct(self) -> "_MapStruct":
+        """The whole flat map (all tiles) for a C entry, its colour flag up to date."""
+        self._struct.colors_current = 1 if self.colors_current else 0
+        return self._struct
+
+    def tile_struct(self, tile_id: int) -> "_MapStruct":
+        """One tile as a map of m_tile slots (tile-local slot indices), as the reference's per-tile
+        operators see it."""
+        s0, n = self.tile_range(tile_id)
+        st = _MapStruct.from_buffer_copy(self._struct)
+        st.m_slots = n
+        st.colors_current = 1 if self._tile_cc[int(tile_id)] else 0
+        for k, p in self.ptrs.items():
+            setattr(st, k, p + s0 * (self.slot_bytes or self._row_bytes(k)))
+        return st
 
     def set_tile_keys(self, keys) -> None:
         keys = [int(k) for k in keys]
@@ -90,12 +140,35 @@ class DevicePrimitiveMap:
         except ValueError:
             return -1
 
+    def _row_bytes(self, k: str) -> int:
+        return int(np.prod(self.shapes[k][1:], dtype=np.int64)) * self.dtypes[k].itemsize
+
     def upload(self, **arrays):
         for k, v in arrays.items():
-            self.fields[k].upload(v)
+            if k not in self.ptrs:
+                raise KeyError(k)
+            if k in _COL:
+                self.colors_current = False  # arbitrary colours / accumulators: the next fuse recomputes all
+            if not self.packed:
+                self.fields[k].upload(v)
+                continue
+            tmp = _abi.DeviceArray.from_host(self.ctx, np.asarray(v).reshape(self.shapes[k]), self.dtypes[k])
+            rb = self._row_bytes(k)
+            _abi.call("gc_copy_strided", self.ctx.handle, self.ptrs[k], self.slot_bytes, tmp.ptr, rb, rb, self.M,
+                      ctx=self.ctx)
+            self.ctx.sync()
 
     def download(self, *names):
-        return {k: self.fields[k].download() for k in (names or self.fields.keys())}
+        if not self.packed:
+            return {k: self.fields[k].download() for k in (names or self.fields.keys())}
+        out = {}
+        for k in (names or self.ptrs.keys()):
+            tmp = _abi.DeviceArray(self.ctx, self.shapes[k], self.dtypes[k])
+            rb = self._row_bytes(k)
+            _abi.call("gc_copy_strided", self.ctx.handle, tmp.ptr, rb, self.ptrs[k], self.slot_bytes, rb, self.M,
+                      ctx=self.ctx)
+            out[k] = tmp.download()
+        return out
 
     def tile_slot(self, tile_id: int, slots) -> np.ndarray:
         return int(tile_id) * self.m_tile + np.asarray(slots, dtype=np.int64)
@@ -140,25 +213,34 @@ class DeviceFuseBatch:
 
 def fuse_device(dmap: DevicePrimitiveMap, batch: DeviceFuseBatch, timestamp: float, scan_seq: int = 0,
                 world_pose=None, eps_lift: float = GC_EPS_LIFT, eps_mass: float = GC_EPS_MASS,
-                count: bool = True) -> int:
-    """Fuse a resident batch in place; returns the distinct slots touched (count=False: -1, no sync)."""
+                count: bool = True, tile_id: Optional[int] = None) -> int:
+    """Fuse a resident batch in place; returns the distinct slots touched (count=False: -1, no sync).
+    tile_id=None: the rows hold flat slots of the whole map; else tile-local slots of that tile (the
+    colour estimate then covers that tile, as the reference's per-tile fuse)."""
     pose = None if world_pose is None else np.ascontiguousarray(world_pose, np.float64).reshape(6)
     n = C.c_int64(-1)
-    _abi.call("gc_primitive_map_fuse", dmap.ctx.handle, C.byref(dmap._struct), C.byref(batch.struct),
+    st = dmap.struct() if tile_id is None else dmap.tile_struct(tile_id)
+    _abi.call("gc_primitive_map_fuse", dmap.ctx.handle, C.byref(st), C.byref(batch.struct),
               None if pose is None else pose.ctypes.data, float(eps_lift), float(eps_mass), float(timestamp),
               int(scan_seq), C.byref(n) if count else None, ctx=dmap.ctx)
+    if "cam_mass" in dmap.ptrs:  # the fuse leaves every slot's colour (of the tile) at its estimate
+        if tile_id is None:
+            dmap.colors_current = True
+        else:
+            dmap._tile_cc[int(tile_id)] = True
     return int(n.value)
 
 
 def fuse_rows(dmap: DevicePrimitiveMap, slots, Lambdas, thetas, etas, weights, responsibilities, timestamp: float,
               scan_seq: int = 0, valid_mask=None, colors=None, sources=None, world_pose=None,
-              eps_lift: float = GC_EPS_LIFT, eps_mass: float = GC_EPS_MASS) -> int:
-    """K host rows (flat map slots) -> fused in place; returns the number of distinct slots touched."""
+              eps_lift: float = GC_EPS_LIFT, eps_mass: float = GC_EPS_MASS, tile_id: Optional[int] = None) -> int:
+    """K host rows (flat map slots, or tile-local with tile_id) -> fused in place; returns the number of
+    distinct slots touched."""
     if np.asarray(slots).reshape(-1).shape[0] == 0:
         return 0
     b = DeviceFuseBatch(dmap.ctx, slots, Lambdas, thetas, etas, weights, responsibilities, valid_mask, colors,
                         sources, dmap.n_lobes)
-    return fuse_device(dmap, b, timestamp, scan_seq, world_pose, eps_lift, eps_mass)
+    return fuse_device(dmap, b, timestamp, scan_seq, world_pose, eps_lift, eps_mass, tile_id=tile_id)
 
 
 def primitive_map_fuse(atlas_map: DevicePrimitiveMap, tile_id: int, target_slots, Lambdas_meas, thetas_meas,
@@ -175,10 +257,11 @@ def primitive_map_fuse(atlas_map: DevicePrimitiveMap, tile_id: int, target_slots
         return (PrimitiveMapFuseResult(atlas_map, int(tile_id), 0),
                 CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
                 ExpectedEffect(objective_name="primitive_map_fuse", predicted=0.0, realized=0.0))
-    flat = np.where((sl >= 0) & (sl < atlas_map.m_tile), atlas_map.tile_slot(tile_id, sl), -1)
-    n = fuse_rows(atlas_map, flat, Lambdas_meas, thetas_meas, etas_meas, weights_meas, responsibilities, timestamp,
+    atlas_map.tile_range(tile_id)  # validates the tile
+    local = np.where((sl >= 0) & (sl < atlas_map.m_tile), sl, -1)
+    n = fuse_rows(atlas_map, local, Lambdas_meas, thetas_meas, etas_meas, weights_meas, responsibilities, timestamp,
                   scan_seq, valid_mask, colors_meas if sources_meas is not None else None, sources_meas, world_pose,
-                  eps_lift, eps_mass)
+                  eps_lift, eps_mass, tile_id=tile_id)
     return (PrimitiveMapFuseResult(atlas_map, int(tile_id), n),
             CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
             ExpectedEffect(objective_name="primitive_map_fuse", predicted=float(K), realized=float(n)))
@@ -204,7 +287,7 @@ def primitive_map_forget(atlas_map: DevicePrimitiveMap, tile_id: int,
     """primitive_map_forget (primitive_map.py:1314-1390): weights *= γ on the tile."""
     s0, n = atlas_map.tile_range(tile_id)
     gamma = float(forgetting_factor)
-    _abi.call("gc_primitive_map_forget", atlas_map.ctx.handle, C.byref(atlas_map._struct), s0, n, gamma,
+    _abi.call("gc_primitive_map_forget", atlas_map.ctx.handle, C.byref(atlas_map.struct()), s0, n, gamma,
               ctx=atlas_map.ctx)
     return (PrimitiveMapForgetResult(atlas_map, int(tile_id)),
             CertBundle.create_exact(chart_id=chart_id, anchor_id=anchor_id),
@@ -227,7 +310,7 @@ def primitive_map_recency_inflate(atlas_map: DevicePrimitiveMap, tile_ids: List[
     for tid in tile_ids:
         s0, n = atlas_map.tile_range(tid)
         st = np.zeros(3)
-        _abi.call("gc_primitive_map_recency_inflate", atlas_map.ctx.handle, C.byref(atlas_map._struct), s0, n,
+        _abi.call("gc_primitive_map_recency_inflate", atlas_map.ctx.handle, C.byref(atlas_map.struct()), s0, n,
                   int(scan_seq), float(recency_decay_lambda), float(min_scale), st.ctypes.data, ctx=atlas_map.ctx)
         n_valid += st[0]
         downscale += st[1]
@@ -255,7 +338,7 @@ def primitive_map_cull(atlas_map: DevicePrimitiveMap, tile_id: int,
     """primitive_map_cull (primitive_map.py:1175-1305)."""
     s0, n = atlas_map.tile_range(tile_id)
     out = np.zeros(4)
-    _abi.call("gc_primitive_map_cull", atlas_map.ctx.handle, C.byref(atlas_map._struct), s0, n,
+    _abi.call("gc_primitive_map_cull", atlas_map.ctx.handle, C.byref(atlas_map.struct()), s0, n,
               float(weight_threshold), -1 if max_primitives is None else int(max_primitives), out.ctypes.data,
               ctx=atlas_map.ctx)
     n_culled, mass_dropped, sum_w, n_valid = int(out[0]), float(out[1]), float(out[2]), int(out[3])
@@ -305,10 +388,12 @@ def primitive_map_insert_masked(atlas_map: DevicePrimitiveMap, tile_id: int, Lam
     d_slots = _abi.DeviceArray(ctx, K, np.int32)
     d_ids = _abi.DeviceArray(ctx, K, np.int64)
     out = np.zeros(2, np.int64)
-    _abi.call("gc_primitive_map_insert_masked", ctx.handle, C.byref(atlas_map._struct), s0, n, C.byref(batch),
+    _abi.call("gc_primitive_map_insert_masked", ctx.handle, C.byref(atlas_map.struct()), s0, n, C.byref(batch),
               float(timestamp), int(scan_seq), float(recency_decay_lambda), int(atlas_map.next_global_id),
               d_slots.ptr, d_ids.ptr, out.ctypes.data, ctx=ctx)
     n_ins, count = int(out[0]), int(out[1])
+    if n_ins > 0:
+        atlas_map._tile_cc[int(tile_id)] = False  # inserted colours are clip(c), not the estimate clip(c·cam / cam)
     atlas_map.next_global_id += n_ins
     atlas_map.total_count += n_ins
     atlas_map.tile_count[int(tile_id)] = count
@@ -356,12 +441,13 @@ def primitive_map_merge_reduce(atlas_map: DevicePrimitiveMap, tile_id: int,
         return no_op(float(max_pairs), ["merge_reduce_budget_cap"],
                      InfluenceCert.identity().with_overrides(mass_epsilon_ratio=over))
     out = np.zeros(2, np.int64)
-    _abi.call("gc_primitive_map_merge_reduce", atlas_map.ctx.handle, C.byref(atlas_map._struct), s0, M,
+    _abi.call("gc_primitive_map_merge_reduce", atlas_map.ctx.handle, C.byref(atlas_map.struct()), s0, M,
               float(merge_threshold), int(max_pairs), float(eps_psd), float(eps_lift), out.ctypes.data,
               ctx=atlas_map.ctx)
     n_merged, count = int(out[0]), int(out[1])
     if n_merged <= 0:
         return no_op(float(max_pairs))
+    atlas_map._tile_cc[int(tile_id)] = False  # merged colours use max(denom, eps_psd) (primitive_map.py:1976-1983)
     atlas_map.tile_count[int(tile_id)] = count
     atlas_map.total_count -= n_merged
     cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=["primitive_map_merge_reduce"],

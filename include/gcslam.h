@@ -500,14 +500,26 @@ int32_t gc_hypothesis_barycenter(gc_ctx* ctx, int32_t H, const double* d_L, cons
 /* ------------------------------------------------------------------------------------------
  * C5 map update (a13 C5 analogue): transform_gaussian_to_world (backend/pipeline.py:1248-1256)
  * fused into primitive_map_fuse (backend/structures/primitive_map.py:992-1163). The map is one
- * flat tile of m_slots slots in device memory (SoA, row-major per slot); tile t / local slot j of
- * the reference map to slot t * m_tile + j. Colour fields are all NULL (no camera colour
- * tracking) or all set. All pointers inside the structs are device pointers.
+ * flat tile of m_slots slots in device memory; tile t / local slot j of the reference map to slot
+ * t * m_tile + j. Two layouts:
+ *   slot_bytes = 0  the reference's per-field arrays (SoA, row-major per slot): slot s of a field
+ *                   of width w at field + s * w;
+ *   slot_bytes > 0  one packed record per slot (gc_primitive_map_record_layout): every field
+ *                   pointer is the record array plus the field's offset, slot s of every field at
+ *                   (char*)field + s * slot_bytes. The fuse's read-modify-write fields share the
+ *                   record's first two 128-B lines, so a touched slot moves 2 lines each way
+ *                   instead of one partial line per field.
+ * Colour fields are all NULL (no camera colour tracking) or all set. All pointers inside the
+ * structs are device pointers.
  * ------------------------------------------------------------------------------------------ */
 typedef struct gc_primitive_map {
   int64_t m_slots;
   int32_t n_lobes;          /* GC_VMF_N_LOBES (3) */
-  int32_t pad_;
+  /* 1 when every slot's rgb and colors already equal the fuse's colour estimate of its camera
+     accumulators (the state a fuse leaves): the fuse then recomputes the colour of the slots it
+     touches only, which gives the same map as the reference's all-slot recompute
+     (primitive_map.py:1090-1098). 0: the fuse recomputes every slot. */
+  int32_t colors_current;
   double* Lambdas;          /* (M, 3, 3) */
   double* thetas;           /* (M, 3) */
   double* etas;             /* (M, n_lobes, 3) */
@@ -526,7 +538,21 @@ typedef struct gc_primitive_map {
   uint8_t* valid_mask;      /* (M) */
   double* created_timestamps;        /* (M) or NULL */
   int64_t* primitive_ids;            /* (M) or NULL */
+  int64_t slot_bytes;                /* 0 = per-field arrays; else the packed record's size */
 } gc_primitive_map;
+
+/* Packed slot record for n_lobes lobes (build-defined device layout; the reference's per-field
+   arrays are honoured at upload / download through gc_copy_strided). offsets_out (host, 16) =
+   byte offsets of Lambdas, thetas, etas, weights, timestamps, last_supported_scan_seq,
+   last_update_scan_seq, cam_mass, lidar_mass, rgb_cam_accum, rgb_cam_denom, rgb, colors,
+   valid_mask, created_timestamps, primitive_ids (the struct's field order); *slot_bytes_out = the
+   record size, a multiple of 128 B. */
+int32_t gc_primitive_map_record_layout(int32_t n_lobes, int64_t* offsets_out, int64_t* slot_bytes_out);
+/* rows x elem_bytes copied between device buffers with the given pitches (bytes; pitch >=
+   elem_bytes, elem_bytes a multiple of 1, rows >= 0): the transposes between a packed map and
+   per-field arrays. Asynchronous on the context's stream. */
+int32_t gc_copy_strided(gc_ctx* ctx, void* d_dst, int64_t dst_pitch, const void* d_src, int64_t src_pitch,
+                        int64_t elem_bytes, int64_t rows);
 
 typedef struct gc_fuse_batch {
   int64_t K;

@@ -156,13 +156,14 @@ def _compare(dm, tile_id, ref, rtol=1e-12):
 
 
 @pytest.mark.gpu
-def test_gpu_map_maintenance_sequence_matches_oracle(ctx):
+@pytest.mark.parametrize("packed", [True, False])
+def test_gpu_map_maintenance_sequence_matches_oracle(ctx, packed):
     """recency -> cull(max_primitives) -> insert_masked -> merge_reduce -> forget on tile 1 of a
-    3-tile map; tiles 0 and 2 must stay untouched."""
+    3-tile map; tiles 0 and 2 must stay untouched (either device layout)."""
     from gcslam import primitive_map as PM
     rng = np.random.default_rng(42)
     M = 300
-    dm = PM.DevicePrimitiveMap(3, M, ctx=ctx)
+    dm = PM.DevicePrimitiveMap(3, M, ctx=ctx, packed=packed)
     tiles = [_random_tile(rng, M) for _ in range(3)]
     for t_id, t in enumerate(tiles):
         _upload(dm, t_id, t)

@@ -1,5 +1,5 @@
-"""Summarise tools/pmc_fuse.sh: per C5 map kernel, HBM bytes per dispatch (2 x FETCH_SIZE, the gfx950
-correction of MI355X_MICROARCH.md 'HBM', + WRITE_SIZE) and the average duration from the kernel
+"""Summarise tools/pmc_fuse.sh: per C5 map kernel, HBM bytes per dispatch (reads by EA request size,
+with 2 x FETCH_SIZE beside it, + WRITE_SIZE) and the average duration from the kernel
 trace of the same command; the leg's algorithmic bytes from its bench JSON line."""
 import collections
 import csv
@@ -36,9 +36,16 @@ for leg in ("map-only", "c5-only"):
         if not (k.startswith("k_fuse") or k.startswith("k_smap") or k.startswith("rocprim:")):
             continue
         m = {c: sum(v) / len(v) for c, v in cs.items()}
-        rd, wr = 2.0 * m.get("FETCH_SIZE", 0.0) * 1024, m.get("WRITE_SIZE", 0.0) * 1024
+        # reads by request size (TCC_EA0_RDREQ_{128B,64B,32B}): these kernels' scattered 8-B loads are
+        # not the wide streaming reads the 2 x FETCH_SIZE correction is calibrated on; 2 x FETCH_SIZE is
+        # kept beside it
+        rd2 = 2.0 * m.get("FETCH_SIZE", 0.0) * 1024
+        sized = 128 * m.get("TCC_EA0_RDREQ_128B", 0.0) + 64 * m.get("TCC_EA0_RDREQ_64B", 0.0) + \
+            32 * m.get("TCC_EA0_RDREQ_32B", 0.0)
+        rd = sized if sized > 0 else rd2
+        wr = m.get("WRITE_SIZE", 0.0) * 1024
         us = sum(dur[k]) / len(dur[k]) if dur.get(k) else None
-        per[k[:90]] = {"read_bytes": rd, "write_bytes": wr, "avg_us": us,
+        per[k[:90]] = {"read_bytes": rd, "read_bytes_2x_fetch_size": rd2, "write_bytes": wr, "avg_us": us,
                        "GB/s": (rd + wr) / (us * 1e-6) / 1e9 if us else None}
     line = [l for l in open(os.path.join(src, leg + ".kt.log")) if l.startswith("{")]
     out[leg] = {"kernels": per, "bench": json.loads(line[-1]) if line else None}

@@ -7,8 +7,10 @@ round=${1:-r01}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 out=gpurun_out/$round
 rm -rf $out; mkdir -p $out
-timeout -k 10 300 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > $out/gpu_tests.log 2>&1
+# a failing assertion does not stop the evidence run; a fault, abort or time limit does
+rc=0; timeout -k 10 400 python -u -m pytest tests -q -m gpu --timeout 120 --timeout-method thread > $out/gpu_tests.log 2>&1 || rc=$?
 tail -2 $out/gpu_tests.log
+case $rc in 124|134|137|139) echo "gpu tests stopped rc=$rc"; exit $rc;; esac
 timeout -k 10 300 python3 bench.py > $out/bench.json 2> $out/bench.err
 tail -c 400 $out/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $out/kt -o kt --output-format csv -- python3 bench.py --no-cpu > $out/bench_rocprof.json 2> $out/bench_rocprof.err
