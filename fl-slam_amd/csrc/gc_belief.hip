@@ -252,9 +252,7 @@ static size_t lds_predict() {
 }
 
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  if (hipError_t e = hipFuncSetAttribute((const void*)k_predict_imu, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                         (int)lds_predict()))
-    return e;
+  if (hipError_t e = ensure_dyn_lds((const void*)k_predict_imu, lds_predict())) return e;
   // P.Hl hypothesis workgroups + kBudgetBlocks a1 budget workgroups (S.w_raw, S.n_in)
   hipLaunchKernelGGL(k_predict_imu, dim3(P.Hl + kBudgetBlocks), dim3(256), lds_predict(), st, P, S);
   return hipGetLastError();

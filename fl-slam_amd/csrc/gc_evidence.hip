@@ -596,7 +596,7 @@ static size_t lds_final() { return sizeof(double) * (2 * NN + 2 * NN + 4 * kDZ +
 
 namespace gc {
 static hipError_t allow_big_lds(const void* fn, size_t bytes) {
-  return bytes > 65536 ? hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) : hipSuccess;
+  return bytes > 65536 ? ensure_dyn_lds(fn, bytes) : hipSuccess;
 }
 hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
   if (hipError_t e = allow_big_lds((const void*)k_evidence, lds_evidence())) return e;

@@ -22,6 +22,11 @@ void set_error(gc_ctx* ctx, const std::string& msg);
 // device scratch of at least `bytes` (synchronises the stream before growing)
 int scratch(gc_ctx* ctx, size_t bytes, void** out);
 
+// hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) only when fn has not yet been allowed that
+// much: the runtime call is not free (it waited for an in-flight ingest copy on another stream,
+// delaying the next launch by its duration), so the per-scan launches skip it after the first
+hipError_t ensure_dyn_lds(const void* fn, size_t bytes);
+
 }  // namespace gc
 
 #define GC_CHECK_ARG(ctx, cond, msg)                   \

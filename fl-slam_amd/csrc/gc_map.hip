@@ -38,7 +38,9 @@ struct FuseArgs {
 
 // One measurement row in the world frame (pipeline.py:1248-1256): Λ_w = R Λ Rᵀ,
 // μ_b = (Λ + ε I)⁻¹ θ, μ_w = R μ_b + t, θ_w = Λ_w μ_w, η_w = R η (each lobe).
-GC_DEV void meas_world(const FuseArgs& A, const double* R, int64_t k, int L, double* Lw, double* th, double* et) {
+template <int LT>  // LT > 0: the lobe count at compile time (registers, no scratch); 0: A.map.n_lobes
+GC_DEV void meas_world(const FuseArgs& A, const double* R, int64_t k, double* Lw, double* th, double* et) {
+  const int L = LT > 0 ? LT : A.map.n_lobes;
   const double* Lb = A.meas.Lambdas + 9 * k;
   const double* tb = A.meas.thetas + 3 * k;
   const double* eb = A.meas.etas + (int64_t)3 * L * k;
@@ -74,12 +76,14 @@ __host__ __device__ constexpr int stage_doubles(int L) { return (19 + 3 * L + 15
 // Rows leave through a wave-private LDS slab (row stride SD + 2), so the wave's 64 consecutive staged
 // records go out as one contiguous block, 16 B per lane (whole-line stores; lane-private records of
 // 8-B stores left partially written lines in the L2s: ~3.4x the staged bytes reached HBM).
+template <int LT>
 __global__ void __launch_bounds__(256) k_fuse_keys(FuseArgs A, int64_t K, uint32_t* keys, uint32_t* vals,
                                                    double* stage) {
 #pragma clang fp contract(off)  // the products rounded as the reference's r * X
   typedef double dvec2 __attribute__((ext_vector_type(2)));
   extern __shared__ __attribute__((aligned(16))) double fk_lds[];
-  const int L = A.map.n_lobes;
+  constexpr int LM = LT > 0 ? LT : kMaxLobes;
+  const int L = LT > 0 ? LT : A.map.n_lobes;
   const int SD = stage_doubles(L), RS = SD + 2;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   double* slab = fk_lds + wv * 64 * RS;
@@ -97,8 +101,8 @@ __global__ void __launch_bounds__(256) k_fuse_keys(FuseArgs A, int64_t K, uint32
       double R[9];
       if (A.world) so3_exp(A.pose + 3, R);
       const double r = A.meas.responsibilities[k] * ((A.meas.valid_mask && !A.meas.valid_mask[k]) ? 0.0 : 1.0);
-      double Lw[9], th[3], et[3 * kMaxLobes];
-      meas_world(A, R, k, L, Lw, th, et);
+      double Lw[9], th[3], et[3 * LM];
+      meas_world<LT>(A, R, k, Lw, th, et);
       for (int q = 0; q < 9; ++q) o[q] = r * Lw[q];
       for (int q = 0; q < 3; ++q) o[9 + q] = r * th[q];
       for (int q = 0; q < 3 * L; ++q) o[12 + q] = r * et[q];
@@ -214,19 +218,17 @@ GC_DEV void fuse_segment32(const FuseArgs& A, int64_t i, int64_t K, uint32_t key
 }
 
 // the segment of sorted rows starting at i (its head) summed in row order and applied to its slot
+template <int LT>
 GC_DEV void fuse_segment(const FuseArgs& A, int64_t i, int64_t K, uint32_t key, const uint32_t* __restrict__ keys,
                          const uint32_t* __restrict__ vals, const double* __restrict__ stage) {
 #pragma clang fp contract(off)
+  constexpr int LM = LT > 0 ? LT : kMaxLobes;
   const gc_primitive_map& m = A.map;
-  const int L = m.n_lobes;
+  const int L = LT > 0 ? LT : m.n_lobes;
   const int64_t s = key;
-  if (A.rec32) {
-    fuse_segment32(A, i, K, key, keys, vals, stage);
-    return;
-  }
   // the slot's current values are loaded first: they do not depend on the rows, so their latency
   // overlaps the row gathers (one dependent memory round trip fewer per slot)
-  double mL[9], mth[3], met[3 * kMaxLobes], mw, mcam = 0.0, mlid = 0.0, macc[3] = {0, 0, 0}, mden = 0.0;
+  double mL[9], mth[3], met[3 * LM], mw, mcam = 0.0, mlid = 0.0, macc[3] = {0, 0, 0}, mden = 0.0;
   const double* Ls0 = mLam(m, s);
   const double* th0 = mTh(m, s);
   const double* et0 = mEta(m, s);
@@ -241,7 +243,7 @@ GC_DEV void fuse_segment(const FuseArgs& A, int64_t i, int64_t K, uint32_t key, 
     for (int q = 0; q < 3; ++q) macc[q] = a0[q];
     mden = mDen(m, s);
   }
-  double dL[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, dth[3] = {0, 0, 0}, det[3 * kMaxLobes], dw = 0.0, dr = 0.0;
+  double dL[9] = {0, 0, 0, 0, 0, 0, 0, 0, 0}, dth[3] = {0, 0, 0}, det[3 * LM], dw = 0.0, dr = 0.0;
   double dcam = 0.0, dlid = 0.0, dacc[3] = {0, 0, 0}, dden = 0.0;
   for (int q = 0; q < 3 * L; ++q) det[q] = 0.0;
   const bool col = A.meas.sources && A.meas.colors;  // colour accumulators only with colours (:1079-1083)
@@ -289,6 +291,7 @@ GC_DEV void fuse_segment(const FuseArgs& A, int64_t i, int64_t K, uint32_t key, 
 }
 
 // one thread per sorted row; the head of each slot's segment fuses it
+template <int LT, bool R32>  // R32: the packed 3-lobe record (A.rec32, fuse_segment32)
 __global__ void __launch_bounds__(256) k_fuse_segments(FuseArgs A, int64_t K, const uint32_t* __restrict__ keys,
                                                        const uint32_t* __restrict__ vals,
                                                        const double* __restrict__ stage,
@@ -297,7 +300,10 @@ __global__ void __launch_bounds__(256) k_fuse_segments(FuseArgs A, int64_t K, co
   const uint32_t key = i < K ? keys[i] : 0u;
   // in range, and not a dropped row or the continuation of a segment
   const bool head = i < K && (int64_t)key < A.map.m_slots && (i == 0 || keys[i - 1] != key);
-  if (head) fuse_segment(A, i, K, key, keys, vals, stage);
+  if (head) {
+    if constexpr (R32) fuse_segment32(A, i, K, key, keys, vals, stage);
+    else fuse_segment<LT>(A, i, K, key, keys, vals, stage);
+  }
   const unsigned long long b = __ballot(head);  // the distinct-slot count, one atomic per wave
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_unique, (unsigned long long)__popcll(b));
 }
@@ -399,16 +405,28 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   const unsigned grid = (unsigned)((K + 255) / 256);
   GC_HIP(ctx, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), ctx->stream));
   const size_t lds_keys = sizeof(double) * 4 * 64 * (stage_doubles(map->n_lobes) + 2);
-  GC_HIP(ctx, hipFuncSetAttribute((const void*)k_fuse_keys, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_keys));
-  hipLaunchKernelGGL(k_fuse_keys, dim3(grid), dim3(256), lds_keys, ctx->stream, A, K, keys_in, vals_in, stage);
+  const bool l3 = map->n_lobes == 3;  // GC_VMF_N_LOBES: the compile-time lobe count
+  const void* fk = l3 ? (const void*)k_fuse_keys<3> : (const void*)k_fuse_keys<0>;
+  GC_HIP(ctx, gc::ensure_dyn_lds(fk, lds_keys));
+  if (l3)
+    hipLaunchKernelGGL(k_fuse_keys<3>, dim3(grid), dim3(256), lds_keys, ctx->stream, A, K, keys_in, vals_in, stage);
+  else
+    hipLaunchKernelGGL(k_fuse_keys<0>, dim3(grid), dim3(256), lds_keys, ctx->stream, A, K, keys_in, vals_in, stage);
   GC_LAUNCH_CHECK(ctx);
   if (hipcub::DeviceRadixSort::SortPairs(tmp, temp, keys_in, keys, vals_in, vals, (int)K, 0, key_bits(map->m_slots),
                                          ctx->stream) != hipSuccess) {
     gc::set_error(ctx, "radix sort failed");
     return GC_ERR_RUNTIME;
   }
-  hipLaunchKernelGGL(k_fuse_segments, dim3(grid), dim3(256), 0, ctx->stream, A, K, keys, vals,
-                     (const double*)stage, cnt);
+  if (A.rec32)
+    hipLaunchKernelGGL((k_fuse_segments<3, true>), dim3(grid), dim3(256), 0, ctx->stream, A, K, keys, vals,
+                       (const double*)stage, cnt);
+  else if (l3)
+    hipLaunchKernelGGL((k_fuse_segments<3, false>), dim3(grid), dim3(256), 0, ctx->stream, A, K, keys, vals,
+                       (const double*)stage, cnt);
+  else
+    hipLaunchKernelGGL((k_fuse_segments<0, false>), dim3(grid), dim3(256), 0, ctx->stream, A, K, keys, vals,
+                       (const double*)stage, cnt);
   GC_LAUNCH_CHECK(ctx);
   if (color && !map->colors_current) {
     hipLaunchKernelGGL(k_fuse_colors, dim3((unsigned)((map->m_slots + 255) / 256)), dim3(256), 0, ctx->stream, *map,

@@ -569,7 +569,7 @@ __global__ void __launch_bounds__(256) k_op_barycenter(int H, const double* L, c
 
 size_t lds_bytes(int doubles) { return sizeof(double) * (size_t)doubles; }
 hipError_t allow_lds(const void* fn, size_t bytes) {
-  return bytes > 65536 ? hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes) : hipSuccess;
+  return bytes > 65536 ? ensure_dyn_lds(fn, bytes) : hipSuccess;
 }
 
 }  // namespace

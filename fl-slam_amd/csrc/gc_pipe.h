@@ -113,6 +113,7 @@ namespace gc {
 // a1 -> a6 bins of the local hypotheses (+ the IMU/odom branch's workgroups in the same launch when
 // io) and their finalize into P.stats / P.bincert (gc_points.hip)
 int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
-                           const double* d_pts, const double* d_t, const double* d_w, int64_t n_in);
+                           const double* d_pts, const double* d_t, const double* d_w, int64_t n_in,
+                           hipEvent_t done = nullptr);  // done: recorded with the finalize's completion
 
 }  // namespace gc

@@ -410,10 +410,14 @@ int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_pts
   GC_TRY(slot_stage_imu_host(p, s, h_imu_t, h_imu_g, h_imu_a));
   GC_TRY(slot_wait_consumed(p, s));
   const hipMemcpyKind k = hipMemcpyHostToDevice;
-  GC_HIP(p->ctx, hipMemcpyAsync(s.pts, s.host, 3 * n * sizeof(double), k, p->cstream));
-  GC_HIP(p->ctx, hipMemcpyAsync(s.t, s.host + Ly.t, n * sizeof(double), k, p->cstream));
-  GC_HIP(p->ctx, hipMemcpyAsync(s.w, s.host + Ly.w, n * sizeof(double), k, p->cstream));
-  GC_HIP(p->ctx, hipMemcpyAsync(s.imu_t, s.host + Ly.imu, 7 * M * sizeof(double), k, p->cstream));
+  if (n == (size_t)p->P.n_in) {  // a full scan: points, times, weights and IMU are one contiguous block
+    GC_HIP(p->ctx, hipMemcpyAsync(s.pts, s.host, (Ly.imu + 7 * M) * sizeof(double), k, p->cstream));
+  } else {
+    GC_HIP(p->ctx, hipMemcpyAsync(s.pts, s.host, 3 * n * sizeof(double), k, p->cstream));
+    GC_HIP(p->ctx, hipMemcpyAsync(s.t, s.host + Ly.t, n * sizeof(double), k, p->cstream));
+    GC_HIP(p->ctx, hipMemcpyAsync(s.w, s.host + Ly.w, n * sizeof(double), k, p->cstream));
+    GC_HIP(p->ctx, hipMemcpyAsync(s.imu_t, s.host + Ly.imu, 7 * M * sizeof(double), k, p->cstream));
+  }
   GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));
   s.ready_rec = true;
   s.n_in = n_in;
@@ -601,13 +605,11 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   // a1 -> a4 -> a5 -> a6 fused over all local hypotheses, and the a9a IMU/odom evidence branch
   // (pipeline.py:595-776: it needs the prediction, not the bins) as extra workgroups of the same
   // launch
-  GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in));
   // nothing after the bins reads the slot (but the in-scan map update in scan_finish, when a map
-  // is attached): the next staging into it may proceed from here
-  if (!p->smap_on) {
-    GC_HIP(ctx, hipEventRecord(s.consumed, ctx->stream));
-    s.consumed_rec = true;
-  }
+  // is attached): the next staging into it may proceed from here; `consumed` completes with the
+  // bins' finalize launch
+  GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in, p->smap_on ? nullptr : s.consumed));
+  if (!p->smap_on) s.consumed_rec = true;
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
   p->sig_cached = true;

@@ -12,6 +12,7 @@
 // record per (hypothesis, chunk). A finalize kernel sums the records in chunk order, so every
 // result is bit-reproducible run to run (no float atomics anywhere).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include <algorithm>
 #include <cstdint>
 #include <type_traits>
@@ -1558,13 +1559,11 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
   do {                                                                                                   \
     const size_t sh = sizeof(double) * (size_t)sa_lds_doubles(BP, full);                                 \
     if (full) {                                                                                          \
-      GC_HIP(ctx, hipFuncSetAttribute((const void*)k_soft_assign<BP, true>,                              \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));            \
+      GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_soft_assign<BP, true>, sh));                          \
       hipLaunchKernelGGL((k_soft_assign<BP, true>), grid, dim3(256), sh, ctx->stream, n, B, iters, d_dirs, \
                          d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr);                    \
     } else {                                                                                             \
-      GC_HIP(ctx, hipFuncSetAttribute((const void*)k_soft_assign<BP, false>,                             \
-                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));            \
+      GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_soft_assign<BP, false>, sh));                         \
       hipLaunchKernelGGL((k_soft_assign<BP, false>), grid, dim3(256), sh, ctx->stream, n, B, iters, d_dirs, \
                          d_bins, inv_tau, d_resp_out, d_bin_index_out, (double*)scr);                    \
     }                                                                                                    \
@@ -1663,8 +1662,7 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const FusedArgs FA{n_cap, B, iters, d_points_raw, d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins,
                      1.0 / tau, h_origin3[0], h_origin3[1], h_origin3[2], (double*)scr, nullptr, chunks, iters};
 #define GC_FUSED(BP, FULL)                                                                                     \
-  GC_HIP(ctx, hipFuncSetAttribute((const void*)k_bins_fused<BP, FULL>,                                          \
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, (int)sh));                        \
+  GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_bins_fused<BP, FULL>, sh));                                   \
   hipLaunchKernelGGL((k_bins_fused<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA)
   const bool full = B == 16 * bpl;
   switch (bpl) {
@@ -1684,7 +1682,8 @@ namespace gc {
 // The batched pipeline's a1 -> a6 bins for its Hl local hypotheses, with the IMU/odom branch's
 // workgroups in the same launch when io (k_bins_io), then the chunk-order finalize.
 int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
-                           const double* d_pts, const double* d_t, const double* d_w, int64_t n_in) {
+                           const double* d_pts, const double* d_t, const double* d_w, int64_t n_in,
+                           hipEvent_t done) {
   (void)n_in;
   if (ctx->cu_count == 0) {
     int cus = 0;
@@ -1731,8 +1730,7 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   const size_t sh = sizeof(double) * std::max<size_t>(fused_lds_doubles(B), io ? (size_t)kIoLdsDoubles : 0);
   const dim3 grid((unsigned)(n_io + pullers));
 #define GC_BIO(BP, FULL)                                                                                       \
-  GC_HIP(ctx, hipFuncSetAttribute((const void*)k_bins_io<BP, FULL>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                                  (int)sh));                                                                   \
+  GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_bins_io<BP, FULL>, sh));                                      \
   hipLaunchKernelGGL((k_bins_io<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA, P, S, d_odom, n_io, H, chunks, \
                      P.task_ctr)
   const int bpl = bpl_for(B);
@@ -1746,8 +1744,10 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
 #undef GC_BIO
   GC_LAUNCH_CHECK(ctx);
   const dim3 fgrid((unsigned)((B + kFinBins - 1) / kFinBins), (unsigned)H);
-  hipLaunchKernelGGL(k_bins_finalize_split, fgrid, dim3(kFinSplitWG), 0, ctx->stream, B, NF, chunks,
-                     (const double*)scr, P.eps_psd, P.eps_mass, P.stats, P.bincert, P.binaux);
+  // `done` rides on the finalize's own completion signal (no separate barrier packet in the stream:
+  // a standalone event record cost a ~5 us gap before the next kernel at H = 32)
+  hipExtLaunchKernelGGL(k_bins_finalize_split, fgrid, dim3(kFinSplitWG), 0, ctx->stream, nullptr, done, 0, B, NF,
+                        chunks, (const double*)scr, P.eps_psd, P.eps_mass, P.stats, P.bincert, P.binaux);
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
 }
@@ -1781,7 +1781,7 @@ int32_t gc_domain_projection_psd_batch(gc_ctx* ctx, int32_t batch, int32_t d, co
     const int dp = d + (d & 1);
     const size_t ws = sizeof(double) * (size_t)psd_ws_len(dp);
     if (dp <= 64) {
-      GC_HIP(ctx, hipFuncSetAttribute((const void*)k_psd_any, hipFuncAttributeMaxDynamicSharedMemorySize, (int)ws));
+      GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_psd_any, ws));
       hipLaunchKernelGGL(k_psd_any, dim3(batch), dim3(256), ws, ctx->stream, d, d_M, eps_psd, d_M_out, d_cert_out,
                          (double*)nullptr);
     } else {

@@ -2,6 +2,8 @@
 #include <hip/hip_runtime.h>
 #include <cstring>
 #include <string>
+#include <mutex>
+#include <unordered_map>
 #include "gc_internal.h"
 
 struct gc_event {
@@ -17,6 +19,17 @@ namespace gc {
 void set_error(gc_ctx* ctx, const std::string& msg) {
   if (ctx) ctx->err = msg;
   tl_error = msg;
+}
+
+hipError_t ensure_dyn_lds(const void* fn, size_t bytes) {
+  static std::mutex mu;
+  static std::unordered_map<const void*, size_t> allowed;
+  std::lock_guard<std::mutex> lock(mu);
+  size_t& a = allowed[fn];
+  if (bytes <= a) return hipSuccess;
+  const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess) a = bytes;
+  return e;
 }
 
 int scratch(gc_ctx* ctx, size_t bytes, void** out) {
