@@ -490,6 +490,9 @@ GC_DEV void sa_store_block(const double* S, double* Rh, int64_t wbase, int64_t n
 #ifndef GC_SA_NT
 #define GC_SA_NT 1
 #endif
+#ifndef GC_SA_SBINS
+#define GC_SA_SBINS 1
+#endif
 #ifndef GC_SA_OCC
 // 2 waves per SIMD: the 48 similarities / exps of a lane's point stay in registers with no spill
 // (at 3, the 168-VGPR budget spilled ~12-27 VGPRs per point to scratch: 0.6 GB of extra HBM reads and
@@ -566,7 +569,15 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
     int bidx = 0;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
+#if GC_SA_SBINS
+      // bin directions as wave-uniform scalar loads (SGPR operands; the LDS pipe keeps the exp table
+      // and the row transposes)
+      const double bx = FULL || j < B ? bins[3 * j] : 0.0, by = FULL || j < B ? bins[3 * j + 1] : 0.0,
+                   bz = FULL || j < B ? bins[3 * j + 2] : 0.0;
+      ex[j] = sim_nofma(d0, d1, d2, bx, by, bz);
+#else
       ex[j] = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
+#endif
       if ((FULL || j < B) && ex[j] > best) { best = ex[j]; bidx = j; }
     }
     // exponent in units of ln2/2048 (the 2048-entry table exp, exp2s_n): y = S ysc - S_max ysc by one
