@@ -929,6 +929,9 @@ constexpr int kFusedFS = 66;
 #ifndef GC_FUSED_OCC
 #define GC_FUSED_OCC 2  // waves per SIMD the register budget is sized for (tuning knob, probes)
 #endif
+#ifndef GC_FUSED_UNR
+#define GC_FUSED_UNR 8  // softmax steps unrolled per block (Π Z renormalised after each block: exact)
+#endif
 #ifndef GC_FUSED_NACC
 #define GC_FUSED_NACC 2  // MFMA accumulator sets (even / odd steps)
 #endif
@@ -1070,9 +1073,9 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
         F[(NF + 3) * kFusedFS + lane] = inr ? 1.0 : 0.0;
       }
       lds_wave_sync();
-      for (int s8 = 0; s8 < 16; s8 += 8) {
+      for (int s8 = 0; s8 < 16; s8 += GC_FUSED_UNR) {
   #pragma unroll
-      for (int s = s8; s < s8 + 8; ++s) {
+      for (int s = s8; s < s8 + GC_FUSED_UNR; ++s) {
         const int pl = s * 4 + g;
         const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
         const double vf = PAD ? F[(NF + 3) * kFusedFS + pl] : 1.0;  // 1 for a point of the chunk, 0 for padding
