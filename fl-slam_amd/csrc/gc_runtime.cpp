@@ -3,7 +3,7 @@
 #include <cstring>
 #include <string>
 #include <mutex>
-#include <unordered_map>
+#include <map>
 #include "gc_internal.h"
 
 struct gc_event {
@@ -23,9 +23,11 @@ void set_error(gc_ctx* ctx, const std::string& msg) {
 
 hipError_t ensure_dyn_lds(const void* fn, size_t bytes) {
   static std::mutex mu;
-  static std::unordered_map<const void*, size_t> allowed;
+  static std::map<std::pair<int, const void*>, size_t> allowed;  // per (device, kernel)
+  int dev = 0;
+  if (hipError_t e = hipGetDevice(&dev)) return e;
   std::lock_guard<std::mutex> lock(mu);
-  size_t& a = allowed[fn];
+  size_t& a = allowed[{dev, fn}];
   if (bytes <= a) return hipSuccess;
   const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
   if (e == hipSuccess) a = bytes;
