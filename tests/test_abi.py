@@ -42,3 +42,28 @@ def test_version_and_null_ctx_errors():
     assert _abi.lib().gc_version() >= 10000
     with pytest.raises(ValueError):
         _abi.check(_abi.lib().gc_ctx_synchronize(None))
+
+
+@pytest.mark.skipif(not os.path.exists(LIB), reason="libgcslam.so not built")
+def test_packed_map_record_layout():
+    """gc_primitive_map_record_layout (host-only): the fuse's read-modify-write fields in the first
+    two 128-B lines of a 128-B-multiple record, no two fields overlapping, any lobe count; the Python
+    map struct matches the header's field order and size."""
+    import numpy as np
+    from gcslam import _abi
+    from gcslam.primitive_map import _MapStruct
+    widths = lambda L: [72, 24, 24 * L, 8, 8, 8, 8, 8, 8, 24, 8, 24, 24, 1, 8, 8]  # struct field order
+    for L in range(1, 9):
+        off = np.zeros(16, np.int64)
+        sb = ctypes.c_int64(0)
+        _abi.call("gc_primitive_map_record_layout", L, off.ctypes.data, ctypes.byref(sb))
+        w = widths(L)
+        spans = sorted((int(o), int(o) + w[k]) for k, o in enumerate(off))
+        assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:])), (L, spans)
+        assert sb.value % 128 == 0 and spans[-1][1] <= sb.value
+        if L <= 3:  # Λ θ η w stamp seqs cam lidar accum denom: the first two lines
+            assert max(int(off[k]) + w[k] for k in range(11)) <= 256
+    with pytest.raises(ValueError):
+        _abi.call("gc_primitive_map_record_layout", 9, off.ctypes.data, ctypes.byref(sb))
+    # int64 m_slots, int32 n_lobes, int32 colors_current, 16 pointers, int64 slot_bytes
+    assert ctypes.sizeof(_MapStruct) == 8 + 4 + 4 + 16 * 8 + 8
