@@ -146,6 +146,9 @@ def bytes_moment_match(n, B):
     return n * (24 + 72 + 8 + 8 + B * 8) + 24 + B * (1 + 3 + 9 + 3 + 9 + 1) * 8
 
 
+INGEST_SLOTS = 3  # scan slots in the ingest rotation of the C3 step
+
+
 def warmup_map_record(ctx, _abi, scan, n, B, bins, origin):
     """Initial MapBinStats from one warm-up scan at the identity pose (zero pose covariance):
     the GPU bin statistics of the un-deskewed scan, pushed forward with R = I, t = 0."""
@@ -243,16 +246,18 @@ def main():
 
     def step(timed=False):
         # with ingest, step k stages scan k+1 from host memory (pinned mirror + DMA on the copy
-        # stream) into the other of two slots, then runs scan k: the copy of the next scan overlaps
-        # this scan's compute (double-buffered ingest, as a live node receives scan k+1 while it
-        # processes scan k); every step stages exactly one scan
+        # stream) into the next of three slots in rotation, then runs scan k: the copy of the next
+        # scan overlaps this scan's compute (as a live node receives scan k+1 while it processes scan
+        # k); every step stages exactly one scan. The slot it overwrites was read by scan k-2, whose
+        # bins have normally published their completion already, so the DMA needs no ordering
+        # event in the compute stream (gc_pipeline.cpp, done_word)
         k = count[0]
         sc = scans[k % len(scans)]
         if ingest:
             ts = time.perf_counter()
-            pipe.stage_scan((k + 1) % 2, scans[(k + 1) % len(scans)])
+            pipe.stage_scan((k + 1) % INGEST_SLOTS, scans[(k + 1) % len(scans)])
             tr = time.perf_counter()
-            pipe.run_scan(k % 2, sc, k)
+            pipe.run_scan(k % INGEST_SLOTS, sc, k)
             if timed:
                 stage_s[0] += tr - ts
                 stage_s[1] += 1
@@ -320,7 +325,7 @@ def main():
                                "barycenter combine)" % H_total,
                    "points": n, "hypotheses": H_total, "bins": B, "parallelism": "hypotheses/%d" % dist.world,
                    "ingest": ("every step stages one scan host -> HBM (pinned mirror + DMA on a copy stream): "
-                              "step k stages scan k+1 while scan k computes (double-buffered)") if ingest else
+                              "step k stages scan k+1 while scan k computes (three slots in rotation)") if ingest else
                              "scans pre-staged in HBM before the timed region"},
     }
     if exchange is not None:

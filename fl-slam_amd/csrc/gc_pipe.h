@@ -114,6 +114,7 @@ namespace gc {
 // io) and their finalize into P.stats / P.bincert (gc_points.hip)
 int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
                            const double* d_pts, const double* d_t, const double* d_w, int64_t n_in,
-                           hipEvent_t done = nullptr);  // done: recorded with the finalize's completion
+                           int64_t* done_word = nullptr, int64_t ticket = 0);  // done_word: `ticket` stored
+                                                                                // once the bins have completed
 
 }  // namespace gc

@@ -40,7 +40,18 @@ struct gc_pipeline {
     hipEvent_t odom_done = nullptr;  // copy stream: the odometry DMA has read its pinned area
     hipEvent_t consumed = nullptr;   // compute stream: the last scan that read the slot is past it
     bool ready_rec = false, odom_rec = false, consumed_rec = false;
+    // without a PrimitiveMap the slot's last reader is the bins launch of the scan with this ticket
+    // (0 = not read since staged); see done_word
+    int64_t consumed_ticket = 0;
   } slots[GC_PIPE_MAX_SLOTS];
+  // Host-coherent pinned word: the ticket of the last scan whose bins have completed, written by that
+  // scan's finalize kernel (one system-scope store). Staging into a slot whose last scan has already
+  // published its ticket needs no ordering on the device at all; only otherwise is an event recorded
+  // on the compute stream for the copy stream to wait on. A per-scan event between two kernels cost a
+  // ~5 us gap before the next one, and with three or more slots in rotation the word almost always
+  // suffices.
+  int64_t* done_word = nullptr;
+  int64_t ticket = 0;
   hipStream_t cstream = nullptr;  // ingest (copy) stream
   int io_mode = GC_IO_COMPUTED;
   gc_comm* comm = nullptr;
@@ -144,7 +155,16 @@ int slot_check_restage(gc_pipeline* p, int slot) {
 }
 
 int slot_wait_consumed(gc_pipeline* p, gc_pipeline::Slot& s) {
+  if (s.consumed_ticket > 0) {
+    if (__atomic_load_n(p->done_word, __ATOMIC_ACQUIRE) < s.consumed_ticket) {
+      // its bins may still be running: order the DMA after everything enqueued on the compute stream
+      GC_HIP(p->ctx, hipEventRecord(s.consumed, p->ctx->stream));
+      s.consumed_rec = true;
+    }
+    s.consumed_ticket = 0;
+  }
   if (s.consumed_rec) GC_HIP(p->ctx, hipStreamWaitEvent(p->cstream, s.consumed, 0));
+  s.consumed_rec = false;
   return GC_OK;
 }
 
@@ -227,6 +247,11 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   if (rc == GC_OK) rc = dalloc(p, 1, &ctr);  // zeroed: k_bins_io's task counter + finished pullers
   P.task_ctr = reinterpret_cast<unsigned*>(ctr);
   if (rc == GC_OK) rc = dalloc(p, (size_t)P.n_cap, &P.w_win);
+  if (rc == GC_OK && hipHostMalloc((void**)&p->done_word, sizeof(int64_t), hipHostMallocCoherent) != hipSuccess) {
+    gc::set_error(ctx, "hipHostMalloc failed for the slot completion word");
+    rc = GC_ERR_RUNTIME;
+  }
+  if (p->done_word) *p->done_word = 0;
   if (rc == GC_OK && hipStreamCreateWithFlags(&p->cstream, hipStreamNonBlocking) != hipSuccess) {
     gc::set_error(ctx, "hipStreamCreateWithFlags failed for the ingest stream");
     rc = GC_ERR_RUNTIME;
@@ -257,6 +282,7 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
     if (e) (void)hipEventDestroy(e);
   if (p->smapW.buf) (void)hipFree(p->smapW.buf);
   if (p->cstream) (void)hipStreamDestroy(p->cstream);
+  if (p->done_word) (void)hipHostFree(p->done_word);
   delete p;
   return GC_OK;
 }
@@ -606,10 +632,12 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   // (pipeline.py:595-776: it needs the prediction, not the bins) as extra workgroups of the same
   // launch
   // nothing after the bins reads the slot (but the in-scan map update in scan_finish, when a map
-  // is attached): the next staging into it may proceed from here; `consumed` completes with the
-  // bins' finalize launch
-  GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in, p->smap_on ? nullptr : s.consumed));
-  if (!p->smap_on) s.consumed_rec = true;
+  // is attached): the next staging into it may proceed once the bins are done, which the finalize
+  // kernel publishes as this scan's ticket (done_word)
+  ++p->ticket;
+  GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in, p->smap_on ? nullptr : p->done_word,
+                                p->ticket));
+  if (!p->smap_on) s.consumed_ticket = p->ticket;
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
   p->sig_cached = true;

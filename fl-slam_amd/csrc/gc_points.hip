@@ -12,7 +12,6 @@
 // record per (hypothesis, chunk). A finalize kernel sums the records in chunk order, so every
 // result is bit-reproducible run to run (no float atomics anywhere).
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 #include <algorithm>
 #include <cstdint>
 #include <type_traits>
@@ -1342,8 +1341,15 @@ static_assert(kFinBins * NF_BASE + REC_EXTRA <= kFinSplitWG, "one lane per recor
 __global__ void __launch_bounds__(kFinSplitWG) k_bins_finalize_split(int B, int NF, int64_t chunks,
                                                                      const double* __restrict__ partials,
                                                                      double eps_psd, double eps_mass, double* stats,
-                                                                     double* cert, double* aux) {
+                                                                     double* cert, double* aux, int64_t* done_word,
+                                                                     int64_t ticket) {
   __shared__ double sm[kFinBins * NF_BASE + REC_EXTRA];
+  // the bins launch before this one on the stream has completed, its reads of the scan slot
+  // included: publish the scan's ticket to the host-coherent word the pipeline's staging checks.
+  // Relaxed at system scope: one write-through store, no L2 writeback (nothing written before it
+  // has to be visible to the host).
+  if (done_word && blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0)
+    __hip_atomic_store(done_word, ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   const int h = blockIdx.y, s = blockIdx.x;
   const int RL = B * NF + REC_EXTRA;
   const int b0 = s * kFinBins, nb = min(kFinBins, B - b0);
@@ -1697,7 +1703,7 @@ namespace gc {
 // workgroups in the same launch when io (k_bins_io), then the chunk-order finalize.
 int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
                            const double* d_pts, const double* d_t, const double* d_w, int64_t n_in,
-                           hipEvent_t done) {
+                           int64_t* done_word, int64_t ticket) {
   (void)n_in;
   if (ctx->cu_count == 0) {
     int cus = 0;
@@ -1758,10 +1764,8 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
 #undef GC_BIO
   GC_LAUNCH_CHECK(ctx);
   const dim3 fgrid((unsigned)((B + kFinBins - 1) / kFinBins), (unsigned)H);
-  // `done` rides on the finalize's own completion signal (no separate barrier packet in the stream:
-  // a standalone event record cost a ~5 us gap before the next kernel at H = 32)
-  hipExtLaunchKernelGGL(k_bins_finalize_split, fgrid, dim3(kFinSplitWG), 0, ctx->stream, nullptr, done, 0, B, NF,
-                        chunks, (const double*)scr, P.eps_psd, P.eps_mass, P.stats, P.bincert, P.binaux);
+  hipLaunchKernelGGL(k_bins_finalize_split, fgrid, dim3(kFinSplitWG), 0, ctx->stream, B, NF, chunks,
+                     (const double*)scr, P.eps_psd, P.eps_mass, P.stats, P.bincert, P.binaux, done_word, ticket);
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
 }
