@@ -346,6 +346,8 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   GC_CHECK_ARG(ctx, map && meas, "NULL map or measurement batch");
   GC_CHECK_ARG(ctx, map->m_slots > 0 && map->m_slots < (int64_t)kDropped, "m_slots out of range");
   GC_CHECK_ARG(ctx, map->n_lobes >= 1 && map->n_lobes <= kMaxLobes, "n_lobes must be in [1, 8]");
+  GC_CHECK_ARG(ctx, map->slot_bytes == 0 || (map->slot_bytes % 8 == 0 && map->slot_bytes >= 176 + 24 * map->n_lobes),
+               "slot_bytes must be 0 (per-field arrays) or a packed record size");
   GC_CHECK_ARG(ctx, map->Lambdas && map->thetas && map->etas && map->weights && map->timestamps &&
                         map->last_supported_scan_seq && map->last_update_scan_seq,
                "NULL map field");

@@ -577,6 +577,8 @@ int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const gc_primitive_map*
   }
   GC_CHECK_ARG(p->ctx, map->m_slots > 0 && map->m_slots < (int64_t)0xFFFFFFFF, "m_slots out of range");
   GC_CHECK_ARG(p->ctx, map->n_lobes >= 1 && map->n_lobes <= 8, "n_lobes must be in [1, 8]");
+  GC_CHECK_ARG(p->ctx, map->slot_bytes == 0 || (map->slot_bytes % 8 == 0 && map->slot_bytes >= 176 + 24 * map->n_lobes),
+               "slot_bytes must be 0 (per-field arrays) or a packed record size");
   GC_CHECK_ARG(p->ctx, map->Lambdas && map->thetas && map->etas && map->weights && map->timestamps &&
                            map->last_supported_scan_seq && map->last_update_scan_seq,
                "NULL map field");
