@@ -298,6 +298,7 @@ def main():
         # the per-scan all-gather's device time (HIP events around ncclAllGather on the pipeline
         # stream), untimed scans after the timed region: median over 20, max over ranks
         xs = []
+        pipe.set_exchange_timing(True)  # events around the all-gather: off in the timed loop
         for _ in range(20):
             step()
             xs.append(pipe.exchange_ms())

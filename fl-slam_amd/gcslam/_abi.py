@@ -87,6 +87,7 @@ SIGNATURES = {
     "gc_pipeline_attach_primitive_map": [_vp, _vp, _f64],
     "gc_pipeline_get_scan_map_pose": [_vp, _vp],
     "gc_pipeline_get_scan_map_count": [_vp, C.POINTER(C.c_int64)],
+    "gc_pipeline_set_exchange_timing": [_vp, _i32],
     "gc_pipeline_exchange_ms": [_vp, C.POINTER(C.c_float)],
     "gc_comm_unique_id": [_vp],
     "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],

@@ -291,8 +291,13 @@ class BatchedScanPipeline:
         """Size of the attached RCCL communicator (0 without one)."""
         return int(_abi.lib().gc_pipeline_comm_size(self.handle))
 
+    def set_exchange_timing(self, on: bool = True) -> None:
+        """Bracket every later scan's exchange with HIP events (off by default: each event between
+        kernels costs the stream a few microseconds)."""
+        self._call("gc_pipeline_set_exchange_timing", 1 if on else 0)
+
     def exchange_ms(self) -> float:
-        """Device time of the last scan's exchange (all-gather or host-record upload), in ms."""
+        """Device time of the last timed scan's exchange (all-gather or host-record upload), in ms."""
         ms = C.c_float(0.0)
         self._call("gc_pipeline_exchange_ms", C.byref(ms))
         return float(ms.value)

@@ -321,9 +321,13 @@ int32_t gc_pipeline_get_hyp_stats(gc_pipeline* p, double* h_dPsi_proc, double* h
 int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm);
 /* Size of the attached RCCL communicator (0 when none is attached). */
 int32_t gc_pipeline_comm_size(const gc_pipeline* p);
-/* Device time (ms, HIP events on the pipeline stream) of the last scan's exchange: the RCCL
- * all-gather of the partial records, or the upload of the host-gathered records. Synchronises on
- * it. GC_ERR_ARG when no exchange has run (one rank without a communicator). */
+/* Exchange timing (off by default): with on != 0, every later scan's exchange is bracketed by two
+ * HIP events on the pipeline stream (each event between kernels costs the stream a few us, so the
+ * timed product loop leaves it off). */
+int32_t gc_pipeline_set_exchange_timing(gc_pipeline* p, int32_t on);
+/* Device time (ms) of the last timed scan's exchange: the RCCL all-gather of the partial records,
+ * or the upload of the host-gathered records. Synchronises on it. GC_ERR_ARG when no timed
+ * exchange has run (timing off, or one rank without a communicator). */
 int32_t gc_pipeline_exchange_ms(gc_pipeline* p, float* ms);
 
 /* The C5 in-scan PrimitiveMap update (config C5; the reference's step 12b, pipeline.py:1236-1327,

@@ -61,6 +61,8 @@ def test_host_gathered_shards_match_unsharded(ctx):
     case = cases.build(H=8, n_az=256, n_scans=3)
     full = _make(case, ctx, 0, 1)
     shards = [_make(case, ctx, r, 2) for r in range(2)]
+    for p in shards:
+        p.set_exchange_timing(True)
     assert [(p.h0, p.h1) for p in shards] == [(0, 4), (4, 8)]
     for k, s in enumerate(case["scans"]):
         full.stage_scan(0, s)

@@ -107,5 +107,5 @@ def test_state_locked_between_scan_halves(ctx):
     p.combined()
     p.run_scan(1, s1, 1)
     ctx.sync()
-    with pytest.raises(ValueError, match="no exchange"):
+    with pytest.raises(ValueError, match="no timed exchange"):
         p.exchange_ms()
