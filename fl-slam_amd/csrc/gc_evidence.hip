@@ -525,8 +525,24 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     map_derive_wg(P, red, tab);
     return;
   }
+  if (blockIdx.x == 3) {
+    // ---- the measurement-noise IW apply (measurement_noise_iw_jax.py:59-100) on a fourth
+    // workgroup, beside the process-noise apply and Q rebuild of workgroup 2 (neither reads what
+    // the other writes; nothing on this stream reads the measurement IW state before the next
+    // scan's bins launch): its record entries reduced in the same rank order, 0.0 + Σ_g
+    double* Ri = Lc;  // record entries [kPDPSIM, kPX0)
+    for (int e = kPDPSIM + t; e < kPX0; e += kWG) {
+      double s = 0.0;
+      for (int g = 0; g < P.G; ++g) s += P.gather[(int64_t)g * PLn + e];
+      Ri[e - kPDPSIM] = s;
+    }
+    __syncthreads();
+    wg_iw_meas_apply(P.nu_meas, P.Psi_meas, Ri, Ri + (kPDNUM - kPDPSIM), P.eps_psd, P.nu_max, P.nu_meas, P.Psi_meas,
+                     P.iw_cert + 2, tab);
+    return;
+  }
   if (blockIdx.x == 2) {
-    // ---- the IW applies and the Q rebuild on a third workgroup, beside workgroup 0's barycenter:
+    // ---- the process-noise IW apply and the Q rebuild on a third workgroup, beside workgroup 0's barycenter:
     // they read only the records' IW statistics (reduced here in the same rank order as workgroup
     // 0's record, 0.0 + Σ_g) and the IW state, and nothing of theirs is read there
     double* Ri = Lc;  // record entries [kPDPSIP, kPX0)
@@ -541,9 +557,6 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     wg_iw_proc_apply(P.nu_proc, P.Psi_proc, Ri, Ri + (kPDNUP - kPDPSIP), S.w_process, P.eps_psd, P.nu_max, P.nu_proc,
                      P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab);
     GC_PHASE_WG(P, 23, 2);
-    // measurement-noise IW apply (measurement_noise_iw_jax.py:59-100)
-    wg_iw_meas_apply(P.nu_meas, P.Psi_meas, Ri + (kPDPSIM - kPDPSIP), Ri + (kPDNUM - kPDPSIP), P.eps_psd, P.nu_max,
-                     P.nu_meas, P.Psi_meas, P.iw_cert + 2, tab);
     GC_PHASE_WG(P, 24, 2);
     iw_Q_wg(P, Qs, Qp, Sx, red);
     GC_PHASE_WG(P, 25, 2);
@@ -609,8 +622,9 @@ hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
 }
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
   if (hipError_t e = allow_big_lds((const void*)k_combine_final, lds_final())) return e;
-  // workgroup 0: record reduction, barycenter, certificates; 1: map update + derive; 2: IW apply, Q
-  hipLaunchKernelGGL(k_combine_final, dim3(3), dim3(256), lds_final(), st, P, S);
+  // workgroup 0: record reduction, barycenter, certificates; 1: map update + derive; 2: process IW
+  // apply, Q; 3: measurement IW apply
+  hipLaunchKernelGGL(k_combine_final, dim3(4), dim3(256), lds_final(), st, P, S);
   return hipGetLastError();
 }
 hipError_t launch_map_derive(const PipeDev& P, hipStream_t st) {
