@@ -34,8 +34,6 @@
 namespace gc {
 namespace {
 
-constexpr int kSmapMaxLobes = 8;
-
 struct ScanMapArgs {
   gc_primitive_map map;
   const double *pts, *t, *w_win, *bscal;  // the scan slot and predict's per-point w x window, budget
