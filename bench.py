@@ -545,8 +545,12 @@ def map_fuse_leg(ctx, _abi, m_slots=1 << 20, rows=1 << 17, reps=5, packed=True):
     # slots' rgb / colors are rewritten (the same map as the reference's all-slot recompute)
     colour = n_unique * (24 + 24)
     b = K * row_b + n_unique * slot_rmw + colour
+    # round 2's accounting: the reference's all-slot colour pass (every slot's cam/denom/accum read,
+    # rgb/colors written) counted as algorithmic bytes
+    b_all = K * row_b + n_unique * slot_rmw + M * (8 + 8 + 24 + 24 + 24)
     return {"slots": M, "rows": K, "distinct_slots": n_unique, "ms": ms, "bytes": b,
-            "GB/s": b / (ms * 1e-3) / 1e9, "layout": "packed" if packed else "fields",
+            "GB/s": b / (ms * 1e-3) / 1e9, "bytes_all_slot_colour": b_all,
+            "GB/s_all_slot_colour": b_all / (ms * 1e-3) / 1e9, "layout": "packed" if packed else "fields",
             "kernel": "k_fuse_keys + radix sort + k_fuse_segments (colour estimate of the touched slots)"}
 
 
