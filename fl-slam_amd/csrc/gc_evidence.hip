@@ -512,6 +512,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
   const int t = threadIdx.x, n = kDZ;
   const int PLn = partial_len(P.B);
   if (blockIdx.x == 1) {
+    GC_PHASE_WG(P, 44, 1);
     // ---- map update on a second workgroup, beside the IW / Q chain of workgroup 0 (nothing there
     // reads the map): γ·map + increments of hypothesis 0 (bin_atlas.py:137-163, :232-257), the
     // increments reduced in the same rank order as workgroup 0's record (0.0 + Σ_g, so the value
@@ -523,9 +524,11 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     }
     __syncthreads();
     map_derive_wg(P, red, tab);
+    GC_PHASE_WG(P, 45, 1);
     return;
   }
   if (blockIdx.x == 3) {
+    GC_PHASE_WG(P, 46, 3);
     // ---- the measurement-noise IW apply (measurement_noise_iw_jax.py:59-100) on a fourth
     // workgroup, beside the process-noise apply and Q rebuild of workgroup 2 (neither reads what
     // the other writes; nothing on this stream reads the measurement IW state before the next
@@ -539,9 +542,11 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     __syncthreads();
     wg_iw_meas_apply(P.nu_meas, P.Psi_meas, Ri, Ri + (kPDNUM - kPDPSIM), P.eps_psd, P.nu_max, P.nu_meas, P.Psi_meas,
                      P.iw_cert + 2, tab);
+    GC_PHASE_WG(P, 47, 3);
     return;
   }
   if (blockIdx.x == 2) {
+    GC_PHASE_WG(P, 48, 2);
     // ---- the process-noise IW apply and the Q rebuild on a third workgroup, beside workgroup 0's barycenter:
     // they read only the records' IW statistics (reduced here in the same rank order as workgroup
     // 0's record, 0.0 + Σ_g) and the IW state, and nothing of theirs is read there
@@ -599,6 +604,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     for (int i = 0; i < n; ++i) mm += R[kPMU + i] * R[kPMU + i];
     cc[10] = R[kPMU2] - mm;  // spread proxy Σ w‖μ_j‖² − ‖Σ w μ_j‖²
   }
+  GC_PHASE(P, 49);
 }
 
 // ------------------------------------------------------------------------------ launchers

@@ -73,5 +73,9 @@ for i in sorted(names):
         print(f"{names[i]:36s} {t[i] - t[i - 1]:10.0f} cycles")
 # combine_final's workgroups 0 (slots 20-21) and 2 (22-25) run side by side: their counters are
 # compared only within a workgroup
+for a, b, nm in ((20, 49, "combine wg0: whole (record, barycenter, certs)"), (44, 45, "combine wg1: map update + derive"),
+                 (48, 25, "combine wg2: whole (process IW, Q)"), (46, 47, "combine wg3: meas IW apply")):
+    if t[a] and t[b]:
+        print(f"{nm:36s} {t[b] - t[a]:10.0f} cycles")
 print("predict total", t[8] - t[0], "evidence 10..19", t[19] - t[10], "combine wg0 20..21", t[21] - t[20],
       "combine wg2 22..25", t[25] - t[22])
