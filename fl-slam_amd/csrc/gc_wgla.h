@@ -267,12 +267,18 @@ GC_DEV void wg_chol_solve(const double* C, const double* b, double* x, int n) {
 
 // Ainv = C^{-ᵀ} C^{-1} (primitives.py:186-191: L_chol_inv.T @ L_chol_inv). scratch: n*n.
 // Phase 1 (wave 0): lane j forward-substitutes column j of W = C^{-1} in registers, C read by
-// same-address LDS broadcast, the row sums split over 4 accumulators (short dependency chain) and
-// the 1/C_ii off the chain; W is stored transposed (scratch row j = column j). Phase 2 (all 4
+// same-address LDS broadcast, the row sums split over 4 accumulators (short dependency chain); the
+// 1/C_ii are divided once, lane i's, and broadcast by readlane (the same correctly rounded
+// quotients as a division per lane and row, 6.0k -> 4.0k cycles for 22x22,
+// profiles/r03/chol_latency_micro.txt); W is stored transposed (scratch row j = column j).
+// j must be the calling lane's index within its wave (lanes j >= n only contribute their 1/C_jj
+// slot, unread). Phase 2 (all 4
 // waves): thread (g = t/32, j = t%32) forms Ainv[i][j] = Σ_k W[k][i] W[k][j] for i ≡ g (mod 8),
 // its column j of W in registers and column i broadcast; k ascends over the full range (the
 // entries below the triangles are exact zeros), the order of the reference's product.
 GC_DEV void chol_inverse_phase1_lane(const double* C, double* scratch, int n, int j) {
+  const int lane = threadIdx.x & 63;
+  const double rdiag = 1.0 / (lane < n ? C[lane * n + lane] : 1.0);
   if (j < n) {
     double col[kDZ];
 #pragma unroll
@@ -284,8 +290,7 @@ GC_DEV void chol_inverse_phase1_lane(const double* C, double* scratch, int n, in
 #pragma unroll
         for (int k = 0; k < i; ++k) s[k & 3] = fma(Ci[k], col[k], s[k & 3]);
         const double v = ((i == j) ? 1.0 : 0.0) - ((s[0] + s[1]) + (s[2] + s[3]));
-        const double inv = 1.0 / Ci[i];
-        col[i] = i >= j ? v * inv : 0.0;
+        col[i] = i >= j ? v * readlane_f64(rdiag, i) : 0.0;
       }
     }
 #pragma unroll

@@ -48,7 +48,8 @@ __device__ void lane_chol_v(double (&a)[NM], int lane, bool& ok) {
     g = fma(g, r, g);
     h = fma(h, r, h);
     const double inv = h + h;
-    a[k] = lane == k ? g : (lane > k ? a[k] * inv : a[k]);
+    if (VAR & 8) a[k] = lane == k ? g : a[k] * inv;  // rows above k hold unread values either way
+    else a[k] = lane == k ? g : (lane > k ? a[k] * inv : a[k]);
     if (k + 1 < NM) {
       if (k + 2 < NM) colbuf[lane < NM ? lane : NM + 1] = a[k];
       if (VAR & 1) a[k + 1] -= a[k] * readlane_f64(a[k], k + 1);
@@ -99,6 +100,61 @@ void runvar(const double* dA, double* dO, double* dR, const std::vector<double>&
   for (int i = 0; i < N2; ++i) diff += (r[i] != ref[i]);
   printf("chol variant %-28s %8.0f cycles, %d entries differ from the product\n", nm, o, diff);
 }
+
+// chol_inverse_phase1_lane with the 22 reciprocals 1/C_ii formed once (lane i) and broadcast by
+// readlane, instead of every lane dividing by every pivot (the same correctly rounded quotients)
+__device__ void phase1_rcp(const double* C, double* scratch, int n, int j) {
+  const int lane = threadIdx.x & 63;
+  const double rdiag = 1.0 / (lane < n ? C[lane * n + lane] : 1.0);
+  if (j < n) {
+    double col[kDZ];
+#pragma unroll
+    for (int i = 0; i < kDZ; ++i) {
+      col[i] = 0.0;
+      if (i < n) {
+        const double* Ci = C + i * n;
+        double s[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int k = 0; k < i; ++k) s[k & 3] = fma(Ci[k], col[k], s[k & 3]);
+        const double v = ((i == j) ? 1.0 : 0.0) - ((s[0] + s[1]) + (s[2] + s[3]));
+        const double inv = readlane_f64(rdiag, i);
+        col[i] = i >= j ? v * inv : 0.0;
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < kDZ; ++k)
+      if (k < n) scratch[j * n + k] = col[k];
+  }
+}
+template <int VAR>
+__global__ void __launch_bounds__(256) kinv(const double* A, double* out, double* res) {
+  __shared__ double S[N2], W[N2];
+  const int t = threadIdx.x;
+  for (int i = t; i < N2; i += 256) S[i] = A[i];
+  __syncthreads();
+  if (t < 64) wave0_chol<kDZ, true>(S, kDZ);
+  __syncthreads();
+  long c0 = __builtin_readcyclecounter();
+  if (t < 64) {
+    if (VAR == 0) chol_inverse_phase1_lane(S, W, kDZ, t);
+    else phase1_rcp(S, W, kDZ, t);
+  }
+  __syncthreads();
+  long c1 = __builtin_readcyclecounter();
+  if (t == 0) out[0] = (double)(c1 - c0);
+  for (int i = t; i < N2; i += 256) res[i] = W[i];
+}
+template <int VAR>
+void runinv(const double* dA, double* dO, double* dR, std::vector<double>& ref, const char* nm, bool set) {
+  for (int it = 0; it < 5; ++it) { hipLaunchKernelGGL(kinv<VAR>, dim3(1), dim3(256), 0, 0, dA, dO, dR); (void)hipDeviceSynchronize(); }
+  double o; std::vector<double> r(N2);
+  (void)hipMemcpy(&o, dO, 8, hipMemcpyDeviceToHost);
+  (void)hipMemcpy(r.data(), dR, N2 * 8, hipMemcpyDeviceToHost);
+  if (set) ref = r;
+  int diff = 0;
+  for (int i = 0; i < N2; ++i) diff += (r[i] != ref[i]);
+  printf("inverse phase1 %-26s %8.0f cycles, %d entries differ from the product\n", nm, o, diff);
+}
 int main() {
   std::vector<double> A(N2);
   // SPD: B Bᵀ + 22 I
@@ -132,5 +188,13 @@ int main() {
   runvar<3>(dA, dO, dR, ref, "readlane + pin all");
   runvar<4>(dA, dO, dR, ref, "pin next pivot");
   runvar<5>(dA, dO, dR, ref, "readlane + pin next");
+  runvar<8>(dA, dO, dR, ref, "scale every row");
+  runvar<0>(dA, dO, dR, ref, "copy of product");
+  runvar<8>(dA, dO, dR, ref, "scale every row");
+  runvar<9>(dA, dO, dR, ref, "scale every row + readlane");
+  runinv<0>(dA, dO, dR, ref, "product", true);
+  runinv<1>(dA, dO, dR, ref, "reciprocals by readlane", false);
+  runinv<0>(dA, dO, dR, ref, "product", false);
+  runinv<1>(dA, dO, dR, ref, "reciprocals by readlane", false);
   return 0;
 }
