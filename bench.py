@@ -133,6 +133,18 @@ class Dist:
         return float(t.item())
 
 
+def workload_label(H_total: int, n: int, world: int) -> str:
+    """The BASELINE.json config a run measures: C3 (64k x 256, 1 GPU), C4 (the same total over N
+    ranks), C2 (H = 1); any other --hyps / --n-az is labelled by its own shape."""
+    if n == 65536 and H_total == 256:
+        return "C3" if world == 1 else "C4 (%d ranks)" % world
+    if n == 65536 and H_total == 1:
+        return "C2"
+    if n == 65536 and 256 % H_total == 0:
+        return "H=%d (one rank's shard of C4 at N=%d)" % (H_total, 256 // H_total)
+    return "H=%d, %d points" % (H_total, n)
+
+
 def pipe_partial_len(pipe):
     from gcslam.pipeline import partial_len
     return partial_len(pipe.B)
@@ -193,7 +205,8 @@ def main():
         print(json.dumps({"c5_map_fuse": map_fuse_leg(ctx, _abi, packed=args.map_layout == "packed")}), flush=True)
         return
     if args.c5_only:
-        print(json.dumps({"c5": c5_leg(ctx, _abi, args)}), flush=True)
+        print(json.dumps({"c5": c5_leg(ctx, _abi, args), "c5_dense": c5_leg(ctx, _abi, args, cap=131072)}),
+              flush=True)
         return
     if args.roofline_only:
         from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
@@ -284,12 +297,14 @@ def main():
     ctx.sync()
     dist.barrier()
     ctx.sync()
+    pipe.host_stats(reset=True)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step(timed=True)
     ctx.sync()
     dist.barrier()
     t1 = time.perf_counter()
+    hs = pipe.host_stats(reset=True)
     elapsed = dist.max(t1 - t0)
     scans_per_s = args.steps / elapsed
     n_gpus = pipe.comm_size() if dist.world > 1 else 1  # the RCCL communicator's size
@@ -320,17 +335,38 @@ def main():
         "dtype": "f64",
         "data": "synthetic (VLP-16-like 16x%d ray-cast box room + 200 Hz IMU + wheel odometry, SURVEY §8d)"
                 % args.n_az,
-        "config": {"workload": "C3: one 64k-point scan x %d hypotheses through the full batched pipeline "
+        "config": {"workload": "%s: one %d-point scan x %d hypotheses through the full batched pipeline "
                                "(a1-a16: budget, predict, IMU preint, deskew, soft-assign, moment-match, "
                                "Matrix-Fisher, planar, tempering, fusion, recompose, IW, map, anchor drift, "
-                               "barycenter combine)" % H_total,
+                               "barycenter combine)" % (workload_label(H_total, n, dist.world), n, H_total),
                    "points": n, "hypotheses": H_total, "bins": B, "parallelism": "hypotheses/%d" % dist.world,
                    "ingest": ("every step stages one scan host -> HBM (pinned mirror + DMA on a copy stream): "
                               "step k stages scan k+1 while scan k computes (three slots in rotation)") if ingest else
                              "scans pre-staged in HBM before the timed region"},
     }
+    # per-stage device time of the same step (HIP events around each launch group, untimed scans after
+    # the timed region: the events themselves cost the stream a few us each), median over 20
+    pipe.set_stage_timing(True)
+    st_runs = []
+    for _ in range(20):
+        step()
+        st_runs.append(pipe.stage_ms())
+    pipe.set_stage_timing(False)
+    out_stages = {k: float(np.median([r[k] for r in st_runs])) for k in st_runs[0]}
     if exchange is not None:
         out["exchange"] = exchange
+    out["stages_ms"] = dict(out_stages, scans=len(st_runs), note="HIP events around each launch group, untimed scans")
+    ns = max(hs["scans"], 1.0)
+    nst = max(hs["stages"], 1.0)
+    out["host"] = {"scan_enqueue_ms": {"mean": hs["scan_enqueue_ms"] / ns, "max": hs["scan_enqueue_max_ms"]},
+                   "scan_wait_ms": {"mean": hs["scan_wait_ms"] / ns, "max": hs["scan_wait_max_ms"]},
+                   "stage_work_ms": {"mean": hs["stage_work_ms"] / nst, "max": hs["stage_work_max_ms"]},
+                   "stage_wait_ms": {"mean": hs["stage_wait_ms"] / nst, "max": hs["stage_wait_max_ms"]},
+                   "host_syncs": hs["host_syncs"], "h2d_bytes_per_scan": hs["h2d_bytes"] / ns,
+                   "scans": hs["scans"],
+                   "note": "libgcslam's own clock (gc_pipeline_host_stats): enqueue = the C entries' host work "
+                           "(checks, launches, DMA issue), wait = polls / syncs on the device; the Python "
+                           "run_scan_host_ms below also holds the ctypes overhead"}
     if ingest:
         out["ingest_host_ms_per_scan"] = 1e3 * stage_s[0] / max(stage_s[1], 1)
         out["run_scan_host_ms"] = {"mean": 1e3 * float(np.mean(run_s)), "max": 1e3 * float(np.max(run_s))}
@@ -347,6 +383,7 @@ def main():
         out["c5_map_fuse"] = map_fuse_leg(ctx, _abi, packed=args.map_layout == "packed")
     if dist.rank == 0 and dist.world == 1 and not args.no_c5:
         out["c5"] = c5_leg(ctx, _abi, args)
+        out["c5_dense"] = c5_leg(ctx, _abi, args, cap=131072)
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args.n_az, H_total, args.cpu_budget_s)
     if dist.rank == 0:
@@ -493,9 +530,11 @@ def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5, m_
     dt = (time.perf_counter() - t0) / steps
     touched = pipe.scan_map_count()
     pipe.close()
-    return {"workload": "C5 shape on 1 GPU: %d-point scans (staged every step), budget cap %d (stride 2), %d "
+    stride = -(-n_in // cap)
+    return {"workload": "C5 shape on 1 GPU: %d-point scans (staged every step), budget cap %d (%s), %d "
                         "hypotheses, full pipeline + the in-scan PrimitiveMap update (%d rows into a %d-slot map, "
-                        "voxel %.2f m)" % (n_in, cap, H, cap, m_slots, voxel),
+                        "voxel %.2f m)" % (n_in, cap, "dense: every point" if stride == 1 else "stride %d" % stride,
+                                           H, cap, m_slots, voxel),
             "ms_per_scan": 1e3 * dt, "scans_per_s": 1.0 / dt, "steps": steps, "warmup": warmup,
             "map_slots_touched_last_scan": touched}
 

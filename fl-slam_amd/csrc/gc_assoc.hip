@@ -364,8 +364,10 @@ int32_t gc_extract_map_view(gc_ctx* ctx, const gc_primitive_map* map, int64_t m_
                             const int64_t* h_tile_ids, double eps_lift, double eps_mass, const gc_map_view* view) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   GC_CHECK_ARG(ctx, map && view && h_dense_tiles && h_tile_ids, "NULL argument");
-  GC_CHECK_ARG(ctx, map->slot_bytes == 0 || (map->slot_bytes % 8 == 0 && map->slot_bytes >= 176 + 24 * map->n_lobes),
-               "slot_bytes must be 0 (per-field arrays) or a packed record size");
+  {
+    const char* lay_ = gc::map_layout_error(*map);
+    GC_CHECK_ARG(ctx, lay_ == nullptr, lay_ ? lay_ : "");
+  }
   const int T = view->n_tiles, k = view->m_tile_view;
   GC_CHECK_ARG(ctx, T >= 1 && k >= 1 && m_tile >= k && m_tile < (int64_t)INT32_MAX, "bad view shape");
   GC_CHECK_ARG(ctx, view->n_lobes == map->n_lobes && map->n_lobes <= kMaxLobesA, "n_lobes mismatch");

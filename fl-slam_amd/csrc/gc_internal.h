@@ -12,6 +12,11 @@ struct gc_ctx {
   void* scratch = nullptr;  // growable device scratch (per ctx, stream-ordered use only)
   size_t scratch_bytes = 0;
   int cu_count = 0;  // compute units of the device (queried on first use)
+  // per-slot list heads of the map reduce-by-key (gc_map.hip, gc_scanmap.hip): all 0xFFFFFFFF between
+  // calls (each call's owners restore the heads they used); re-filled when grown or after a failed call
+  uint32_t* slot_head = nullptr;
+  int64_t slot_head_n = 0;
+  bool slot_head_dirty = true;
 };
 
 namespace gc {
@@ -22,10 +27,19 @@ void set_error(gc_ctx* ctx, const std::string& msg);
 // device scratch of at least `bytes` (synchronises the stream before growing)
 int scratch(gc_ctx* ctx, size_t bytes, void** out);
 
+// the context's slot-head array for a map of m_slots slots, every entry 0xFFFFFFFF on return (stream-
+// ordered: a fill is enqueued on ctx->stream when the array is new, grown or marked dirty)
+int slot_heads(gc_ctx* ctx, int64_t m_slots, uint32_t** out);
+
 // hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) only when fn has not yet been allowed that
 // much: the runtime call is not free (it waited for an in-flight ingest copy on another stream,
 // delaying the next launch by its duration), so the per-scan launches skip it after the first
 hipError_t ensure_dyn_lds(const void* fn, size_t bytes);
+
+// GC_OK when kernel fn has no static LDS (its dynamic block starts at LDS address 0, which the fused
+// bins kernels' absolute table addressing relies on, gc_points.hip exp2s_shift8_n); checked once per
+// kernel and device
+int ensure_no_static_lds(gc_ctx* ctx, const void* fn);
 
 }  // namespace gc
 

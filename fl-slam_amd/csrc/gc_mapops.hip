@@ -326,8 +326,10 @@ int check_tile(gc_ctx* ctx, const gc_primitive_map* map, int64_t slot0, int64_t 
   GC_CHECK_ARG(ctx, map->m_slots > 0 && slot0 >= 0 && n_slots >= 0 && slot0 + n_slots <= map->m_slots,
                "tile range outside the map");
   GC_CHECK_ARG(ctx, map->n_lobes >= 1 && map->n_lobes <= kMaxLobesOps, "n_lobes must be in [1, 8]");
-  GC_CHECK_ARG(ctx, map->slot_bytes == 0 || (map->slot_bytes % 8 == 0 && map->slot_bytes >= 176 + 24 * map->n_lobes),
-               "slot_bytes must be 0 (per-field arrays) or a packed record size");
+  {
+    const char* lay_ = gc::map_layout_error(*map);
+    GC_CHECK_ARG(ctx, lay_ == nullptr, lay_ ? lay_ : "");
+  }
   GC_CHECK_ARG(ctx, map->Lambdas && map->thetas && map->etas && map->weights && map->timestamps &&
                         map->last_supported_scan_seq && map->last_update_scan_seq,
                "NULL map field");

@@ -73,4 +73,27 @@ inline void map_record_layout(int n_lobes, int64_t* off, int64_t* slot_bytes) {
   *slot_bytes = up128(b2 + 65);
 }
 
+// Host check of a map's layout before any kernel dereferences it: per-field arrays (slot_bytes 0),
+// or exactly the packed record of map_record_layout(n_lobes) with every non-NULL field inside the
+// record that Lambdas starts (a shorter slot_bytes would let a fuse write into the next slot's
+// record). Returns nullptr when the layout is sound, else the reason.
+inline const char* map_layout_error(const gc_primitive_map& m) {
+  if (m.slot_bytes == 0) return nullptr;
+  int64_t off[kRecFields], sb = 0;
+  map_record_layout(m.n_lobes, off, &sb);
+  if (m.slot_bytes != sb) return "slot_bytes must be 0 (per-field arrays) or gc_primitive_map_record_layout(n_lobes)";
+  if (!m.Lambdas) return "NULL Lambdas";
+  const char* b0 = (const char*)m.Lambdas;
+  const void* f[kRecFields] = {m.Lambdas, m.thetas, m.etas, m.weights, m.timestamps, m.last_supported_scan_seq,
+                               m.last_update_scan_seq, m.cam_mass, m.lidar_mass, m.rgb_cam_accum, m.rgb_cam_denom,
+                               m.rgb, m.colors, m.valid_mask, m.created_timestamps, m.primitive_ids};
+  const int64_t width[kRecFields] = {72, 24, 24 * (int64_t)m.n_lobes, 8, 8, 8, 8, 8, 8, 24, 8, 24, 24, 1, 8, 8};
+  for (int k = 0; k < kRecFields; ++k) {
+    if (!f[k]) continue;
+    const int64_t d = (const char*)f[k] - b0;
+    if (d < 0 || d + width[k] > sb) return "a packed field pointer lies outside its slot record";
+  }
+  return nullptr;
+}
+
 }  // namespace gc

@@ -121,6 +121,13 @@ GC_DEV void se3_BC(double ts, double* B, double* C) {
   }
 }
 
+// se3_jax.py:137-175
+GC_DEV void se3_V(const double* phi, double* V) {
+  double B, C;
+  se3_BC(dot3(phi, phi), &B, &C);
+  rodrigues_form(phi, B, C, V);
+}
+
 // se3_jax.py:473-504 : out = [V(φ)ρ, φ]
 GC_DEV void se3_exp(const double* xi, double* out) {
   const double* phi = xi + 3;
@@ -198,6 +205,18 @@ GC_DEV void se3_compose(const double* a, const double* b, double* out) {
   double o[6];
   o[0] = a[0] + t[0]; o[1] = a[1] + t[1]; o[2] = a[2] + t[2];
   so3_log(Rab, o + 3);
+  for (int i = 0; i < 6; ++i) out[i] = o[i];
+}
+
+// se3_jax.py:442-453 : [-Rᵀ t, log(Rᵀ)]
+GC_DEV void se3_inverse(const double* a, double* out) {
+  double R[9], Rt[9], o[6];
+  so3_exp(a + 3, R);
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Rt[3 * i + j] = R[3 * j + i];
+  mat3_vec(Rt, a, o);
+  o[0] = -o[0]; o[1] = -o[1]; o[2] = -o[2];
+  so3_log(Rt, o + 3);
   for (int i = 0; i < 6; ++i) out[i] = o[i];
 }
 

@@ -58,6 +58,8 @@ struct PipeDev {
   double *map_inc;                         // (B, 26) written by hypothesis 0's owner
   double *h0rec;                           // (kH0Len) hypothesis 0's pose block (its owner's k_evidence)
   double *nu_proc, *Psi_proc, *nu_meas, *Psi_meas;  // (7), (7,36), (3), (3,9)
+  double *lidar_iw;                        // [ν_2, Ψ_2 (9)]: the scan's measurement-IW LiDAR block before its
+                                           // IW apply (k_combine_final wg 3), read by the in-scan map update
   double *budget;                          // 8 budget scalars
   double *budget_part;                     // (64, 3) a1 partials, written by predict's extra workgroups
   unsigned *budget_ticket;                 // arrival counter of those workgroups (reset by the last)

@@ -2,9 +2,12 @@
 // backend_node.py:2036-2119): one rank's shard of hypotheses lives in HBM; gc_pipeline_run_scan
 // enqueues the whole 14-step scan for all of them plus the combine/IW exchange on one stream.
 #include <hip/hip_runtime.h>
+#include <algorithm>
+#include <chrono>
 #include <cstring>
 #include <vector>
 #include "gc_internal.h"
+#include "gc_mapslot.h"
 #include "gc_pipe.h"
 #include "gc_scanmap.h"
 
@@ -73,6 +76,18 @@ struct gc_pipeline {
   gc::ScanMapWork smapW;
   int pending_slot = -1;
   int64_t pending_seq = 0;
+  // Host-side accounting (gc_pipeline_host_stats): the reference's RuntimeCounters
+  // (common/runtime_counters.py:19-108: host syncs, host<->device bytes) and the split of every
+  // scan's and every staging call's host time into enqueue / copy work and waits for the device.
+  double hs[GC_HOST_STATS] = {};
+  double wait_acc_ms = 0.0;  // host waits (event polls, stream syncs) since the current entry began
+  double scan_enq_ms = 0.0, scan_wait_ms = 0.0;  // the pending scan's local half
+  // per-stage device timing (gc_pipeline_set_stage_timing): events around each launch group
+  bool st_timing = false, st_rec = false;
+  hipEvent_t st_ev[GC_STAGE_N] = {};
+  // getter workspace (conditioning certificates), allocated with the pipeline: no hipMalloc / hipFree
+  // (device-synchronising) on a getter a live node calls every scan
+  double* ws = nullptr;
 };
 
 namespace {
@@ -86,30 +101,72 @@ int dalloc(gc_pipeline* p, size_t count, double** out) {
   return GC_OK;
 }
 
+double now_ms() {
+  return 1e-6 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(
+                    std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// a stream synchronisation on the host, counted as a host sync and as waiting time
+int sync_counted(gc_pipeline* p) {
+  const double t0 = now_ms();
+  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
+  p->wait_acc_ms += now_ms() - t0;
+  p->hs[GC_HS_HOST_SYNCS] += 1.0;
+  return GC_OK;
+}
+
 int up(gc_pipeline* p, double* d, const double* h, size_t count) {
   if (!h || count == 0) return GC_OK;
   GC_HIP(p->ctx, hipMemcpyAsync(d, h, count * sizeof(double), hipMemcpyHostToDevice, p->ctx->stream));
-  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
-  return GC_OK;
+  p->hs[GC_HS_H2D_BYTES] += (double)(count * sizeof(double));
+  return sync_counted(p);
 }
 
 int down(gc_pipeline* p, double* h, const double* d, size_t count) {
   if (!h || count == 0) return GC_OK;
   GC_HIP(p->ctx, hipMemcpyAsync(h, d, count * sizeof(double), hipMemcpyDeviceToHost, p->ctx->stream));
-  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
-  return GC_OK;
+  p->hs[GC_HS_D2H_BYTES] += (double)(count * sizeof(double));
+  return sync_counted(p);
 }
 
 // Host wait for a copy-stream event by polling: hipEventSynchronize may sleep on an interrupt and
 // take tens to hundreds of microseconds to wake, enough to make the host, not the device, the
-// bottleneck of a 0.3 ms scan. Falls back to the blocking wait after ~10^5 polls.
-int wait_event(gc_ctx* ctx, hipEvent_t e) {
+// bottleneck of a 0.3 ms scan. Falls back to the blocking wait after ~10^5 polls. An event already
+// complete costs one query and is not counted as a sync.
+int wait_event(gc_pipeline* p, hipEvent_t e) {
+  gc_ctx* ctx = p->ctx;
+  hipError_t q = hipEventQuery(e);
+  if (q == hipSuccess) return GC_OK;
+  if (q != hipErrorNotReady) GC_HIP(ctx, q);
+  const double t0 = now_ms();
+  p->hs[GC_HS_HOST_SYNCS] += 1.0;
   for (int spin = 0; spin < 100000; ++spin) {
-    const hipError_t q = hipEventQuery(e);
-    if (q == hipSuccess) return GC_OK;
+    q = hipEventQuery(e);
+    if (q == hipSuccess) {
+      p->wait_acc_ms += now_ms() - t0;
+      return GC_OK;
+    }
     if (q != hipErrorNotReady) GC_HIP(ctx, q);
   }
   GC_HIP(ctx, hipEventSynchronize(e));
+  p->wait_acc_ms += now_ms() - t0;
+  return GC_OK;
+}
+
+// host time of one entry split into work and waits: sum / max per kind (GC_HS_* layout)
+void account(gc_pipeline* p, int base, double t_entry0) {
+  const double total = now_ms() - t_entry0, w = p->wait_acc_ms, e = total - w;
+  double* h = p->hs;
+  h[base] += 1.0;
+  h[base + 1] += e;
+  h[base + 2] = std::max(h[base + 2], e);
+  h[base + 3] += w;
+  h[base + 4] = std::max(h[base + 4], w);
+}
+
+int stage_event(gc_pipeline* p, int i) {
+  if (!p->st_timing) return GC_OK;
+  GC_HIP(p->ctx, hipEventRecord(p->st_ev[i], p->ctx->stream));
   return GC_OK;
 }
 
@@ -228,10 +285,10 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert,
-                       &P.h0rec};
+                       &P.h0rec, &P.lidar_iw};
   const size_t ssz[] = {(size_t)P.H, (size_t)NN, (size_t)B * 3, (size_t)B * gc::kMapRec, (size_t)B * gc::kMapDer, 8,
                         (size_t)B * gc::kMapRec, 7, 7 * 36, 3, 27, 8, (size_t)PL, (size_t)PL * P.G,
-                        GC_COMB_LEN, 4, gc::kH0Len};
+                        GC_COMB_LEN, 4, gc::kH0Len, 10};
   for (size_t i = 0; i < sizeof(ssz) / sizeof(ssz[0]) && rc == GC_OK; ++i) rc = dalloc(p, ssz[i], shared[i]);
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
@@ -248,6 +305,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   if (rc == GC_OK) rc = dalloc(p, 1, &ctr);  // zeroed: k_bins_io's task counter + finished pullers
   P.task_ctr = reinterpret_cast<unsigned*>(ctr);
   if (rc == GC_OK) rc = dalloc(p, (size_t)P.n_cap, &P.w_win);
+  if (rc == GC_OK) rc = dalloc(p, (size_t)2 * Hl * (NN + 6), &p->ws);  // getter workspace (conditioning certs)
   if (rc == GC_OK && hipHostMalloc((void**)&p->done_word, sizeof(int64_t), hipHostMallocCoherent) != hipSuccess) {
     gc::set_error(ctx, "hipHostMalloc failed for the slot completion word");
     rc = GC_ERR_RUNTIME;
@@ -280,6 +338,8 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
       if (e) (void)hipEventDestroy(e);
   }
   for (hipEvent_t e : {p->x0, p->x1})
+    if (e) (void)hipEventDestroy(e);
+  for (hipEvent_t e : p->st_ev)
     if (e) (void)hipEventDestroy(e);
   if (p->smapW.buf) (void)hipFree(p->smapW.buf);
   if (p->cstream) (void)hipStreamDestroy(p->cstream);
@@ -342,15 +402,14 @@ int32_t gc_pipeline_set_io_mode(gc_pipeline* p, int32_t mode) {
   return GC_OK;
 }
 
-int32_t gc_pipeline_stage_odom(gc_pipeline* p, int32_t slot, const double* h_pose6, const double* h_cov36,
+static int32_t gc_pipeline_stage_odom_impl(gc_pipeline* p, int32_t slot, const double* h_pose6, const double* h_cov36,
                                const double* h_twist6, const double* h_twist_cov36) {
-  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
   GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS, "slot out of range");
   GC_TRY(slot_check_restage(p, slot));
   GC_CHECK_ARG(p->ctx, h_pose6 && h_cov36 && h_twist6 && h_twist_cov36, "NULL odometry array");
   auto& s = p->slots[slot];
   GC_TRY(slot_alloc(p, s));
-  if (s.odom_rec) GC_TRY(wait_event(p->ctx, s.odom_done));  // the last odometry DMA read its area
+  if (s.odom_rec) GC_TRY(wait_event(p, s.odom_done));  // the last odometry DMA read its area
   double* buf = s.host + SlotLayout(p->P).odom;
   std::memcpy(buf, h_pose6, 6 * sizeof(double));
   std::memcpy(buf + 6, h_cov36, 36 * sizeof(double));
@@ -358,11 +417,22 @@ int32_t gc_pipeline_stage_odom(gc_pipeline* p, int32_t slot, const double* h_pos
   std::memcpy(buf + 48, h_twist_cov36, 36 * sizeof(double));
   GC_TRY(slot_wait_consumed(p, s));
   GC_HIP(p->ctx, hipMemcpyAsync(s.odom, buf, gc::kOdomLen * sizeof(double), hipMemcpyHostToDevice, p->cstream));
+  p->hs[GC_HS_H2D_BYTES] += (double)(gc::kOdomLen * sizeof(double));
   GC_HIP(p->ctx, hipEventRecord(s.odom_done, p->cstream));
   GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));  // scan_local's wait covers the odometry too
   s.odom_rec = s.ready_rec = true;
   s.has_odom = true;
   return GC_OK;
+}
+
+int32_t gc_pipeline_stage_odom(gc_pipeline* p, int32_t slot, const double* h_pose6, const double* h_cov36,
+                               const double* h_twist6, const double* h_twist_cov36) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const double t0 = now_ms();
+  p->wait_acc_ms = 0.0;
+  const int32_t rc = gc_pipeline_stage_odom_impl(p, slot, h_pose6, h_cov36, h_twist6, h_twist_cov36);
+  account(p, GC_HS_STAGES, t0);
+  return rc;
 }
 
 int32_t gc_pipeline_get_io_parts(gc_pipeline* p, double* h_parts) {
@@ -418,17 +488,16 @@ int32_t gc_pipeline_get_map(gc_pipeline* p, double* h_map, double* h_map_der, do
   return down(p, h_misc2, p->P.map_misc, 2);
 }
 
-int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_pts, const double* h_t,
+static int32_t gc_pipeline_stage_scan_impl(gc_pipeline* p, int32_t slot, const double* h_pts, const double* h_t,
                                const double* h_w, int64_t n_in, const double* h_imu_t, const double* h_imu_g,
                                const double* h_imu_a) {
-  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
   GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS, "slot out of range");
   GC_TRY(slot_check_restage(p, slot));
   GC_CHECK_ARG(p->ctx, n_in > 0 && n_in <= p->P.n_in, "n_in must be in [1, n_in_max]");
   GC_CHECK_ARG(p->ctx, h_pts && h_t && h_w && h_imu_t && h_imu_g && h_imu_a, "NULL scan array");
   auto& s = p->slots[slot];
   GC_TRY(slot_alloc(p, s));
-  if (s.ready_rec) GC_TRY(wait_event(p->ctx, s.ready));  // the last DMA out of the mirror is done
+  if (s.ready_rec) GC_TRY(wait_event(p, s.ready));  // the last DMA out of the mirror is done
   const SlotLayout Ly(p->P);
   const size_t n = (size_t)n_in, M = (size_t)p->P.M;
   std::memcpy(s.host, h_pts, 3 * n * sizeof(double));
@@ -446,16 +515,27 @@ int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_pts
     GC_HIP(p->ctx, hipMemcpyAsync(s.imu_t, s.host + Ly.imu, 7 * M * sizeof(double), k, p->cstream));
   }
   GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));
+  p->hs[GC_HS_H2D_BYTES] += (double)((5 * n + 7 * M) * sizeof(double));
   s.ready_rec = true;
   s.n_in = n_in;
   return GC_OK;
 }
 
-int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_t* h_data, int64_t n_points,
+int32_t gc_pipeline_stage_scan(gc_pipeline* p, int32_t slot, const double* h_pts, const double* h_t,
+                               const double* h_w, int64_t n_in, const double* h_imu_t, const double* h_imu_g,
+                               const double* h_imu_a) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const double t0 = now_ms();
+  p->wait_acc_ms = 0.0;
+  const int32_t rc = gc_pipeline_stage_scan_impl(p, slot, h_pts, h_t, h_w, n_in, h_imu_t, h_imu_g, h_imu_a);
+  account(p, GC_HS_STAGES, t0);
+  return rc;
+}
+
+static int32_t gc_pipeline_stage_pointcloud2_impl(gc_pipeline* p, int32_t slot, const uint8_t* h_data, int64_t n_points,
                                       int32_t point_step, const int32_t* h_fields, double header_stamp,
                                       const double* h_R9, const double* h_t3, const double* h_imu_t,
                                       const double* h_imu_g, const double* h_imu_a) {
-  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
   GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS, "slot out of range");
   GC_TRY(slot_check_restage(p, slot));
   GC_CHECK_ARG(p->ctx, n_points >= 0 && n_points <= p->P.n_in, "n_points must be in [0, n_in_max]");
@@ -463,7 +543,7 @@ int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_
   GC_CHECK_ARG(p->ctx, n_points == 0 || (h_data && point_step > 0), "NULL message data");
   if (n_points == 0) {  // one zero-weight dummy point (backend_node.py:1700-1707)
     const double z3[3] = {0.0, 0.0, 0.0}, z1 = 0.0;
-    return gc_pipeline_stage_scan(p, slot, z3, &z1, &z1, 1, h_imu_t, h_imu_g, h_imu_a);
+    return gc_pipeline_stage_scan_impl(p, slot, z3, &z1, &z1, 1, h_imu_t, h_imu_g, h_imu_a);
   }
   auto& s = p->slots[slot];
   GC_TRY(slot_alloc(p, s));
@@ -472,7 +552,7 @@ int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_
     GC_HIP(p->ctx, hipMalloc((void**)&s.tag, (size_t)p->P.n_in));
     GC_HIP(p->ctx, hipMalloc((void**)&s.flag, 4 * sizeof(int32_t)));
   }
-  if (s.ready_rec) GC_TRY(wait_event(p->ctx, s.ready));  // the last DMA / parse from this slot is done
+  if (s.ready_rec) GC_TRY(wait_event(p, s.ready));  // the last DMA / parse from this slot is done
   const size_t nb = (size_t)n_points * (size_t)point_step;
   if (s.bytes_cap < nb) {
     if (s.bytes) GC_HIP(p->ctx, hipFree(s.bytes));
@@ -492,9 +572,22 @@ int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_
   GC_HIP(p->ctx, hipMemcpyAsync(s.imu_t, s.host + SlotLayout(p->P).imu, 7 * (size_t)p->P.M * sizeof(double),
                                 hipMemcpyHostToDevice, p->cstream));
   GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));
+  p->hs[GC_HS_H2D_BYTES] += (double)(nb + 7 * (size_t)p->P.M * sizeof(double));
   s.ready_rec = true;
   s.n_in = n_points;
   return GC_OK;
+}
+
+int32_t gc_pipeline_stage_pointcloud2(gc_pipeline* p, int32_t slot, const uint8_t* h_data, int64_t n_points,
+                                      int32_t point_step, const int32_t* h_fields, double header_stamp,
+                                      const double* h_R9, const double* h_t3, const double* h_imu_t,
+                                      const double* h_imu_g, const double* h_imu_a) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const double t0 = now_ms();
+  p->wait_acc_ms = 0.0;
+  const int32_t rc = gc_pipeline_stage_pointcloud2_impl(p, slot, h_data, n_points, point_step, h_fields, header_stamp, h_R9, h_t3, h_imu_t, h_imu_g, h_imu_a);
+  account(p, GC_HS_STAGES, t0);
+  return rc;
 }
 
 int32_t gc_pipeline_attach_comm(gc_pipeline* p, gc_comm* comm) {
@@ -527,8 +620,7 @@ int32_t gc_pipeline_get_partial(gc_pipeline* p, double* h_record) {
   return down(p, h_record, p->P.send, (size_t)gc::partial_len(p->P.B));
 }
 
-int32_t gc_pipeline_scan_finish(gc_pipeline* p, const double* h_gather) {
-  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
   GC_CHECK_ARG(p->ctx, p->pending, "no pending scan (gc_pipeline_scan_local)");
   GC_CHECK_ARG(p->ctx, h_gather || p->P.G == 1 || p->comm,
                "world_size > 1 needs a communicator or the host-gathered records");
@@ -553,23 +645,64 @@ int32_t gc_pipeline_scan_finish(gc_pipeline* p, const double* h_gather) {
       p->x_rec = true;
     }
   }
+  GC_TRY(stage_event(p, 5));
   p->pending = false;
   GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream));
+  GC_TRY(stage_event(p, 6));
   if (p->smap_on) {
     auto& s = p->slots[p->pending_slot];
     const gc::ScanArgs& S = p->pending_S;
     const gc::ScanMapInput in{s.pts, s.t, S.t0, S.t1, p->smap_voxel, S.t1, p->pending_seq};
-    GC_TRY(gc::scan_map_update(ctx, ctx->stream, &p->smapW, p->smap, P, in));
-    if (p->smap_colors) {
+    int rc = gc::scan_map_update(ctx, ctx->stream, &p->smapW, p->smap, P, in);
+    if (rc == GC_OK && p->smap_colors) {
       // primitive_map_fuse ends with colors = rgb = the estimate from the camera accumulators on
-      // every slot (primitive_map.py:1090-1098); LiDAR rows leave those inputs unchanged, so after
-      // the first pass the assignment is idempotent and later updates skip it
-      GC_HIP(ctx, gc::launch_fuse_colors(p->smap, P.eps_mass, ctx->stream));
-      p->smap_colors = false;
+      // every slot (primitive_map.py:1090-1098); LiDAR rows leave those inputs unchanged, so the
+      // assignment is idempotent until a host operation (insert, merge, a colour upload) writes the
+      // colour fields and marks them stale again (gc_pipeline_map_colors_stale)
+      const hipError_t e = gc::launch_fuse_colors(p->smap, P.eps_mass, ctx->stream);
+      if (e != hipSuccess) {
+        gc::set_error(ctx, std::string("HIP error ") + hipGetErrorString(e) + " in the map colour pass");
+        rc = GC_ERR_RUNTIME;
+      } else {
+        p->smap_colors = false;
+      }
     }
-    GC_HIP(ctx, hipEventRecord(s.consumed, ctx->stream));  // the map update was the slot's last reader
-    s.consumed_rec = true;
+    // the map update was the slot's last reader: the next staging into the slot orders after this
+    // event on every path, a failed launch of the update included (its earlier kernels may be queued)
+    const hipError_t er = hipEventRecord(s.consumed, ctx->stream);
+    s.consumed_rec = er == hipSuccess;
+    s.consumed_ticket = 0;
+    if (rc != GC_OK) return rc;
+    GC_HIP(ctx, er);
   }
+  GC_TRY(stage_event(p, 7));
+  p->st_rec = p->st_timing;
+  return GC_OK;
+}
+
+int32_t gc_pipeline_scan_finish(gc_pipeline* p, const double* h_gather) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const double t0 = now_ms();
+  p->wait_acc_ms = 0.0;
+  const bool was_pending = p->pending;
+  const int32_t rc = scan_finish_impl(p, h_gather);
+  if (was_pending) {
+    // one scan = its local half and this finish: enqueue work and waits, each summed and maxed per scan
+    const double enq = p->scan_enq_ms + (now_ms() - t0 - p->wait_acc_ms), w = p->scan_wait_ms + p->wait_acc_ms;
+    double* h = p->hs;
+    h[GC_HS_SCANS] += 1.0;
+    h[GC_HS_SCAN_ENQ_MS] += enq;
+    h[GC_HS_SCAN_ENQ_MAX] = std::max(h[GC_HS_SCAN_ENQ_MAX], enq);
+    h[GC_HS_SCAN_WAIT_MS] += w;
+    h[GC_HS_SCAN_WAIT_MAX] = std::max(h[GC_HS_SCAN_WAIT_MAX], w);
+  }
+  return rc;
+}
+
+int32_t gc_pipeline_map_colors_stale(gc_pipeline* p) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, p->smap_on, "no PrimitiveMap attached");
+  p->smap_colors = p->smap.cam_mass != nullptr;
   return GC_OK;
 }
 
@@ -582,8 +715,10 @@ int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const gc_primitive_map*
   }
   GC_CHECK_ARG(p->ctx, map->m_slots > 0 && map->m_slots < (int64_t)0xFFFFFFFF, "m_slots out of range");
   GC_CHECK_ARG(p->ctx, map->n_lobes >= 1 && map->n_lobes <= 8, "n_lobes must be in [1, 8]");
-  GC_CHECK_ARG(p->ctx, map->slot_bytes == 0 || (map->slot_bytes % 8 == 0 && map->slot_bytes >= 176 + 24 * map->n_lobes),
-               "slot_bytes must be 0 (per-field arrays) or a packed record size");
+  {
+    const char* lay_ = gc::map_layout_error(*map);
+    GC_CHECK_ARG(p->ctx, lay_ == nullptr, lay_ ? lay_ : "");
+  }
   GC_CHECK_ARG(p->ctx, map->Lambdas && map->thetas && map->etas && map->weights && map->timestamps &&
                            map->last_supported_scan_seq && map->last_update_scan_seq,
                "NULL map field");
@@ -615,9 +750,8 @@ int32_t gc_pipeline_get_scan_map_count(gc_pipeline* p, int64_t* n_slots) {
   return GC_OK;
 }
 
-int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
+static int32_t scan_local_impl(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
                                double t_scan, double dt_sec, int64_t scan_count) {
-  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
   GC_CHECK_ARG(p->ctx, !p->pending, "the previous scan's exchange is pending (gc_pipeline_scan_finish)");
   GC_CHECK_ARG(p->ctx, slot >= 0 && slot < GC_PIPE_MAX_SLOTS && p->slots[slot].n_in > 0, "scan slot not staged");
   GC_CHECK_ARG(p->ctx, p->io_mode == GC_IO_GIVEN || p->slots[slot].has_odom,
@@ -627,14 +761,16 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   // the slot's staged scan must have landed. The host waits for the copy rather than the compute
   // stream: a cross-queue barrier costs ~6 us of device time per scan, while the host is normally a
   // scan or more ahead of the device and the copy (ordered after an earlier scan's bins) long done
-  if (s.ready_rec) GC_TRY(wait_event(ctx, s.ready));
+  if (s.ready_rec) GC_TRY(wait_event(p, s.ready));
   gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
                  scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in, s.t, p->sig_cached ? 1 : 0};
   gc::PipeDev& P = p->P;
   const bool io = p->io_mode == GC_IO_COMPUTED;
   // a1 budget scalars (the fused kernel reads the selection / mass scale from them) on extra
   // workgroups of the predict grid; a2 + a3
+  GC_TRY(stage_event(p, 0));
   GC_HIP(ctx, gc::launch_predict_imu(P, S, ctx->stream));
+  GC_TRY(stage_event(p, 1));
   // a1 -> a4 -> a5 -> a6 fused over all local hypotheses, and the a9a IMU/odom evidence branch
   // (pipeline.py:595-776: it needs the prediction, not the bins) as extra workgroups of the same
   // launch
@@ -645,16 +781,30 @@ int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, 
   GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in, p->smap_on ? nullptr : p->done_word,
                                 p->ticket));
   if (!p->smap_on) s.consumed_ticket = p->ticket;
+  GC_TRY(stage_event(p, 2));
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
   p->sig_cached = true;
+  GC_TRY(stage_event(p, 3));
   // a16 local part: this rank's partial record (weighted sums, IW statistics, map increment)
   GC_HIP(ctx, gc::launch_combine_local(P, ctx->stream));
+  GC_TRY(stage_event(p, 4));
   p->pending_S = S;
   p->pending_slot = slot;
   p->pending_seq = scan_count;
   p->pending = true;
   return GC_OK;
+}
+
+int32_t gc_pipeline_scan_local(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,
+                               double t_scan, double dt_sec, int64_t scan_count) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  const double t0 = now_ms();
+  p->wait_acc_ms = 0.0;
+  const int32_t rc = scan_local_impl(p, slot, scan_start, scan_end, t_last, t_scan, dt_sec, scan_count);
+  p->scan_wait_ms = p->wait_acc_ms;
+  p->scan_enq_ms = now_ms() - t0 - p->wait_acc_ms;
+  return rc;
 }
 
 int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out) {
@@ -667,13 +817,10 @@ int32_t gc_pipeline_get_combined(gc_pipeline* p, double* h_out) {
     // its eigen-decomposition was skipped on the scan path); the reference's ConditioningCert of the
     // combined belief (hypothesis.py:186-202) is the clamped spectrum of that same matrix, computed
     // here on demand by the Jacobi projection of the stored combined L
-    double* ws = nullptr;
-    GC_HIP(p->ctx, hipMalloc((void**)&ws, sizeof(double) * (484 + 6)));
-    int32_t rc = gc_domain_projection_psd_batch(p->ctx, 1, 22, p->P.comb, p->P.eps_psd, ws, ws + 484);
+    double* ws = p->ws;  // the pipeline's workspace (>= 2 Hl (484 + 6) doubles): no allocation here
+    GC_TRY(gc_domain_projection_psd_batch(p->ctx, 1, 22, p->P.comb, p->P.eps_psd, ws, ws + 484));
     double c6[6];
-    if (rc == GC_OK) rc = down(p, c6, ws + 484, 6);
-    (void)hipFree(ws);
-    if (rc != GC_OK) return rc;
+    GC_TRY(down(p, c6, ws + 484, 6));
     cc[2] = c6[2]; cc[3] = c6[3]; cc[4] = c6[4]; cc[5] = c6[5];
   }
   return GC_OK;
@@ -703,9 +850,8 @@ int32_t gc_pipeline_get_hyp_conditioning(gc_pipeline* p, double* h_out) {
   // stored matrix, computed here on demand by the Jacobi projection (off the scan path, as
   // gc_pipeline_get_combined does for the combined belief)
   const int Hl = p->P.Hl, NN = 484;
-  double* ws = nullptr;
+  double* ws = p->ws;  // 2 Hl (NN + 6) doubles, allocated with the pipeline
   const size_t len = (size_t)Hl * (NN + 6);
-  GC_HIP(p->ctx, hipMalloc((void**)&ws, sizeof(double) * 2 * len));
   const double* mats[2] = {p->P.Lpred, p->P.L};
   int32_t rc = GC_OK;
   for (int m = 0; m < 2 && rc == GC_OK; ++m)
@@ -714,7 +860,6 @@ int32_t gc_pipeline_get_hyp_conditioning(gc_pipeline* p, double* h_out) {
   std::vector<double> c6((size_t)2 * Hl * 6);
   if (rc == GC_OK) rc = down(p, c6.data(), ws + (size_t)Hl * NN, (size_t)Hl * 6);
   if (rc == GC_OK) rc = down(p, c6.data() + (size_t)Hl * 6, ws + len + (size_t)Hl * NN, (size_t)Hl * 6);
-  (void)hipFree(ws);
   if (rc != GC_OK) return rc;
   for (int h = 0; h < Hl; ++h)
     for (int m = 0; m < 2; ++m)
@@ -746,6 +891,37 @@ int32_t gc_pipeline_get_bin_stats(gc_pipeline* p, double* h_stats, double* h_cer
   GC_TRY(down(p, h_stats, p->P.stats, (size_t)p->P.Hl * p->P.B * 38));
   GC_TRY(down(p, h_cert, p->P.bincert, (size_t)p->P.Hl * 8));
   return down(p, h_xi, p->P.xi, (size_t)p->P.Hl * 6);
+}
+
+int32_t gc_pipeline_set_stage_timing(gc_pipeline* p, int32_t on) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  if (on && !p->st_ev[0])
+    for (hipEvent_t& e : p->st_ev) GC_HIP(p->ctx, hipEventCreate(&e));
+  p->st_timing = on != 0;
+  p->st_rec = false;
+  return GC_OK;
+}
+
+int32_t gc_pipeline_stage_ms(gc_pipeline* p, float* h_ms) {
+  GC_CHECK_ARG(nullptr, p && h_ms, "NULL argument");
+  GC_CHECK_ARG(p->ctx, p->st_rec, "no scan has finished with stage timing on (gc_pipeline_set_stage_timing)");
+  const double t0 = now_ms();
+  GC_HIP(p->ctx, hipEventSynchronize(p->st_ev[GC_STAGE_N - 1]));
+  p->wait_acc_ms += now_ms() - t0;
+  p->hs[GC_HS_HOST_SYNCS] += 1.0;
+  for (int i = 0; i + 1 < GC_STAGE_N; ++i)
+    GC_HIP(p->ctx, hipEventElapsedTime(&h_ms[i], p->st_ev[i], p->st_ev[i + 1]));
+  GC_HIP(p->ctx, hipEventElapsedTime(&h_ms[GC_STAGE_N - 1], p->st_ev[0], p->st_ev[GC_STAGE_N - 1]));
+  return GC_OK;
+}
+
+int32_t gc_pipeline_host_stats(gc_pipeline* p, double* h_out, int32_t reset) {
+  GC_CHECK_ARG(nullptr, p && h_out, "NULL argument");
+  for (int i = 0; i < GC_HOST_STATS; ++i) h_out[i] = p->hs[i];
+  if (reset)
+    for (double& v : p->hs) v = 0.0;
+  return GC_OK;
 }
 
 }  // extern "C"

@@ -34,6 +34,25 @@ hipError_t ensure_dyn_lds(const void* fn, size_t bytes) {
   return e;
 }
 
+int ensure_no_static_lds(gc_ctx* ctx, const void* fn) {
+  static std::mutex mu;
+  static std::map<std::pair<int, const void*>, bool> checked;
+  int dev = 0;
+  GC_HIP(ctx, hipGetDevice(&dev));
+  std::lock_guard<std::mutex> lock(mu);
+  auto it = checked.find({dev, fn});
+  if (it == checked.end()) {
+    hipFuncAttributes a{};
+    GC_HIP(ctx, hipFuncGetAttributes(&a, fn));
+    it = checked.emplace(std::make_pair(dev, fn), a.sharedSizeBytes == 0).first;
+  }
+  if (!it->second) {
+    set_error(ctx, "internal: a fused bins kernel has static LDS (its exp table is addressed from LDS 0)");
+    return GC_ERR_RUNTIME;
+  }
+  return GC_OK;
+}
+
 int scratch(gc_ctx* ctx, size_t bytes, void** out) {
   if (bytes > ctx->scratch_bytes) {
     GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
@@ -45,6 +64,24 @@ int scratch(gc_ctx* ctx, size_t bytes, void** out) {
     ctx->scratch_bytes = sz;
   }
   *out = ctx->scratch;
+  return GC_OK;
+}
+
+int slot_heads(gc_ctx* ctx, int64_t m_slots, uint32_t** out) {
+  if (m_slots > ctx->slot_head_n) {
+    GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (ctx->slot_head) GC_HIP(ctx, hipFree(ctx->slot_head));
+    ctx->slot_head = nullptr;
+    ctx->slot_head_n = 0;
+    GC_HIP(ctx, hipMalloc((void**)&ctx->slot_head, (size_t)m_slots * sizeof(uint32_t)));
+    ctx->slot_head_n = m_slots;
+    ctx->slot_head_dirty = true;
+  }
+  if (ctx->slot_head_dirty) {
+    GC_HIP(ctx, hipMemsetAsync(ctx->slot_head, 0xFF, (size_t)ctx->slot_head_n * sizeof(uint32_t), ctx->stream));
+    ctx->slot_head_dirty = false;
+  }
+  *out = ctx->slot_head;
   return GC_OK;
 }
 
@@ -94,6 +131,7 @@ int32_t gc_ctx_destroy(gc_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
+  if (ctx->slot_head) (void)hipFree(ctx->slot_head);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return GC_OK;

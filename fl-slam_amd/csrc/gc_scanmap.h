@@ -9,19 +9,16 @@ struct gc_ctx;
 
 namespace gc {
 
-// device work buffers of one pipeline's update: keys / row indices in and sorted, the rows, the
-// run-piece sums, the touched-slot counter and the sort's temporary storage (sized for n_cap rows
-// and the map's key width)
+// device work buffers of one pipeline's update (sized for n_cap rows): the sorted key of every block
+// position, the run links and run-piece sums (gc_runs.h), the touched-slot counter; the slot heads are
+// the context's (gc_ctx::slot_head)
 struct ScanMapWork {
   void* buf = nullptr;
   size_t bytes = 0;
-  uint32_t *keys_in = nullptr, *vals_in = nullptr, *keys = nullptr, *vals = nullptr;
-  double *rows = nullptr, *pieces = nullptr;  // (n_cap, 16) rows by row index; run-piece sums by sorted index
+  uint32_t *sslot = nullptr, *run_next = nullptr;
+  double* pieces = nullptr;  // (n_cap, 16) the run sums, at each run's last block position
   unsigned long long* count = nullptr;
-  void* temp = nullptr;  // radix sort temporary storage
-  size_t temp_bytes = 0;
-  int64_t n_cap = 0;
-  int bits = 0;
+  int64_t n_cap = 0, m_slots = 0;
 };
 
 struct ScanMapInput {

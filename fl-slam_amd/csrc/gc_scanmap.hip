@@ -10,7 +10,9 @@
 // inflates a bin centroid:
 //   μ_w = R p + t,   Σ_w = R Σ_lidar Rᵀ + J Σ_pose Jᵀ,   J = [R | −R [p]×],
 //   Λ_w = Σ_w⁻¹,     θ_w = Λ_w μ_w,   η_w = [R d, 0, ..] (d = the unit ray direction),
-// with Σ_lidar the measurement-IW LiDAR block's mode Ψ_2 / (ν_2 + 4) and the row's weight the
+// with Σ_lidar the measurement-IW LiDAR block's mode Ψ_2 / (ν_2 + 4) of the IW state the scan started
+// from (before its own measurement-IW apply, as the reference's step 12b reads the scan's config) and the
+// row's weight the
 // deskewed point weight (a4). Its slot is the spatial hash of the world voxel of μ_w. The rows are
 // fused with responsibility 1 and source LiDAR by a reduce-by-key: a stable radix sort of (slot,
 // row) and a two-pass segmented reduction in a fixed order (k_smap_pieces / k_smap_apply:
@@ -19,16 +21,17 @@
 // (~65k rows into ~5k slots, runs of thousands near the sensor), so rows are computed one per
 // thread and the runs reduced in parallel: one thread per run summing its rows serially took
 // ~1 ms per scan. LiDAR rows leave the camera accumulators unchanged,
-// so the all-slot colour recompute (colors = rgb) runs only on the first update after the map is
-// attached (gc_pipeline.cpp), when it may change colours an empty tile holds.
+// so the all-slot colour recompute (colors = rgb) runs only when the colours are stale: on the first
+// update after the map is attached, and after a host operation wrote colour fields (an insert, a
+// merge, a colour upload: gc_pipeline_map_colors_stale; gc_pipeline.cpp).
 //
 // Every rank runs the update from the reduced record, so the maps stay bit-identical across ranks.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include "gc_internal.h"
 #include "gc_math.h"
 #include "gc_mapslot.h"
 #include "gc_pipe.h"
+#include "gc_runs.h"
 #include "gc_scanmap.h"
 
 namespace gc {
@@ -38,7 +41,7 @@ struct ScanMapArgs {
   gc_primitive_map map;
   const double *pts, *t, *w_win, *bscal;  // the scan slot and predict's per-point w x window, budget
   const double* h0;                       // reduced record: [z_t 6, Σ_pose 36, ξ 6] of hypothesis 0
-  const double *nu_meas, *Psi_meas;       // measurement IW state (LiDAR block 2)
+  const double* lidar_iw;                 // [ν_2, Ψ_2] of the scan, before its measurement-IW apply
   int64_t n_cap;
   double t0, t1, o0, o1, o2, voxel, timestamp, eps_mass;
   int64_t scan_seq;
@@ -135,96 +138,103 @@ GC_DEV void smap_row(const double* C, const double* o, double eps_mass, const do
   mat3_vec(R, d, e0);
 }
 
-// one thread per row: its slot key (m_slots for a dropped row, sorted after every slot) and its
-// world row [Λ_w 9, θ_w 3, η_w lobe 0 3, w] (zeros when dropped)
-__global__ void k_smap_rows(ScanMapArgs A, uint32_t* keys, uint32_t* vals, SmapRow* rows) {
+// Pass 1, one workgroup per block of kSmapBlk rows (gc_runs.h): every thread forms one row's slot key
+// (m_slots for a dropped row, sorted after every slot) and world row [Λ_w 9, θ_w 3, η_w lobe 0 3, w]
+// into LDS; the block sorts (key, row) and sums each run of equal keys by a segmented inclusive scan
+// in sorted order (Hillis-Steele: a step adds the entry d back when it has the same key; the order
+// depends on the positions only); each run's last position holds the run's sum, written as the run's
+// piece and linked into its slot's list. A scan's points crowd into few voxels (~65k rows into ~5k
+// slots), so most of the work is this in-block reduction; the lists hold one piece per block.
+constexpr int kSmapBlk = 256;
+__global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, uint32_t* head, uint32_t* sslot,
+                                                         uint32_t* run_next, SmapRow* pieces) {
   __shared__ double C[kSmapC + 3];
-  if (threadIdx.x == 0) {  // the scan's constants: R, tt, Rᵀ t, Σ_lidar, Σ_pose
+  __shared__ double v[kSmapRow][kSmapBlk];
+  __shared__ uint64_t a[kSmapBlk];
+  const int t = threadIdx.x;
+  if (t == 0) {  // the scan's constants: R, tt, Rᵀ t, Σ_lidar, Σ_pose
     double R[9], tt[3];
     smap_pose(A, R, tt);
     for (int q = 0; q < 9; ++q) C[q] = R[q];
     mat3_tvec(R, tt, C + 9);
-    const double den = A.nu_meas[2] + 3.0 + 1.0;  // measurement_noise_mean_jax, LiDAR block
-    for (int q = 0; q < 9; ++q) C[12 + q] = A.Psi_meas[18 + q] / den;
+    const double den = A.lidar_iw[0] + 3.0 + 1.0;  // measurement_noise_mean_jax, LiDAR block
+    for (int q = 0; q < 9; ++q) C[12 + q] = A.lidar_iw[1 + q] / den;
     for (int q = 0; q < 36; ++q) C[21 + q] = A.h0[6 + q];
     for (int q = 0; q < 3; ++q) C[kSmapC + q] = tt[q];
   }
   __syncthreads();
-  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= A.n_cap) return;
+  const int64_t j = (int64_t)blockIdx.x * kSmapBlk + t;
+  const int64_t M = A.map.m_slots;
   double p0[3], w, mw[3];
   SmapRow row;
   for (int q = 0; q < kSmapRow; ++q) row.v[q] = 0.0;
-  uint32_t key = (uint32_t)A.map.m_slots;
-  if (smap_point(A, j, p0, &w)) {
+  uint32_t key = j < A.n_cap ? (uint32_t)M : kNoRun;
+  if (j < A.n_cap && smap_point(A, j, p0, &w)) {
     smap_world_mean(C, C + kSmapC, p0, mw);
-    key = smap_slot(mw, A.voxel, A.map.m_slots);
+    key = smap_slot(mw, A.voxel, M);
     const double o[3] = {A.o0, A.o1, A.o2};
     smap_row(C, o, A.eps_mass, p0, row.v, row.v + 9, row.v + 12);
     row.v[15] = w;
   }
-  keys[j] = key;
-  vals[j] = (uint32_t)j;
-  rows[j] = row;
-}
-
-// Runs of the sorted keys summed in a fixed order, in two passes. Pass 1: one workgroup per 256
-// sorted rows gathers them into LDS and runs a segmented inclusive scan (Hillis-Steele, a step
-// adds the entry d back when it has the same key: sorted keys make that the same run); the last
-// entry of each run piece in the block writes the piece's sum. Pass 2: one thread per run head
-// adds its pieces block by block in ascending order and applies the total to the slot. The order
-// depends on the row positions only: bit-reproducible.
-constexpr int kSmapBlk = 256;
-__global__ void __launch_bounds__(kSmapBlk) k_smap_pieces(int64_t n, const uint32_t* __restrict__ keys,
-                                                          const uint32_t* __restrict__ vals,
-                                                          const SmapRow* __restrict__ rows, SmapRow* pieces) {
-  __shared__ double v[kSmapRow][kSmapBlk];
-  __shared__ uint32_t k[kSmapBlk];
-  const int t = threadIdx.x;
-  const int64_t i = (int64_t)blockIdx.x * kSmapBlk + t;
-  const bool in = i < n;
-  k[t] = in ? keys[i] : 0xFFFFFFFFu;
-  SmapRow r;
-  if (in) r = rows[vals[i]];
-  else
-    for (int q = 0; q < kSmapRow; ++q) r.v[q] = 0.0;
-  for (int q = 0; q < kSmapRow; ++q) v[q][t] = r.v[q];
+  for (int q = 0; q < kSmapRow; ++q) v[q][t] = row.v[q];
+  a[t] = ((uint64_t)key << 32) | (uint32_t)t;
+  lds_bitonic_sort<kSmapBlk>(a);
+  // position t of the sorted block: its row's values, then the segmented scan in sorted order
+  const uint32_t k_t = (uint32_t)(a[t] >> 32);
+  const int src = (int)(uint32_t)a[t];
+  double x[kSmapRow];
+  for (int q = 0; q < kSmapRow; ++q) x[q] = v[q][src];
+  __syncthreads();
+  for (int q = 0; q < kSmapRow; ++q) v[q][t] = x[q];
   __syncthreads();
   for (int d = 1; d < kSmapBlk; d <<= 1) {
-    const bool take = t >= d && k[t - d] == k[t];
-    double a[kSmapRow];
-    for (int q = 0; q < kSmapRow; ++q) a[q] = take ? v[q][t - d] : 0.0;
+    const bool take = t >= d && (uint32_t)(a[t - d] >> 32) == k_t;
+    double y[kSmapRow];
+    for (int q = 0; q < kSmapRow; ++q) y[q] = take ? v[q][t - d] : 0.0;
     __syncthreads();
     if (take)
-      for (int q = 0; q < kSmapRow; ++q) v[q][t] = a[q] + v[q][t];
+      for (int q = 0; q < kSmapRow; ++q) v[q][t] = y[q] + v[q][t];
     __syncthreads();
   }
-  if (in && (t == kSmapBlk - 1 || i == n - 1 || k[t + 1] != k[t])) {
+  const int64_t p = (int64_t)blockIdx.x * kSmapBlk + t;
+  if (p < A.n_cap) sslot[p] = k_t;
+  const bool tail = (int64_t)k_t < M && (t == kSmapBlk - 1 || (uint32_t)(a[t + 1] >> 32) != k_t);
+  if (tail) {
     SmapRow o;
     for (int q = 0; q < kSmapRow; ++q) o.v[q] = v[q][t];
-    pieces[i] = o;
+    pieces[p] = o;
+    run_next[p] = atomicExch(&head[k_t], (uint32_t)p);
   }
 }
 
-// one thread per run tail: the run's pieces are at the ends of the blocks it covers and at the tail
-// itself; the head's block is found by stepping back over block boundaries (one load per block of
-// the run), then the pieces are added in ascending block order and the total applied to the slot
-// (the fuse's read-modify-write)
-__global__ void k_smap_apply(ScanMapArgs A, int64_t n, const uint32_t* __restrict__ keys,
-                             const SmapRow* __restrict__ pieces, unsigned long long* n_unique) {
+// Pass 2, one thread per position: the owner of each slot (the run its list ends on) adds the slot's
+// pieces in block order and read-modify-writes the slot (the fuse with responsibility 1, source LiDAR)
+__global__ void k_smap_apply(ScanMapArgs A, int64_t n, uint32_t* head, const uint32_t* __restrict__ sslot,
+                             const uint32_t* __restrict__ run_next, const SmapRow* __restrict__ pieces,
+                             unsigned long long* n_unique) {
 #pragma clang fp contract(off)
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= n) return;
-  const uint32_t key = keys[e];
-  if ((int64_t)key >= A.map.m_slots || (e + 1 < n && keys[e + 1] == key)) return;  // dropped / not a run tail
-  const int64_t bt = e / kSmapBlk;
-  int64_t bh = bt;
-  while (bh > 0 && keys[bh * kSmapBlk - 1] == key) --bh;
+  const uint32_t key = sslot[e];
+  if ((int64_t)key >= A.map.m_slots || head[key] != (uint32_t)e) return;  // dropped / not the owner
   SmapRow d;
   for (int q = 0; q < kSmapRow; ++q) d.v[q] = 0.0;
-  for (int64_t b = bh; b <= bt; ++b) {
-    const SmapRow p = pieces[b < bt ? (b + 1) * kSmapBlk - 1 : e];
-    for (int q = 0; q < kSmapRow; ++q) d.v[q] = d.v[q] + p.v[q];
+  const auto add = [&](uint32_t r) {
+    const SmapRow pc = pieces[r];
+    for (int q = 0; q < kSmapRow; ++q) d.v[q] = d.v[q] + pc.v[q];
+  };
+  if (run_next[e] == kNoRun) {
+    add((uint32_t)e);
+  } else {
+    RunList<32> rl;
+    rl.collect((uint32_t)e, run_next, (int)((n + kSmapBlk - 1) / kSmapBlk));
+    uint32_t prev = 0;
+    for (int i = 0; i < rl.n; ++i) {
+      const uint32_t r = rl.at(i, (uint32_t)e, run_next, prev);
+      if (r == kNoRun) break;  // only a corrupt list: never index past the runs
+      prev = r;
+      add(r);
+    }
   }
   const int64_t s = key;
   const int L = A.map.n_lobes;
@@ -238,30 +248,18 @@ __global__ void k_smap_apply(ScanMapArgs A, int64_t n, const uint32_t* __restric
   mSup(A.map, s) = A.scan_seq;
   mUpd(A.map, s) = A.scan_seq;
   if (A.map.lidar_mass) mLid(A.map, s) = mLid(A.map, s) + d.v[15];
+  head[key] = kNoRun;       // the list is consumed
   atomicAdd(n_unique, 1ull);  // integer count: order-independent
-}
-
-inline int key_bits(int64_t M) {
-  int b = 1;
-  while (b < 32 && (M >> b) != 0) ++b;
-  return b;
 }
 
 }  // namespace
 
 int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_slots) {
   W->n_cap = n_cap;
-  W->bits = key_bits(m_slots);
-  size_t t_sort = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, t_sort, (const uint32_t*)nullptr, (uint32_t*)nullptr,
-                                         (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)n_cap, 0, W->bits,
-                                         ctx->stream) != hipSuccess) {
-    set_error(ctx, "radix sort sizing failed");
-    return GC_ERR_RUNTIME;
-  }
+  W->m_slots = m_slots;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t kv = up((size_t)n_cap * sizeof(uint32_t)), rv = up((size_t)n_cap * sizeof(SmapRow));
-  const size_t bytes = 4 * kv + 2 * rv + 256 + up(t_sort);
+  const size_t bytes = 2 * kv + rv + 256;
   if (bytes > W->bytes) {
     if (W->buf) GC_HIP(ctx, hipFree(W->buf));
     W->buf = nullptr;
@@ -270,16 +268,12 @@ int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_s
     W->bytes = bytes;
   }
   char* base = (char*)W->buf;
-  W->keys_in = (uint32_t*)base;
-  W->vals_in = (uint32_t*)(base + kv);
-  W->keys = (uint32_t*)(base + 2 * kv);
-  W->vals = (uint32_t*)(base + 3 * kv);
-  W->rows = (double*)(base + 4 * kv);
-  W->pieces = (double*)(base + 4 * kv + rv);
-  W->count = (unsigned long long*)(base + 4 * kv + 2 * rv);
-  W->temp = base + 4 * kv + 2 * rv + 256;
-  W->temp_bytes = up(t_sort);
-  return GC_OK;
+  W->sslot = (uint32_t*)base;
+  W->run_next = (uint32_t*)(base + kv);
+  W->pieces = (double*)(base + 2 * kv);
+  W->count = (unsigned long long*)(base + 2 * kv + rv);
+  uint32_t* head = nullptr;
+  return slot_heads(ctx, m_slots, &head);  // allocated (and filled) now, outside any scan
 }
 
 int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_primitive_map& map,
@@ -288,30 +282,24 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
   A.map = map;
   A.pts = in.pts; A.t = in.t; A.w_win = P.w_win; A.bscal = P.budget;
   A.h0 = P.send + rec_h0(P.B);  // the reduced record (k_combine_final, earlier on this stream)
-  A.nu_meas = P.nu_meas; A.Psi_meas = P.Psi_meas;
+  A.lidar_iw = P.lidar_iw;  // written by k_combine_final, earlier on this stream
   A.n_cap = P.n_cap;
   A.t0 = in.t0; A.t1 = in.t1;
   A.o0 = P.o0; A.o1 = P.o1; A.o2 = P.o2;
   A.voxel = in.voxel; A.timestamp = in.timestamp; A.eps_mass = P.eps_mass;
   A.scan_seq = in.scan_seq;
   const int64_t n = P.n_cap;
-  const unsigned grid = (unsigned)((n + 255) / 256);
+  uint32_t* head = nullptr;
+  if (int rc = slot_heads(ctx, map.m_slots, &head)) return rc;
   GC_HIP(ctx, hipMemsetAsync(W->count, 0, sizeof(unsigned long long), st));
-  hipLaunchKernelGGL(k_smap_rows, dim3(grid), dim3(256), 0, st, A, W->keys_in, W->vals_in, (SmapRow*)W->rows);
+  ctx->slot_head_dirty = true;  // until both passes are enqueued
+  hipLaunchKernelGGL(k_smap_block, dim3((unsigned)((n + kSmapBlk - 1) / kSmapBlk)), dim3(kSmapBlk), 0, st, A, head,
+                     W->sslot, W->run_next, (SmapRow*)W->pieces);
   GC_LAUNCH_CHECK(ctx);
-  size_t t1 = W->temp_bytes;
-  if (hipcub::DeviceRadixSort::SortPairs(W->temp, t1, W->keys_in, W->keys, W->vals_in, W->vals, (int)n, 0, W->bits,
-                                         st) != hipSuccess) {
-    set_error(ctx, "radix sort failed");
-    return GC_ERR_RUNTIME;
-  }
-  hipLaunchKernelGGL(k_smap_pieces, dim3((unsigned)((n + kSmapBlk - 1) / kSmapBlk)), dim3(kSmapBlk), 0, st, n,
-                     (const uint32_t*)W->keys, (const uint32_t*)W->vals, (const SmapRow*)W->rows,
-                     (SmapRow*)W->pieces);
+  hipLaunchKernelGGL(k_smap_apply, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, n, head,
+                     (const uint32_t*)W->sslot, (const uint32_t*)W->run_next, (const SmapRow*)W->pieces, W->count);
   GC_LAUNCH_CHECK(ctx);
-  hipLaunchKernelGGL(k_smap_apply, dim3(grid), dim3(256), 0, st, A, n, (const uint32_t*)W->keys,
-                     (const SmapRow*)W->pieces, W->count);
-  GC_LAUNCH_CHECK(ctx);
+  ctx->slot_head_dirty = false;
   return GC_OK;
 }
 

@@ -86,13 +86,18 @@ SIGNATURES = {
     "gc_pipeline_comm_size": [_vp],
     "gc_pipeline_attach_primitive_map": [_vp, _vp, _f64],
     "gc_pipeline_get_scan_map_pose": [_vp, _vp],
+    "gc_pipeline_map_colors_stale": [_vp],
     "gc_pipeline_get_scan_map_count": [_vp, C.POINTER(C.c_int64)],
     "gc_pipeline_set_exchange_timing": [_vp, _i32],
     "gc_pipeline_exchange_ms": [_vp, C.POINTER(C.c_float)],
+    "gc_pipeline_set_stage_timing": [_vp, _i32],
+    "gc_pipeline_stage_ms": [_vp, _vp],
+    "gc_pipeline_host_stats": [_vp, _vp, _i32],
     "gc_comm_unique_id": [_vp],
     "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],
     "gc_comm_destroy": [_vp],
     "gc_comm_allgather_f64": [_vp, _vp, _vp, _vp, _i64],
+    "gc_lie_batch": [_vp, _i32, _i64, _vp, _vp],
     "gc_belief_world_pose_batch": [_vp, _i32, _vp, _vp, _vp, _f64, _vp, _vp],
     "gc_predict_diffusion_batch": [_vp, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _f64, _vp, _vp, _vp],
     "gc_smooth_window_weights": [_vp, _i32, _vp, _f64, _f64, _f64, _vp],
@@ -137,6 +142,12 @@ GC_IOF_OUT = 484 + 22 + 16
  GC_IOF_VELOCITY_Z_PRIOR, GC_IOF_ODOM_VELOCITY, GC_IOF_ODOM_YAWRATE, GC_IOF_KINEMATIC, GC_IOF_IMU_DEPENDENCE,
  GC_IOF_ODOM_DEPENDENCE) = range(10)
 GC_HYP_DIAG = 40
+GC_STAGE_N = 8
+GC_STAGE_NAMES = ("predict", "bins", "evidence", "combine_local", "exchange", "combine_final", "map_update", "total")
+GC_HOST_STATS = 16
+GC_HS_NAMES = ("scans", "scan_enqueue_ms", "scan_enqueue_max_ms", "scan_wait_ms", "scan_wait_max_ms", "stages",
+               "stage_work_ms", "stage_work_max_ms", "stage_wait_ms", "stage_wait_max_ms", "host_syncs", "h2d_bytes",
+               "d2h_bytes", "jit_recompiles")
 GC_COMB_LEN = 484 + 22 + 22 + 6 + 16
 GC_COMM_ID_BYTES = 128
 GC_PRED_CERT = 8

@@ -262,6 +262,25 @@ def tape_from_pipeline(pipe, scan_number: int, timestamp: float, dt_sec: float, 
         **{f"t_{k}": float(v) for k, v in tm.items() if f"t_{k}" in _TYPES})
 
 
+def tape_timing_ms(stage_ms: Dict[str, float]) -> Dict[str, float]:
+    """The tape's t_*_ms labels (pipeline.py:383-394, :1560-1569) from the batched pipeline's device
+    stage times (BatchedScanPipeline.stage_ms). The device fuses several reference steps into one
+    launch; each launch is reported under the first reference step it contains:
+      imu_preint_scan_ms  the predict launch (a1 budget scalars, a2 predict, a3 scan-window preintegration)
+      deskew_ms           the bins launch (a1 selection, a4 deskew, a5, a6, and the IMU/odom branch with
+                          its integration-window preintegration) and its finalize
+      map_update_ms       combine_final (a16, the IW applies, the bin-map update) + the PrimitiveMap update
+      total_ms            the whole scan, evidence, combine and exchange included.
+    point_budget_ms and imu_preint_int_ms run inside those launches (0 here); surfel extraction,
+    association, visual pose and the map branch are not on this path (0, as the reference reports
+    for steps it does not run)."""
+    g = lambda k: float(stage_ms.get(k, 0.0))
+    return {"total_ms": g("total_ms"), "point_budget_ms": 0.0, "deskew_ms": g("bins_ms"),
+            "imu_preint_scan_ms": g("predict_ms"), "imu_preint_int_ms": 0.0, "surfel_extraction_ms": 0.0,
+            "association_ms": 0.0, "visual_pose_evidence_ms": 0.0, "map_branch_ms": 0.0,
+            "map_update_ms": g("combine_final_ms") + g("map_update_ms")}
+
+
 def runtime_manifest(**overrides) -> Dict[str, Any]:
     """RuntimeManifest.to_dict (pipeline.py:1629-1793) for the batched GPU pipeline: the constants it
     runs with and the device implementation behind each backend key."""

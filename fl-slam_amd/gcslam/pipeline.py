@@ -11,6 +11,7 @@ rank ends the scan with a bit-identical combined belief, IW state and map.
 from __future__ import annotations
 
 import ctypes as C
+import weakref
 from dataclasses import dataclass
 from typing import Optional
 
@@ -96,6 +97,7 @@ class BatchedScanPipeline:
         _abi.call("gc_pipeline_create", self.ctx.handle, C.addressof(d), cfgv.ctypes.data, C.byref(h), ctx=self.ctx)
         self.handle = h.value
         self._comm = None
+        self._smap = None
         self.io_computed = True  # GC_IO_COMPUTED is the device default
         self.set_bins(create_fibonacci_atlas(self.B).dirs)
         self.set_weights(np.full(H_total, 1.0 / H_total))
@@ -194,6 +196,8 @@ class BatchedScanPipeline:
     def run_scan(self, slot: int, scan: dict, scan_count: int):
         self._call("gc_pipeline_run_scan", int(slot), float(scan["scan_start"]), float(scan["scan_end"]),
                    float(scan["t_last"]), float(scan["t_scan"]), float(scan["dt_sec"]), int(scan_count))
+        if self._smap is not None:
+            self._map_updated()
 
     def run_scan_local(self, slot: int, scan: dict, scan_count: int):
         """a1-a15 for this rank's hypotheses and its partial record; finish with finish_scan."""
@@ -211,6 +215,8 @@ class BatchedScanPipeline:
         rank order (any transport), or None for the RCCL all-gather / the single-rank record."""
         g = None if gathered is None else _f(gathered, (self.world, partial_len(self.B)))
         self._call("gc_pipeline_scan_finish", _p(g))
+        if self._smap is not None:
+            self._map_updated()
 
     def combined(self):
         o = np.empty(_abi.GC_COMB_LEN)
@@ -260,6 +266,20 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_attach_primitive_map", None if dmap is None else C.addressof(dmap.struct()),
                    float(voxel_m))
         self._smap = dmap  # the device arrays must outlive the attachment
+        if dmap is not None:
+            dmap._listeners.append(weakref.ref(self))
+
+    def _map_colors_stale(self):
+        """The attached map's colour fields were written by a host operation (DevicePrimitiveMap
+        .colors_stale): the next in-scan update recomputes every slot's colour estimate."""
+        self._call("gc_pipeline_map_colors_stale")
+
+    def _map_updated(self):
+        """After a scan_finish with a map attached the map's colours are the fuse's estimate on every
+        slot (the update's colour pass ran if they were stale; LiDAR rows keep them otherwise)."""
+        m = getattr(self, "_smap", None)
+        if m is not None and "cam_mass" in m.ptrs:
+            m._tile_cc = [True] * m.n_tiles
 
     def scan_map_pose(self):
         """(z_t (6), Σ_pose (6,6), ξ_body (6)) of hypothesis 0 that the last scan's map update used."""
@@ -301,6 +321,38 @@ class BatchedScanPipeline:
         ms = C.c_float(0.0)
         self._call("gc_pipeline_exchange_ms", C.byref(ms))
         return float(ms.value)
+
+    # ---------------------------------------------------------------- observability
+    def set_stage_timing(self, on: bool = True) -> None:
+        """Record HIP events around every launch group of later scans (off by default: each event
+        between kernels costs the stream ~1-5 us)."""
+        self._call("gc_pipeline_set_stage_timing", 1 if on else 0)
+
+    def stage_ms(self) -> dict:
+        """Device time (ms) of each stage of the last scan finished with stage timing on
+        (_abi.GC_STAGE_NAMES: predict, bins, evidence, combine_local, exchange, combine_final,
+        map_update, total)."""
+        o = (C.c_float * _abi.GC_STAGE_N)()
+        self._call("gc_pipeline_stage_ms", C.addressof(o))
+        return {f"{k}_ms": float(v) for k, v in zip(_abi.GC_STAGE_NAMES, o)}
+
+    def host_stats(self, reset: bool = False) -> dict:
+        """Host-side accounting (include/gcslam.h GC_HS_*): per-scan enqueue work vs waits on the
+        device, staging work vs waits, host syncs, host<->device bytes."""
+        o = np.zeros(_abi.GC_HOST_STATS)
+        self._call("gc_pipeline_host_stats", _p(o), 1 if reset else 0)
+        return {k: float(v) for k, v in zip(_abi.GC_HS_NAMES, o)}
+
+    def device_runtime_cert(self, consume: bool = True):
+        """DeviceRuntimeCert of the work since the last consume (backend_node.py:2182-2190 with
+        consume_runtime_counters, common/runtime_counters.py:94-108): this pipeline's host syncs and
+        host<->device bytes; jit_recompile_count is 0 (ahead-of-time compiled library)."""
+        from .certificates import DeviceRuntimeCert
+        h = self.host_stats(reset=consume)
+        return DeviceRuntimeCert(host_sync_count_est=int(h["host_syncs"]),
+                                 device_to_host_bytes_est=int(h["d2h_bytes"]),
+                                 host_to_device_bytes_est=int(h["h2d_bytes"]),
+                                 jit_recompile_count=int(h["jit_recompiles"]))
 
     def close(self):
         if getattr(self, "handle", None):

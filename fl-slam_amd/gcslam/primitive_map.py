@@ -11,7 +11,7 @@ from __future__ import annotations
 
 import ctypes as C
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Tuple
+from typing import Any, Dict, List, Optional, Tuple
 
 import numpy as np
 
@@ -88,12 +88,15 @@ class DevicePrimitiveMap:
                 self.ptrs[k] = self.fields[k].ptr
         self._struct = _MapStruct(M, self.n_lobes, 0, *[self.ptrs.get(k) for k in _F64 + _I64 + _COL + _MAINT],
                                   self.slot_bytes)
-        if track_colors:
-            self.upload(rgb=np.full((M, 3), 0.5))
         # per tile: every slot's rgb and colors = the fuse's estimate of its camera accumulators. Not so
         # for an empty tile (create_empty_tile: rgb gray, colors 0); a fuse leaves its tile current,
         # insert / merge / a colour upload do not
         self._tile_cc = [False] * self.n_tiles
+        # pipelines with this map attached (BatchedScanPipeline.attach_primitive_map): told when a host
+        # operation makes the colours stale, so their next in-scan update recomputes every slot's
+        self._listeners: List[Any] = []
+        if track_colors:
+            self.upload(rgb=np.full((M, 3), 0.5))
         # AtlasMap bookkeeping (primitive_map.py:183-201): host integers, as in the reference
         self.next_global_id = 0
         self.total_count = 0
@@ -109,7 +112,26 @@ class DevicePrimitiveMap:
 
     @colors_current.setter
     def colors_current(self, v: bool) -> None:
-        self._tile_cc = [bool(v)] * self.n_tiles
+        if not v:
+            self.colors_stale()
+        else:
+            self._tile_cc = [True] * self.n_tiles
+
+    def colors_stale(self, tile_id: Optional[int] = None) -> None:
+        """A host operation wrote colour fields (insert, merge, a colour upload): rgb / colors of the
+        tile (None: every tile) are no longer the fuse's estimate. Attached pipelines are told, so
+        their next in-scan update recomputes them (gc_pipeline_map_colors_stale)."""
+        if tile_id is None:
+            self._tile_cc = [False] * self.n_tiles
+        else:
+            self._tile_cc[int(tile_id)] = False
+        alive = []
+        for ref in self._listeners:
+            pipe = ref()
+            if pipe is not None and getattr(pipe, "_smap", None) is self:
+                pipe._map_colors_stale()
+                alive.append(ref)
+        self._listeners = alive
 
     def struct(self) -> "_MapStruct":
         """The whole flat map (all tiles) for a C entry, its colour flag up to date."""
@@ -148,7 +170,7 @@ class DevicePrimitiveMap:
             if k not in self.ptrs:
                 raise KeyError(k)
             if k in _COL:
-                self.colors_current = False  # arbitrary colours / accumulators: the next fuse recomputes all
+                self.colors_stale()  # arbitrary colours / accumulators: the next fuse recomputes all
             if not self.packed:
                 self.fields[k].upload(v)
                 continue
@@ -393,7 +415,7 @@ def primitive_map_insert_masked(atlas_map: DevicePrimitiveMap, tile_id: int, Lam
               d_slots.ptr, d_ids.ptr, out.ctypes.data, ctx=ctx)
     n_ins, count = int(out[0]), int(out[1])
     if n_ins > 0:
-        atlas_map._tile_cc[int(tile_id)] = False  # inserted colours are clip(c), not the estimate clip(c·cam / cam)
+        atlas_map.colors_stale(tile_id)  # inserted colours are clip(c), not the estimate clip(c·cam / cam)
     atlas_map.next_global_id += n_ins
     atlas_map.total_count += n_ins
     atlas_map.tile_count[int(tile_id)] = count
@@ -447,7 +469,7 @@ def primitive_map_merge_reduce(atlas_map: DevicePrimitiveMap, tile_id: int,
     n_merged, count = int(out[0]), int(out[1])
     if n_merged <= 0:
         return no_op(float(max_pairs))
-    atlas_map._tile_cc[int(tile_id)] = False  # merged colours use max(denom, eps_psd) (primitive_map.py:1976-1983)
+    atlas_map.colors_stale(tile_id)  # merged colours use max(denom, eps_psd) (primitive_map.py:1976-1983)
     atlas_map.tile_count[int(tile_id)] = count
     atlas_map.total_count -= n_merged
     cert = CertBundle.create_approx(chart_id=chart_id, anchor_id=anchor_id, triggers=["primitive_map_merge_reduce"],

@@ -77,12 +77,24 @@ def make_scan(scan_idx: int = 0, n_rings: int = 16, n_az: int = 4096, room=(10.0
                 odom_pose=odom_pose, odom_cov=odom_cov, odom_twist=odom_twist, odom_twist_cov=odom_twist_cov)
 
 
-def make_hypotheses(H: int, seed: int = SEED0, prior_precision: float = 1e-6):
-    """Identity-prior beliefs (belief.py:328-371) with perturbed anchors."""
+def make_hypotheses(H: int, seed: int = SEED0, prior_precision: float = 1e-6, yaws=None, tilt: float = 0.0):
+    """Identity-prior beliefs (belief.py:328-371) with perturbed anchors.
+
+    yaws: optional world yaws (rad) cycled over the hypotheses; each anchor's rotation is then
+    Rz(yaw) · Exp(N(0, tilt²) roll/pitch + N(0, 0.02²)) (a robot that has turned around: rotation
+    vectors near ±π). Translations stay N(0, 5 cm)."""
     rng = np.random.default_rng(seed + 777)
     X = np.zeros((H, 6))
     X[:, 0:3] = rng.normal(0.0, 0.05, size=(H, 3))
     X[:, 3:6] = rng.normal(0.0, 0.02, size=(H, 3))
+    if yaws is not None:
+        from scipy.spatial.transform import Rotation
+        yaws = np.asarray(yaws, dtype=np.float64)
+        pert = X[:, 3:6].copy()
+        pert[:, 0:2] += rng.normal(0.0, tilt, size=(H, 2))
+        yaw = yaws[np.arange(H) % yaws.shape[0]]
+        R = Rotation.from_rotvec(np.stack([np.zeros(H), np.zeros(H), yaw], 1)) * Rotation.from_rotvec(pert)
+        X[:, 3:6] = R.as_rotvec()
     L = np.broadcast_to(prior_precision * np.eye(D_Z), (H, D_Z, D_Z)).copy()
     return dict(X_anchor=X, z_lin=np.zeros((H, D_Z)), L=L, h=np.zeros((H, D_Z)),
                 stamp=np.zeros(H), weights=np.full(H, 1.0 / H))

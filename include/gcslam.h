@@ -330,17 +330,57 @@ int32_t gc_pipeline_set_exchange_timing(gc_pipeline* p, int32_t on);
  * exchange has run (timing off, or one rank without a communicator). */
 int32_t gc_pipeline_exchange_ms(gc_pipeline* p, float* ms);
 
+/* Per-stage device timing (off by default; the reference fills MinimalScanTape.t_*_ms per stage,
+ * pipeline.py:383-394, :1560-1569). With on != 0 every later scan records GC_STAGE_N HIP events on the
+ * pipeline stream, before predict and after each launch group; gc_pipeline_stage_ms returns the last
+ * finished scan's stage times (ms) [predict (a1 scalars, a2, a3), bins (a1 selection, a4, a5, a6 and
+ * the IMU/odom branch, + finalize), evidence (a7-a15), combine_local, exchange, combine_final (a16, IW
+ * apply, bin-map update), map_update (the attached PrimitiveMap's, 0 without one), total]. Each event
+ * between kernels costs the stream ~1-5 us, so the timed product loop leaves it off. stage_ms
+ * synchronises on the last event. */
+#define GC_STAGE_N 8
+int32_t gc_pipeline_set_stage_timing(gc_pipeline* p, int32_t on);
+int32_t gc_pipeline_stage_ms(gc_pipeline* p, float* h_ms_out);
+/* Host-side accounting since creation or the last reset (GC_HOST_STATS doubles): the reference's
+ * RuntimeCounters / DeviceRuntimeCert (common/runtime_counters.py:19-108, backend_node.py:2182-2190:
+ * host syncs, host->device and device->host bytes, JIT recompiles = 0 for this AOT library), and the
+ * split of the host time of every scan (scan_local + scan_finish) and every staging call into its
+ * own work (argument checks, pinned copies, launch / DMA enqueue) and its waits on the device (slot
+ * events, stream syncs). Times in ms. reset != 0 zeroes the counters after reading them. */
+#define GC_HOST_STATS 16
+#define GC_HS_SCANS 0
+#define GC_HS_SCAN_ENQ_MS 1
+#define GC_HS_SCAN_ENQ_MAX 2
+#define GC_HS_SCAN_WAIT_MS 3
+#define GC_HS_SCAN_WAIT_MAX 4
+#define GC_HS_STAGES 5
+#define GC_HS_STAGE_WORK_MS 6
+#define GC_HS_STAGE_WORK_MAX 7
+#define GC_HS_STAGE_WAIT_MS 8
+#define GC_HS_STAGE_WAIT_MAX 9
+#define GC_HS_HOST_SYNCS 10
+#define GC_HS_H2D_BYTES 11
+#define GC_HS_D2H_BYTES 12
+#define GC_HS_JIT_RECOMPILES 13
+int32_t gc_pipeline_host_stats(gc_pipeline* p, double* h_out, int32_t reset);
+
 /* The C5 in-scan PrimitiveMap update (config C5; the reference's step 12b, pipeline.py:1236-1327,
  * transform_gaussian_to_world :1248-1256 + primitive_map_fuse, primitive_map.py:992-1163).
  * BUILD-DEFINED, parity unpinned (csrc/gc_scanmap.hip): with a map attached,
  * scan_finish fuses every budgeted point of the scan, deskewed with hypothesis 0's twist, as one
  * world-frame Gaussian row (pose z_t of hypothesis 0 with t_z = 0, covariance Σ_lidar inflated by
  * J Σ_pose Jᵀ) into the slot hashed from its voxel (edge voxel_m), responsibility 1, source
- * LiDAR, timestamp scan_end, scan_seq = scan_count. Every rank runs it from the reduced record,
+ * LiDAR, timestamp scan_end, scan_seq = scan_count. Σ_lidar is the measurement-IW LiDAR mode of the
+ * state the scan started from (before its own IW apply). Every rank runs it from the reduced record,
  * so replicated maps stay bit-identical. The map's device arrays must outlive the attachment;
  * map == NULL detaches. */
 struct gc_primitive_map; /* defined with the PrimitiveMap entries below */
 int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const struct gc_primitive_map* map, double voxel_m);
+/* The attached map's colour fields were written outside the pipeline (an insert, a merge, a colour
+ * upload): the next in-scan update recomputes rgb / colors on every slot, as primitive_map_fuse does
+ * on every fuse (primitive_map.py:1097-1105); while they stay current it only touches its rows' slots.
+ * Allowed while a scan is pending (the pass then runs in that scan's finish). */
+int32_t gc_pipeline_map_colors_stale(gc_pipeline* p);
 /* Hypothesis 0's [z_t 6, Σ_post pose block 36 (row-major 6x6), ξ_body 6] that the last scan's
  * update used (from the reduced record). */
 int32_t gc_pipeline_get_scan_map_pose(gc_pipeline* p, double* h_out48);
@@ -424,6 +464,29 @@ int32_t gc_io_factor_batch(gc_ctx* ctx, int32_t kind, int32_t H, const double* d
 int32_t gc_imu_vmf_gravity_tr_batch(gc_ctx* ctx, int32_t H, int32_t M, const double* d_rotvec, const double* d_accel,
                                     const double* d_gyro, const double* d_w, const double* d_ba, const double* g3,
                                     double dt_imu, double eps_psd, double eps_mass, double* d_out);
+
+/* SO(3)/SE(3) maps of common/geometry/se3_jax.py, batched: n items of the op's input row
+ * (d_in (n, in)) to its output row (d_out (n, out)), one thread per item. These are the device
+ * routines every kernel of the scan path uses (recompose, world pose, ξ_body, MF δ, IMU/odom
+ * residuals). Rotations are row-major 3x3; poses [t 3, rotvec 3]; twists [ρ 3, φ 3].
+ *   GC_LIE_SO3_EXP     so3_exp      (se3_jax.py:259-301)   in 3  out 9
+ *   GC_LIE_SO3_LOG     so3_log      (se3_jax.py:304-366)   in 9  out 3  (softmax near-π axis)
+ *   GC_LIE_SE3_EXP     se3_exp      (se3_jax.py:473-504)   in 6  out 6
+ *   GC_LIE_SE3_LOG     se3_log      (se3_jax.py:220-256)   in 6  out 6
+ *   GC_LIE_SE3_V       se3_V        (se3_jax.py:137-175)   in 3  out 9
+ *   GC_LIE_SE3_V_INV   _se3_V_inv   (se3_jax.py:177-217)   in 3  out 9
+ *   GC_LIE_SE3_COMPOSE se3_compose  (se3_jax.py:420-438)   in 12 (a, b) out 6
+ *   GC_LIE_SE3_INVERSE se3_inverse  (se3_jax.py:441-453)   in 6  out 6 */
+#define GC_LIE_SO3_EXP 0
+#define GC_LIE_SO3_LOG 1
+#define GC_LIE_SE3_EXP 2
+#define GC_LIE_SE3_LOG 3
+#define GC_LIE_SE3_V 4
+#define GC_LIE_SE3_V_INV 5
+#define GC_LIE_SE3_COMPOSE 6
+#define GC_LIE_SE3_INVERSE 7
+#define GC_LIE_NOPS 8
+int32_t gc_lie_batch(gc_ctx* ctx, int32_t op, int64_t n, const double* d_in, double* d_out);
 
 /* BeliefGaussianInfo.mean_increment + world pose X ∘ Exp(δz) (common/belief.py:373-425). */
 int32_t gc_belief_world_pose_batch(gc_ctx* ctx, int32_t H, const double* d_X, const double* d_L, const double* d_h,

@@ -78,9 +78,10 @@ def _pipeline(case, ctx, H, cap, io_computed, rank=0, world=1, geometry_hyps=0):
     return pipe
 
 
-def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None):
+def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None, hooks=None):
     """pipe: a BatchedScanPipeline, or any object with its scan / getter surface (the sharded
-    view of test_gpu_shards.py); default: one unsharded pipeline."""
+    view of test_gpu_shards.py); default: one unsharded pipeline. hooks: (before(k), after(k, x))
+    run around each scan (x = before's return), e.g. the attached PrimitiveMap's own check."""
     cfg = O.PipeConfig(n_points_cap=cap)
     bins = case["bins"]
     pipe = pipe if pipe is not None else _pipeline(case, ctx, H, cap, io_computed)
@@ -94,9 +95,12 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None)
         Sga = (O.iw_meas_mode(iw0["nu_meas"], iw0["Psi_meas"], 0), O.iw_meas_mode(iw0["nu_meas"], iw0["Psi_meas"], 1))
         md = O.map_derived(mapst)
         scan = cases.scan_input(s)
+        hx = hooks[0](k) if hooks else None
         pipe.stage_scan(0, s)
         pipe.run_scan(0, s, k)
         ctx.sync()
+        if hooks:
+            hooks[1](k, hx)
         diag = pipe.hyp_diag()
         hcond = pipe.hyp_conditioning()
         stats, bcert, xi = pipe.bin_stats()
@@ -208,10 +212,60 @@ def test_c3_bench_workload_matches_oracle(ctx):
     _run_and_compare(ctx, case, 256, case["n"], [0, 1, 127, 255], 2, True)
 
 
+TURNED_YAWS = [np.pi - 0.02, -np.pi + 0.02, 2.5, np.pi - 0.02]
+
+
+def test_c3_turned_around_matches_oracle(ctx):
+    """C3 (65,536 points x 256 hypotheses, IMU/odom branch computed, two scans) for a robot that
+    has turned around: the world frame (warm-up map, odometry) is turned by π - 0.02, and the
+    anchors' yaws cycle over π - 0.02, -π + 0.02, 2.5 rad with N(0, 0.1²) roll/pitch. Every
+    world pose, recompose, anchor drift, ξ_body, MF δ and odom residual then goes through the Lie
+    maps at large angles, and hypotheses cross the ±π cut of the rotation vector
+    (se3_jax.py:304-366). Same bars as C3; sampled hypotheses cover every yaw."""
+    case = cases.build(H=256, n_az=4096, n_scans=2, io="computed", yaw0=np.pi - 0.02, hyp_yaws=TURNED_YAWS,
+                       tilt=0.1)
+    assert np.any(np.abs(np.linalg.norm(case["hyp"]["X_anchor"][:, 3:6], axis=1)) > 3.1)
+    _run_and_compare(ctx, case, 256, case["n"], [0, 1, 2, 3, 254], 2, True)
+
+
 def test_c5_shape_matches_oracle(ctx):
     """C5 shape on one GPU: 131,072 points budgeted to 65,536 (stride 2) x 1024 hypotheses."""
     case = cases.build(H=1024, n_az=8192, n_scans=1, io="computed", cap=65536)
     _run_and_compare(ctx, case, 1024, 65536, [0, 511, 1023], 1, True)
+
+
+def _c5_with_map(ctx, cap):
+    """C5 at its full size on one GPU: 131,072-point scans, H = 1024, the IMU/odom branch computed
+    and the 1,048,576-slot PrimitiveMap attached (the in-scan update inside every scan). Sampled
+    hypotheses against the oracle at the C3 bars, and the whole map against the oracle's
+    scan_map_update after the scan (test_gpu_scanmap.py's bars)."""
+    from test_gpu_scanmap import _check_scan, _map
+    case = cases.build(H=1024, n_az=8192, n_scans=1, io="computed", cap=cap)
+    pipe = _pipeline(case, ctx, 1024, cap, True)
+    M, voxel = 1 << 20, 0.1
+    dm = _map(ctx, M, 5)
+    pipe.attach_primitive_map(dm, voxel)
+    touched = []
+
+    def before(k):
+        return dm.download(), pipe.get_iw()
+
+    def after(k, x):
+        touched.append(_check_scan(pipe, dm, x[0], case["scans"][k], k, cap, M, voxel, x[1]))
+
+    _run_and_compare(ctx, case, 1024, cap, [0, 511, 1023], 1, True, pipe=pipe, hooks=(before, after))
+    assert touched and touched[0] > 1000, touched
+    pipe.close()
+
+
+def test_c5_with_map_matches_oracle(ctx):
+    """C5 budgeted (stride 2: 131,072 -> 65,536 points) with the 1M-slot map attached."""
+    _c5_with_map(ctx, 65536)
+
+
+def test_c5_dense_with_map_matches_oracle(ctx):
+    """C5 dense: every one of the 131,072 points kept (cap = 131,072, no stride) with the 1M-slot map."""
+    _c5_with_map(ctx, 131072)
 
 
 def test_c3_is_bit_reproducible(ctx):

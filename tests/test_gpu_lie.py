@@ -1,0 +1,168 @@
+"""The device Lie maps (gc_math.h through gc_lie_batch) on the reference's own fixed vectors and
+against the oracle across the whole angle range, near π included.
+
+Reference: fl_ws/src/fl_slam_poc/test/test_audit_invariants.py:224-328 (TestLieGroupRoundtrip),
+common/geometry/se3_jax.py:259-366 (so3_exp / so3_log with the softmax-mixed near-π axis). The
+round trips below run entirely on the device (exp, log and exp again are all device calls), with
+the reference test's own tolerances; the jax.random draws of the random round trip are replaced
+by seeded NumPy draws of the same shape and scale.
+"""
+
+import math
+
+import numpy as np
+import pytest
+
+from oracle import gc_oracle as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def L():
+    from gcslam.ops import se3
+    return se3
+
+
+# ---- test_audit_invariants.py:224-263 (so3 round trips, fixed vectors and tolerances)
+@pytest.mark.parametrize("w,atol", [([0.01, -0.02, 0.015], 1e-10), ([0.5, -0.7, 0.3], 1e-10),
+                                    ([1.5, -1.2, 0.8], 1e-9), ([math.pi - 0.01, 0.0, 0.0], 1e-8)])
+def test_so3_exp_log_roundtrip_reference_vectors(L, ctx, w, atol):
+    R = L.so3_exp(np.array(w), ctx=ctx)
+    R2 = L.so3_exp(L.so3_log(R, ctx=ctx), ctx=ctx)
+    np.testing.assert_allclose(R2, R, atol=atol)
+
+
+# ---- :265-279 (log(exp(ω)) ≈ ω, 10 draws of N(0, 0.5²))
+def test_so3_log_exp_random(L, ctx):
+    w = np.random.default_rng(456).normal(size=(10, 3)) * 0.5
+    np.testing.assert_allclose(L.so3_log(L.so3_exp(w, ctx=ctx), ctx=ctx), w, atol=1e-9)
+
+
+# ---- :281-297 (se3 round trips)
+@pytest.mark.parametrize("xi,atol", [([0.1, -0.05, 0.02, 0.2, -0.1, 0.05], 1e-9),
+                                     ([1.0, -0.5, 0.3, 0.8, -0.6, 0.4], 1e-8)])
+def test_se3_exp_log_roundtrip_reference_vectors(L, ctx, xi, atol):
+    T = L.se3_exp(np.array(xi), ctx=ctx)
+    T2 = L.se3_exp(L.se3_log(T, ctx=ctx), ctx=ctx)
+    np.testing.assert_allclose(T2, T, atol=atol)
+
+
+# ---- :299-328 (V⁻¹ V = I at φ = (0.3, -0.2, 0.1) and in the Taylor regime)
+def test_se3_V_inv_reference_vectors(L, ctx):
+    phi = np.array([0.3, -0.2, 0.1])
+    rho = np.array([1.0, 2.0, 3.0])
+    V, Vi = L.se3_V(phi, ctx=ctx), L._se3_V_inv(phi, ctx=ctx)
+    np.testing.assert_allclose(Vi @ V, np.eye(3), atol=1e-10)
+    np.testing.assert_allclose(Vi @ V @ rho, rho, atol=1e-10)
+    tiny = np.array([1e-9, -1e-9, 1e-9])
+    V, Vi = L.se3_V(tiny, ctx=ctx), L._se3_V_inv(tiny, ctx=ctx)
+    np.testing.assert_allclose(V, np.eye(3), atol=1e-7)
+    np.testing.assert_allclose(Vi, np.eye(3), atol=1e-7)
+    np.testing.assert_allclose(Vi @ V, np.eye(3), atol=1e-10)
+
+
+# ---- device vs oracle over the angle range, every branch of so3_log
+_THETAS = [0.0, 1e-9, 9.9e-8, 1.01e-7, 1e-4, 0.01, 0.5, 1.0, 2.0, 2.5, 3.0, math.pi - 0.02, math.pi - 0.01,
+           math.pi - 1e-4, math.pi - 1e-6, math.pi - 5e-8, math.pi - 1e-12, math.pi]
+
+
+def _axes(n, seed):
+    a = np.random.default_rng(seed).normal(size=(n, 3))
+    a[0] = [1.0, 0.0, 0.0]
+    a[1] = [0.0, 0.0, 1.0]
+    a[2] = [0.0, 0.0, -1.0]
+    a[3] = [1.0, 1.0, 0.0]
+    return a / np.linalg.norm(a, axis=1, keepdims=True)
+
+
+def _rotvecs():
+    ax = _axes(12, 7)
+    return np.array([t * a for t in _THETAS for a in ax])
+
+
+def test_so3_exp_matches_oracle_all_angles(L, ctx):
+    w = _rotvecs()
+    R = L.so3_exp(w, ctx=ctx)
+    ref = np.stack([O.so3_exp(v) for v in w])
+    np.testing.assert_allclose(R, ref, rtol=0, atol=1e-15)
+
+
+def test_so3_log_matches_oracle_all_branches(L, ctx):
+    """The same R (the oracle's so3_exp) into both logs. Near π the generic branch divides by
+    sin θ, so an ulp of R becomes ~ulp/sin θ of ω: the bound scales with it. θ within 1e-7 of π
+    runs the softmax-mixed axis (se3_jax.py:340-364) on both sides."""
+    w = _rotvecs()
+    Rs = np.stack([O.so3_exp(v) for v in w])
+    got = L.so3_log(Rs, ctx=ctx)
+    n_pi = 0
+    for R, g, v in zip(Rs, got, w):
+        ref = O.so3_log(R)
+        th = float(np.linalg.norm(ref))
+        n_pi += abs(math.acos(min(max(0.5 * (np.trace(R) - 1.0), -1.0), 1.0)) - math.pi) < O.NEAR_PI
+        bound = 1e-15 * (1.0 + 4.0 / max(abs(math.sin(th)), 1e-7) * (th > 1.0))
+        assert np.max(np.abs(g - ref)) <= max(bound, 2e-15), (v, g, ref)
+        # and it is a logarithm of R
+        np.testing.assert_allclose(O.so3_exp(g), R, atol=2e-8)
+    assert n_pi >= 12, "the near-π branch was not exercised"
+
+
+def test_se3_maps_match_oracle_large_angles(L, ctx):
+    rng = np.random.default_rng(11)
+    w = _rotvecs()
+    t = rng.normal(size=w.shape) * 3.0
+    T = np.concatenate([t, w], 1)
+    got = L.se3_exp(T, ctx=ctx)
+    np.testing.assert_allclose(got, np.stack([O.se3_exp(x) for x in T]), rtol=0, atol=1e-14)
+    # se3_log canonicalises the rotation vector through exp/log: bound as so3_log's
+    got = L.se3_log(T, ctx=ctx)
+    ref = np.stack([O.se3_log(x) for x in T])
+    far = np.array([abs(math.pi - np.linalg.norm(x[3:6])) for x in T])
+    ok = far > 1e-3
+    np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=1e-11)
+    # near π the canonical rotvec may sit on either side of the ±π cut for both: compare maps
+    np.testing.assert_allclose(np.stack([O.se3_exp(x) for x in got]), np.stack([O.se3_exp(x) for x in ref]),
+                               atol=1e-7)
+    Vi = L._se3_V_inv(w, ctx=ctx)
+    # D = 1/θ² - (1 + cos θ)/(2θ sin θ + 1e-12): 1 + cos θ cancels near π, an ulp of cos is ~1e-11 of D
+    np.testing.assert_allclose(Vi, np.stack([O.se3_V_inv(v) for v in w]), rtol=0, atol=1e-9)
+
+
+def test_se3_compose_inverse_relative_match_oracle_near_pi(L, ctx):
+    """Poses whose yaw is near ±π (a robot that has turned around) composed with small and large
+    increments: the recompose / world-pose / odom-residual shapes of the scan path."""
+    rng = np.random.default_rng(5)
+    n = 256
+    a = np.zeros((n, 6))
+    b = np.zeros((n, 6))
+    yaws = np.array([math.pi - 0.02, -math.pi + 0.02, 2.5, math.pi - 1e-9])[np.arange(n) % 4]
+    for i in range(n):
+        Rz = O.so3_exp(np.array([0.0, 0.0, yaws[i]]))
+        tilt = O.so3_exp(rng.normal(size=3) * 0.1)
+        a[i, 3:6] = O.so3_log(Rz @ tilt)
+        a[i, 0:3] = rng.normal(size=3) * 5.0
+        b[i, 0:3] = rng.normal(size=3) * 0.2
+        b[i, 3:6] = rng.normal(size=3) * (0.05 if i % 2 else 0.6)
+    got = L.se3_compose(a, b, ctx=ctx)
+    ref = np.stack([O.se3_compose(x, y) for x, y in zip(a, b)])
+    np.testing.assert_allclose(got[:, 0:3], ref[:, 0:3], rtol=0, atol=1e-13)
+    # an ulp of R_a R_b is ~ulp/sin θ of the log near π: compare the rotations they encode
+    np.testing.assert_allclose(np.stack([O.so3_exp(x) for x in got[:, 3:6]]),
+                               np.stack([O.so3_exp(x) for x in ref[:, 3:6]]), atol=1e-10)
+    same_side = np.abs(np.linalg.norm(ref[:, 3:6], axis=1) - math.pi) > 1e-6
+    np.testing.assert_allclose(got[same_side, 3:6], ref[same_side, 3:6], rtol=0, atol=1e-9)
+    inv = L.se3_inverse(a, ctx=ctx)
+    refi = np.stack([O.se3_inverse(x) for x in a])
+    np.testing.assert_allclose(inv[:, 0:3], refi[:, 0:3], rtol=0, atol=1e-13)
+    np.testing.assert_allclose(np.stack([O.so3_exp(x) for x in inv[:, 3:6]]),
+                               np.stack([O.so3_exp(x) for x in refi[:, 3:6]]), atol=1e-10)
+    rel = L.se3_relative(a, b, ctx=ctx)
+    refr = np.stack([O.se3_relative(x, y) for x, y in zip(a, b)])
+    np.testing.assert_allclose(np.stack([O.se3_exp(x) for x in rel]), np.stack([O.se3_exp(x) for x in refr]),
+                               atol=1e-9)
+
+
+def test_lie_batch_rejects_bad_op(ctx):
+    from gcslam import _abi
+    with pytest.raises(ValueError):
+        _abi.call("gc_lie_batch", ctx.handle, 99, 1, None, None, ctx=ctx)

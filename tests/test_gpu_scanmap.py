@@ -38,13 +38,14 @@ def _map(ctx, M, seed):
     return dm
 
 
-def _check_scan(pipe, dm, tile0, s, k, cap, M, voxel):
+def _check_scan(pipe, dm, tile0, s, k, cap, M, voxel, iw):
+    """iw: the pipeline's IW state before the scan (Σ_lidar of the update is the LiDAR mode the scan
+    started from, before its own measurement-IW apply)."""
     zt, Sp, xi = pipe.scan_map_pose()
     _, _, xi_all = pipe.bin_stats()
     _, _, Sig = pipe.hyp_stats()
     assert np.array_equal(xi, xi_all[0]), "pose block: ξ is not hypothesis 0's"
     assert np.array_equal(Sp, Sig[0][0:6, 0:6]), "pose block: Σ_pose is not hypothesis 0's Σ_post"
-    iw = pipe.get_iw()
     h0 = np.concatenate([zt, Sp.reshape(-1), xi])
     rows = O.scan_map_rows(s["points"], s["timestamps"], s["weights"], cap, s["scan_start"], s["scan_end"], h0,
                            iw["nu_meas"], iw["Psi_meas"], np.asarray(pipe.cfg.lidar_origin), voxel, M)
@@ -70,11 +71,45 @@ def test_scan_map_update_matches_oracle(ctx, n_az, cap, M):
     pipe.attach_primitive_map(dm, voxel)
     touched = []
     for k, s in enumerate(case["scans"]):
-        tile0 = dm.download()
+        tile0, iw0 = dm.download(), pipe.get_iw()
         pipe.stage_scan(0, s)
         pipe.run_scan(0, s, k)
-        touched.append(_check_scan(pipe, dm, tile0, s, k, cap, M, voxel))
+        touched.append(_check_scan(pipe, dm, tile0, s, k, cap, M, voxel, iw0))
     assert all(t > 1000 for t in touched), touched
+    pipe.close()
+
+
+def test_scan_map_colours_recomputed_after_host_writes(ctx):
+    """The map's colours stop being the fuse's estimate when a host operation writes colour fields
+    (a colour upload before scan 1, a camera-sourced insert before scan 2): the next in-scan update
+    recomputes rgb / colors on every slot, as primitive_map_fuse does on every fuse
+    (primitive_map.py:1097-1105), and the map reports its colours current afterwards."""
+    from gcslam.primitive_map import primitive_map_insert_masked
+    voxel, cap, M = 0.1, 16384, 1 << 14
+    case = cases.build(H=4, n_az=1024, n_scans=3, io="computed", cap=cap)
+    pipe = _pipeline(case, ctx, 4, cap, True)
+    dm = _map(ctx, M, 11)
+    rng = np.random.default_rng(12)
+    den = rng.uniform(0.0, 2.0, M) * (rng.uniform(size=M) > 0.3)
+    dm.upload(cam_mass=den, rgb_cam_denom=den, rgb_cam_accum=rng.uniform(0, 1.5, (M, 3)) * den[:, None])
+    pipe.attach_primitive_map(dm, voxel)
+    for k, s in enumerate(case["scans"]):
+        if k == 1:
+            dm.upload(rgb=rng.uniform(size=(M, 3)), colors=rng.uniform(size=(M, 3)))
+            assert not dm.colors_current
+        if k == 2:
+            K = 64
+            Bq = rng.normal(size=(K, 3, 3))
+            primitive_map_insert_masked(dm, 0, Bq @ np.swapaxes(Bq, 1, 2) + np.eye(3), rng.normal(size=(K, 3)),
+                                        rng.normal(size=(K, 3, 3)), rng.uniform(0.5, 2.0, K), 7.0, np.ones(K, bool),
+                                        scan_seq=k, colors_new=rng.uniform(0.2, 3.0, (K, 3)),
+                                        sources_new=np.zeros(K, np.int32))
+            assert not dm.colors_current
+        tile0, iw0 = dm.download(), pipe.get_iw()
+        pipe.stage_scan(0, s)
+        pipe.run_scan(0, s, k)
+        _check_scan(pipe, dm, tile0, s, k, cap, M, voxel, iw0)
+        assert dm.colors_current
     pipe.close()
 
 
