@@ -344,6 +344,20 @@ def main():
                               "step k stages scan k+1 while scan k computes (three slots in rotation)") if ingest else
                              "scans pre-staged in HBM before the timed region"},
     }
+    # the same step with the reference's per-call ConditioningCerts computed inside every scan
+    # (gc_pipeline_set_inscan_certs): 50 scans after 10 untimed, max over ranks
+    pipe.set_inscan_certs(True)
+    for _ in range(10):
+        step()
+    ctx.sync()
+    dist.barrier()
+    tc0 = time.perf_counter()
+    for _ in range(50):
+        step()
+    ctx.sync()
+    dist.barrier()
+    certs_ms = 1e3 * dist.max(time.perf_counter() - tc0) / 50
+    pipe.set_inscan_certs(False)
     # per-stage device time of the same step (HIP events around each launch group, untimed scans after
     # the timed region: the events themselves cost the stream a few us each), median over 20
     pipe.set_stage_timing(True)
@@ -356,6 +370,9 @@ def main():
     if exchange is not None:
         out["exchange"] = exchange
     out["stages_ms"] = dict(out_stages, scans=len(st_runs), note="HIP events around each launch group, untimed scans")
+    out["inscan_certs"] = {"ms_per_step": certs_ms, "scans": 50,
+                           "note": "the same step with every hypothesis's predict and fusion ConditioningCert "
+                                   "computed inside the scan (gc_pipeline_set_inscan_certs)"}
     ns = max(hs["scans"], 1.0)
     nst = max(hs["stages"], 1.0)
     out["host"] = {"scan_enqueue_ms": {"mean": hs["scan_enqueue_ms"] / ns, "max": hs["scan_enqueue_max_ms"]},

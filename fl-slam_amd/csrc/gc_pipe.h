@@ -50,6 +50,7 @@ struct PipeDev {
   double *dPsiP, *mu_fin, *diag;
   double *lpose;                           // (Hl, 36) pose block of L_evidence (diagnostics tape)
   double *Sig;                             // (Hl, 22, 22) Σ_post = (L_post + εI)⁻¹ of the last scan
+  double *hcond;                           // (Hl, 2, 4) in-scan ConditioningCerts [L_pred, L_post] (gc_certs.hip)
   // shared
   double *weights;                         // (H)
   double *Q;                               // (22, 22)
@@ -108,6 +109,8 @@ hipError_t launch_combine_local(const PipeDev& P, hipStream_t st);
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st);
 hipError_t launch_map_derive(const PipeDev& P, hipStream_t st);
 hipError_t launch_iw_Q(const PipeDev& P, hipStream_t st);
+// the per-hypothesis ConditioningCerts of L_pred and L_post into P.hcond (gc_certs.hip)
+hipError_t launch_hyp_certs(const PipeDev& P, hipStream_t st);
 }  // namespace gc
 
 struct gc_ctx;

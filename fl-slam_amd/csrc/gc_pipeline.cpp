@@ -85,6 +85,9 @@ struct gc_pipeline {
   // per-stage device timing (gc_pipeline_set_stage_timing): events around each launch group
   bool st_timing = false, st_rec = false;
   hipEvent_t st_ev[GC_STAGE_N] = {};
+  // in-scan ConditioningCerts (gc_pipeline_set_inscan_certs): launched after every scan's evidence;
+  // hcond_scan: P.hcond holds the certificates of the current L_pred / L (cleared by a belief upload)
+  bool inscan_certs = false, hcond_scan = false;
   // getter workspace (conditioning certificates), allocated with the pipeline: no hipMalloc / hipFree
   // (device-synchronising) on a getter a live node calls every scan
   double* ws = nullptr;
@@ -275,13 +278,14 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   int rc = GC_OK;
   double** fields[] = {&P.X, &P.z, &P.L, &P.h, &P.stamp, &P.Lpred, &P.hpred, &P.pred_cert, &P.pose_pred, &P.xi,
                        &P.imu_out, &P.dPsiM, &P.stats, &P.bincert, &P.io_L, &P.io_h, &P.io_cert, &P.dPsiP,
-                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose, &P.Sig, &P.binaux};
+                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose, &P.Sig, &P.binaux, &P.hcond};
   const size_t sizes[] = {(size_t)Hl * 6, (size_t)Hl * 22, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl,
                           (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kPredCert, (size_t)Hl * 6,
                           (size_t)Hl * 6, (size_t)Hl * gc::kImuOut, (size_t)Hl * 27, (size_t)Hl * B * 38,
                           (size_t)Hl * 8, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kIoCert,
                           (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag, (size_t)Hl * gc::kMuAux,
-                          (size_t)Hl * gc::kIoParts, (size_t)Hl * 36, (size_t)Hl * NN, (size_t)Hl * B * 2};
+                          (size_t)Hl * gc::kIoParts, (size_t)Hl * 36, (size_t)Hl * NN, (size_t)Hl * B * 2,
+                          (size_t)Hl * 8};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert,
@@ -360,6 +364,7 @@ int32_t gc_pipeline_set_beliefs(gc_pipeline* p, const double* h_X, const double*
   GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
   const size_t Hl = p->P.Hl;
   p->sig_cached = false;
+  p->hcond_scan = false;
   GC_TRY(up(p, p->P.X, h_X, Hl * 6));
   GC_TRY(up(p, p->P.z, h_z, Hl * 22));
   GC_TRY(up(p, p->P.L, h_L, Hl * 484));
@@ -785,6 +790,8 @@ static int32_t scan_local_impl(gc_pipeline* p, int32_t slot, double scan_start, 
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
   p->sig_cached = true;
+  if (p->inscan_certs) GC_HIP(ctx, gc::launch_hyp_certs(P, ctx->stream));
+  p->hcond_scan = p->inscan_certs;
   GC_TRY(stage_event(p, 3));
   // a16 local part: this rank's partial record (weighted sums, IW statistics, map increment)
   GC_HIP(ctx, gc::launch_combine_local(P, ctx->stream));
@@ -850,6 +857,7 @@ int32_t gc_pipeline_get_hyp_conditioning(gc_pipeline* p, double* h_out) {
   // stored matrix, computed here on demand by the Jacobi projection (off the scan path, as
   // gc_pipeline_get_combined does for the combined belief)
   const int Hl = p->P.Hl, NN = 484;
+  if (p->hcond_scan) return down(p, h_out, p->P.hcond, (size_t)Hl * 8);  // computed inside the scan
   double* ws = p->ws;  // 2 Hl (NN + 6) doubles, allocated with the pipeline
   const size_t len = (size_t)Hl * (NN + 6);
   const double* mats[2] = {p->P.Lpred, p->P.L};
@@ -913,6 +921,13 @@ int32_t gc_pipeline_stage_ms(gc_pipeline* p, float* h_ms) {
   for (int i = 0; i + 1 < GC_STAGE_N; ++i)
     GC_HIP(p->ctx, hipEventElapsedTime(&h_ms[i], p->st_ev[i], p->st_ev[i + 1]));
   GC_HIP(p->ctx, hipEventElapsedTime(&h_ms[GC_STAGE_N - 1], p->st_ev[0], p->st_ev[GC_STAGE_N - 1]));
+  return GC_OK;
+}
+
+int32_t gc_pipeline_set_inscan_certs(gc_pipeline* p, int32_t on) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  p->inscan_certs = on != 0;
   return GC_OK;
 }
 

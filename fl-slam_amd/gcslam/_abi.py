@@ -93,6 +93,7 @@ SIGNATURES = {
     "gc_pipeline_set_stage_timing": [_vp, _i32],
     "gc_pipeline_stage_ms": [_vp, _vp],
     "gc_pipeline_host_stats": [_vp, _vp, _i32],
+    "gc_pipeline_set_inscan_certs": [_vp, _i32],
     "gc_comm_unique_id": [_vp],
     "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],
     "gc_comm_destroy": [_vp],

@@ -231,10 +231,16 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_get_hyp_diag", _p(o))
         return o
 
+    def set_inscan_certs(self, on: bool = True) -> None:
+        """Compute the per-hypothesis predict / fusion ConditioningCerts inside every later scan
+        (right after its evidence kernel), as the reference emits them on every call."""
+        self._call("gc_pipeline_set_inscan_certs", 1 if on else 0)
+
     def hyp_conditioning(self):
         """(Hl, 2, 4): the ConditioningCert [eig_min, eig_max, cond, near_null_count] of each
         hypothesis's predict (L_pred, predict.py:183-188) and fusion (L_post, fusion.py:150-230)
-        PSD projections of the last scan (computed on demand, off the scan path)."""
+        PSD projections of the last scan (computed inside the scan with set_inscan_certs, else on
+        demand, off the scan path)."""
         o = np.empty((self.Hl, 2, 4))
         self._call("gc_pipeline_get_hyp_conditioning", _p(o))
         return o

@@ -306,9 +306,15 @@ int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag);
 /* Per-hypothesis ConditioningCert (Hl, 2, 4) of the last scan's two 22x22 PSD projections,
  * [L_pred (predict.py:183-188), L_post (fusion.py:150-230)] x [eig_min, eig_max, cond,
  * near_null_count] of the clamped spectrum. The scan certifies both by Cholesky and skips their
- * eigen-decompositions; this getter computes them on demand (Jacobi, off the scan path) from the
- * stored matrices, so call it before the beliefs are set again. Synchronises the stream. */
+ * eigen-decompositions. With in-scan certificates on (gc_pipeline_set_inscan_certs) every scan
+ * computes them right after its evidence kernel (Householder tridiagonalisation + Sturm
+ * multisection, gc_certs.hip) and this getter reads them back; otherwise it computes them on demand
+ * (Jacobi, off the scan path) from the stored matrices, so call it before the beliefs are set again.
+ * Synchronises the stream. */
 int32_t gc_pipeline_get_hyp_conditioning(gc_pipeline* p, double* h_out);
+/* In-scan ConditioningCerts (off by default): on != 0 makes every later scan emit the certificates
+ * gc_pipeline_get_hyp_conditioning reads, as the reference emits them on every predict / fusion call. */
+int32_t gc_pipeline_set_inscan_certs(gc_pipeline* p, int32_t on);
 /* L_evidence[pose, pose] (Hl, 6, 6) of the last scan, as the reference's MinimalScanTape.L_pose6
    (pipeline.py:1537). */
 int32_t gc_pipeline_get_lpose6(gc_pipeline* p, double* h_lpose);

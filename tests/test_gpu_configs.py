@@ -191,8 +191,10 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None,
             mp = pipe.get_map()
             _close(mp["map"], cases.map_to_record(O.map_forget_and_add(mapst, res0["map_inc"])), 1e-8, 1e-12,
                    f"scan{k} map")
-        # full-size properties of every hypothesis: Σ_b N_b = Σ w_deskew (bin cert [6]), finite
-        np.testing.assert_allclose(stats[:, :, 0].sum(1), bcert[:, 6], rtol=1e-12)
+        # full-size properties of every hypothesis: Σ_b N_b = Σ w_deskew (bin cert [6]), finite. The fused
+        # kernel forms N_b as the trace of the unit-direction scatter, Σ R w |d|² with |d|² = 1 − 2e-12/ρ
+        # (ρ the range, >= 0.4 m here): the two sums agree to ~5e-12 relative
+        np.testing.assert_allclose(stats[:, :, 0].sum(1), bcert[:, 6], rtol=2e-11)
         assert np.all(np.isfinite(bel["L"])) and np.all(np.isfinite(diag))
     return pipe
 
@@ -232,6 +234,16 @@ def test_c5_shape_matches_oracle(ctx):
     """C5 shape on one GPU: 131,072 points budgeted to 65,536 (stride 2) x 1024 hypotheses."""
     case = cases.build(H=1024, n_az=8192, n_scans=1, io="computed", cap=65536)
     _run_and_compare(ctx, case, 1024, 65536, [0, 511, 1023], 1, True)
+
+
+def test_c3_inscan_certs_match_oracle(ctx):
+    """C3 with the in-scan ConditioningCerts on (gc_certs.hip, computed inside the scan right after the
+    evidence kernel): every bar of the C3 test, the per-hypothesis predict / fusion certificates among
+    them, now read from the scan itself."""
+    case = cases.build(H=256, n_az=4096, n_scans=1, io="computed")
+    pipe = _pipeline(case, ctx, 256, case["n"], True)
+    pipe.set_inscan_certs(True)
+    _run_and_compare(ctx, case, 256, case["n"], [0, 1, 255], 1, True, pipe=pipe)
 
 
 def _c5_with_map(ctx, cap):

@@ -92,3 +92,28 @@ def test_conditioning_getters_allocate_nothing_per_call(ctx):
     a, c1 = pipe.hyp_conditioning(), pipe.combined()
     b, c2 = pipe.hyp_conditioning(), pipe.combined()
     assert np.array_equal(a, b) and c1["eig_min"] == c2["eig_min"]
+
+
+def test_inscan_certs_agree_with_on_demand_jacobi(ctx):
+    """The in-scan certificates (Householder + Sturm multisection) against the on-demand Jacobi
+    projection of the same stored matrices: eigenvalue extremes at eigh's accuracy, counts exact; the
+    scan's other results bit-identical with the certificates on or off."""
+    case = cases.build(H=8, n_az=1024, n_scans=2, io="computed")
+    outs = []
+    for on in (False, True):
+        pipe = _pipeline(case, ctx, 8, case["n"], True)
+        pipe.set_inscan_certs(on)
+        conds = []
+        for k, s in enumerate(case["scans"]):
+            pipe.stage_scan(0, s)
+            pipe.run_scan(0, s, k)
+            conds.append(pipe.hyp_conditioning())
+        b = pipe.get_beliefs()
+        outs.append((conds, b["L"], b["X_anchor"], pipe.combined()["L"]))
+    for a, b in zip(outs[0][1:], outs[1][1:]):
+        assert np.array_equal(a, b)
+    for k, (ref, got) in enumerate(zip(outs[0][0], outs[1][0])):
+        np.testing.assert_allclose(got[..., 1], ref[..., 1], rtol=1e-10, atol=0, err_msg=f"scan{k} eig_max")
+        assert np.all(np.abs(got[..., 0] - ref[..., 0]) <= 1e-12 * ref[..., 1]), f"scan{k} eig_min"
+        np.testing.assert_array_equal(got[..., 3], ref[..., 3], err_msg=f"scan{k} near-null count")
+        np.testing.assert_allclose(got[..., 2], got[..., 1] / got[..., 0], rtol=1e-15)
