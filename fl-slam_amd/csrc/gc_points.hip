@@ -27,17 +27,10 @@ typedef double v4d __attribute__((ext_vector_type(4)));  // f64 MFMA accumulator
 constexpr int NF_BASE = 19;   // [1, d(3), dd(6: 00 01 02 11 12 22), p(3), pp(6)] x w
 constexpr int NF_COV = 9;     // full 3x3 point covariance x w
 constexpr int REC_EXTRA = 4;  // [entropy_sum, max_resp, sum_w, n_points]
-#ifndef GC_NT_RESP
 // the moment kernel reads the responsibility stream exactly once: non-temporal loads for the 8-B
 // per-lane tiles (A/B on one box, C3 contract launch: 1.548 -> 1.49 ms; the paired 16-B loads of bins
 // 0-31 stay temporal: non-temporal there too measured 1.52, profiles/r02/ab_contract_pair_nt.txt)
-#define GC_NT_RESP 1
-#endif
-#if GC_NT_RESP
 #define GC_RESP_LOAD(ptr) __builtin_nontemporal_load(ptr)
-#else
-#define GC_RESP_LOAD(ptr) (*(ptr))
-#endif
 
 // 16-lane (DPP row) butterflies: quad_perm [1,0,3,2], quad_perm [2,3,0,1], row_half_mirror,
 // row_mirror. Every step pairs each lane with a distinct partner holding a disjoint partial, so
@@ -518,25 +511,17 @@ GC_DEV void sa_store_block(const double* S, double* Rh, int64_t wbase, int64_t n
     }
   }
 }
-#ifndef GC_SA_NT
-#define GC_SA_NT 1
-#endif
-#ifndef GC_SA_SBINS
-#define GC_SA_SBINS 1
-#endif
-#ifndef GC_SA_OCC
 // 2 waves per SIMD: the 48 similarities / exps of a lane's point stay in registers with no spill
 // (at 3, the 168-VGPR budget spilled ~12-27 VGPRs per point to scratch: 0.6 GB of extra HBM reads and
 // 0.9 GB of extra writes per C3 launch, tools/probe/probe_sa3.hip; 1.74 -> 1.32 ms)
-#define GC_SA_OCC 2
-#endif
+constexpr int kSaOcc = 2;
 // dynamic LDS of a soft-assign workgroup (doubles): exp table | bins (x, y, z rows of 64) | reduction |
 // 4 wave slabs (FULL: 32 rows of 16 BPL + 2; ragged: 64 rows of 18)
 __host__ __device__ constexpr bool sa_linear(int BPL, bool full) { return full && BPL <= 3; }  // B = 64: 16-bin blocks (register budget)
 __host__ __device__ constexpr int sa_slab_doubles(int BPL, bool full) { return sa_linear(BPL, full) ? 32 * (16 * BPL + 2) : 64 * 18; }
 __host__ __device__ constexpr int sa_lds_doubles(int BPL, bool full) { return kExpTab2 + 192 + 8 + 4 * sa_slab_doubles(BPL, full); }
 template <int BPL, bool FULL>
-__global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
+__global__ void __launch_bounds__(256, kSaOcc) k_soft_assign(int64_t n, int B, int iters, const double* __restrict__ dirs,
                                                      const double* __restrict__ bins, double inv_tau,
                                                      double* resp, int32_t* bin_idx, double* partial) {
   constexpr int NB = 16 * BPL;
@@ -545,15 +530,8 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
   typedef double dvec2 __attribute__((ext_vector_type(2)));
   extern __shared__ __attribute__((aligned(16))) double sa_lds[];
   double* Tx = sa_lds;
-  double* Lb = Tx + kExpTab2;  // bin directions, x / y / z rows of 64 (zero past B)
-  double* red = Lb + 192;
+  double* red = Tx + kExpTab2 + 192;  // (192 doubles after the table unused: the bins are scalar loads)
   exp_table2_init(Tx);
-  if (threadIdx.x < 64) {
-    const int b = threadIdx.x;
-    Lb[b] = b < B ? bins[3 * b] : 0.0;
-    Lb[64 + b] = b < B ? bins[3 * b + 1] : 0.0;
-    Lb[128 + b] = b < B ? bins[3 * b + 2] : 0.0;
-  }
   __syncthreads();
   const int h = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -600,15 +578,11 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
     int bidx = 0;
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-#if GC_SA_SBINS
       // bin directions as wave-uniform scalar loads (SGPR operands; the LDS pipe keeps the exp table
       // and the row transposes)
       const double bx = FULL || j < B ? bins[3 * j] : 0.0, by = FULL || j < B ? bins[3 * j + 1] : 0.0,
                    bz = FULL || j < B ? bins[3 * j + 2] : 0.0;
       ex[j] = sim_nofma(d0, d1, d2, bx, by, bz);
-#else
-      ex[j] = sim_nofma(d0, d1, d2, Lb[j], Lb[64 + j], Lb[128 + j]);
-#endif
       if ((FULL || j < B) && ex[j] > best) { best = ex[j]; bidx = j; }
     }
     // exponent in units of ln2/2048 (the 2048-entry table exp, exp2s_n): y = S ysc - S_max ysc by one
@@ -664,11 +638,7 @@ __global__ void __launch_bounds__(256, GC_SA_OCC) k_soft_assign(int64_t n, int B
         const int64_t pbase = wbase + 32 * hf;
         double* dst = Rh + pbase * NB;
         const auto put = [&](int o, const dvec2& v) {
-#if GC_SA_NT
           __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(dst + o));
-#else
-          *reinterpret_cast<dvec2*>(dst + o) = v;
-#endif
         };
         if (pbase + 32 <= n) {  // wave-uniform: the whole block is in range (every block but the tail's)
 #pragma unroll
@@ -963,15 +933,9 @@ GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL
 // feature slab row stride: the B-operand read F[l][4s + g] of the 32 lanes of a ds_read_b64
 // group lands on 32 distinct bank pairs (4 l + 2 g + 8 s mod 64)
 constexpr int kFusedFS = 66;
-#ifndef GC_FUSED_OCC
-#define GC_FUSED_OCC 2  // waves per SIMD the register budget is sized for (tuning knob, probes)
-#endif
-#ifndef GC_FUSED_UNR
-#define GC_FUSED_UNR 8  // softmax steps unrolled per block (Π Z renormalised after each block: exact)
-#endif
-#ifndef GC_FUSED_NACC
-#define GC_FUSED_NACC 2  // MFMA accumulator sets (even / odd steps)
-#endif
+constexpr int kFusedOcc = 2;   // waves per SIMD the register budget is sized for (3 spills: §5 of DESIGN.md)
+constexpr int kFusedUnr = 8;   // softmax steps unrolled per block (Π Z renormalised after each block: exact)
+constexpr int kFusedNacc = 2;  // MFMA accumulator sets (even / odd steps)
 // Per-launch constants of the fused kernel and its LDS tables (exp table, scaled bins), set up once
 // per workgroup by bins_prologue; a workgroup then runs one (grid form) or many (persistent form)
 // (hypothesis, chunk) tasks with bins_task.
@@ -1046,7 +1010,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   double* Tx = lds + 4 * kFusedFS * NS;
   double* Lb = Tx + kExpTab2;
   const double ysc = A.inv_tau * kTab2OverLn2;
-  constexpr int NACC = GC_FUSED_NACC;
+  constexpr int NACC = kFusedNacc;
   v4d acc4[NACC][BPL];  // NACC = 2: even / odd steps, 2*BPL independent MFMA accumulation chains
   double accx[BPL][NX];
 #pragma unroll
@@ -1113,9 +1077,9 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
         F[(NF + 3) * kFusedFS + lane] = inr ? 1.0 : 0.0;
       }
       lds_wave_sync();
-      for (int s8 = 0; s8 < 16; s8 += GC_FUSED_UNR) {
+      for (int s8 = 0; s8 < 16; s8 += kFusedUnr) {
   #pragma unroll
-      for (int s = s8; s < s8 + GC_FUSED_UNR; ++s) {
+      for (int s = s8; s < s8 + kFusedUnr; ++s) {
         const int pl = s * 4 + g;
         const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
         const double vf = PAD ? F[(NF + 3) * kFusedFS + pl] : 1.0;  // 1 for a point of the chunk, 0 for padding
@@ -1192,7 +1156,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
 // counter; the predict launch that precedes every k_bins_io on the stream zeroes it, so a launch
 // never depends on how the previous one ended. No workgroup waits on another.
 template <int BPL, bool FULL>
-__global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
+__global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
                                                              const double* __restrict__ odom, int n_io, int H,
                                                              int64_t chunks, unsigned* ctr) {
   extern __shared__ double lds[];
@@ -1223,7 +1187,7 @@ __global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_io(FusedArgs A, Pipe
 
 // Grid form (the gc_scan_bins_fused entry): grid (chunks, H), one task per workgroup.
 template <int BPL, bool FULL>
-__global__ void __launch_bounds__(256, GC_FUSED_OCC) k_bins_fused(FusedArgs A) {
+__global__ void __launch_bounds__(256, kFusedOcc) k_bins_fused(FusedArgs A) {
   extern __shared__ double lds[];
   bins_prologue(A, lds);
   const int RL = A.B * NF_BASE + REC_EXTRA;
@@ -1605,10 +1569,8 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
   GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
   GC_CHECK_ARG(ctx, tau > 0.0, "tau must be positive");
   GC_CHECK_ARG(ctx, d_dirs && d_bins && d_resp_out && d_cert_out, "NULL buffer");
-#ifndef GC_SA_ITERS
-#define GC_SA_ITERS 8
-#endif
-  int iters = GC_SA_ITERS;
+constexpr int kSaIters = 8;
+  int iters = kSaIters;
   while (iters > 1 && ((n + iters * 256 - 1) / (iters * 256)) * (int64_t)H < 4096) iters >>= 1;
   const int64_t blocks = (n + iters * 256 - 1) / (iters * 256);
   void* scr;
@@ -1670,10 +1632,7 @@ int32_t gc_scan_bin_moment_match(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, c
   const int bpl = bpl_for(B);
   const int NT = (NF + 15) / 16;
   const size_t sh = sizeof(double) * std::max<size_t>((size_t)4 * 16 * NT * kMomFS, (size_t)4 * B * NF);
-#ifndef GC_MOM_PAIR
-#define GC_MOM_PAIR 1
-#endif
-  const bool pair = GC_MOM_PAIR && B >= 32 && ((uintptr_t)d_resp & 15) == 0;
+  const bool pair = B >= 32 && ((uintptr_t)d_resp & 15) == 0;
 #define GC_MOM_L(BP, CV, LM, PR)                                                                                 \
   hipLaunchKernelGGL((k_moment_partials<BP, CV, LM, 1, PR>), grid, dim3(256), sh, ctx->stream, n, B, groups,    \
                      d_points, d_covs, d_w, d_resp, d_lambda, o[0], o[1], o[2], (double*)scr)
@@ -1763,19 +1722,15 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   // same for every shard size)
   const int64_t U = (P.n_cap + 255) / 256;  // 256-point units per hypothesis
   const int Hg = P.geom_H > 0 ? P.geom_H : H;
-#ifndef GC_BINS_MIN_TASKS
-#define GC_BINS_MIN_TASKS 3
-#endif
+constexpr int kBinsMinTasks = 3;
   int iters = 16;
-  while (iters > 2 && (int64_t)Hg * U < GC_BINS_MIN_TASKS * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
-#ifndef GC_SHORT_DIV
-#define GC_SHORT_DIV 2
-#endif
+  while (iters > 2 && (int64_t)Hg * U < kBinsMinTasks * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
+constexpr int kShortDiv = 2;
   // short tasks of half a long one, at least 2 iterations: H = 256 8-iteration short tasks (interleaved
   // A/B on one box, 1.2499/1.2463 ms/scan with 4 -> 1.2377/1.2391 with 8); H = 32 (4-iteration long
   // tasks) 2, which stays best there (0.3013/0.3004/0.3003 ms against 0.305-0.313 for 8-iteration long
   // tasks with 2- or 4-iteration short ones and for 4-iteration tasks only; tools/ab32.sh)
-  const int kItersShort = std::max(2, iters / GC_SHORT_DIV);
+  const int kItersShort = std::max(2, iters / kShortDiv);
   int64_t Us = std::max<int64_t>(iters, ((int64_t)pullers * iters + Hg - 1) / Hg);
   Us = std::min(Us, U);
   const int64_t k1 = (U - Us) / iters;  // long chunks; the short tier takes the rest

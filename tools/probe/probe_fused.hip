@@ -1,5 +1,6 @@
 // Dev probe (not product): the fused a1->a6 bins kernel at C3 size (64k points x 256 hypotheses),
-// built per tuning variant with -DGC_FUSED_OCC / -DGC_FUSED_NACC / -DGC_LP_OCC; times the
+// times the shipped configuration (kFusedOcc / kFusedNacc are constants of gc_points.hip: a variant is
+// an edit of those constants, built here, never a knob of the product); times the
 // bin-distributed product kernel (k_bins_fused) and the lane-per-point experiment (k_bins_fused_lp,
 // kept here only).
 #include "../../fl-slam_amd/csrc/gc_points.hip"
@@ -208,7 +209,7 @@ int main() {
   for (int w = 0; w < 20; ++w) run(); hipDeviceSynchronize();
   hipEventRecord(e0); for (int r = 0; r < 10; ++r) run(); hipEventRecord(e1); hipEventSynchronize(e1);
   float ms; hipEventElapsedTime(&ms, e0, e1);
-  printf("k_bins_fused<3> occ=%d nacc=%d: %.3f ms/launch (%s)\n", GC_FUSED_OCC, GC_FUSED_NACC, ms / 10, hipGetErrorString(hipGetLastError()));
+  printf("k_bins_fused<3> occ=%d nacc=%d: %.3f ms/launch (%s)\n", gc::kFusedOcc, gc::kFusedNacc, ms / 10, hipGetErrorString(hipGetLastError()));
   // lane-per-point variant (product path)
   double* bsc; hipMalloc(&bsc, 8 * 3 * 64);
   hipLaunchKernelGGL(gc::k_scale_bins, dim3(1), dim3(192), 0, 0, B, 48, bins, 10.0, bsc);
