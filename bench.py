@@ -49,6 +49,9 @@ def parse():
     ap.add_argument("--cpu-budget-s", type=float, default=30.0)
     ap.add_argument("--no-map", action="store_true", help="skip the C5 PrimitiveMap fuse leg")
     ap.add_argument("--no-c5", action="store_true", help="skip the C5 single-GPU pipeline leg")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the certs-on step and the per-stage timing scans after the timed region "
+                         "(kernel traces whose last scans must be plain product scans)")
     ap.add_argument("--roofline-only", action="store_true",
                     help="run only the contract-pair roofline leg (PMC traffic passes, tools/pmc_traffic.sh)")
     ap.add_argument("--map-only", action="store_true",
@@ -344,35 +347,12 @@ def main():
                               "step k stages scan k+1 while scan k computes (three slots in rotation)") if ingest else
                              "scans pre-staged in HBM before the timed region"},
     }
-    # the same step with the reference's per-call ConditioningCerts computed inside every scan
-    # (gc_pipeline_set_inscan_certs): 50 scans after 10 untimed, max over ranks
-    pipe.set_inscan_certs(True)
-    for _ in range(10):
-        step()
-    ctx.sync()
-    dist.barrier()
-    tc0 = time.perf_counter()
-    for _ in range(50):
-        step()
-    ctx.sync()
-    dist.barrier()
-    certs_ms = 1e3 * dist.max(time.perf_counter() - tc0) / 50
-    pipe.set_inscan_certs(False)
-    # per-stage device time of the same step (HIP events around each launch group, untimed scans after
-    # the timed region: the events themselves cost the stream a few us each), median over 20
-    pipe.set_stage_timing(True)
-    st_runs = []
-    for _ in range(20):
-        step()
-        st_runs.append(pipe.stage_ms())
-    pipe.set_stage_timing(False)
-    out_stages = {k: float(np.median([r[k] for r in st_runs])) for k in st_runs[0]}
+    if not args.no_extras:  # certs-on step time and per-stage device times (extras_leg)
+        out_extra = extras_leg(pipe, ctx, dist, step)
     if exchange is not None:
         out["exchange"] = exchange
-    out["stages_ms"] = dict(out_stages, scans=len(st_runs), note="HIP events around each launch group, untimed scans")
-    out["inscan_certs"] = {"ms_per_step": certs_ms, "scans": 50,
-                           "note": "the same step with every hypothesis's predict and fusion ConditioningCert "
-                                   "computed inside the scan (gc_pipeline_set_inscan_certs)"}
+    if not args.no_extras:
+        out.update(out_extra)
     ns = max(hs["scans"], 1.0)
     nst = max(hs["stages"], 1.0)
     out["host"] = {"scan_enqueue_ms": {"mean": hs["scan_enqueue_ms"] / ns, "max": hs["scan_enqueue_max_ms"]},
@@ -405,6 +385,36 @@ def main():
         out["cpu_baseline"] = cpu_leg(args.n_az, H_total, args.cpu_budget_s)
     if dist.rank == 0:
         print(json.dumps(out), flush=True)
+
+
+def extras_leg(pipe, ctx, dist, step):
+    """After the timed region: (1) the same step with the reference's per-call ConditioningCerts
+    computed inside every scan (gc_pipeline_set_inscan_certs), 50 scans after 10 untimed, max over
+    ranks; (2) the per-stage device time of the step (HIP events around each launch group; the
+    events themselves cost the stream a few us each), median over 20 scans."""
+    pipe.set_inscan_certs(True)
+    for _ in range(10):
+        step()
+    ctx.sync()
+    dist.barrier()
+    tc0 = time.perf_counter()
+    for _ in range(50):
+        step()
+    ctx.sync()
+    dist.barrier()
+    certs_ms = 1e3 * dist.max(time.perf_counter() - tc0) / 50
+    pipe.set_inscan_certs(False)
+    pipe.set_stage_timing(True)
+    st_runs = []
+    for _ in range(20):
+        step()
+        st_runs.append(pipe.stage_ms())
+    pipe.set_stage_timing(False)
+    stages = {k: float(np.median([r[k] for r in st_runs])) for k in st_runs[0]}
+    return {"stages_ms": dict(stages, scans=len(st_runs), note="HIP events around each launch group, untimed scans"),
+            "inscan_certs": {"ms_per_step": certs_ms, "scans": 50,
+                             "note": "the same step with every hypothesis's predict and fusion ConditioningCert "
+                                     "computed inside the scan (gc_pipeline_set_inscan_certs)"}}
 
 
 def measured_traffic(H, n, B):
