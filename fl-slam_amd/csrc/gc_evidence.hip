@@ -387,10 +387,6 @@ __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
   __shared__ double red[8];
   const int t = threadIdx.x, lane = t & 15, g = t >> 4;
   const int n = kDZ, Hl = P.Hl;
-  // floored / renormalised weights over ALL hypotheses (hypothesis.py:77-82), replicated
-  double loc = 0.0;
-  for (int k = t; k < P.H; k += kWG) loc += fmax(P.weights[k], P.weight_floor);
-  const double wsum = wg_sum(loc, red);
   const int e = blockIdx.x * 16 + lane;
   const int PLn = partial_len(P.B);
   // this lane's record entry as (source row, stride, weight kind), resolved once; the hypothesis
@@ -409,10 +405,9 @@ __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
   else if (e < kPDNUM) { src = P.dPsiM + (e - kPDPSIM); stride = 27; use_src = 1.0; }
   else if (e < kPDNUM + 2) { }  // dν_meas gyro/accel: w
   else live = 0.0;
-  const double inv_wsum = 1.0 / wsum;
   double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int k0 = g; k0 < Hl; k0 += 256) {
-    double v[16], wr[16], m[16];
+  double v[16], wr[16], m[16];
+  const auto load_batch = [&](int k0) {
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const int k = k0 + 16 * j;
@@ -421,6 +416,16 @@ __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
       wr[j] = W[kc];
       v[j] = src[(int64_t)kc * stride];
     }
+  };
+  // the first batch of values is in flight while the weight sum is formed (it needs neither)
+  load_batch(g);
+  // floored / renormalised weights over ALL hypotheses (hypothesis.py:77-82), replicated
+  double loc = 0.0;
+  for (int k = t; k < P.H; k += kWG) loc += fmax(P.weights[k], P.weight_floor);
+  const double wsum = wg_sum(loc, red);
+  const double inv_wsum = 1.0 / wsum;
+  for (int k0 = g; k0 < Hl; k0 += 256) {
+    if (k0 != g) load_batch(k0);
 #pragma unroll
     for (int j = 0; j < 16; ++j) {
       const double wk = use_norm != 0.0 ? fmax(wr[j], P.weight_floor) * inv_wsum : wr[j];

@@ -199,35 +199,27 @@ GC_DEV void exp2s_shift_n(const double (&y)[N], double Mp, const double* T, doub
     out[j] = t * p;
   }
 }
-// exp2s_shift_n on arguments pre-scaled by 8 (y8 = 8 y, exact: the bins carry the factor): the rounding
-// constant with ulp 8 (1.5·2^55) leaves 8·(rint(y) − m) in the low word of ks, which masked with
-// 2047·8 is the table entry's byte offset (one v_and; the table's LDS base rides in the ds_read's
-// immediate offset) and shifted left by 6 is (k << 9) for the exponent splice; r8 = 8 (y − rint(y))
-// exactly, and the cubic takes it with its coefficients divided by 8, 64 and 512 (exact scalings).
-// M8 = 1.5·2^55 − 8 m for the integer shift m. Same values as exp2s_shift_n, one integer op fewer.
-constexpr double kRoundMagic8 = 54043195528445952.0;  // 1.5 * 2^55
-constexpr double kExp2C1o8 = kExp2C1 / 8.0, kExp2C2o64 = kExp2C2 / 64.0, kExp2C3o512 = kExp2C3 / 512.0;
-// TAB: the table's absolute LDS byte address. The kernels calling this have no static LDS (their
-// dynamic block starts at address 0; the launchers check it, lds_base_is_zero), so the address is a
-// compile-time constant that folds into the ds_read's immediate offset (a pointer into the dynamic
-// block would cost a v_add of its relocated base per exp).
+// exp2s_shift_n reading the table at a fixed LDS byte address TAB. The kernels calling this have no
+// static LDS (their dynamic block starts at address 0; the launchers check it, ensure_no_static_lds), so
+// the table base folds into the ds_read's immediate offset: the entry's address is (k & 2047) << 3
+// with no add of a relocated base per exp. Same values as exp2s_shift_n.
 typedef const __attribute__((address_space(3))) char* lds_cptr;
 template <int N, unsigned TAB>
-GC_DEV void exp2s_shift8_n(const double (&y8)[N], double M8, double (&out)[N]) {
+GC_DEV void exp2s_shift_tab_n(const double (&y)[N], double Mp, double (&out)[N]) {
   double r[N], tv[N];
   int ki[N];
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    const double ks = y8[j] + M8;
+    const double ks = y[j] + Mp;
     ki[j] = __double2loint(ks);
-    r[j] = y8[j] - (ks - M8);
+    r[j] = y[j] - (ks - Mp);
     tv[j] = *reinterpret_cast<const __attribute__((address_space(3))) double*>(
-        reinterpret_cast<lds_cptr>((uintptr_t)TAB) + (ki[j] & ((kExpTab2 - 1) << 3)));
+        reinterpret_cast<lds_cptr>((uintptr_t)TAB) + ((unsigned)(ki[j] & (kExpTab2 - 1)) << 3));
   }
 #pragma unroll
   for (int j = 0; j < N; ++j) {
-    const double p = fma(fma(fma(kExp2C3o512, r[j], kExp2C2o64), r[j], kExp2C1o8), r[j], 1.0);
-    const double t = __hiloint2double(__double2hiint(tv[j]) + (ki[j] << 6), __double2loint(tv[j]));
+    const double p = fma(fma(fma(kExp2C3, r[j], kExp2C2), r[j], kExp2C1), r[j], 1.0);
+    const double t = __hiloint2double(__double2hiint(tv[j]) + (ki[j] << 9), __double2loint(tv[j]));
     out[j] = t * p;
   }
 }
@@ -870,13 +862,17 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
 // MFMA epilogue: reduce per-lane tiles over the 4 waves (LDS, fixed order) into one partial
 // record. Lane (g, l) holds D_j[row g + 4r][col l] = Σ R[·][16j + g + 4r] F[·][l] for the 16
 // MFMA features, and per-group partial sums accx[j][t] (bin 16j + l, feature 16 + t).
-// F0 = 1: the MFMA tile holds features 1..16 and the VALU ones 17.. ; feature 0 (N = Σ R w) is the trace
-// of the unit-direction scatter, features 4 + 7 + 9 (Σ R w |d|², |d|² = 1 within 1e-12 / range).
-template <int BPL, int NX, int F0 = 0>
+// DF = 9: feature 9 (Σ R w d_z²) is not accumulated; the MFMA columns hold features 0..8, 10..16 and
+// the VALU ones 17.. . It is recovered from the trace of the direction scatter, Σ R w |d|² = N − ε_d
+// with ε_d = Σ R w (1 − |d|²) ≤ 2·1e-12 / range of N (|d| = |r| / (|r| + 1e-12)): d_z² = N − d_x² − d_y²,
+// an absolute error ~1e-12 N in that one scatter entry; N, the resultant and κ stay exact sums.
+template <int BPL, int NX, int DF = -1>
 GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL][NX], double ent, double mxr,
                                       double sumw, double npts, int B, double* lds, double* rec) {
-  constexpr int NF = F0 + 16 + NX;
+  constexpr int ND = DF >= 0 ? 1 : 0;
+  constexpr int NF = ND + 16 + NX;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, bl = lane & 15;
+  const int fcol = (DF >= 0 && bl >= DF) ? bl + 1 : bl;  // the feature of MFMA column bl
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
 #pragma unroll
@@ -892,12 +888,12 @@ GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int b = 16 * j + g + 4 * r;
-      if (b < B) lds[(wv * B + b) * NF + F0 + bl] = acc4[j][r];
+      if (b < B) lds[(wv * B + b) * NF + fcol] = acc4[j][r];
     }
     const int b = 16 * j + bl;
     if (g == 0 && b < B)
 #pragma unroll
-      for (int t = 0; t < NX; ++t) lds[(wv * B + b) * NF + F0 + 16 + t] = accx[j][t];
+      for (int t = 0; t < NX; ++t) lds[(wv * B + b) * NF + ND + 16 + t] = accx[j][t];
   }
   double e = wave_sum(ent), m = wave_max(mxr), s = wave_sum(sumw);
   if (lane == 0) {
@@ -908,8 +904,7 @@ GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL
   __syncthreads();
   for (int i = threadIdx.x; i < B * NF; i += kWG) {
     const auto sum4 = [&](int e) { return (lds[e] + lds[B * NF + e]) + (lds[2 * B * NF + e] + lds[3 * B * NF + e]); };
-    const int f = i % NF;
-    if (F0 == 1 && f == 0) rec[i] = (sum4(i + 4) + sum4(i + 7)) + sum4(i + 9);
+    if (DF >= 0 && i % NF == DF) rec[i] = (sum4(i - DF) - sum4(i - DF + 4)) - sum4(i - DF + 7);  // N − xx − yy
     else rec[i] = sum4(i);
   }
   if (threadIdx.x == 0) {
@@ -963,9 +958,9 @@ __host__ __device__ inline size_t fused_lds_doubles(int B) {
 
 GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
   double* Tx = lds + 4 * kFusedFS * kFusedNS;
-  double* Lb = Tx + kExpTab2;  // bin directions pre-scaled by 8·2048/(τ ln2) (x, y, z rows of 64)
+  double* Lb = Tx + kExpTab2;  // bin directions pre-scaled by 2048/(τ ln2) (x, y, z rows of 64)
   exp_table2_init(Tx);
-  const double ysc = 8.0 * (A.inv_tau * kTab2OverLn2);  // the logit comes out as y8 = 8 y (exp2s_shift8_n)
+  const double ysc = A.inv_tau * kTab2OverLn2;
   if (threadIdx.x < 64) {
     const int b = threadIdx.x;
     Lb[b] = b < A.B ? A.bins[3 * b] * ysc : 0.0;
@@ -980,10 +975,10 @@ GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
 template <int BPL, bool FULL, bool PRE>
 GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec) {
   constexpr int NF = NF_BASE;
-  // features 1..16 on the matrix core, 17..18 on the VALU; feature 0 (N) is the trace of the direction
-  // scatter (features 4 + 7 + 9, write_partial_record_mfma<.., 1>): one VALU feature fewer per step
-  constexpr int F0 = 1;
-  constexpr int NX = NF - 16 - F0;
+  // features 0..8 and 10..16 on the matrix core, 17..18 on the VALU; feature 9 (w d_z²) is the trace
+  // complement N − w d_x² − w d_y² (write_partial_record_mfma<.., 9>): one VALU feature fewer per step
+  constexpr int DF = 9;
+  constexpr int NX = NF - 16 - 1;
   constexpr int NS = kFusedNS;
   const int64_t n_cap = A.n_cap;
   const int B = A.B;
@@ -992,6 +987,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   const int64_t chunk0 = big ? c * A.iters * 256 : (A.k1 * A.iters + (c - A.k1) * A.iters_s) * 256;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, bl = lane & 15;
+  const int fcol = bl >= DF ? bl + 1 : bl;  // the feature of this lane's MFMA column
   double* F = lds + wv * (NS * kFusedFS);
   const double o[3] = {A.o0, A.o1, A.o2};
   double xr[6];
@@ -1029,7 +1025,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   // S <= 1 for unit vectors: the exp argument y - ymax = (S·ysc - ymax) <= 0 with an integer ymax
   // >= ysc (the shift cancels in R and is added back to the entropy below)
   const double ymax = ceil(ysc);
-  const double M8 = kRoundMagic8 - 8.0 * ymax;  // the shift in the rounding constant (exp2s_shift8_n)
+  const double Mp = kRoundMagic - ymax;  // the shift rides in the rounding constant (exp2s_shift_n)
   const double Beps = (double)B * 1e-12;
   // raw point of the next iteration, loaded one iteration ahead (its HBM latency hides behind
   // this iteration's soft assignment)
@@ -1070,7 +1066,8 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
         point_features_w(q, d, wd, f);
         sumw += wd;
   #pragma unroll
-        for (int k = F0; k < NF; ++k) F[k * kFusedFS + lane] = f[k];
+        for (int k = 0; k < NF; ++k)
+          if (k != DF) F[k * kFusedFS + lane] = f[k];
         F[(NF + 0) * kFusedFS + lane] = d[0];
         F[(NF + 1) * kFusedFS + lane] = d[1];
         F[(NF + 2) * kFusedFS + lane] = d[2];
@@ -1083,14 +1080,14 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
         const int pl = s * 4 + g;
         const double d0 = F[(NF + 0) * kFusedFS + pl], d1 = F[(NF + 1) * kFusedFS + pl], d2 = F[(NF + 2) * kFusedFS + pl];
         const double vf = PAD ? F[(NF + 3) * kFusedFS + pl] : 1.0;  // 1 for a point of the chunk, 0 for padding
-        const double fb = F[(F0 + bl) * kFusedFS + pl];  // MFMA B operand: feature F0 + bl of point 4s + g
+        const double fb = F[fcol * kFusedFS + pl];  // MFMA B operand: feature fcol of point 4s + g
         double e[BPL], x[BPL], ex[BPL];
   #pragma unroll
         for (int j = 0; j < BPL; ++j) {
           const int b = bl + 16 * j;  // Lb is zero past B: y = -ymax stays in range, then masked
           x[j] = fma(d0, Lb[b], fma(d1, Lb[64 + b], d2 * Lb[128 + b]));
         }
-        exp2s_shift8_n<BPL, 8u * 4u * kFusedFS * kFusedNS>(x, M8, ex);  // Tx at that absolute address
+        exp2s_shift_tab_n<BPL, 8u * 4u * kFusedFS * kFusedNS>(x, Mp, ex);  // Tx at that absolute address
   #pragma unroll
         for (int j = 0; j < BPL; ++j) e[j] = (FULL || bl + 16 * j < B) ? ex[j] : 0.0;
         double zl = e[0];
@@ -1116,7 +1113,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
           acc4[s % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(r[j], fb, acc4[s % NACC][j], 0, 0, 0);
   #pragma unroll
         for (int t = 0; t < NX; ++t) {
-          const double fk = F[(F0 + 16 + t) * kFusedFS + pl];
+          const double fk = F[(17 + t) * kFusedFS + pl];
   #pragma unroll
           for (int j = 0; j < BPL; ++j) accx[j][t] = fma(r[j], fk, accx[j][t]);
         }
@@ -1137,12 +1134,12 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   // its log. Σ log Z' (shifted by ymax) - Σ R y + ymax per valid point - B ε per point (lane 0 of
   // each wave)
   const double logacc = log(zst) + (double)zex * 0.69314718055994530942;
-  const double ent = (bl == 0 ? logacc : 0.0) - entq * kExp2C1o8 +
+  const double ent = (bl == 0 ? logacc : 0.0) - entq * kExp2C1 +
                      ((lane == 0) ? (ymax * kExp2C1 - Beps) * (double)npts * 0.25 : 0.0);
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
     if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
-  write_partial_record_mfma<BPL, NX, F0>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec);
+  write_partial_record_mfma<BPL, NX, DF>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec);
   __syncthreads();  // the epilogue's LDS reads are done before the next task writes the slabs
 }
 
@@ -1569,7 +1566,7 @@ int32_t gc_bin_soft_assign(gc_ctx* ctx, int32_t H, int64_t n, int32_t B, const d
   GC_CHECK_ARG(ctx, B >= 1 && B <= 64, "B must be in [1, 64]");
   GC_CHECK_ARG(ctx, tau > 0.0, "tau must be positive");
   GC_CHECK_ARG(ctx, d_dirs && d_bins && d_resp_out && d_cert_out, "NULL buffer");
-constexpr int kSaIters = 8;
+  constexpr int kSaIters = 8;
   int iters = kSaIters;
   while (iters > 1 && ((n + iters * 256 - 1) / (iters * 256)) * (int64_t)H < 4096) iters >>= 1;
   const int64_t blocks = (n + iters * 256 - 1) / (iters * 256);
@@ -1722,10 +1719,10 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   // same for every shard size)
   const int64_t U = (P.n_cap + 255) / 256;  // 256-point units per hypothesis
   const int Hg = P.geom_H > 0 ? P.geom_H : H;
-constexpr int kBinsMinTasks = 3;
+  constexpr int kBinsMinTasks = 3;
   int iters = 16;
   while (iters > 2 && (int64_t)Hg * U < kBinsMinTasks * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
-constexpr int kShortDiv = 2;
+  constexpr int kShortDiv = 2;
   // short tasks of half a long one, at least 2 iterations: H = 256 8-iteration short tasks (interleaved
   // A/B on one box, 1.2499/1.2463 ms/scan with 4 -> 1.2377/1.2391 with 8); H = 32 (4-iteration long
   // tasks) 2, which stays best there (0.3013/0.3004/0.3003 ms against 0.305-0.313 for 8-iteration long
@@ -1745,7 +1742,7 @@ constexpr int kShortDiv = 2;
                      P.o0, P.o1, P.o2, (double*)scr, P.w_win, k1, kItersShort};
   const int n_io = io ? H : 0;
   // + 1: the pullers' task slot after the fused layout (no static LDS in k_bins_io: the dynamic block
-  // starts at LDS address 0, so the exp table's byte offsets need no base add, exp2s_shift8_n)
+  // starts at LDS address 0, so the exp table's addresses need no base add, exp2s_shift_tab_n)
   const size_t sh = sizeof(double) * (std::max<size_t>(fused_lds_doubles(B), io ? (size_t)kIoLdsDoubles : 0) + 1);
   const dim3 grid((unsigned)(n_io + pullers));
 #define GC_BIO(BP, FULL)                                                                                       \

@@ -191,10 +191,8 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None,
             mp = pipe.get_map()
             _close(mp["map"], cases.map_to_record(O.map_forget_and_add(mapst, res0["map_inc"])), 1e-8, 1e-12,
                    f"scan{k} map")
-        # full-size properties of every hypothesis: Σ_b N_b = Σ w_deskew (bin cert [6]), finite. The fused
-        # kernel forms N_b as the trace of the unit-direction scatter, Σ R w |d|² with |d|² = 1 − 2e-12/ρ
-        # (ρ the range, >= 0.4 m here): the two sums agree to ~5e-12 relative
-        np.testing.assert_allclose(stats[:, :, 0].sum(1), bcert[:, 6], rtol=2e-11)
+        # full-size properties of every hypothesis: Σ_b N_b = Σ w_deskew (bin cert [6]), finite
+        np.testing.assert_allclose(stats[:, :, 0].sum(1), bcert[:, 6], rtol=1e-12)
         assert np.all(np.isfinite(bel["L"])) and np.all(np.isfinite(diag))
     return pipe
 

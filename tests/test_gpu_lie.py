@@ -102,8 +102,10 @@ def test_so3_log_matches_oracle_all_branches(L, ctx):
         n_pi += abs(math.acos(min(max(0.5 * (np.trace(R) - 1.0), -1.0), 1.0)) - math.pi) < O.NEAR_PI
         bound = 1e-15 * (1.0 + 4.0 / max(abs(math.sin(th)), 1e-7) * (th > 1.0))
         assert np.max(np.abs(g - ref)) <= max(bound, 2e-15), (v, g, ref)
-        # and it is a logarithm of R
-        np.testing.assert_allclose(O.so3_exp(g), R, atol=2e-8)
+        # and it is a logarithm of R, as closely as the reference's own log is (the softmax-mixed
+        # axis within 1e-7 of π is accurate to ~1e-8 only, on both sides)
+        own = np.max(np.abs(O.so3_exp(ref) - R))
+        assert np.max(np.abs(O.so3_exp(g) - R)) <= own + 1e-13, (v, own)
     assert n_pi >= 12, "the near-π branch was not exercised"
 
 
@@ -119,7 +121,11 @@ def test_se3_maps_match_oracle_large_angles(L, ctx):
     ref = np.stack([O.se3_log(x) for x in T])
     far = np.array([abs(math.pi - np.linalg.norm(x[3:6])) for x in T])
     ok = far > 1e-3
-    np.testing.assert_allclose(got[ok], ref[ok], rtol=0, atol=1e-11)
+    # the rotation's rounding near π (~ulp / sin θ) passes through V⁻¹ into the translation: the
+    # bound grows as 1 / (π − θ) times |t| (measured: up to 1.1e-13 (1 + |t|) / (π − θ))
+    tol = 4e-13 * (1.0 + np.linalg.norm(t, axis=1)) / np.minimum(far, 1.0)
+    err = np.max(np.abs(got - ref), axis=1)
+    assert np.all(err[ok] <= np.maximum(tol[ok], 1e-11)), np.max(err[ok] / np.maximum(tol[ok], 1e-11))
     # near π the canonical rotvec may sit on either side of the ±π cut for both: compare maps
     np.testing.assert_allclose(np.stack([O.se3_exp(x) for x in got]), np.stack([O.se3_exp(x) for x in ref]),
                                atol=1e-7)

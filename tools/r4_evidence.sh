@@ -7,6 +7,8 @@ o=gpurun_out/r4/ev; rm -rf $o; mkdir -p $o
 stop() { case $1 in 0) ;; *) echo "stopped rc=$1 at $2" >> $o/summary.txt; exit $1;; esac; }
 timeout -k 10 420 python3 bench.py > $o/bench.json 2> $o/bench.err; stop $? bench
 echo "bench $(tail -1 $o/bench.json | cut -c1-300)" >> $o/summary.txt
+timeout -k 10 420 rocprofv3 --kernel-trace --stats -d $o/kt_bench -o kt --output-format csv -- python3 bench.py --no-cpu > $o/bench_rocprof.json 2> $o/bench_rocprof.err; stop $? bench_rocprof
+cp "$(find $o/kt_bench -name '*kernel_stats.csv' | head -1)" $o/kernel_stats_bench.csv; find $o/kt_bench -name "*kernel_trace.csv" -delete
 timeout -k 10 180 python3 bench.py --hyps 32 --no-cpu --no-map --no-c5 --no-roofline --steps 400 --warmup 50 > $o/bench_h32.json 2>> $o/bench.err; stop $? bench_h32
 for H in 256 32; do
   d=$o/kt_h$H
