@@ -63,6 +63,8 @@ def parse():
     ap.add_argument("--roofline-reps", type=int, default=10)
     ap.add_argument("--no-ingest", action="store_true",
                     help="stage the scans once before the timed region (round-2 methodology) instead of every step")
+    ap.add_argument("--ingest-slots", type=int, default=INGEST_SLOTS,
+                    help="scan slots in the ingest rotation (the slot staged at step k was last read by scan k - slots + 1)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and exchange the communicator id, then exit (no GPU work)")
     return ap.parse_args()
@@ -161,7 +163,7 @@ def bytes_moment_match(n, B):
     return n * (24 + 72 + 8 + 8 + B * 8) + 24 + B * (1 + 3 + 9 + 3 + 9 + 1) * 8
 
 
-INGEST_SLOTS = 3  # scan slots in the ingest rotation of the C3 step
+INGEST_SLOTS = 3  # scan slots in the ingest rotation of the C3 step (--ingest-slots)
 
 
 def warmup_map_record(ctx, _abi, scan, n, B, bins, origin):
@@ -271,9 +273,9 @@ def main():
         sc = scans[k % len(scans)]
         if ingest:
             ts = time.perf_counter()
-            pipe.stage_scan((k + 1) % INGEST_SLOTS, scans[(k + 1) % len(scans)])
+            pipe.stage_scan((k + 1) % args.ingest_slots, scans[(k + 1) % len(scans)])
             tr = time.perf_counter()
-            pipe.run_scan(k % INGEST_SLOTS, sc, k)
+            pipe.run_scan(k % args.ingest_slots, sc, k)
             if timed:
                 stage_s[0] += tr - ts
                 stage_s[1] += 1

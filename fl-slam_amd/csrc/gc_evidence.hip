@@ -129,6 +129,8 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     const double* m = P.map + t * kMapRec;
     const double* md = P.map_der + t * kMapDer;
     planar_bin_row(mf, s[0], s + 13, s + 16, m[13], md + 4, md + 7, eps, tab + t * 13);
+  } else if (t == 64) {  // log R_mf for the tape on wave 1 beside the planar rows (B <= 64)
+    so3_log(mf, sc + 110);
   }
   __syncthreads();
   GC_PHASE(P, 32);
@@ -357,17 +359,12 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   if (t == 0) {
     for (int k = 0; k < 6; ++k) P.X[(int64_t)hl * 6 + k] = sc[92 + k];
     P.stamp[hl] += S.dt;
-    double* dg = P.diag + (int64_t)hl * kHypDiag;
-    double pose[6];
-    compose_exp2(sc + 92, mufin, pose);
-    for (int k = 0; k < 6; ++k) dg[k] = pose[k];
+    double* dg = P.diag + (int64_t)hl * kHypDiag;  // [0, 6): the world pose, k_combine_local
     dg[6] = sc[61]; dg[7] = sc[50]; dg[8] = alpha; dg[9] = s_dt; dg[10] = s_ex; dg[11] = rho;
     dg[12] = sc[63]; dg[13] = sc[60]; dg[14] = sc[53]; dg[15] = sc[51]; dg[16] = sc[52]; dg[17] = sc[56];
     dg[18] = mf[30]; dg[19] = pt[22]; dg[20] = sc[62];
     for (int k = 0; k < 3; ++k) dg[21 + k] = pt[k];       // t_wls
-    double wmf[3];
-    so3_log(mf, wmf);
-    for (int k = 0; k < 3; ++k) dg[24 + k] = wmf[k];      // log R_mf
+    for (int k = 0; k < 3; ++k) dg[24 + k] = sc[110 + k];  // log R_mf
     for (int k = 0; k < 3; ++k) dg[27 + k] = mf[24 + k];  // MF singular values
     for (int k = 0; k < 6; ++k) dg[30 + k] = P.xi[(int64_t)hl * 6 + k];
     double mu2 = 0.0;
@@ -379,12 +376,24 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
 // ==================================================================== a16 partial sums (local)
 // grid: ceil(P_len / 64) blocks x 256 threads; block covers 64 record entries, its 4 waves sum
 // interleaved hypothesis subsets, combined in fixed order (deterministic).
+// The workgroups past the record's are one thread per hypothesis: the tape's world pose
+// X_fin ⊞ μ_fin (a single-lane chain of SE(3) maps, ~3 µs) off k_evidence's critical tail.
 __global__ void __launch_bounds__(256) k_combine_local(PipeDev P) {
   // 16 record entries per workgroup x 16 hypothesis groups (hypotheses g, g+16, ...): at H = 256 a
   // thread's 16 hypotheses are one batch of loads in flight; the 16 group partials are then
   // summed in a fixed tree
   __shared__ double part[16][16];
   __shared__ double red[8];
+  const int nrec = (partial_len(P.B) + 15) / 16;
+  if ((int)blockIdx.x >= nrec) {
+    const int h = ((int)blockIdx.x - nrec) * kWG + (int)threadIdx.x;
+    if (h < P.Hl) {
+      double pose[6];
+      compose_exp2(P.X + (int64_t)h * 6, P.mu_fin + (int64_t)h * kDZ, pose);
+      for (int k = 0; k < 6; ++k) P.diag[(int64_t)h * kHypDiag + k] = pose[k];
+    }
+    return;
+  }
   const int t = threadIdx.x, lane = t & 15, g = t >> 4;
   const int n = kDZ, Hl = P.Hl;
   const int e = blockIdx.x * 16 + lane;
@@ -631,7 +640,8 @@ hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) 
   return hipGetLastError();
 }
 hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
-  hipLaunchKernelGGL(k_combine_local, dim3((partial_len(P.B) + 15) / 16), dim3(256), 0, st, P);
+  const int nrec = (partial_len(P.B) + 15) / 16, npose = (P.Hl + kWG - 1) / kWG;
+  hipLaunchKernelGGL(k_combine_local, dim3(nrec + npose), dim3(256), 0, st, P);
   return hipGetLastError();
 }
 hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {

@@ -218,7 +218,9 @@ int slot_wait_consumed(gc_pipeline* p, gc_pipeline::Slot& s) {
   if (s.consumed_ticket > 0) {
     if (__atomic_load_n(p->done_word, __ATOMIC_ACQUIRE) < s.consumed_ticket) {
       // its bins may still be running: order the DMA after everything enqueued on the compute
-      // stream (a host wait here instead let the host fall behind: H = 32 0.296 -> 0.308 ms)
+      // stream. This event costs a ~5 us gap before the next kernel; a host poll of the word instead
+      // removes the gap but the step gets slower (H = 32 0.2924 -> 0.2977 ms with 3 or 4 slots,
+      // H = 256 1.212 -> 1.221: profiles/r04/ab_slot_poll.txt)
       GC_HIP(p->ctx, hipEventRecord(s.consumed, p->ctx->stream));
       s.consumed_rec = true;
     }

@@ -209,14 +209,19 @@ __global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, uint32_t
 
 // Pass 2, one thread per position: the owner of each slot (the run its list ends on) adds the slot's
 // pieces in block order and read-modify-writes the slot (the fuse with responsibility 1, source LiDAR)
-__global__ void k_smap_apply(ScanMapArgs A, int64_t n, uint32_t* head, const uint32_t* __restrict__ sslot,
-                             const uint32_t* __restrict__ run_next, const SmapRow* __restrict__ pieces,
-                             unsigned long long* n_unique) {
+__global__ void __launch_bounds__(256) k_smap_apply(ScanMapArgs A, int64_t n, uint32_t* head,
+                                                    const uint32_t* __restrict__ sslot,
+                                                    const uint32_t* __restrict__ run_next,
+                                                    const SmapRow* __restrict__ pieces, unsigned long long* n_unique) {
 #pragma clang fp contract(off)
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (e >= n) return;
-  const uint32_t key = sslot[e];
-  if ((int64_t)key >= A.map.m_slots || head[key] != (uint32_t)e) return;  // dropped / not the owner
+  const uint32_t key = e < n ? sslot[e] : kNoRun;
+  const bool own = (int64_t)key < A.map.m_slots && head[key] == (uint32_t)e;  // not dropped, the owner
+  // the touched-slot count: one atomic per wave (one per owner would serialise thousands of atomics
+  // on one address)
+  const unsigned long long b = __ballot(own);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_unique, (unsigned long long)__popcll(b));
+  if (!own) return;
   SmapRow d;
   for (int q = 0; q < kSmapRow; ++q) d.v[q] = 0.0;
   const auto add = [&](uint32_t r) {
@@ -248,8 +253,7 @@ __global__ void k_smap_apply(ScanMapArgs A, int64_t n, uint32_t* head, const uin
   mSup(A.map, s) = A.scan_seq;
   mUpd(A.map, s) = A.scan_seq;
   if (A.map.lidar_mass) mLid(A.map, s) = mLid(A.map, s) + d.v[15];
-  head[key] = kNoRun;       // the list is consumed
-  atomicAdd(n_unique, 1ull);  // integer count: order-independent
+  head[key] = kNoRun;  // the list is consumed
 }
 
 }  // namespace

@@ -126,9 +126,19 @@ def test_se3_maps_match_oracle_large_angles(L, ctx):
     tol = 4e-13 * (1.0 + np.linalg.norm(t, axis=1)) / np.minimum(far, 1.0)
     err = np.max(np.abs(got - ref), axis=1)
     assert np.all(err[ok] <= np.maximum(tol[ok], 1e-11)), np.max(err[ok] / np.maximum(tol[ok], 1e-11))
-    # near π the canonical rotvec may sit on either side of the ±π cut for both: compare maps
-    np.testing.assert_allclose(np.stack([O.se3_exp(x) for x in got]), np.stack([O.se3_exp(x) for x in ref]),
-                               atol=1e-7)
+    # near π (δ = π − θ < 1e-3) the reference's log takes θ from acos of the trace (condition 1/sin θ)
+    # and scales the axis by θ / (2 sin θ): an ulp of R moves the rotation vector by ~ulp·π/δ², on the
+    # device and in the oracle alike (measured 1.8e-3 at δ = 1e-6, the oracle's own round trip the
+    # same size); the near-π branch (δ < 1e-7) holds ~1e-8. So the rotation is bounded by that
+    # conditioning, and the translation must be consistent with the device's own rotation vector:
+    # V(φ) ρ = t to rounding
+    for x, g, r, d in zip(T[~ok], got[~ok], ref[~ok], far[~ok]):
+        Rin = O.so3_exp(x[3:6])
+        eg = np.max(np.abs(O.so3_exp(g[3:6]) - Rin))
+        er = np.max(np.abs(O.so3_exp(r[3:6]) - Rin))
+        bound = 2e-8 if d < 1e-7 else min(2e-15 * math.pi / d ** 2, 1e-2)
+        assert eg <= max(bound, 4.0 * er), (x, eg, er)
+        assert np.max(np.abs(O.se3_exp(g)[:3] - x[:3])) <= 1e-11 * (1.0 + np.linalg.norm(x[:3])), x
     Vi = L._se3_V_inv(w, ctx=ctx)
     # D = 1/θ² - (1 + cos θ)/(2θ sin θ + 1e-12): 1 + cos θ cancels near π, an ulp of cos is ~1e-11 of D
     np.testing.assert_allclose(Vi, np.stack([O.se3_V_inv(v) for v in w]), rtol=0, atol=1e-9)
