@@ -350,7 +350,9 @@ __global__ void __launch_bounds__(kSinkT) k_sinkhorn(int64_t N, const uint8_t* _
 
 __global__ void k_count_u8(int64_t n, const uint8_t* __restrict__ m, unsigned long long* out) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n && m[i]) atomicAdd(out, 1ull);  // integer count: order-independent
+  // integer count: order-independent; one atomic per wave (one per element serialises on the counter)
+  const unsigned long long b = __ballot(i < n && m[i] != 0);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
 }
 
 }  // namespace

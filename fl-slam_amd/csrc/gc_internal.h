@@ -12,11 +12,12 @@ struct gc_ctx {
   void* scratch = nullptr;  // growable device scratch (per ctx, stream-ordered use only)
   size_t scratch_bytes = 0;
   int cu_count = 0;  // compute units of the device (queried on first use)
-  // per-slot list heads of the map reduce-by-key (gc_map.hip, gc_scanmap.hip): all 0xFFFFFFFF between
-  // calls (each call's owners restore the heads they used); re-filled when grown or after a failed call
-  uint32_t* slot_head = nullptr;
-  int64_t slot_head_n = 0;
-  bool slot_head_dirty = true;
+  // per-slot run entries of the map reduce-by-key (gc_runs.h SlotRuns, 256 B per slot; gc_map.hip,
+  // gc_scanmap.hip): all zero between calls (each call's owners clear the entries they used);
+  // re-zeroed when grown or after a failed call
+  void* slot_runs = nullptr;
+  int64_t slot_runs_n = 0;
+  bool slot_runs_dirty = true;
 };
 
 namespace gc {
@@ -27,9 +28,13 @@ void set_error(gc_ctx* ctx, const std::string& msg);
 // device scratch of at least `bytes` (synchronises the stream before growing)
 int scratch(gc_ctx* ctx, size_t bytes, void** out);
 
-// the context's slot-head array for a map of m_slots slots, every entry 0xFFFFFFFF on return (stream-
-// ordered: a fill is enqueued on ctx->stream when the array is new, grown or marked dirty)
-int slot_heads(gc_ctx* ctx, int64_t m_slots, uint32_t** out);
+// the context's per-slot run table (gc_runs.h SlotRuns) for a map of m_slots slots, every entry zero on
+// return (stream-ordered: a fill is enqueued on ctx->stream when the table is new, grown or dirty)
+int slot_runs(gc_ctx* ctx, int64_t m_slots, void** out);
+
+// the table exp's 2048-entry table in device memory (gc_points.hip), enqueued once per context
+hipError_t init_exp_table(hipStream_t st);
+constexpr size_t kSlotRunsBytes = 256;
 
 // hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) only when fn has not yet been allowed that
 // much: the runtime call is not free (it waited for an in-flight ingest copy on another stream,

@@ -5,13 +5,14 @@
 //  primitive_map_fuse            backend/structures/primitive_map.py:992-1163
 //
 // The fuse is a reduce-by-key of K measurement rows into M map slots (gc_runs.h): each block of
-// 1024 rows is sorted by (slot, row) in LDS and its runs linked into per-slot lists; one owner thread
+// 1024 rows is sorted by (slot, row) in LDS and its runs registered in per-slot entries; one owner thread
 // per distinct slot then sums the slot's rows in row order (runs in block order) and
 // read-modify-writes the slot once. The per-slot sums are therefore formed in the same order as the
 // reference's sequential scatter-add (bit-reproducible, no float atomics); nothing is staged in HBM
 // (each row is read once, by its slot's owner) and a slot's record is touched exactly twice (read +
 // write).
 #include <hip/hip_runtime.h>
+#include <vector>
 #include "gc_internal.h"
 #include "gc_math.h"
 #include "gc_mapslot.h"
@@ -109,8 +110,8 @@ GC_DEV void slot_colour(const gc_primitive_map& m, int64_t s, double cam, const 
 // ---- pass 1: per block of kFuseBlk rows, the (slot, row) sort and the run links (gc_runs.h)
 constexpr int kFuseBlk = 1024;
 __global__ void __launch_bounds__(256) k_fuse_runs(const int32_t* __restrict__ target, int64_t K, int64_t M,
-                                                   uint32_t* head, uint32_t* sslot, uint32_t* order,
-                                                   uint32_t* run_len, uint32_t* run_next) {
+                                                   SlotRuns* T, uint32_t* sslot, uint32_t* order,
+                                                   uint32_t* run_len, uint32_t* run_next, uint32_t* rank) {
   __shared__ uint64_t a[kFuseBlk];
   const int64_t base = (int64_t)blockIdx.x * kFuseBlk;
   for (int i = threadIdx.x; i < kFuseBlk; i += blockDim.x) {
@@ -129,12 +130,14 @@ __global__ void __launch_bounds__(256) k_fuse_runs(const int32_t* __restrict__ t
     const uint32_t key = (uint32_t)(a[i] >> 32);
     order[p] = (uint32_t)(base + (uint32_t)a[i]);
     sslot[p] = key;
+    uint32_t rk = kNoRun;
     if ((int64_t)key < M && (i == 0 || (uint32_t)(a[i - 1] >> 32) != key)) {
       int len = 1;
       while (i + len < kFuseBlk && (uint32_t)(a[i + len] >> 32) == key) ++len;
       run_len[p] = (uint32_t)len;
-      run_next[p] = atomicExch(&head[key], (uint32_t)p);
+      rk = register_run(T, key, (uint32_t)p, run_next);
     }
+    rank[p] = rk;
   }
 }
 
@@ -214,12 +217,13 @@ GC_DEV void fuse_apply_slot32(const FuseArgs& A, int64_t s, const double* d) {
 
 // one thread per sorted position; the owner of each slot (the run its list ends on) fuses the slot
 template <int LT, bool R32>  // R32: the packed 3-lobe record (A.rec32)
-__global__ void __launch_bounds__(256) k_fuse_apply(FuseArgs A, int64_t K, uint32_t* head,
+__global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, SlotRuns* T,
                                                     const uint32_t* __restrict__ sslot,
                                                     const uint32_t* __restrict__ order,
                                                     const uint32_t* __restrict__ run_len,
                                                     const uint32_t* __restrict__ run_next,
-                                                    unsigned long long* n_unique) {
+                                                    const uint32_t* __restrict__ rank,
+                                                    uint32_t* wg_count) {
 #pragma clang fp contract(off)
   constexpr int LM = LT > 0 ? LT : kMaxLobes;
   constexpr int NT = row_terms_len(LM);
@@ -228,7 +232,7 @@ __global__ void __launch_bounds__(256) k_fuse_apply(FuseArgs A, int64_t K, uint3
   uint32_t s = 0;
   if (p < K) {
     s = sslot[p];
-    own = (int64_t)s < A.map.m_slots && head[s] == (uint32_t)p;
+    own = (int64_t)s < A.map.m_slots && rank[p] == 0u;
   }
   if (own) {
     const int L = LT > 0 ? LT : A.map.n_lobes;
@@ -244,25 +248,33 @@ __global__ void __launch_bounds__(256) k_fuse_apply(FuseArgs A, int64_t K, uint3
         for (int e = 0; e < nt; ++e) d[e] += t[e];
       }
     };
-    if (run_next[p] == kNoRun) {  // the slot's rows all lie in one block (the common case)
+    __shared__ uint32_t slices[kApplyWG * kRunCap];
+    SlotRunList<kRunCap> rl(slices + threadIdx.x * kRunCap);
+    if (T[s].cnt == 1u) {  // the slot's rows all lie in one block (the common case)
       add_run((uint32_t)p);
     } else {
-      RunList<32> rl;
-      rl.collect((uint32_t)p, run_next, (int)((K + kFuseBlk - 1) / kFuseBlk));
+      rl.collect(T, s, run_next, (int)((K + kFuseBlk - 1) / kFuseBlk));
       uint32_t prev = 0;
       for (int i = 0; i < rl.n; ++i) {  // runs in block order
-        const uint32_t r = rl.at(i, (uint32_t)p, run_next, prev);
-        if (r == kNoRun) break;  // only a corrupt list: never index past the runs
+        const uint32_t r = rl.at(i, prev);
+        if (r == kNoRun) break;  // only a corrupt entry: never index past the runs
         prev = r;
         add_run(r);
       }
     }
     if constexpr (R32) fuse_apply_slot32(A, s, d);
     else fuse_apply_slot<LT>(A, s, d);
-    head[s] = kNoRun;  // the list is consumed: the head is free for the next call
+    rl.clear(T, s);  // the entry is zero for the next call
   }
-  const unsigned long long b = __ballot(own);  // the distinct-slot count, one atomic per wave
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_unique, (unsigned long long)__popcll(b));
+  // the distinct-slot count per workgroup (an LDS sum: one global counter for every wave serialised
+  // the kernel's end)
+  __shared__ uint32_t owned;
+  if (threadIdx.x == 0) owned = 0u;
+  __syncthreads();
+  const unsigned long long b = __ballot(own);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&owned, (uint32_t)__popcll(b));
+  __syncthreads();
+  if (threadIdx.x == 0) wg_count[blockIdx.x] = owned;
 }
 
 // every slot's colour estimate (primitive_map.py:1090-1098)
@@ -343,47 +355,51 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   }
   A.timestamp = timestamp;
   A.scan_seq = scan_seq;
-  // scratch: the sorted slot, row order, run length and run link of every position, the unique counter
+  // scratch: the sorted slot, row order, run length, run rank and overflow link of every position, the
+  // apply launch's per-workgroup distinct-slot counts
   const size_t kv = ((size_t)K * sizeof(uint32_t) + 255) / 256 * 256;
+  const unsigned grid = (unsigned)((K + kApplyWG - 1) / kApplyWG);
   void* scr;
-  if (int rc = gc::scratch(ctx, 4 * kv + 256, &scr)) return rc;
+  if (int rc = gc::scratch(ctx, 5 * kv + (size_t)grid * sizeof(uint32_t), &scr)) return rc;
   char* base = (char*)scr;
   uint32_t* sslot = (uint32_t*)base;
   uint32_t* order = (uint32_t*)(base + kv);
   uint32_t* run_len = (uint32_t*)(base + 2 * kv);
   uint32_t* run_next = (uint32_t*)(base + 3 * kv);
-  unsigned long long* cnt = (unsigned long long*)(base + 4 * kv);
-  uint32_t* head = nullptr;
-  if (int rc = gc::slot_heads(ctx, map->m_slots, &head)) return rc;
-  GC_HIP(ctx, hipMemsetAsync(cnt, 0, sizeof(unsigned long long), ctx->stream));
-  // from here a failed launch may leave heads set: the next call re-fills them
-  ctx->slot_head_dirty = true;
+  uint32_t* rank = (uint32_t*)(base + 4 * kv);
+  uint32_t* cnt = (uint32_t*)(base + 5 * kv);
+  void* Tv = nullptr;
+  if (int rc = gc::slot_runs(ctx, map->m_slots, &Tv)) return rc;
+  SlotRuns* T = (SlotRuns*)Tv;
+  // from here a failed launch may leave entries set: the next call re-zeroes them
+  ctx->slot_runs_dirty = true;
   hipLaunchKernelGGL(k_fuse_runs, dim3((unsigned)((K + kFuseBlk - 1) / kFuseBlk)), dim3(256), 0, ctx->stream,
-                     (const int32_t*)meas->target_slots, K, map->m_slots, head, sslot, order, run_len, run_next);
+                     (const int32_t*)meas->target_slots, K, map->m_slots, T, sslot, order, run_len, run_next, rank);
   GC_LAUNCH_CHECK(ctx);
-  const unsigned grid = (unsigned)((K + 255) / 256);
   const bool l3 = map->n_lobes == 3;  // GC_VMF_N_LOBES: the compile-time lobe count
   if (A.rec32)
-    hipLaunchKernelGGL((k_fuse_apply<3, true>), dim3(grid), dim3(256), 0, ctx->stream, A, K, head, sslot, order,
-                       run_len, run_next, cnt);
+    hipLaunchKernelGGL((k_fuse_apply<3, true>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, sslot, order,
+                       run_len, run_next, rank, cnt);
   else if (l3)
-    hipLaunchKernelGGL((k_fuse_apply<3, false>), dim3(grid), dim3(256), 0, ctx->stream, A, K, head, sslot, order,
-                       run_len, run_next, cnt);
+    hipLaunchKernelGGL((k_fuse_apply<3, false>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, sslot, order,
+                       run_len, run_next, rank, cnt);
   else
-    hipLaunchKernelGGL((k_fuse_apply<0, false>), dim3(grid), dim3(256), 0, ctx->stream, A, K, head, sslot, order,
-                       run_len, run_next, cnt);
+    hipLaunchKernelGGL((k_fuse_apply<0, false>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, sslot, order,
+                       run_len, run_next, rank, cnt);
   GC_LAUNCH_CHECK(ctx);
-  ctx->slot_head_dirty = false;  // every head the runs pass set, its owner restored
+  ctx->slot_runs_dirty = false;  // every entry the runs pass set, its owner cleared
   if (color && !map->colors_current) {
     hipLaunchKernelGGL(k_fuse_colors, dim3((unsigned)((map->m_slots + 255) / 256)), dim3(256), 0, ctx->stream, *map,
                        eps_mass);
     GC_LAUNCH_CHECK(ctx);
   }
   if (n_fused_out) {
-    unsigned long long n = 0;
-    GC_HIP(ctx, hipMemcpyAsync(&n, cnt, sizeof(n), hipMemcpyDeviceToHost, ctx->stream));
+    std::vector<uint32_t> c(grid);
+    GC_HIP(ctx, hipMemcpyAsync(c.data(), cnt, c.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
     GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    *n_fused_out = (int64_t)n;
+    int64_t n = 0;
+    for (uint32_t v : c) n += v;
+    *n_fused_out = n;
   }
   return GC_OK;
 }

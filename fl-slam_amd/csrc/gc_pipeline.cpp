@@ -750,11 +750,11 @@ int32_t gc_pipeline_get_scan_map_count(gc_pipeline* p, int64_t* n_slots) {
   GC_CHECK_ARG(nullptr, p && n_slots, "NULL argument");
   GC_CHECK_ARG(p->ctx, p->smap_on, "no PrimitiveMap attached");
   GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
-  unsigned long long n = 0;
-  GC_HIP(p->ctx, hipMemcpyAsync(&n, p->smapW.count, sizeof(n), hipMemcpyDeviceToHost, p->ctx->stream));
-  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
-  *n_slots = (int64_t)n;
-  return GC_OK;
+  size_t bytes = 0;
+  const int32_t rc = gc::scan_map_count(p->ctx, p->smapW, n_slots, &bytes);
+  p->hs[GC_HS_HOST_SYNCS] += 1.0;
+  p->hs[GC_HS_D2H_BYTES] += (double)bytes;
+  return rc;
 }
 
 static int32_t scan_local_impl(gc_pipeline* p, int32_t slot, double scan_start, double scan_end, double t_last,

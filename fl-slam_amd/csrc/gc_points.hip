@@ -160,6 +160,20 @@ GC_DEV void exp_table2_init(double* T) {
     T[j] = __hiloint2double(__double2hiint(v) - (j << 9), __double2loint(v));
   }
 }
+// The table formed once per context on the device (gc_ctx_create -> init_exp_table) by the same
+// exp_table2_init the workgroups used to run themselves: a workgroup now copies 16 KB from L2 instead
+// of evaluating 2048 exp2 (~2 us at the start of every bins launch), the same bits.
+__device__ __attribute__((aligned(16))) double g_exp_tab2[kExpTab2];
+__global__ void __launch_bounds__(256) k_exp_table_init() { exp_table2_init(g_exp_tab2); }
+GC_DEV void exp_table2_load(double* T) {
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
+  for (int j = threadIdx.x; j < kExpTab2 / 2; j += blockDim.x)
+    reinterpret_cast<dvec2*>(T)[j] = reinterpret_cast<const dvec2*>(g_exp_tab2)[j];
+}
+hipError_t init_exp_table(hipStream_t st) {
+  hipLaunchKernelGGL(k_exp_table_init, dim3(1), dim3(256), 0, st);
+  return hipGetLastError();
+}
 template <int N>
 GC_DEV void exp2s_n(const double (&y)[N], const double* T, double (&out)[N]) {
   double r[N], tv[N];
@@ -523,7 +537,7 @@ __global__ void __launch_bounds__(256, kSaOcc) k_soft_assign(int64_t n, int B, i
   extern __shared__ __attribute__((aligned(16))) double sa_lds[];
   double* Tx = sa_lds;
   double* red = Tx + kExpTab2 + 192;  // (192 doubles after the table unused: the bins are scalar loads)
-  exp_table2_init(Tx);
+  exp_table2_load(Tx);
   __syncthreads();
   const int h = blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -959,7 +973,7 @@ __host__ __device__ inline size_t fused_lds_doubles(int B) {
 GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
   double* Tx = lds + 4 * kFusedFS * kFusedNS;
   double* Lb = Tx + kExpTab2;  // bin directions pre-scaled by 2048/(τ ln2) (x, y, z rows of 64)
-  exp_table2_init(Tx);
+  exp_table2_load(Tx);
   const double ysc = A.inv_tau * kTab2OverLn2;
   if (threadIdx.x < 64) {
     const int b = threadIdx.x;

@@ -3,14 +3,15 @@
 // K rows each target one of M map slots; the rows of a slot must be summed in a fixed order and the
 // slot read-modify-written once. Instead of a global radix sort of (slot, row):
 //  1. each workgroup sorts its own block of rows by (slot, local row) in LDS (bitonic), so a slot's
-//     rows in the block form one contiguous run, and links the run into the slot's list:
-//     next[run] = atomicExch(&head[slot], run), run = the run's global sorted position;
-//  2. the one run left in head[slot] belongs to the slot's owner thread, which collects the slot's
-//     runs (at most one per block), orders them by position (= block order), sums them in that order,
-//     applies the slot and restores head[slot] = kNoRun.
-// The order of the atomics only decides who owns a slot, never the order of the sums: results are
-// bit-reproducible. Heads stay kNoRun between calls (gc_ctx::slot_head), so no pass over the M slots
-// is needed.
+//     rows in the block form one contiguous run, and registers the run with its slot's entry of the
+//     per-slot table (register_run): rank = atomicAdd(&cnt, 1), the run's position stored inline at
+//     that rank (the first kInlRuns runs) or linked into the entry's overflow list;
+//  2. the run of rank 0 belongs to the slot's owner thread, which reads the slot's runs from the
+//     entry (no list walk for up to kInlRuns runs), orders them by position (= block
+//     order), sums them in that order, applies the slot and clears the entry.
+// The order of the atomics only decides ranks and ownership, never the order of the sums: results
+// are bit-reproducible. Entries stay zero between calls (gc_ctx::slot_runs), so no pass over the M
+// slots is needed.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -41,46 +42,90 @@ __device__ __forceinline__ void lds_bitonic_sort(uint64_t* a) {
   }
 }
 
-// The runs of the list starting at `first`, in ascending order, into runs[0..n) (n returned). Lists
-// longer than CAP are walked again per element (ascending selection): correct for any length, quadratic
-// only past CAP runs of one slot.
+constexpr int kInlRuns = 62;
+// a slot's entry: two 128-B lines, all zero between calls. 62 inline runs hold every slot of the C5
+// scans (at most one run per 256-row block: ~45 at the busiest voxel of a dense 131k-point scan), so
+// the overflow list is a correctness path only.
+struct alignas(256) SlotRuns {
+  uint32_t cnt;             // runs registered this call
+  uint32_t ovf;             // overflow list head, as position + 1 (0 = none)
+  uint32_t inl[kInlRuns];   // the positions of the first kInlRuns runs, in arrival order
+};
+static_assert(sizeof(SlotRuns) == 256, "two lines per slot");
+
+// pass 1: register the run at position p with slot s; returns its rank (0: p's thread will own the slot)
+__device__ __forceinline__ uint32_t register_run(SlotRuns* T, uint32_t s, uint32_t p, uint32_t* ovf_next) {
+  const uint32_t r = atomicAdd(&T[s].cnt, 1u);
+  if (r < (uint32_t)kInlRuns) T[s].inl[r] = p;
+  else ovf_next[p] = atomicExch(&T[s].ovf, p + 1u);
+  return r;
+}
+
+// pass 2, the owner: the slot's runs in ascending position order in a thread's LDS slice buf[0..CAP)
+// (a register array indexed at run time would live in scratch memory). The inline runs are in arrival
+// order and the overflow list in reverse arrival order; arrival order is close to block order (blocks
+// are dispatched in order and register their runs as they finish), so after reversing the overflow
+// part the insertion sort sees an almost ascending sequence. More than CAP runs (never at the C5
+// sizes: at most one run per block, ~45 at the busiest voxel of a dense scan) fall back to a
+// selection over the entry and its list, correct for any count. Clears the entry.
 template <int CAP>
-struct RunList {
-  uint32_t runs[CAP];
+struct SlotRunList {
+  uint32_t* buf;
+  const SlotRuns* e = nullptr;
+  const uint32_t* next = nullptr;
   int n = 0;
   bool spill = false;
 
-  // max_runs: the number of blocks of the call (a slot has at most one run per block); the walk stops
-  // there whatever the links hold, so no list can make a thread loop
-  __device__ void collect(uint32_t first, const uint32_t* __restrict__ next, int max_runs) {
-    n = 0;
-    spill = false;
-    for (uint32_t r = first; r != kNoRun && n < max_runs; r = next[r]) {
-      if (n < CAP) runs[n] = r;
-      else spill = true;
-      ++n;
-    }
-    if (spill || n <= 1) return;
-    for (int i = 1; i < n; ++i) {  // insertion sort (n is small: one run per block of the slot)
-      const uint32_t v = runs[i];
-      int j = i - 1;
-      while (j >= 0 && runs[j] > v) {
-        runs[j + 1] = runs[j];
-        --j;
+  __device__ explicit SlotRunList(uint32_t* slice) : buf(slice) {}
+
+  __device__ void collect(SlotRuns* T, uint32_t s, const uint32_t* __restrict__ ovf_next, int max_runs) {
+    e = T + s;
+    next = ovf_next;
+    const uint32_t cnt = e->cnt;
+    n = (int)(cnt < (uint32_t)max_runs ? cnt : (uint32_t)max_runs);
+    spill = n > CAP;
+    if (!spill) {
+      const int ni = n < kInlRuns ? n : kInlRuns;
+      for (int i = 0; i < ni; ++i) buf[i] = e->inl[i];
+      int m = n;
+      for (uint32_t r = e->ovf; r != 0u && m > ni; r = ovf_next[r - 1]) buf[--m] = r - 1;  // reversed
+      for (int i = 1; i < n; ++i) {
+        const uint32_t v = buf[i];
+        int j = i - 1;
+        while (j >= 0 && buf[j] > v) {
+          buf[j + 1] = buf[j];
+          --j;
+        }
+        buf[j + 1] = v;
       }
-      runs[j + 1] = v;
     }
   }
 
-  // the i-th smallest run; with spill the i-th call in ascending i walks the list once more
-  __device__ uint32_t at(int i, uint32_t first, const uint32_t* __restrict__ next, uint32_t prev) const {
-    if (!spill) return runs[i];
+  // the i-th smallest run; with spill the i-th call in ascending i scans the entry and its list once
+  __device__ uint32_t at(int i, uint32_t prev) const {
+    if (!spill) return buf[i];
     uint32_t best = kNoRun;
-    int m = 0;
-    for (uint32_t r = first; r != kNoRun && m < n; r = next[r], ++m)
+    for (int k = 0; k < kInlRuns && k < n; ++k) {
+      const uint32_t r = e->inl[k];
       if ((i == 0 || r > prev) && r < best) best = r;
+    }
+    int m = kInlRuns;
+    for (uint32_t r1 = e->ovf; r1 != 0u && m < n; r1 = next[r1 - 1], ++m) {
+      const uint32_t r = r1 - 1;
+      if ((i == 0 || r > prev) && r < best) best = r;
+    }
     return best;
   }
+
+  // after the last at(): the entry is zero for the next call
+  __device__ void clear(SlotRuns* T, uint32_t s) const {
+    T[s].cnt = 0u;
+    T[s].ovf = 0u;
+  }
 };
+
+// the apply kernels' workgroup and per-thread slice capacity: 128 x 64 x 4 B = 32 KB of LDS
+constexpr int kApplyWG = 128;
+constexpr int kRunCap = 64;
 
 }  // namespace gc

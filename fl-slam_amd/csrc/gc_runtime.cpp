@@ -67,21 +67,21 @@ int scratch(gc_ctx* ctx, size_t bytes, void** out) {
   return GC_OK;
 }
 
-int slot_heads(gc_ctx* ctx, int64_t m_slots, uint32_t** out) {
-  if (m_slots > ctx->slot_head_n) {
+int slot_runs(gc_ctx* ctx, int64_t m_slots, void** out) {
+  if (m_slots > ctx->slot_runs_n) {
     GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
-    if (ctx->slot_head) GC_HIP(ctx, hipFree(ctx->slot_head));
-    ctx->slot_head = nullptr;
-    ctx->slot_head_n = 0;
-    GC_HIP(ctx, hipMalloc((void**)&ctx->slot_head, (size_t)m_slots * sizeof(uint32_t)));
-    ctx->slot_head_n = m_slots;
-    ctx->slot_head_dirty = true;
+    if (ctx->slot_runs) GC_HIP(ctx, hipFree(ctx->slot_runs));
+    ctx->slot_runs = nullptr;
+    ctx->slot_runs_n = 0;
+    GC_HIP(ctx, hipMalloc(&ctx->slot_runs, (size_t)m_slots * kSlotRunsBytes));
+    ctx->slot_runs_n = m_slots;
+    ctx->slot_runs_dirty = true;
   }
-  if (ctx->slot_head_dirty) {
-    GC_HIP(ctx, hipMemsetAsync(ctx->slot_head, 0xFF, (size_t)ctx->slot_head_n * sizeof(uint32_t), ctx->stream));
-    ctx->slot_head_dirty = false;
+  if (ctx->slot_runs_dirty) {
+    GC_HIP(ctx, hipMemsetAsync(ctx->slot_runs, 0, (size_t)ctx->slot_runs_n * kSlotRunsBytes, ctx->stream));
+    ctx->slot_runs_dirty = false;
   }
-  *out = ctx->slot_head;
+  *out = ctx->slot_runs;
   return GC_OK;
 }
 
@@ -122,6 +122,13 @@ int32_t gc_ctx_create(int32_t device, gc_ctx** out) {
     delete c;
     return GC_ERR_RUNTIME;
   }
+  e = gc::init_exp_table(c->stream);
+  if (e != hipSuccess) {
+    gc::set_error(nullptr, std::string("exp table: ") + hipGetErrorString(e));
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return GC_ERR_RUNTIME;
+  }
   *out = c;
   return GC_OK;
 }
@@ -131,7 +138,7 @@ int32_t gc_ctx_destroy(gc_ctx* ctx) {
   (void)hipSetDevice(ctx->device);
   (void)hipStreamSynchronize(ctx->stream);
   if (ctx->scratch) (void)hipFree(ctx->scratch);
-  if (ctx->slot_head) (void)hipFree(ctx->slot_head);
+  if (ctx->slot_runs) (void)hipFree(ctx->slot_runs);
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return GC_OK;

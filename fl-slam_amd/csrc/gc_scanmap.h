@@ -10,14 +10,16 @@ struct gc_ctx;
 namespace gc {
 
 // device work buffers of one pipeline's update (sized for n_cap rows): the sorted key of every block
-// position, the run links and run-piece sums (gc_runs.h), the touched-slot counter; the slot heads are
-// the context's (gc_ctx::slot_head)
+// position, each run's rank and overflow link, the run-piece sums (gc_runs.h), the apply launch's
+// per-workgroup touched-slot counts (summed on request); the per-slot run table is the context's
+// (gc_ctx::slot_runs)
 struct ScanMapWork {
   void* buf = nullptr;
   size_t bytes = 0;
-  uint32_t *sslot = nullptr, *run_next = nullptr;
+  uint32_t *sslot = nullptr, *run_next = nullptr, *rank = nullptr;
   double* pieces = nullptr;  // (n_cap, 16) the run sums, at each run's last block position
-  unsigned long long* count = nullptr;
+  uint32_t* wg_count = nullptr;
+  int64_t n_wg = 0;  // the apply launch's workgroups
   int64_t n_cap = 0, m_slots = 0;
 };
 
@@ -35,5 +37,7 @@ hipError_t launch_fuse_colors(const gc_primitive_map& map, double eps_mass, hipS
 int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_slots);
 int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_primitive_map& map,
                         const PipeDev& P, const ScanMapInput& in);
+// the touched-slot count of the last update (downloads the per-workgroup counts; synchronises ctx->stream)
+int32_t scan_map_count(gc_ctx* ctx, const ScanMapWork& W, int64_t* out, size_t* d2h_bytes);
 
 }  // namespace gc

@@ -14,10 +14,11 @@
 // from (before its own measurement-IW apply, as the reference's step 12b reads the scan's config) and the
 // row's weight the
 // deskewed point weight (a4). Its slot is the spatial hash of the world voxel of μ_w. The rows are
-// fused with responsibility 1 and source LiDAR by a reduce-by-key: a stable radix sort of (slot,
-// row) and a two-pass segmented reduction in a fixed order (k_smap_pieces / k_smap_apply:
-// bit-reproducible, within 1e-12 of np.add.at's sequential order), one thread per distinct slot
-// applying its sum. A scan's points crowd into few voxels
+// fused with responsibility 1 and source LiDAR by a deterministic reduce-by-key (gc_runs.h): each
+// 256-row block sorts its rows by slot in LDS and sums every run of one slot by a segmented scan
+// (k_smap_block), the runs are registered per slot, and one owner thread per distinct slot sums its runs
+// in block order and applies the sum (k_smap_apply): bit-reproducible, within 1e-12 of np.add.at's
+// sequential order. A scan's points crowd into few voxels
 // (~65k rows into ~5k slots, runs of thousands near the sensor), so rows are computed one per
 // thread and the runs reduced in parallel: one thread per run summing its rows serially took
 // ~1 ms per scan. LiDAR rows leave the camera accumulators unchanged,
@@ -27,6 +28,7 @@
 //
 // Every rank runs the update from the reduced record, so the maps stay bit-identical across ranks.
 #include <hip/hip_runtime.h>
+#include <vector>
 #include "gc_internal.h"
 #include "gc_math.h"
 #include "gc_mapslot.h"
@@ -143,33 +145,38 @@ GC_DEV void smap_row(const double* C, const double* o, double eps_mass, const do
 // into LDS; the block sorts (key, row) and sums each run of equal keys by a segmented inclusive scan
 // in sorted order (Hillis-Steele: a step adds the entry d back when it has the same key; the order
 // depends on the positions only); each run's last position holds the run's sum, written as the run's
-// piece and linked into its slot's list. A scan's points crowd into few voxels (~65k rows into ~5k
-// slots), so most of the work is this in-block reduction; the lists hold one piece per block.
+// piece and registered with its slot's entry. A scan's points crowd into few voxels (~65k rows into
+// ~5k slots), so most of the work is this in-block reduction; a slot gets at most one piece per block.
 constexpr int kSmapBlk = 256;
-__global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, uint32_t* head, uint32_t* sslot,
-                                                         uint32_t* run_next, SmapRow* pieces) {
+__global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, SlotRuns* T, uint32_t* sslot,
+                                                         uint32_t* run_next, uint32_t* rank, SmapRow* pieces) {
   __shared__ double C[kSmapC + 3];
   __shared__ double v[kSmapRow][kSmapBlk];
   __shared__ uint64_t a[kSmapBlk];
   const int t = threadIdx.x;
-  if (t == 0) {  // the scan's constants: R, tt, Rᵀ t, Σ_lidar, Σ_pose
+  // the scan's constants: Σ_pose and Σ_lidar by lanes of wave 0, R, tt and Rᵀ t by lane 0 of wave 1
+  if (t < 36) {
+    C[21 + t] = A.h0[6 + t];
+  } else if (t < 45) {
+    const double den = A.lidar_iw[0] + 3.0 + 1.0;  // measurement_noise_mean_jax, LiDAR block
+    C[12 + (t - 36)] = A.lidar_iw[1 + (t - 36)] / den;
+  } else if (t == 64) {
     double R[9], tt[3];
     smap_pose(A, R, tt);
     for (int q = 0; q < 9; ++q) C[q] = R[q];
     mat3_tvec(R, tt, C + 9);
-    const double den = A.lidar_iw[0] + 3.0 + 1.0;  // measurement_noise_mean_jax, LiDAR block
-    for (int q = 0; q < 9; ++q) C[12 + q] = A.lidar_iw[1 + q] / den;
-    for (int q = 0; q < 36; ++q) C[21 + q] = A.h0[6 + q];
     for (int q = 0; q < 3; ++q) C[kSmapC + q] = tt[q];
   }
-  __syncthreads();
+  // the row's point and its deskew (they need none of C) while thread 0 forms the constants
   const int64_t j = (int64_t)blockIdx.x * kSmapBlk + t;
   const int64_t M = A.map.m_slots;
-  double p0[3], w, mw[3];
+  double p0[3], w = 0.0, mw[3];
+  const bool live = j < A.n_cap && smap_point(A, j, p0, &w);
+  __syncthreads();
   SmapRow row;
   for (int q = 0; q < kSmapRow; ++q) row.v[q] = 0.0;
   uint32_t key = j < A.n_cap ? (uint32_t)M : kNoRun;
-  if (j < A.n_cap && smap_point(A, j, p0, &w)) {
+  if (live) {
     smap_world_mean(C, C + kSmapC, p0, mw);
     key = smap_slot(mw, A.voxel, M);
     const double o[3] = {A.o0, A.o1, A.o2};
@@ -197,50 +204,104 @@ __global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, uint32_t
     __syncthreads();
   }
   const int64_t p = (int64_t)blockIdx.x * kSmapBlk + t;
-  if (p < A.n_cap) sslot[p] = k_t;
   const bool tail = (int64_t)k_t < M && (t == kSmapBlk - 1 || (uint32_t)(a[t + 1] >> 32) != k_t);
+  uint32_t rk = kNoRun;
   if (tail) {
     SmapRow o;
     for (int q = 0; q < kSmapRow; ++q) o.v[q] = v[q][t];
     pieces[p] = o;
-    run_next[p] = atomicExch(&head[k_t], (uint32_t)p);
+    rk = register_run(T, k_t, (uint32_t)p, run_next);
+  }
+  if (p < A.n_cap) {
+    sslot[p] = k_t;
+    rank[p] = rk;
   }
 }
 
-// Pass 2, one thread per position: the owner of each slot (the run its list ends on) adds the slot's
-// pieces in block order and read-modify-writes the slot (the fuse with responsibility 1, source LiDAR)
-__global__ void __launch_bounds__(256) k_smap_apply(ScanMapArgs A, int64_t n, uint32_t* head,
-                                                    const uint32_t* __restrict__ sslot,
-                                                    const uint32_t* __restrict__ run_next,
-                                                    const SmapRow* __restrict__ pieces, unsigned long long* n_unique) {
+// Pass 2, one thread per position: the owner of each slot (its run of rank 0) adds the slot's pieces
+// in block order and read-modify-writes the slot (the fuse with responsibility 1, source LiDAR)
+__global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t n, SlotRuns* T,
+                                                         const uint32_t* __restrict__ sslot,
+                                                         const uint32_t* __restrict__ run_next,
+                                                         const uint32_t* __restrict__ rank,
+                                                         const SmapRow* __restrict__ pieces,
+                                                         uint32_t* wg_count) {
 #pragma clang fp contract(off)
+  __shared__ uint32_t slices[kApplyWG * kRunCap];
+  __shared__ double wave_sums[(kApplyWG / 64) * kSmapRow];
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t key = e < n ? sslot[e] : kNoRun;
-  const bool own = (int64_t)key < A.map.m_slots && head[key] == (uint32_t)e;  // not dropped, the owner
-  // the touched-slot count: one atomic per wave (one per owner would serialise thousands of atomics
-  // on one address)
+  const bool own = (int64_t)key < A.map.m_slots && rank[e] == 0u;  // not dropped, the owner
+  // the touched-slot count per workgroup (an LDS sum; thousands of global atomics on one counter
+  // serialised the kernel: ~20-40 us)
+  __shared__ uint32_t owned;
+  if (threadIdx.x == 0) owned = 0u;
+  __syncthreads();
   const unsigned long long b = __ballot(own);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(n_unique, (unsigned long long)__popcll(b));
-  if (!own) return;
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&owned, (uint32_t)__popcll(b));
+  __syncthreads();
+  if (threadIdx.x == 0) wg_count[blockIdx.x] = owned;
   SmapRow d;
   for (int q = 0; q < kSmapRow; ++q) d.v[q] = 0.0;
   const auto add = [&](uint32_t r) {
     const SmapRow pc = pieces[r];
     for (int q = 0; q < kSmapRow; ++q) d.v[q] = d.v[q] + pc.v[q];
   };
-  if (run_next[e] == kNoRun) {
-    add((uint32_t)e);
-  } else {
-    RunList<32> rl;
-    rl.collect((uint32_t)e, run_next, (int)((n + kSmapBlk - 1) / kSmapBlk));
-    uint32_t prev = 0;
-    for (int i = 0; i < rl.n; ++i) {
-      const uint32_t r = rl.at(i, (uint32_t)e, run_next, prev);
-      if (r == kNoRun) break;  // only a corrupt list: never index past the runs
-      prev = r;
-      add(r);
+  SlotRunList<kRunCap> rl(slices + threadIdx.x * kRunCap);
+  bool heavy = false;
+  if (own) {
+    if (T[key].cnt == 1u) {  // the slot's rows all lie in one block (the common case)
+      add((uint32_t)e);
+    } else {
+      rl.collect(T, key, run_next, (int)((n + kSmapBlk - 1) / kSmapBlk));
+      if (rl.spill) {  // more runs than a slice holds: correctness path, never at the C5 sizes
+        uint32_t prev = 0;
+        for (int i = 0; i < rl.n; ++i) {
+          const uint32_t r = rl.at(i, prev);
+          if (r == kNoRun) break;  // only a corrupt entry: never index past the runs
+          prev = r;
+          add(r);
+        }
+      } else if (rl.n <= 4) {
+        for (int i = 0; i < rl.n; ++i) add(rl.buf[i]);
+      } else {
+        heavy = true;
+      }
     }
   }
+  // slots of many runs (the voxels next to the sensor): the whole wave sums them, lane c < 16 the
+  // column c over the runs in block order (the same order and bits as one thread's), eight loads in
+  // flight per lane, one owner at a time
+  const int lane = threadIdx.x & 63;
+  double* wsum = wave_sums + (threadIdx.x >> 6) * kSmapRow;
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the owners' slices, then read by the wave
+  __builtin_amdgcn_wave_barrier();
+  for (unsigned long long hb = __ballot(heavy); hb; hb &= hb - 1) {
+    const int src = __ffsll((long long)hb) - 1;
+    const uint32_t* ids = slices + (threadIdx.x - lane + src) * kRunCap;
+    const int m = __shfl(rl.n, src);
+    if (lane < kSmapRow) {
+      const double* col = reinterpret_cast<const double*>(pieces) + lane;
+      double acc = 0.0;
+      int i = 0;
+      for (; i + 8 <= m; i += 8) {
+        double x[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) x[u] = col[(size_t)ids[i + u] * kSmapRow];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) acc = acc + x[u];
+      }
+      for (; i < m; ++i) acc = acc + col[(size_t)ids[i] * kSmapRow];
+      wsum[lane] = acc;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the sums in LDS, then read
+    __builtin_amdgcn_wave_barrier();
+    if (lane == src)
+      for (int q = 0; q < kSmapRow; ++q) d.v[q] = wsum[q];
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");  // the sums in LDS, then read
+    __builtin_amdgcn_wave_barrier();
+  }
+  if (!own) return;
   const int64_t s = key;
   const int L = A.map.n_lobes;
   for (int q = 0; q < 9; ++q) mLam(A.map, s)[q] = mLam(A.map, s)[q] + d.v[q];
@@ -253,7 +314,7 @@ __global__ void __launch_bounds__(256) k_smap_apply(ScanMapArgs A, int64_t n, ui
   mSup(A.map, s) = A.scan_seq;
   mUpd(A.map, s) = A.scan_seq;
   if (A.map.lidar_mass) mLid(A.map, s) = mLid(A.map, s) + d.v[15];
-  head[key] = kNoRun;  // the list is consumed
+  rl.clear(T, key);  // the entry is zero for the next call
 }
 
 }  // namespace
@@ -263,7 +324,8 @@ int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_s
   W->m_slots = m_slots;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t kv = up((size_t)n_cap * sizeof(uint32_t)), rv = up((size_t)n_cap * sizeof(SmapRow));
-  const size_t bytes = 2 * kv + rv + 256;
+  W->n_wg = (n_cap + kApplyWG - 1) / kApplyWG;
+  const size_t bytes = 3 * kv + rv + up((size_t)W->n_wg * sizeof(uint32_t));
   if (bytes > W->bytes) {
     if (W->buf) GC_HIP(ctx, hipFree(W->buf));
     W->buf = nullptr;
@@ -274,10 +336,11 @@ int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_s
   char* base = (char*)W->buf;
   W->sslot = (uint32_t*)base;
   W->run_next = (uint32_t*)(base + kv);
-  W->pieces = (double*)(base + 2 * kv);
-  W->count = (unsigned long long*)(base + 2 * kv + rv);
-  uint32_t* head = nullptr;
-  return slot_heads(ctx, m_slots, &head);  // allocated (and filled) now, outside any scan
+  W->rank = (uint32_t*)(base + 2 * kv);
+  W->pieces = (double*)(base + 3 * kv);
+  W->wg_count = (uint32_t*)(base + 3 * kv + rv);
+  void* T = nullptr;
+  return slot_runs(ctx, m_slots, &T);  // allocated (and zeroed) now, outside any scan
 }
 
 int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_primitive_map& map,
@@ -293,17 +356,28 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
   A.voxel = in.voxel; A.timestamp = in.timestamp; A.eps_mass = P.eps_mass;
   A.scan_seq = in.scan_seq;
   const int64_t n = P.n_cap;
-  uint32_t* head = nullptr;
-  if (int rc = slot_heads(ctx, map.m_slots, &head)) return rc;
-  GC_HIP(ctx, hipMemsetAsync(W->count, 0, sizeof(unsigned long long), st));
-  ctx->slot_head_dirty = true;  // until both passes are enqueued
-  hipLaunchKernelGGL(k_smap_block, dim3((unsigned)((n + kSmapBlk - 1) / kSmapBlk)), dim3(kSmapBlk), 0, st, A, head,
-                     W->sslot, W->run_next, (SmapRow*)W->pieces);
+  void* T = nullptr;
+  if (int rc = slot_runs(ctx, map.m_slots, &T)) return rc;
+  ctx->slot_runs_dirty = true;  // until both passes are enqueued
+  hipLaunchKernelGGL(k_smap_block, dim3((unsigned)((n + kSmapBlk - 1) / kSmapBlk)), dim3(kSmapBlk), 0, st, A,
+                     (SlotRuns*)T, W->sslot, W->run_next, W->rank, (SmapRow*)W->pieces);
   GC_LAUNCH_CHECK(ctx);
-  hipLaunchKernelGGL(k_smap_apply, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, A, n, head,
-                     (const uint32_t*)W->sslot, (const uint32_t*)W->run_next, (const SmapRow*)W->pieces, W->count);
+  hipLaunchKernelGGL(k_smap_apply, dim3((unsigned)((n + kApplyWG - 1) / kApplyWG)), dim3(kApplyWG), 0, st, A, n,
+                     (SlotRuns*)T, (const uint32_t*)W->sslot, (const uint32_t*)W->run_next,
+                     (const uint32_t*)W->rank, (const SmapRow*)W->pieces, W->wg_count);
   GC_LAUNCH_CHECK(ctx);
-  ctx->slot_head_dirty = false;
+  ctx->slot_runs_dirty = false;
+  return GC_OK;
+}
+
+int32_t scan_map_count(gc_ctx* ctx, const ScanMapWork& W, int64_t* out, size_t* d2h_bytes) {
+  std::vector<uint32_t> c((size_t)W.n_wg);
+  GC_HIP(ctx, hipMemcpyAsync(c.data(), W.wg_count, c.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
+  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  int64_t n = 0;
+  for (uint32_t v : c) n += v;
+  *out = n;
+  *d2h_bytes = c.size() * sizeof(uint32_t);
   return GC_OK;
 }
 
