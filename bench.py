@@ -619,7 +619,7 @@ def map_fuse_leg(ctx, _abi, m_slots=1 << 20, rows=1 << 17, reps=5, packed=True):
     return {"slots": M, "rows": K, "distinct_slots": n_unique, "ms": ms, "bytes": b,
             "GB/s": b / (ms * 1e-3) / 1e9, "bytes_all_slot_colour": b_all,
             "GB/s_all_slot_colour": b_all / (ms * 1e-3) / 1e9, "layout": "packed" if packed else "fields",
-            "kernel": "k_fuse_keys + radix sort + k_fuse_segments (colour estimate of the touched slots)"}
+            "kernel": "k_fuse_runs + k_fuse_apply (per-block LDS sort, per-slot run entries; colour estimate of the touched slots)"}
 
 
 def cpu_info():

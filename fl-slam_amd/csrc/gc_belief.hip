@@ -52,7 +52,7 @@ GC_DEV double inv_diag_from_chol(const double* C, int n, int j) {
 // Per hypothesis: predict (OU diffusion, 2 PSD projections), predicted moments, IMU soft
 // windows, parallel-scan preintegration (prefix products of the 512 Exp(ω dt) factors),
 // ξ_body = se3_log(Δpose), and the gyro/accel measurement-noise IW statistics.
-__global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
+GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   extern __shared__ double sm[];
   double* Lp = sm;
   double* W1 = Lp + N2;
@@ -247,14 +247,29 @@ __global__ void __launch_bounds__(256) k_predict_imu(PipeDev P, ScanArgs S) {
   }
 }
 
+// Two register budgets of the same kernel: OCC = 1 (the body's natural ~294 VGPRs, no spill) while
+// the grid fits one workgroup per CU; OCC = 2 (256 VGPRs, ~150 B of spill) when it does not, so the
+// a1 budget workgroups run beside the hypotheses instead of in a second round (at H = 256: 320
+// workgroups on 256 CUs).
+template <int OCC>
+__global__ void __launch_bounds__(256, OCC) k_predict_imu(PipeDev P, ScanArgs S) {
+  predict_imu_body(P, S);
+}
+
 static size_t lds_predict() {
   return sizeof(double) * (5 * N2 + 2 * N2 + 4 * kDZ + 6 * kDZ + 8 + 12 + 64 + 256 * 24);
 }
 
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  if (hipError_t e = ensure_dyn_lds((const void*)k_predict_imu, lds_predict())) return e;
   // P.Hl hypothesis workgroups + kBudgetBlocks a1 budget workgroups (S.w_raw, S.n_in)
-  hipLaunchKernelGGL(k_predict_imu, dim3(P.Hl + kBudgetBlocks), dim3(256), lds_predict(), st, P, S);
+  const unsigned grid = (unsigned)(P.Hl + kBudgetBlocks);
+  if ((int)grid > device_cu_count()) {
+    if (hipError_t e = ensure_dyn_lds((const void*)k_predict_imu<2>, lds_predict())) return e;
+    hipLaunchKernelGGL(k_predict_imu<2>, dim3(grid), dim3(256), lds_predict(), st, P, S);
+  } else {
+    if (hipError_t e = ensure_dyn_lds((const void*)k_predict_imu<1>, lds_predict())) return e;
+    hipLaunchKernelGGL(k_predict_imu<1>, dim3(grid), dim3(256), lds_predict(), st, P, S);
+  }
   return hipGetLastError();
 }
 

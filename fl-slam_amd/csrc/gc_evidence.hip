@@ -6,6 +6,7 @@
 #include "gc_pipe.h"
 #include "gc_wgla.h"
 #include "gc_opsdev.h"
+#include "gc_binfin.h"
 
 namespace gc {
 
@@ -44,7 +45,7 @@ GC_DEV double pose6_cond(double lmin, double lmax, double eps_psd, double* eigmi
   return mx / mn;
 }
 
-__global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
+GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
   extern __shared__ double sm[];
   double* Lpr = sm;          // L_pred
   double* Lev = Lpr + NN;    // L_raw -> L_ev
@@ -86,6 +87,28 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
     zl[t] = P.z[(int64_t)hl * n + t];
   }
   const double* st = P.stats + (int64_t)hl * B * 38;
+  if (S.fin_part) {
+    // the a6 finalize of this hypothesis folded in (scan_bins_pipeline, BinsFold): its chunk records
+    // summed in chunk order (the split kernel's sums, bit for bit) into the per-bin table's space,
+    // then one lane per bin; the split kernel's ticket is published here (the bins have completed)
+    if (hl == 0 && t == 0 && S.done_word)
+      __hip_atomic_store(S.done_word, S.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    const int RL = B * NF_BASE + REC_EXTRA;
+    finalize_reduce<4, 8>(S.fin_part + (int64_t)hl * S.fin_chunks * RL, RL, B * NF_BASE + 1, S.fin_chunks, tab);
+    __syncthreads();
+    if (t < B) {
+      double* ax = P.binaux + ((int64_t)hl * B + t) * 2;
+      finalize_bin(tab + t * NF_BASE, NF_BASE, P.eps_psd, eps, P.stats + ((int64_t)hl * B + t) * GC_BIN_STATS, ax,
+                   ax + 1);
+    } else if (t == 64) {
+      const double* ex = tab + B * NF_BASE;
+      double* c = P.bincert + (int64_t)hl * GC_BIN_CERT;
+      c[4] = ex[0] / (ex[3] + eps);
+      c[5] = ex[1];
+      c[6] = ex[2];
+    }
+    __syncthreads();  // the stats, aux and cert rows written above are read below (workgroup scope)
+  }
   // a6 certificate of the bins (binning.py:285-324): the cross-bin reductions of the split finalize's
   // per-bin terms, on wave 0 in k_bins_finalize's wave_sum order (lane b = bin b, B <= 64); thread 0
   // reads them back below (its own writes)
@@ -373,6 +396,12 @@ __global__ void __launch_bounds__(256) k_evidence(PipeDev P, ScanArgs S) {
   }
 }
 
+// one or two workgroups per CU, as k_predict_imu (gc_belief.hip): two only when H_l exceeds the CUs
+template <int OCC>
+__global__ void __launch_bounds__(256, OCC) k_evidence(PipeDev P, ScanArgs S) {
+  evidence_body(P, S);
+}
+
 // ==================================================================== a16 partial sums (local)
 // grid: ceil(P_len / 64) blocks x 256 threads; block covers 64 record entries, its 4 waves sum
 // interleaved hypothesis subsets, combined in fixed order (deterministic).
@@ -635,8 +664,13 @@ static hipError_t allow_big_lds(const void* fn, size_t bytes) {
   return bytes > 65536 ? ensure_dyn_lds(fn, bytes) : hipSuccess;
 }
 hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  if (hipError_t e = allow_big_lds((const void*)k_evidence, lds_evidence())) return e;
-  hipLaunchKernelGGL(k_evidence, dim3(P.Hl), dim3(256), lds_evidence(), st, P, S);
+  if (P.Hl > device_cu_count()) {
+    if (hipError_t e = allow_big_lds((const void*)k_evidence<2>, lds_evidence())) return e;
+    hipLaunchKernelGGL(k_evidence<2>, dim3(P.Hl), dim3(256), lds_evidence(), st, P, S);
+  } else {
+    if (hipError_t e = allow_big_lds((const void*)k_evidence<1>, lds_evidence())) return e;
+    hipLaunchKernelGGL(k_evidence<1>, dim3(P.Hl), dim3(256), lds_evidence(), st, P, S);
+  }
   return hipGetLastError();
 }
 hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {

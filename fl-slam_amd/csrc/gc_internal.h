@@ -34,6 +34,9 @@ int slot_runs(gc_ctx* ctx, int64_t m_slots, void** out);
 
 // the table exp's 2048-entry table in device memory (gc_points.hip), enqueued once per context
 hipError_t init_exp_table(hipStream_t st);
+
+// compute units of the current device (queried once per device id, cached)
+int device_cu_count();
 constexpr size_t kSlotRunsBytes = 256;
 
 // hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) only when fn has not yet been allowed that

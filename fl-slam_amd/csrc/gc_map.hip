@@ -107,9 +107,13 @@ GC_DEV void slot_colour(const gc_primitive_map& m, int64_t s, double cam, const 
   }
 }
 
-// ---- pass 1: per block of kFuseBlk rows, the (slot, row) sort and the run links (gc_runs.h)
-constexpr int kFuseBlk = 1024;
-__global__ void __launch_bounds__(256) k_fuse_runs(const int32_t* __restrict__ target, int64_t K, int64_t M,
+// ---- pass 1: per block of kFuseBlk rows (one per thread), the (slot, row) sort and the run entries
+// (gc_runs.h). 512-row blocks: 256 workgroups for a 131k-row fuse (1024-row blocks left half the CUs idle)
+#ifndef GC_FUSE_BLK
+#define GC_FUSE_BLK 512
+#endif
+constexpr int kFuseBlk = GC_FUSE_BLK;
+__global__ void __launch_bounds__(kFuseBlk) k_fuse_runs(const int32_t* __restrict__ target, int64_t K, int64_t M,
                                                    SlotRuns* T, uint32_t* sslot, uint32_t* order,
                                                    uint32_t* run_len, uint32_t* run_next, uint32_t* rank) {
   __shared__ uint64_t a[kFuseBlk];
@@ -373,7 +377,7 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   SlotRuns* T = (SlotRuns*)Tv;
   // from here a failed launch may leave entries set: the next call re-zeroes them
   ctx->slot_runs_dirty = true;
-  hipLaunchKernelGGL(k_fuse_runs, dim3((unsigned)((K + kFuseBlk - 1) / kFuseBlk)), dim3(256), 0, ctx->stream,
+  hipLaunchKernelGGL(k_fuse_runs, dim3((unsigned)((K + kFuseBlk - 1) / kFuseBlk)), dim3(kFuseBlk), 0, ctx->stream,
                      (const int32_t*)meas->target_slots, K, map->m_slots, T, sslot, order, run_len, run_next, rank);
   GC_LAUNCH_CHECK(ctx);
   const bool l3 = map->n_lobes == 3;  // GC_VMF_N_LOBES: the compile-time lobe count

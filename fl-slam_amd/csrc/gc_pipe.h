@@ -81,6 +81,12 @@ struct ScanArgs {
   int64_t n_in;                            // raw points of this scan
   const double* t_raw;                     // (n_in) raw point times (the window of P.w_win)
   int sig_cached;                          // P.Sig / P.mu_fin hold (P.L + εI)⁻¹ and its solve with P.h
+  // the a6 finalize folded into k_evidence (few chunk records per hypothesis, BinsFold): the bins
+  // launch's chunk records and count; null when the split finalize kernel ran
+  const double* fin_part;
+  int64_t fin_chunks;
+  int64_t* done_word;                      // with fin_part: the ticket published by k_evidence
+  int64_t ticket;
 };
 
 // dev instrumentation: -DGC_PHASE_TIMING records s_memtime at phase boundaries of workgroup wg
@@ -117,9 +123,15 @@ struct gc_ctx;
 namespace gc {
 // a1 -> a6 bins of the local hypotheses (+ the IMU/odom branch's workgroups in the same launch when
 // io) and their finalize into P.stats / P.bincert (gc_points.hip)
+// (done_word: `ticket` stored once the bins have completed). With fold non-null and few chunk records
+// per hypothesis the finalize is left to k_evidence: fold receives the records, and the evidence
+// launch publishes the ticket
+struct BinsFold {
+  const double* part = nullptr;
+  int64_t chunks = 0;
+};
 int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
                            const double* d_pts, const double* d_t, const double* d_w, int64_t n_in,
-                           int64_t* done_word = nullptr, int64_t ticket = 0);  // done_word: `ticket` stored
-                                                                                // once the bins have completed
+                           int64_t* done_word = nullptr, int64_t ticket = 0, BinsFold* fold = nullptr);
 
 }  // namespace gc

@@ -785,12 +785,18 @@ static int32_t scan_local_impl(gc_pipeline* p, int32_t slot, double scan_start, 
   // is attached): the next staging into it may proceed once the bins are done, which the finalize
   // kernel publishes as this scan's ticket (done_word)
   ++p->ticket;
-  GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in, p->smap_on ? nullptr : p->done_word,
-                                p->ticket));
+  gc::BinsFold fold;
+  int64_t* dw = p->smap_on ? nullptr : p->done_word;
+  GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in, dw, p->ticket, &fold));
+  gc::ScanArgs Se = S;  // the evidence launch's: with the finalize folded in, its records and the ticket
+  Se.fin_part = fold.part;
+  Se.fin_chunks = fold.chunks;
+  Se.done_word = fold.part ? dw : nullptr;
+  Se.ticket = p->ticket;
   if (!p->smap_on) s.consumed_ticket = p->ticket;
   GC_TRY(stage_event(p, 2));
   // a7 .. a15
-  GC_HIP(ctx, gc::launch_evidence(P, S, ctx->stream));
+  GC_HIP(ctx, gc::launch_evidence(P, Se, ctx->stream));
   p->sig_cached = true;
   if (p->inscan_certs) GC_HIP(ctx, gc::launch_hyp_certs(P, ctx->stream));
   p->hcond_scan = p->inscan_certs;

@@ -67,6 +67,17 @@ int scratch(gc_ctx* ctx, size_t bytes, void** out) {
   return GC_OK;
 }
 
+int device_cu_count() {
+  static int cache[64] = {0};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+  if (cache[dev] == 0) {
+    int cus = 0;
+    cache[dev] = (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) ? cus : 256;
+  }
+  return cache[dev];
+}
+
 int slot_runs(gc_ctx* ctx, int64_t m_slots, void** out) {
   if (m_slots > ctx->slot_runs_n) {
     GC_HIP(ctx, hipStreamSynchronize(ctx->stream));

@@ -143,8 +143,8 @@ GC_DEV void smap_row(const double* C, const double* o, double eps_mass, const do
 // Pass 1, one workgroup per block of kSmapBlk rows (gc_runs.h): every thread forms one row's slot key
 // (m_slots for a dropped row, sorted after every slot) and world row [Λ_w 9, θ_w 3, η_w lobe 0 3, w]
 // into LDS; the block sorts (key, row) and sums each run of equal keys by a segmented inclusive scan
-// in sorted order (Hillis-Steele: a step adds the entry d back when it has the same key; the order
-// depends on the positions only); each run's last position holds the run's sum, written as the run's
+// in sorted order (inside each wave by shuffles, then the carries across the waves in wave order; the
+// order depends on the positions only); each run's last position holds the run's sum, written as the run's
 // piece and registered with its slot's entry. A scan's points crowd into few voxels (~65k rows into
 // ~5k slots), so most of the work is this in-block reduction; a slot gets at most one piece per block.
 constexpr int kSmapBlk = 256;
@@ -153,6 +153,8 @@ __global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, SlotRuns
   __shared__ double C[kSmapC + 3];
   __shared__ double v[kSmapRow][kSmapBlk];
   __shared__ uint64_t a[kSmapBlk];
+  __shared__ double wave_tail[kSmapBlk / 64][kSmapRow];
+  __shared__ uint32_t wave_klast[kSmapBlk / 64], wave_kfirst[kSmapBlk / 64];
   const int t = threadIdx.x;
   // the scan's constants: Σ_pose and Σ_lidar by lanes of wave 0, R, tt and Rᵀ t by lane 0 of wave 1
   if (t < 36) {
@@ -191,24 +193,40 @@ __global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, SlotRuns
   const int src = (int)(uint32_t)a[t];
   double x[kSmapRow];
   for (int q = 0; q < kSmapRow; ++q) x[q] = v[q][src];
+  // the segmented inclusive scan, first inside each wave by shuffles (Hillis-Steele: a position adds
+  // the entry d back when that entry has its key; the keys are sorted, so that entry's segment is its)
+  const int lane = t & 63, wv = t >> 6;
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t kd = (uint32_t)__shfl_up((int)k_t, d, 64);
+    const bool take = lane >= d && kd == k_t;
+    for (int q = 0; q < kSmapRow; ++q) {
+      const double y = __shfl_up(x[q], d, 64);
+      if (take) x[q] = y + x[q];
+    }
+  }
+  // then across the waves: the running sum of the segment open at each wave's end, in wave order,
+  // enters the next wave's first segment (carry + partial)
+  if (lane == 63) {
+    for (int q = 0; q < kSmapRow; ++q) wave_tail[wv][q] = x[q];
+    wave_klast[wv] = k_t;
+  }
+  if (lane == 0) wave_kfirst[wv] = k_t;
   __syncthreads();
-  for (int q = 0; q < kSmapRow; ++q) v[q][t] = x[q];
-  __syncthreads();
-  for (int d = 1; d < kSmapBlk; d <<= 1) {
-    const bool take = t >= d && (uint32_t)(a[t - d] >> 32) == k_t;
-    double y[kSmapRow];
-    for (int q = 0; q < kSmapRow; ++q) y[q] = take ? v[q][t - d] : 0.0;
-    __syncthreads();
-    if (take)
-      for (int q = 0; q < kSmapRow; ++q) v[q][t] = y[q] + v[q][t];
-    __syncthreads();
+  if (wv > 0 && wave_klast[wv - 1] == wave_kfirst[wv] && k_t == wave_kfirst[wv]) {
+    double run[kSmapRow];
+    for (int q = 0; q < kSmapRow; ++q) run[q] = wave_tail[0][q];
+    for (int w = 1; w < wv; ++w) {
+      const bool cont = wave_klast[w - 1] == wave_kfirst[w] && wave_kfirst[w] == wave_klast[w];
+      for (int q = 0; q < kSmapRow; ++q) run[q] = cont ? run[q] + wave_tail[w][q] : wave_tail[w][q];
+    }
+    for (int q = 0; q < kSmapRow; ++q) x[q] = run[q] + x[q];
   }
   const int64_t p = (int64_t)blockIdx.x * kSmapBlk + t;
   const bool tail = (int64_t)k_t < M && (t == kSmapBlk - 1 || (uint32_t)(a[t + 1] >> 32) != k_t);
   uint32_t rk = kNoRun;
   if (tail) {
     SmapRow o;
-    for (int q = 0; q < kSmapRow; ++q) o.v[q] = v[q][t];
+    for (int q = 0; q < kSmapRow; ++q) o.v[q] = x[q];
     pieces[p] = o;
     rk = register_run(T, k_t, (uint32_t)p, run_next);
   }

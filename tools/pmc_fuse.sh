@@ -1,7 +1,7 @@
 #!/bin/bash
 # HBM traffic of the C5 PrimitiveMap kernels: the standalone 1M-slot fuse (bench.py --map-only:
-# k_fuse_keys, radix sort, k_fuse_segments, k_fuse_colors) and the in-scan map update
-# (bench.py --c5-only: k_smap_keys, radix sort, k_smap_segments), one rocprofv3 --pmc pass per
+# k_fuse_runs, k_fuse_apply, k_fuse_colors) and the in-scan map update (bench.py --c5-only:
+# k_smap_block, k_smap_apply), one rocprofv3 --pmc pass per
 # counter set; summarised by tools/pmc_fuse.py. Usage (GPU box): bash tools/pmc_fuse.sh r03
 set -e
 round=${1:-r03}
