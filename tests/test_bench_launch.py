@@ -45,3 +45,15 @@ def test_bench_rejects_gpus_world_size_mismatch():
                        timeout=120)
     assert r.returncode != 0
     assert "disagrees with WORLD_SIZE" in r.stderr
+
+
+def test_workload_labels_name_the_config():
+    """The bench line's config.workload names the BASELINE.json config it measures, and any other
+    --hyps by its own shape (round 3 labelled a 32-hypothesis run "C3")."""
+    sys.path.insert(0, ROOT)
+    import bench
+    assert bench.workload_label(256, 65536, 1) == "C3"
+    assert bench.workload_label(256, 65536, 8).startswith("C4")
+    assert bench.workload_label(1, 65536, 1) == "C2"
+    assert bench.workload_label(32, 65536, 1).startswith("H=32 (one rank's shard of C4 at N=8)")
+    assert bench.workload_label(100, 65536, 1) == "H=100, 65536 points"
