@@ -45,6 +45,7 @@ GC_DEV double pose6_cond(double lmin, double lmax, double eps_psd, double* eigmi
   return mx / mn;
 }
 
+template <bool FOLD>
 GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
   extern __shared__ double sm[];
   double* Lpr = sm;          // L_pred
@@ -87,7 +88,7 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     zl[t] = P.z[(int64_t)hl * n + t];
   }
   const double* st = P.stats + (int64_t)hl * B * 38;
-  if (S.fin_part) {
+  if constexpr (FOLD) {
     // the a6 finalize of this hypothesis folded in (scan_bins_pipeline, BinsFold): its chunk records
     // summed in chunk order (the split kernel's sums, bit for bit) into the per-bin table's space,
     // then one lane per bin; the split kernel's ticket is published here (the bins have completed)
@@ -396,10 +397,12 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
   }
 }
 
-// one or two workgroups per CU, as k_predict_imu (gc_belief.hip): two only when H_l exceeds the CUs
-template <int OCC>
+// one or two workgroups per CU, as k_predict_imu (gc_belief.hip): two only when H_l exceeds the CUs;
+// FOLD: the a6 finalize at the start (its own instantiation: compiled into the kernel without it,
+// the shard sizes that keep the split finalize ran 0.7 % slower)
+template <int OCC, bool FOLD>
 __global__ void __launch_bounds__(256, OCC) k_evidence(PipeDev P, ScanArgs S) {
-  evidence_body(P, S);
+  evidence_body<FOLD>(P, S);
 }
 
 // ==================================================================== a16 partial sums (local)
@@ -664,13 +667,20 @@ static hipError_t allow_big_lds(const void* fn, size_t bytes) {
   return bytes > 65536 ? ensure_dyn_lds(fn, bytes) : hipSuccess;
 }
 hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  if (P.Hl > device_cu_count()) {
-    if (hipError_t e = allow_big_lds((const void*)k_evidence<2>, lds_evidence())) return e;
-    hipLaunchKernelGGL(k_evidence<2>, dim3(P.Hl), dim3(256), lds_evidence(), st, P, S);
+  const bool two = P.Hl > device_cu_count(), fold = S.fin_part != nullptr;
+#define GC_EVL(OCC, FOLD)                                                                        \
+  do {                                                                                           \
+    if (hipError_t e = allow_big_lds((const void*)k_evidence<OCC, FOLD>, lds_evidence())) return e; \
+    hipLaunchKernelGGL((k_evidence<OCC, FOLD>), dim3(P.Hl), dim3(256), lds_evidence(), st, P, S);   \
+  } while (0)
+  if (two) {
+    if (fold) GC_EVL(2, true);
+    else GC_EVL(2, false);
   } else {
-    if (hipError_t e = allow_big_lds((const void*)k_evidence<1>, lds_evidence())) return e;
-    hipLaunchKernelGGL(k_evidence<1>, dim3(P.Hl), dim3(256), lds_evidence(), st, P, S);
+    if (fold) GC_EVL(1, true);
+    else GC_EVL(1, false);
   }
+#undef GC_EVL
   return hipGetLastError();
 }
 hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {

@@ -108,11 +108,9 @@ GC_DEV void slot_colour(const gc_primitive_map& m, int64_t s, double cam, const 
 }
 
 // ---- pass 1: per block of kFuseBlk rows (one per thread), the (slot, row) sort and the run entries
-// (gc_runs.h). 512-row blocks: 256 workgroups for a 131k-row fuse (1024-row blocks left half the CUs idle)
-#ifndef GC_FUSE_BLK
-#define GC_FUSE_BLK 512
-#endif
-constexpr int kFuseBlk = GC_FUSE_BLK;
+// (gc_runs.h). 512-row blocks: 256 workgroups for a 131k-row fuse; 1024-row blocks left half the CUs
+// idle (C5 fuse 0.081 -> 0.065 ms, profiles/r04/probe_soft_assign_store_only_and_fuse512.txt)
+constexpr int kFuseBlk = 512;
 __global__ void __launch_bounds__(kFuseBlk) k_fuse_runs(const int32_t* __restrict__ target, int64_t K, int64_t M,
                                                    SlotRuns* T, uint32_t* sslot, uint32_t* order,
                                                    uint32_t* run_len, uint32_t* run_next, uint32_t* rank) {

@@ -596,9 +596,6 @@ __global__ void __launch_bounds__(256, kSaOcc) k_soft_assign(int64_t n, int B, i
     const double ysc = inv_tau * kTab2OverLn2;
     const double nbs = -(best * ysc);
     double Z = 0.0, sl = 0.0;
-#ifdef GC_SA_PROBE_STORE_ONLY
-    Z = (double)NB + nbs * 1e-300;
-#else
 #pragma unroll
     for (int j0 = 0; j0 < NB; j0 += 8) {
       double y[8];
@@ -618,7 +615,6 @@ __global__ void __launch_bounds__(256, kSaOcc) k_soft_assign(int64_t n, int B, i
       }
       asm volatile("" : "+v"(Z), "+v"(sl));  // accumulate now: the y of a group die here
     }
-#endif
     sl *= kExp2C1;  // Σ e x in nats
     // the maximal bin has e = 1 (within an ulp): Z >= 1 and max_b R = 1/Z
     const double rZ = recip(Z);

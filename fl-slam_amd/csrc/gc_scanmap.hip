@@ -76,7 +76,9 @@ GC_DEV uint32_t smap_slot(const double* mw, double voxel, int64_t M) {
   const int64_t vx = (int64_t)floor(mw[0] / voxel), vy = (int64_t)floor(mw[1] / voxel),
                 vz = (int64_t)floor(mw[2] / voxel);
   const uint64_t h = ((uint64_t)vx * 73856093ull) ^ ((uint64_t)vy * 19349663ull) ^ ((uint64_t)vz * 83492791ull);
-  return (uint32_t)(h % (uint64_t)M);
+  // a power-of-two slot count (the C5 map's 2^20) takes the mask: the same key without the 64-bit
+  // software division
+  return (uint32_t)(((uint64_t)M & ((uint64_t)M - 1)) == 0 ? (h & ((uint64_t)M - 1)) : h % (uint64_t)M);
 }
 
 GC_DEV void smap_pose(const ScanMapArgs& A, double* R, double* tt) {
