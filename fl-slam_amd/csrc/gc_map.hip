@@ -229,7 +229,8 @@ __global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, 
 #pragma clang fp contract(off)
   constexpr int LM = LT > 0 ? LT : kMaxLobes;
   constexpr int NT = row_terms_len(LM);
-  const int64_t p = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t wgid = xcd_block(blockIdx.x, gridDim.x);  // a sort block's workgroups on one XCD
+  const int64_t p = wgid * blockDim.x + threadIdx.x;
   bool own = false;
   uint32_t s = 0;
   if (p < K) {

@@ -124,6 +124,18 @@ struct SlotRunList {
   }
 };
 
+// XCD-aware workgroup order: workgroups are dispatched round-robin over the 8 XCDs (each with its own
+// L2), so consecutive workgroup ids land on different XCDs. The apply kernels' workgroups that cover
+// one sort block read the same block's rows (in sorted, i.e. random row order): mapping the ids so
+// that the consecutive logical workgroups of one XCD take consecutive positions keeps a block's row
+// lines in one L2. A bijection on [0, 8 floor(n / 8)); the tail keeps its id.
+__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t n) {
+  constexpr int kXcd = 8;
+  const int64_t full = n / kXcd * kXcd;
+  if (b >= full) return b;
+  return (b % kXcd) * (full / kXcd) + b / kXcd;
+}
+
 // the apply kernels' workgroup and per-thread slice capacity: 128 x 64 x 4 B = 32 KB of LDS
 constexpr int kApplyWG = 128;
 constexpr int kRunCap = 64;
