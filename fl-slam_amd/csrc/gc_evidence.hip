@@ -2,6 +2,7 @@
 // statistics (a15), and the per-scan combine (a16) + IW apply + map update, as batched
 // one-workgroup-per-hypothesis kernels. See gc_belief.hip for the reference map.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 #include "gc_internal.h"
 #include "gc_pipe.h"
 #include "gc_wgla.h"
@@ -688,11 +689,12 @@ hipError_t launch_combine_local(const PipeDev& P, hipStream_t st) {
   hipLaunchKernelGGL(k_combine_local, dim3(nrec + npose), dim3(256), 0, st, P);
   return hipGetLastError();
 }
-hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
+hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st, hipEvent_t done) {
   if (hipError_t e = allow_big_lds((const void*)k_combine_final, lds_final())) return e;
   // workgroup 0: record reduction, barycenter, certificates; 1: map update + derive; 2: process IW
   // apply, Q; 3: measurement IW apply
-  hipLaunchKernelGGL(k_combine_final, dim3(4), dim3(256), lds_final(), st, P, S);
+  if (done) hipExtLaunchKernelGGL(k_combine_final, dim3(4), dim3(256), lds_final(), st, nullptr, done, 0, P, S);
+  else hipLaunchKernelGGL(k_combine_final, dim3(4), dim3(256), lds_final(), st, P, S);
   return hipGetLastError();
 }
 hipError_t launch_map_derive(const PipeDev& P, hipStream_t st) {

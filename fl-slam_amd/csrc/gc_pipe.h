@@ -112,7 +112,8 @@ hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, d
                                hipStream_t st);
 hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st);
 hipError_t launch_combine_local(const PipeDev& P, hipStream_t st);
-hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st);
+hipError_t launch_combine_final(const PipeDev& P, const ScanArgs& S, hipStream_t st,
+                                hipEvent_t done = nullptr);  // recorded at the launch's completion
 hipError_t launch_map_derive(const PipeDev& P, hipStream_t st);
 hipError_t launch_iw_Q(const PipeDev& P, hipStream_t st);
 // the per-hypothesis ConditioningCerts of L_pred and L_post into P.hcond (gc_certs.hip)
@@ -132,6 +133,7 @@ struct BinsFold {
 };
 int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
                            const double* d_pts, const double* d_t, const double* d_w, int64_t n_in,
-                           int64_t* done_word = nullptr, int64_t ticket = 0, BinsFold* fold = nullptr);
+                           int64_t* done_word = nullptr, int64_t ticket = 0, BinsFold* fold = nullptr,
+                           hipEvent_t done_ev = nullptr);  // recorded at the bins launch's completion
 
 }  // namespace gc

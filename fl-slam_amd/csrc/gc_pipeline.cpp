@@ -21,6 +21,13 @@ int32_t cloud_parse_on(gc_ctx* ctx, hipStream_t st, int32_t* flag, const uint8_t
                        uint8_t* d_ring_out, uint8_t* d_tag_out);
 }
 
+// the period (in scans) of the combine_final completion events the slot staging orders on (0: none,
+// every staging that must wait records an event on the compute stream; gc_pipeline::fin_ev)
+#ifndef GC_BIND_EVERY
+#define GC_BIND_EVERY 1
+#endif
+constexpr int64_t kBindEvery = GC_BIND_EVERY;
+
 struct gc_pipeline {
   gc_ctx* ctx = nullptr;
   gc::PipeDev P{};
@@ -54,6 +61,17 @@ struct gc_pipeline {
   // ~5 us gap before the next one; with three slots in rotation the word usually suffices.
   int64_t* done_word = nullptr;
   int64_t ticket = 0;
+  // Completion events carried by the combine_final launch of every kBindEvery-th scan (ticket), the
+  // newest two (hipExtLaunchKernelGGL's stop event: the kernel's own completion signal, no packet of
+  // its own): staging into a slot whose scan has not published its ticket waits on the earliest
+  // bound scan at or after it; with no bound scan far enough yet, `consumed` is recorded instead.
+  // A signalled completion costs the next kernel a ~5 us start gap, as the recorded event does, but
+  // the host then never enqueues into the compute stream at staging time: every scan bound gives
+  // the shortest step and a host max within ~1.1x the mean (period 2 lets the copy of a slot wait a
+  // scan too long at H = 256 with 3 slots, 1.195 -> 1.219 ms; profiles/r04/ab_slot_bind.txt)
+  hipEvent_t fin_ev[2] = {nullptr, nullptr};
+  int64_t fin_ticket[2] = {0, 0};
+  int64_t pending_ticket = 0;
   hipStream_t cstream = nullptr;  // ingest (copy) stream
   int io_mode = GC_IO_COMPUTED;
   gc_comm* comm = nullptr;
@@ -216,13 +234,22 @@ int slot_check_restage(gc_pipeline* p, int slot) {
 
 int slot_wait_consumed(gc_pipeline* p, gc_pipeline::Slot& s) {
   if (s.consumed_ticket > 0) {
-    if (__atomic_load_n(p->done_word, __ATOMIC_ACQUIRE) < s.consumed_ticket) {
-      // its bins may still be running: order the DMA after everything enqueued on the compute
-      // stream. This event costs a ~5 us gap before the next kernel; a host poll of the word instead
-      // removes the gap but the step gets slower (H = 32 0.2924 -> 0.2977 ms with 3 or 4 slots,
-      // H = 256 1.212 -> 1.221: profiles/r04/ab_slot_poll.txt)
-      GC_HIP(p->ctx, hipEventRecord(s.consumed, p->ctx->stream));
-      s.consumed_rec = true;
+    const int64_t k = s.consumed_ticket;
+    if (__atomic_load_n(p->done_word, __ATOMIC_ACQUIRE) < k) {
+      // its bins may still be running: order the DMA after the earliest enqueued scan >= k whose
+      // combine_final carries a completion event (fin_ev), or else after everything enqueued on the
+      // compute stream. (A host poll of the word instead costs more than the gap it removes: H = 32
+      // 0.2924 -> 0.2977 ms with 3 or 4 slots, H = 256 1.212 -> 1.221, profiles/r04/ab_slot_poll.txt;
+      // so does a stream wait on the word, whose blit kernel spins on a CU: profiles/r04/ab_slot_bind.txt)
+      int e = -1;
+      for (int i = 0; i < 2; ++i)
+        if (p->fin_ticket[i] >= k && (e < 0 || p->fin_ticket[i] < p->fin_ticket[e])) e = i;
+      if (e >= 0) {
+        GC_HIP(p->ctx, hipStreamWaitEvent(p->cstream, p->fin_ev[e], 0));
+      } else {
+        GC_HIP(p->ctx, hipEventRecord(s.consumed, p->ctx->stream));
+        s.consumed_rec = true;
+      }
     }
     s.consumed_ticket = 0;
   }
@@ -317,6 +344,9 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
     rc = GC_ERR_RUNTIME;
   }
   if (p->done_word) *p->done_word = 0;
+  for (hipEvent_t& e : p->fin_ev)
+    if (rc == GC_OK && hipEventCreateWithFlags(&e, hipEventDisableTiming | hipEventDisableSystemFence) != hipSuccess)
+      rc = GC_ERR_RUNTIME;
   if (rc == GC_OK && hipStreamCreateWithFlags(&p->cstream, hipStreamNonBlocking) != hipSuccess) {
     gc::set_error(ctx, "hipStreamCreateWithFlags failed for the ingest stream");
     rc = GC_ERR_RUNTIME;
@@ -343,7 +373,7 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
     for (hipEvent_t e : {s.ready, s.odom_done, s.consumed})
       if (e) (void)hipEventDestroy(e);
   }
-  for (hipEvent_t e : {p->x0, p->x1})
+  for (hipEvent_t e : {p->x0, p->x1, p->fin_ev[0], p->fin_ev[1]})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : p->st_ev)
     if (e) (void)hipEventDestroy(e);
@@ -654,7 +684,15 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
   }
   GC_TRY(stage_event(p, 5));
   p->pending = false;
-  GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream));
+  // every kBindEvery-th scan's combine_final carries a completion event for the slot staging
+  // (fin_ev; with a map attached the slots order on the map update instead)
+  hipEvent_t fin = nullptr;
+  if (kBindEvery > 0 && !p->smap_on && p->pending_ticket > 0 && p->pending_ticket % kBindEvery == 0) {
+    const int e = (int)((p->pending_ticket / kBindEvery) & 1);
+    fin = p->fin_ev[e];
+    p->fin_ticket[e] = p->pending_ticket;
+  }
+  GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream, fin));
   GC_TRY(stage_event(p, 6));
   if (p->smap_on) {
     auto& s = p->slots[p->pending_slot];
@@ -794,6 +832,7 @@ static int32_t scan_local_impl(gc_pipeline* p, int32_t slot, double scan_start, 
   Se.done_word = fold.part ? dw : nullptr;
   Se.ticket = p->ticket;
   if (!p->smap_on) s.consumed_ticket = p->ticket;
+  p->pending_ticket = p->ticket;
   GC_TRY(stage_event(p, 2));
   // a7 .. a15
   GC_HIP(ctx, gc::launch_evidence(P, Se, ctx->stream));
