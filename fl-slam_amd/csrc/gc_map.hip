@@ -109,23 +109,27 @@ GC_DEV void slot_colour(const gc_primitive_map& m, int64_t s, double cam, const 
 
 // ---- pass 1: per block of kFuseBlk rows (one per thread), the (slot, row) sort and the run entries
 // (gc_runs.h). 512-row blocks: 256 workgroups for a 131k-row fuse; 1024-row blocks left half the CUs
-// idle (C5 fuse 0.081 -> 0.065 ms, profiles/r04/probe_soft_assign_store_only_and_fuse512.txt)
+// idle (C5 fuse 0.081 -> 0.065 ms, profiles/r04/probe_soft_assign_store_only_and_fuse512.txt). The
+// sort keeps one key per thread in a register (reg_bitonic_sort): 0.062 -> 0.054 ms against the
+// all-LDS network, 256- and 512-row blocks alike (profiles/r04/ab_fuse_regsort.txt)
 constexpr int kFuseBlk = 512;
 __global__ void __launch_bounds__(kFuseBlk) k_fuse_runs(const int32_t* __restrict__ target, int64_t K, int64_t M,
                                                    SlotRuns* T, uint32_t* sslot, uint32_t* order,
                                                    uint32_t* run_len, uint32_t* run_next, uint32_t* rank) {
   __shared__ uint64_t a[kFuseBlk];
   const int64_t base = (int64_t)blockIdx.x * kFuseBlk;
-  for (int i = threadIdx.x; i < kFuseBlk; i += blockDim.x) {
+  {
+    const int i = threadIdx.x;
     const int64_t k = base + i;
     uint32_t key = kNoRun;  // padding past K sorts last
     if (k < K) {
       const int32_t sl = target[k];
       key = (sl >= 0 && (int64_t)sl < M) ? (uint32_t)sl : (uint32_t)M;  // out of range: dropped (JAX scatter)
     }
-    a[i] = ((uint64_t)key << 32) | (uint32_t)i;
+    const uint64_t x = reg_bitonic_sort<kFuseBlk>(((uint64_t)key << 32) | (uint32_t)i, a);
+    a[i] = x;  // the sort ended with a barrier after its last read of a
+    __syncthreads();
   }
-  lds_bitonic_sort<kFuseBlk>(a);
   for (int i = threadIdx.x; i < kFuseBlk; i += blockDim.x) {
     const int64_t p = base + i;
     if (p >= K) break;

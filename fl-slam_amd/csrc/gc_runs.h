@@ -2,7 +2,7 @@
 //
 // K rows each target one of M map slots; the rows of a slot must be summed in a fixed order and the
 // slot read-modify-written once. Instead of a global radix sort of (slot, row):
-//  1. each workgroup sorts its own block of rows by (slot, local row) in LDS (bitonic), so a slot's
+//  1. each workgroup sorts its own block of rows by (slot, local row) (bitonic, reg_bitonic_sort), so a slot's
 //     rows in the block form one contiguous run, and registers the run with its slot's entry of the
 //     per-slot table (register_run): rank = atomicAdd(&cnt, 1), the run's position stored inline at
 //     that rank (the first kInlRuns runs) or linked into the entry's overflow list;
@@ -20,26 +20,34 @@ namespace gc {
 
 constexpr uint32_t kNoRun = 0xFFFFFFFFu;
 
-// ascending bitonic sort of N (power of two) 64-bit keys in LDS by the whole workgroup; ends synchronised
+// ascending bitonic sort of N (power of two) 64-bit keys, one per thread (N == blockDim.x), held in a register:
+// the compare-exchange stages between lanes of one wave (j < 64, 39 of a 512-key sort's 45) are
+// register shuffles with no workgroup barrier; only the stages across waves go through LDS (a[N]).
+// Returns the thread's key of the sorted order (sorted position = threadIdx.x); a is scratch.
 template <int N>
-__device__ __forceinline__ void lds_bitonic_sort(uint64_t* a) {
-  __syncthreads();
+__device__ __forceinline__ uint64_t reg_bitonic_sort(uint64_t x, uint64_t* a) {
+  const int i = threadIdx.x;
+#pragma unroll
   for (int k = 2; k <= N; k <<= 1) {
+#pragma unroll
     for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = threadIdx.x; i < N; i += blockDim.x) {
-        const int l = i ^ j;
-        if (l > i) {
-          const uint64_t x = a[i], y = a[l];
-          const bool up = (i & k) == 0;
-          if ((x > y) == up) {
-            a[i] = y;
-            a[l] = x;
-          }
-        }
+      uint64_t y;
+      if (j >= 64) {
+        a[i] = x;
+        __syncthreads();
+        y = a[i ^ j];
+        __syncthreads();
+      } else {
+        const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)x, j);
+        const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(x >> 32), j);
+        y = ((uint64_t)hi << 32) | lo;
       }
-      __syncthreads();
+      // the lower element of a pair keeps the minimum in an ascending block, the maximum otherwise
+      const bool take_min = ((i & j) == 0) == ((i & k) == 0);
+      x = take_min ? (x < y ? x : y) : (x < y ? y : x);
     }
   }
+  return x;
 }
 
 constexpr int kInlRuns = 62;

@@ -188,8 +188,11 @@ __global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, SlotRuns
     row.v[15] = w;
   }
   for (int q = 0; q < kSmapRow; ++q) v[q][t] = row.v[q];
-  a[t] = ((uint64_t)key << 32) | (uint32_t)t;
-  lds_bitonic_sort<kSmapBlk>(a);
+  {
+    const uint64_t sx = reg_bitonic_sort<kSmapBlk>(((uint64_t)key << 32) | (uint32_t)t, a);
+    a[t] = sx;  // the sort ended with a barrier after its last read of a
+    __syncthreads();
+  }
   // position t of the sorted block: its row's values, then the segmented scan in sorted order
   const uint32_t k_t = (uint32_t)(a[t] >> 32);
   const int src = (int)(uint32_t)a[t];
