@@ -52,6 +52,21 @@ GC_DEV double inv_diag_from_chol(const double* C, int n, int j) {
 // Per hypothesis: predict (OU diffusion, 2 PSD projections), predicted moments, IMU soft
 // windows, parallel-scan preintegration (prefix products of the 512 Exp(ω dt) factors),
 // ξ_body = se3_log(Δpose), and the gyro/accel measurement-noise IW statistics.
+// a4's per-point time window (deskew_constant_twist.py:61-68) depends on the point only, not on the
+// hypothesis: the selected points' w x window once per scan, read by every hypothesis's bins task
+// (k_bins_io) in place of the raw weight (the budget's mass scale is applied there). Points j = first
+// kWG + t, stepping by step workgroups.
+GC_DEV double window_point(const ScanArgs& S, int64_t j, int64_t n_sel, double w, double tr) {
+  const double denom = fmax(S.t1 - S.t0, 1e-12);
+  return j < n_sel ? w * window_weight(tr, S.t0, S.t1, 0.1 * denom) : 0.0;
+}
+GC_DEV void window_points(const PipeDev& P, const ScanArgs& S, int64_t first, int64_t step) {
+  const int64_t stride = budget_stride(S.n_in, P.n_cap), n_sel = (S.n_in + stride - 1) / stride;
+  for (int64_t j = first * kWG + threadIdx.x; j < P.n_cap; j += step * kWG)
+    P.w_win[j] = j < n_sel ? window_point(S, j, n_sel, S.w_raw[j * stride], S.t_raw[j * stride]) : 0.0;
+}
+
+template <int OCC>
 GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   extern __shared__ double sm[];
   double* Lp = sm;
@@ -73,26 +88,16 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   const int t = threadIdx.x;
   const int n = kDZ;
   if (h >= P.Hl) {
-    // a1 budget statistics (point_budget.py:60-113) on kBudgetBlocks extra workgroups of this
-    // grid: they only read the staged weights, so they run beside the hypotheses' chains with no
-    // second stream. The last workgroup to arrive (agent-scope acq_rel ticket) sums the partials
-    // in block order — the same fixed order as k_budget_final — and re-arms the ticket.
+    // kBudgetBlocks extra workgroups when they fit beside the hypotheses (launch_predict_imu): the a1
+    // budget statistics (point_budget.py:60-113; they only read the staged weights) and the window of
+    // the points. The last workgroup to arrive (agent-scope acq_rel ticket) sums the partials in
+    // block order, the same fixed order as k_budget_final, and re-arms the ticket. The first re-arms
+    // k_bins_io's task counter for this scan's bins launch (next on the stream).
     const int b = h - P.Hl;
-    // re-arm k_bins_io's task counter for this scan's bins launch (next on the stream)
     if (b == 0 && t == 0) P.task_ctr[0] = 0u;
     const int64_t stride = budget_stride(S.n_in, P.n_cap);
     budget_partial_block(S.w_raw, S.n_in, stride, b, P.budget_part, sm);
-    // a4's per-point time window (deskew_constant_twist.py:61-68) depends on the point only, not
-    // on the hypothesis: the selected points' w x window once per scan here, read by every
-    // hypothesis's bins task (k_bins_io) in place of the raw weight (the budget's mass scale is
-    // applied there)
-    {
-      const int64_t n_sel = (S.n_in + stride - 1) / stride;
-      const double denom = fmax(S.t1 - S.t0, 1e-12);
-      for (int64_t j = (int64_t)b * kWG + t; j < P.n_cap; j += (int64_t)kBudgetBlocks * kWG)
-        P.w_win[j] = j < n_sel ? S.w_raw[j * stride] * window_weight(S.t_raw[j * stride], S.t0, S.t1, 0.1 * denom)
-                               : 0.0;
-    }
+    window_points(P, S, b, kBudgetBlocks);
     if (t == 0) {
       const unsigned prev =
           __hip_atomic_fetch_add(P.budget_ticket, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
@@ -102,6 +107,23 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
       }
     }
     return;
+  }
+  // otherwise the hypothesis workgroups take the window's points themselves: at one occupancy the
+  // first kWinPre of this thread's points are loaded here, beside the belief, and written at the end
+  const bool win_extra = (int)gridDim.x > P.Hl, win_here = !win_extra;
+  if (win_here && h == 0 && t == 0) P.task_ctr[0] = 0u;
+  // without the budget workgroups the scalars were formed at staging (S.budget): copied for the
+  // kernels after this one (the slot may be restaged once the bins are done, before evidence reads them)
+  if (!win_extra && h == 0 && t < 8) P.budget[t] = S.budget[t];
+  constexpr int kWinPre = OCC == 1 ? 2 : 0;
+  const int64_t w_stride = budget_stride(S.n_in, P.n_cap), w_sel = (S.n_in + w_stride - 1) / w_stride;
+  double pw[kWinPre > 0 ? kWinPre : 1], pt[kWinPre > 0 ? kWinPre : 1];
+#pragma unroll
+  for (int k = 0; k < kWinPre; ++k) {
+    const int64_t j = ((int64_t)h + (int64_t)k * P.Hl) * kWG + t;
+    const bool in = win_here && j < w_sel;
+    pw[k] = in ? S.w_raw[j * w_stride] : 0.0;
+    pt[k] = in ? S.t_raw[j * w_stride] : 0.0;
   }
   double* hprev = vec;
   double* mu_prev = vec + kDZ;
@@ -245,25 +267,40 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
     io[0] = ess_scan; io[1] = sigma_warp; io[2] = dt_imu;
     io[3] = om[0]; io[4] = om[1]; io[5] = om[2]; io[6] = 0.0; io[7] = 0.0;
   }
+  if (win_here) {
+#pragma unroll
+    for (int k = 0; k < kWinPre; ++k) {
+      const int64_t j = ((int64_t)h + (int64_t)k * P.Hl) * kWG + t;
+      if (j < P.n_cap) P.w_win[j] = window_point(S, j, w_sel, pw[k], pt[k]);
+    }
+    window_points(P, S, (int64_t)h + (int64_t)kWinPre * P.Hl, P.Hl);  // the rest, if any
+  }
 }
 
 // Two register budgets of the same kernel: OCC = 1 (the body's natural ~294 VGPRs, no spill) while
-// the grid fits one workgroup per CU; OCC = 2 (256 VGPRs, ~150 B of spill) when it does not, so the
-// a1 budget workgroups run beside the hypotheses instead of in a second round (at H = 256: 320
-// workgroups on 256 CUs).
+// the hypotheses fit one workgroup per CU; OCC = 2 (256 VGPRs, ~150 B of spill) when they do not
+// (C5's 1024). With the a1 budget formed at staging, H = 256 runs at OCC = 1 (its predict had been
+// OCC = 2 beside 64 budget workgroups, 320 on 256 CUs: 46 -> ~41 us).
 template <int OCC>
 __global__ void __launch_bounds__(256, OCC) k_predict_imu(PipeDev P, ScanArgs S) {
-  predict_imu_body(P, S);
+  predict_imu_body<OCC>(P, S);
 }
 
 static size_t lds_predict() {
   return sizeof(double) * (5 * N2 + 2 * N2 + 4 * kDZ + 6 * kDZ + 8 + 12 + 64 + 256 * 24);
 }
 
+bool predict_budget_inline(int Hl) { return Hl + kBudgetBlocks <= device_cu_count(); }
+
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  // P.Hl hypothesis workgroups + kBudgetBlocks a1 budget workgroups (S.w_raw, S.n_in)
-  const unsigned grid = (unsigned)(P.Hl + kBudgetBlocks);
-  if ((int)grid > device_cu_count()) {
+  // P.Hl hypothesis workgroups + kBudgetBlocks budget / window workgroups when they all fit one round
+  // (they then run beside the hypotheses for free); otherwise the budget scalars were formed when the
+  // slot was staged (S.budget, predict_budget_inline) and the hypotheses' workgroups form the window
+  const bool extra = predict_budget_inline(P.Hl);
+  if (!extra && !S.budget) return hipErrorInvalidValue;
+  const unsigned grid = (unsigned)(P.Hl + (extra ? kBudgetBlocks : 0));
+  const int cus = device_cu_count();
+  if ((int)grid > cus) {
     if (hipError_t e = ensure_dyn_lds((const void*)k_predict_imu<2>, lds_predict())) return e;
     hipLaunchKernelGGL(k_predict_imu<2>, dim3(grid), dim3(256), lds_predict(), st, P, S);
   } else {

@@ -61,12 +61,13 @@ struct PipeDev {
   double *nu_proc, *Psi_proc, *nu_meas, *Psi_meas;  // (7), (7,36), (3), (3,9)
   double *lidar_iw;                        // [ν_2, Ψ_2 (9)]: the scan's measurement-IW LiDAR block before its
                                            // IW apply (k_combine_final wg 3), read by the in-scan map update
-  double *budget;                          // 8 budget scalars
-  double *budget_part;                     // (64, 3) a1 partials, written by predict's extra workgroups
-  unsigned *budget_ticket;                 // arrival counter of those workgroups (reset by the last)
+  double *budget;                          // the scan's 8 a1 budget scalars: formed by the predict launch's
+                                           // extra workgroups, or copied there from S.budget
+  double *budget_part;                     // (64, 3) a1 partials of those workgroups
+  unsigned *budget_ticket;                 // their arrival counter (reset by the last)
   unsigned *task_ctr;                      // k_bins_io task counter (zeroed by the predict launch)
-  double *w_win;                           // (n_cap) selected points' w x time window, written by predict's
-                                           // budget workgroups (per point, shared by every hypothesis)
+  double *w_win;                           // (n_cap) selected points' w x time window, written by the predict
+                                           // launch (per point, shared by every hypothesis)
   double *send, *gather;                   // (P), (G, P)
   int G;                                   // ranks
   double *comb;                            // combined belief: L 484, h 22, z 22, X 6, stamp, cert 16
@@ -77,8 +78,10 @@ struct ScanArgs {
   const double *imu_t, *imu_g, *imu_a;     // (M), (M,3), (M,3)
   double t0, t1, t_last, t_scan, dt;
   double w_process;                        // min(1, scan_count)
-  const double* w_raw;                     // (n_in) raw point weights (a1 budget, fused into predict)
+  const double* w_raw;                     // (n_in) raw point weights
   int64_t n_in;                            // raw points of this scan
+  const double* budget;                    // (8) the a1 budget scalars of w_raw when they were formed at
+                                           // staging (the slot's, !predict_budget_inline); read through P.budget
   const double* t_raw;                     // (n_in) raw point times (the window of P.w_win)
   int sig_cached;                          // P.Sig / P.mu_fin hold (P.L + εI)⁻¹ and its solve with P.h
   // the a6 finalize folded into k_evidence (few chunk records per hypothesis, BinsFold): the bins
@@ -107,6 +110,9 @@ struct ScanArgs {
 
 // launchers (gc_belief.hip)
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st);
+// the predict launch forms the a1 budget itself (its extra workgroups fit beside Hl hypotheses);
+// otherwise the staging must (S.budget)
+bool predict_budget_inline(int Hl);
 // a1 budget scalars into out (8) with 3 x 64 partials in part (gc_points.hip)
 hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, double* part, double* out,
                                hipStream_t st);
@@ -133,7 +139,6 @@ struct BinsFold {
 };
 int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
                            const double* d_pts, const double* d_t, const double* d_w, int64_t n_in,
-                           int64_t* done_word = nullptr, int64_t ticket = 0, BinsFold* fold = nullptr,
-                           hipEvent_t done_ev = nullptr);  // recorded at the bins launch's completion
+                           int64_t* done_word = nullptr, int64_t ticket = 0, BinsFold* fold = nullptr);
 
 }  // namespace gc

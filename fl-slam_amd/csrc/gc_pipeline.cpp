@@ -41,6 +41,7 @@ struct gc_pipeline {
     double* host = nullptr;  // pinned mirror of dev (same layout)
     double *pts = nullptr, *t = nullptr, *w = nullptr, *imu_t = nullptr, *imu_g = nullptr, *imu_a = nullptr;
     double* odom = nullptr;
+    double *budget = nullptr, *bpart = nullptr;  // the staged scan's a1 budget scalars and partials
     bool has_odom = false;
     uint8_t *bytes = nullptr, *hbytes = nullptr, *ring = nullptr, *tag = nullptr;  // PointCloud2 staging
     int32_t* flag = nullptr;  // device word of the parse's seconds / nanoseconds test
@@ -61,6 +62,7 @@ struct gc_pipeline {
   // ~5 us gap before the next one; with three slots in rotation the word usually suffices.
   int64_t* done_word = nullptr;
   int64_t ticket = 0;
+  bool stage_budget = false;  // the a1 budget is formed at staging (gc::predict_budget_inline false)
   // Completion events carried by the combine_final launch of every kBindEvery-th scan (ticket), the
   // newest two (hipExtLaunchKernelGGL's stop event: the kernel's own completion signal, no packet of
   // its own): staging into a slot whose scan has not published its ticket waits on the earliest
@@ -191,12 +193,15 @@ int stage_event(gc_pipeline* p, int i) {
   return GC_OK;
 }
 
-// slot block layout (doubles): pts 3n | t n | w n | imu_t M | imu_g 3M | imu_a 3M | odom
+// slot block layout (doubles): pts 3n | t n | w n | imu_t M | imu_g 3M | imu_a 3M | odom | a1 budget
+// scalars 8 | their 3 x 64 partials (written on the device at staging; the pinned mirror's copy of
+// this tail is unused)
 struct SlotLayout {
-  size_t t, w, imu, odom, len;
+  size_t t, w, imu, odom, budget, bpart, len;
   explicit SlotLayout(const gc::PipeDev& P) {
     const size_t n = (size_t)P.n_in, M = (size_t)P.M;
-    t = 3 * n; w = 4 * n; imu = 5 * n; odom = imu + 7 * M; len = odom + gc::kOdomLen;
+    t = 3 * n; w = 4 * n; imu = 5 * n; odom = imu + 7 * M; budget = odom + gc::kOdomLen;
+    bpart = budget + 8; len = bpart + 3 * gc::kBudgetBlocks;
   }
 };
 
@@ -214,6 +219,8 @@ int slot_alloc(gc_pipeline* p, gc_pipeline::Slot& s) {
   s.pts = s.dev; s.t = s.dev + Ly.t; s.w = s.dev + Ly.w;
   s.imu_t = s.dev + Ly.imu; s.imu_g = s.imu_t + p->P.M; s.imu_a = s.imu_g + 3 * p->P.M;
   s.odom = s.dev + Ly.odom;
+  s.budget = s.dev + Ly.budget;
+  s.bpart = s.dev + Ly.bpart;
   return GC_OK;
 }
 
@@ -255,6 +262,17 @@ int slot_wait_consumed(gc_pipeline* p, gc_pipeline::Slot& s) {
   }
   if (s.consumed_rec) GC_HIP(p->ctx, hipStreamWaitEvent(p->cstream, s.consumed, 0));
   s.consumed_rec = false;
+  return GC_OK;
+}
+
+// a1 budget scalars of the staged weights (point_budget.py:60-113), on the copy stream after them, when
+// the predict launch has no room for its budget workgroups beside the hypotheses (stage_budget): they
+// depend on the scan's weights and sizes only, so that launch is left its hypotheses (and the window
+// of the points, which needs the scan window). H = 256: predict 46 -> ~41 us, 1.2010 -> 1.1984 ms per
+// scan; at H = 32 the budget workgroups run beside the hypotheses for free and stay there (staged,
+// 0.2873 -> 0.2890: profiles/r04/ab_staged_budget.txt)
+int slot_budget(gc_pipeline* p, gc_pipeline::Slot& s, int64_t n_in) {
+  if (p->stage_budget) GC_HIP(p->ctx, gc::launch_budget_stats(s.w, n_in, p->P.n_cap, s.bpart, s.budget, p->cstream));
   return GC_OK;
 }
 
@@ -334,6 +352,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   double* ticket = nullptr;
   if (rc == GC_OK) rc = dalloc(p, 1, &ticket);  // zeroed: the predict grid's budget arrival counter
   P.budget_ticket = reinterpret_cast<unsigned*>(ticket);
+  p->stage_budget = !gc::predict_budget_inline(Hl);
   double* ctr = nullptr;
   if (rc == GC_OK) rc = dalloc(p, 1, &ctr);  // zeroed: k_bins_io's task counter + finished pullers
   P.task_ctr = reinterpret_cast<unsigned*>(ctr);
@@ -551,6 +570,7 @@ static int32_t gc_pipeline_stage_scan_impl(gc_pipeline* p, int32_t slot, const d
     GC_HIP(p->ctx, hipMemcpyAsync(s.w, s.host + Ly.w, n * sizeof(double), k, p->cstream));
     GC_HIP(p->ctx, hipMemcpyAsync(s.imu_t, s.host + Ly.imu, 7 * M * sizeof(double), k, p->cstream));
   }
+  GC_TRY(slot_budget(p, s, n_in));
   GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));
   p->hs[GC_HS_H2D_BYTES] += (double)((5 * n + 7 * M) * sizeof(double));
   s.ready_rec = true;
@@ -606,6 +626,7 @@ static int32_t gc_pipeline_stage_pointcloud2_impl(gc_pipeline* p, int32_t slot, 
   GC_HIP(p->ctx, hipMemcpyAsync(s.bytes, s.hbytes, nb, hipMemcpyHostToDevice, p->cstream));
   GC_TRY(gc::cloud_parse_on(p->ctx, p->cstream, s.flag, s.bytes, n_points, point_step, h_fields, header_stamp, h_R9,
                             h_t3, s.pts, s.t, s.w, s.ring, s.tag));
+  GC_TRY(slot_budget(p, s, n_points));
   GC_HIP(p->ctx, hipMemcpyAsync(s.imu_t, s.host + SlotLayout(p->P).imu, 7 * (size_t)p->P.M * sizeof(double),
                                 hipMemcpyHostToDevice, p->cstream));
   GC_HIP(p->ctx, hipEventRecord(s.ready, p->cstream));
@@ -808,11 +829,11 @@ static int32_t scan_local_impl(gc_pipeline* p, int32_t slot, double scan_start, 
   // scan or more ahead of the device and the copy (ordered after an earlier scan's bins) long done
   if (s.ready_rec) GC_TRY(wait_event(p, s.ready));
   gc::ScanArgs S{s.imu_t, s.imu_g, s.imu_a, scan_start, scan_end, t_last, t_scan, dt_sec,
-                 scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in, s.t, p->sig_cached ? 1 : 0};
+                 scan_count >= 1 ? 1.0 : 0.0, s.w, s.n_in, p->stage_budget ? s.budget : nullptr, s.t, p->sig_cached ? 1 : 0};
   gc::PipeDev& P = p->P;
   const bool io = p->io_mode == GC_IO_COMPUTED;
-  // a1 budget scalars (the fused kernel reads the selection / mass scale from them) on extra
-  // workgroups of the predict grid; a2 + a3
+  // a2 + a3 (and the points' time window; the a1 budget scalars the fused kernel reads the
+  // selection / mass scale from were formed when the slot was staged)
   GC_TRY(stage_event(p, 0));
   GC_HIP(ctx, gc::launch_predict_imu(P, S, ctx->stream));
   GC_TRY(stage_event(p, 1));

@@ -12,7 +12,6 @@
 // record per (hypothesis, chunk). A finalize kernel sums the records in chunk order, so every
 // result is bit-reproducible run to run (no float atomics anywhere).
 #include <hip/hip_runtime.h>
-#include <hip/hip_ext.h>
 #include <algorithm>
 #include <cstdint>
 #include <type_traits>
@@ -1633,7 +1632,7 @@ namespace gc {
 // workgroups in the same launch when io (k_bins_io), then the chunk-order finalize.
 int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, const double* d_odom, bool io,
                            const double* d_pts, const double* d_t, const double* d_w, int64_t n_in,
-                           int64_t* done_word, int64_t ticket, BinsFold* fold, hipEvent_t done_ev) {
+                           int64_t* done_word, int64_t ticket, BinsFold* fold) {
   (void)n_in;
   if (ctx->cu_count == 0) {
     int cus = 0;
@@ -1680,12 +1679,8 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
 #define GC_BIO(BP, FULL)                                                                                       \
   GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_bins_io<BP, FULL>, sh));                                      \
   if (int rc_ = gc::ensure_no_static_lds(ctx, (const void*)k_bins_io<BP, FULL>)) return rc_;                  \
-  if (done_ev)                                                                                                 \
-    hipExtLaunchKernelGGL((k_bins_io<BP, FULL>), grid, dim3(256), sh, ctx->stream, nullptr, done_ev, 0, FA, P, S,   \
-                          d_odom, n_io, H, chunks, P.task_ctr);                                                    \
-  else                                                                                                         \
-    hipLaunchKernelGGL((k_bins_io<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA, P, S, d_odom, n_io, H, chunks, \
-                       P.task_ctr)
+  hipLaunchKernelGGL((k_bins_io<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA, P, S, d_odom, n_io, H, chunks, \
+                     P.task_ctr)
   const int bpl = bpl_for(B);
   const bool full = B == 16 * bpl;
   switch (bpl) {
