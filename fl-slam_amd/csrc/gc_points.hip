@@ -956,10 +956,13 @@ struct FusedArgs {
   double inv_tau, o0, o1, o2;
   double* partials;      // (H, chunks, RL) records
   const double* w_win;   // (n_cap) selected w x time window (the pipeline's predict), or NULL: per task
-  // two chunk tiers: chunks [0, k1) hold iters x 256 points, the rest iters_s x 256 (the persistent
-  // form ends on short tasks, so the pullers finish together); grid form: k1 = chunks, iters_s = iters
+  // three chunk tiers: chunks [0, k1) hold iters x 256 points, the next k2 iters_s x 256, the rest
+  // iters_t x 256 (the persistent form ends on ever shorter tasks, so the pullers finish together);
+  // grid form: k1 = chunks
   int64_t k1;
   int iters_s;
+  int64_t k2;
+  int iters_t;
 };
 constexpr int kFusedNS = NF_BASE + 4;  // feature slab rows: 19 features + d(3) + valid flag
 // dynamic LDS of a fused workgroup (doubles): 4 wave slabs | exp table | scaled bins | epilogue
@@ -986,7 +989,8 @@ GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
 // One task: hypothesis h, chunk c (its points: the tiers of FusedArgs) of the budgeted scan,
 // its partial record written to rec. Ends with the workgroup synchronised (LDS free for the next task).
 template <int BPL, bool FULL, bool PRE>
-GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec) {
+GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec, unsigned* ctr = nullptr,
+                      unsigned* next = nullptr) {
   constexpr int NF = NF_BASE;
   // features 0..8 and 10..16 on the matrix core, 17..18 on the VALU; feature 9 (w d_z²) is the trace
   // complement N − w d_x² − w d_y² (write_partial_record_mfma<.., 9>): one VALU feature fewer per step
@@ -995,9 +999,11 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   constexpr int NS = kFusedNS;
   const int64_t n_cap = A.n_cap;
   const int B = A.B;
-  const bool big = c < A.k1;
-  const int iters = big ? A.iters : A.iters_s;
-  const int64_t chunk0 = big ? c * A.iters * 256 : (A.k1 * A.iters + (c - A.k1) * A.iters_s) * 256;
+  const bool big = c < A.k1, mid = !big && c < A.k1 + A.k2;
+  const int iters = big ? A.iters : (mid ? A.iters_s : A.iters_t);
+  const int64_t chunk0 = big ? c * A.iters * 256
+                             : (mid ? (A.k1 * A.iters + (c - A.k1) * A.iters_s) * 256
+                                    : (A.k1 * A.iters + A.k2 * A.iters_s + (c - A.k1 - A.k2) * A.iters_t) * 256);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, bl = lane & 15;
   const int fcol = bl >= DF ? bl + 1 : bl;  // the feature of this lane's MFMA column
@@ -1152,6 +1158,9 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
     if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
+  // persistent form: the workgroup's next task ticket, taken here so that its round trip overlaps
+  // the epilogue (and the ticket is held only that long, not for a whole task)
+  if (ctr && threadIdx.x == 0) *next = atomicAdd(ctr, 1u);
   write_partial_record_mfma<BPL, NX, DF>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec);
   __syncthreads();  // the epilogue's LDS reads are done before the next task writes the slabs
 }
@@ -1165,21 +1174,45 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
 // device and shard size: the chunk geometry follows the CU count and H_l). ctr[0] is the task
 // counter; the predict launch that precedes every k_bins_io on the stream zeroes it, so a launch
 // never depends on how the previous one ended. No workgroup waits on another.
+#ifdef GC_BINS_TIMING
+// dev instrumentation: per workgroup of the last k_bins_io launch [start, prologue end, end, tasks] in
+// device real-time ticks (100 MHz, one clock for every XCD); tasks = -1 for a branch workgroup
+__device__ double g_bins_trace[4 * 8192];
+__device__ double g_task_trace[4 * 16384];  // per task [start, end, puller, XCD id]
+#define GC_BT_NOW() ((double)__builtin_amdgcn_s_memrealtime())
+#endif
 template <int BPL, bool FULL>
 __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
                                                              const double* __restrict__ odom, int n_io, int H,
                                                              int64_t chunks, unsigned* ctr) {
   extern __shared__ double lds[];
   unsigned& task_s = *reinterpret_cast<unsigned*>(lds + fused_lds_doubles(A.B));  // the launch's extra double
+#ifdef GC_BINS_TIMING
+  const double bt0 = GC_BT_NOW();
+  double bt1 = bt0;
+  int bt_n = 0;
+#endif
   if ((int)blockIdx.x < n_io) {
     io_branch_wg(P, S, odom, blockIdx.x, lds);
+#ifdef GC_BINS_TIMING
+    if (threadIdx.x == 0 && blockIdx.x < 8192) {
+      double* g = g_bins_trace + 4 * blockIdx.x;
+      g[0] = bt0; g[1] = bt0; g[2] = GC_BT_NOW(); g[3] = -1.0;
+    }
+#endif
     return;
   }
   bins_prologue(A, lds);
+#ifdef GC_BINS_TIMING
+  bt1 = GC_BT_NOW();
+#endif
   const int RL = A.B * NF_BASE + REC_EXTRA;
   const unsigned T = (unsigned)(H * chunks);
-  // the next task's ticket is taken at the start of the current one, so the atomic's round trip
-  // overlaps the task (bins_task ends with a barrier: task_s is read by all before it is rewritten)
+  // the next task's ticket is taken inside the current task before its epilogue, so the atomic's
+  // round trip overlaps the epilogue (bins_task ends with a barrier: task_s is read by all before it
+  // is rewritten). Taken at the start of the task instead, a ticket was held for the whole task: at
+  // the end of the launch a workgroup pairing a long task with another on its CU (each then runs at
+  // half speed) started its reserved one ~180 us late (GC_BINS_TIMING task traces)
   unsigned next = 0;
   if (threadIdx.x == 0) next = atomicAdd(ctr, 1u);
   for (;;) {
@@ -1187,12 +1220,29 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
     __syncthreads();
     const unsigned t = task_s;
     if (t >= T) break;
-    if (threadIdx.x == 0) next = atomicAdd(ctr, 1u);
     // chunk-major: the workgroups in flight share a chunk's raw points across hypotheses (L2)
     const int64_t c = t / H;
     const int h = t % H;
-    bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL);
+#ifdef GC_BINS_TIMING
+    const double tt0 = GC_BT_NOW();
+#endif
+    bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &next);
+#ifdef GC_BINS_TIMING
+    ++bt_n;
+    if (threadIdx.x == 0 && t < 16384) {
+      unsigned xcc = 0;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      double* g = g_task_trace + 4 * t;
+      g[0] = tt0; g[1] = GC_BT_NOW(); g[2] = (double)blockIdx.x; g[3] = (double)(xcc & 0xf);
+    }
+#endif
   }
+#ifdef GC_BINS_TIMING
+  if (threadIdx.x == 0 && blockIdx.x < 8192) {
+    double* g = g_bins_trace + 4 * blockIdx.x;
+    g[0] = bt0; g[1] = bt1; g[2] = GC_BT_NOW(); g[3] = (double)bt_n;
+  }
+#endif
 }
 
 // Grid form (the gc_scan_bins_fused entry): grid (chunks, H), one task per workgroup.
@@ -1608,7 +1658,8 @@ int32_t gc_scan_bins_fused(gc_ctx* ctx, int32_t H, int64_t n_in, int64_t n_cap, 
   const size_t sh = sizeof(double) * fused_lds_doubles(B);
   dim3 grid((unsigned)chunks, H);
   const FusedArgs FA{n_cap, B, iters, d_points_raw, d_t_raw, d_w_raw, d_budget_scalars, t0, t1, d_xi, d_bins,
-                     1.0 / tau, h_origin3[0], h_origin3[1], h_origin3[2], (double*)scr, nullptr, chunks, iters};
+                     1.0 / tau, h_origin3[0], h_origin3[1], h_origin3[2], (double*)scr, nullptr, chunks, iters,
+                     0, iters};
 #define GC_FUSED(BP, FULL)                                                                                     \
   GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_bins_fused<BP, FULL>, sh));                                   \
   if (int rc_ = gc::ensure_no_static_lds(ctx, (const void*)k_bins_fused<BP, FULL>)) return rc_;               \
@@ -1654,23 +1705,34 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   int iters = 16;
   while (iters > 2 && (int64_t)Hg * U < kBinsMinTasks * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
   constexpr int kShortDiv = 2;
+  constexpr int kTinyDiv = 4, kTinyPerPuller = 1;
   // short tasks of half a long one, at least 2 iterations: H = 256 8-iteration short tasks (interleaved
   // A/B on one box, 1.2499/1.2463 ms/scan with 4 -> 1.2377/1.2391 with 8); H = 32 (4-iteration long
   // tasks) 2, which stays best there (0.3013/0.3004/0.3003 ms against 0.305-0.313 for 8-iteration long
   // tasks with 2- or 4-iteration short ones and for 4-iteration tasks only; tools/ab32.sh)
   const int kItersShort = std::max(2, iters / kShortDiv);
+  // a third tier of tiny tasks (a quarter of a short one) at the very end, about one per puller: with
+  // the next ticket taken before each task's epilogue (k_bins_io) the pullers' end spread fell from
+  // 57 to ~24 us at H = 256 (GC_BINS_TIMING traces); interleaved A/B against the two tiers and the
+  // ticket taken at the task start, 1.1999 -> 1.1950 ms at H = 256, 0.2930 -> 0.2903 at H = 32
+  // (profiles/r04/ab_bins_tail.txt; 2 tiny tasks per puller, or an eighth or a half of a short task,
+  // no better)
+  const int kItersTiny = std::max(1, kItersShort / kTinyDiv);
+  int64_t Ut = ((int64_t)pullers * kItersTiny * kTinyPerPuller + Hg - 1) / Hg;
+  Ut = std::min<int64_t>((Ut + kItersTiny - 1) / kItersTiny * kItersTiny, U);
   int64_t Us = std::max<int64_t>(iters, ((int64_t)pullers * iters + Hg - 1) / Hg);
-  Us = std::min(Us, U);
-  const int64_t k1 = (U - Us) / iters;  // long chunks; the short tier takes the rest
-  Us = U - k1 * iters;
-  const int64_t chunks = k1 + (Us + kItersShort - 1) / kItersShort;
+  Us = std::min(Us, U - Ut);
+  const int64_t k1 = (U - Ut - Us) / iters;  // long chunks; the short and tiny tiers take the rest
+  const int64_t k2 = (U - Ut - k1 * iters) / kItersShort;
+  Ut = U - k1 * iters - k2 * kItersShort;
+  const int64_t chunks = k1 + k2 + (Ut + kItersTiny - 1) / kItersTiny;
   GC_CHECK_ARG(ctx, (int64_t)H * chunks < (int64_t)0xFFFFFFFF, "too many bin tasks");
   const int NF = NF_BASE;
   const int RL = B * NF + REC_EXTRA;
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
   const FusedArgs FA{P.n_cap, B, iters, d_pts, d_t, d_w, P.budget, S.t0, S.t1, P.xi, P.bins, 1.0 / P.tau,
-                     P.o0, P.o1, P.o2, (double*)scr, P.w_win, k1, kItersShort};
+                     P.o0, P.o1, P.o2, (double*)scr, P.w_win, k1, kItersShort, k2, kItersTiny};
   const int n_io = io ? H : 0;
   // + 1: the pullers' task slot after the fused layout (no static LDS in k_bins_io: the dynamic block
   // starts at LDS address 0, so the exp table's addresses need no base add, exp2s_shift_tab_n)
@@ -1706,6 +1768,20 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
 }  // namespace gc
 
 extern "C" {
+
+#ifdef GC_BINS_TIMING
+// dev: the last k_bins_io launch's per-workgroup trace (4 doubles each) into h_out
+int32_t gc_dev_bins_trace(double* h_out, int64_t n_wg) {
+  if (n_wg < 0 || n_wg > 8192) return GC_ERR_RUNTIME;
+  return hipMemcpyFromSymbol(h_out, HIP_SYMBOL(gc::g_bins_trace), sizeof(double) * 4 * n_wg) == hipSuccess
+             ? GC_OK : GC_ERR_RUNTIME;
+}
+int32_t gc_dev_task_trace(double* h_out, int64_t n_tasks) {
+  if (n_tasks < 0 || n_tasks > 16384) return GC_ERR_RUNTIME;
+  return hipMemcpyFromSymbol(h_out, HIP_SYMBOL(gc::g_task_trace), sizeof(double) * 4 * n_tasks) == hipSuccess
+             ? GC_OK : GC_ERR_RUNTIME;
+}
+#endif
 
 int32_t gc_kappa_from_resultant_batch(gc_ctx* ctx, int64_t n, const double* d_R, double eps_r, double d,
                                       double r0, double tau, double* d_kappa_out) {
