@@ -432,7 +432,7 @@ def measured_traffic(H, n, B):
     return None
 
 
-def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=8):
+def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=8, warm_s=0.3):
     """BinSoftAssign + ScanBinMomentMatch contract kernels over H hypotheses, HBM-bound."""
     from gcslam.constants import GC_TAU_SOFT_ASSIGN
     dxi = _abi.DeviceArray.from_host(ctx, xi)
@@ -458,11 +458,18 @@ def roofline_leg(ctx, _abi, s, d, xi, dbins, B, n, H, origin, reps=10, warm=8):
         ev[2 * r + 2].record()
 
     ev = [_abi.Event(ctx) for _ in range(2 * reps + 1)]
-    for r in range(warm):
-        _abi.call("gc_bin_soft_assign", ctx.handle, H, n, B, dirs.ptr, dbins.ptr, GC_TAU_SOFT_ASSIGN, resp.ptr,
-                  idx.ptr, sac.ptr, ctx=ctx)
-        _abi.call("gc_scan_bin_moment_match", ctx.handle, H, n, B, pts.ptr, covs.ptr, w.ptr, resp.ptr, lam.ptr, op,
-                  1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
+    # warm pairs for at least warm_s of sustained load: the host-side set-up above leaves the GPU idle
+    # long enough for its clocks to drop, and 8 pairs (~23 ms) did not always ramp them back (a box
+    # measured the soft-assign at 1.52 ms here and 1.39 in the same command under rocprofv3)
+    t_w, done = time.perf_counter(), 0
+    while done < warm or time.perf_counter() - t_w < warm_s:
+        for _ in range(4):
+            _abi.call("gc_bin_soft_assign", ctx.handle, H, n, B, dirs.ptr, dbins.ptr, GC_TAU_SOFT_ASSIGN, resp.ptr,
+                      idx.ptr, sac.ptr, ctx=ctx)
+            _abi.call("gc_scan_bin_moment_match", ctx.handle, H, n, B, pts.ptr, covs.ptr, w.ptr, resp.ptr, lam.ptr,
+                      op, 1e-12, 1e-12, st.ptr, ce.ptr, ctx=ctx)
+        done += 4
+        ctx.sync()
     ev[0].record()
     for r in range(reps):
         pair(r)
