@@ -96,7 +96,9 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     if (hl == 0 && t == 0 && S.done_word)
       __hip_atomic_store(S.done_word, S.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int RL = B * NF_BASE + REC_EXTRA;
-    finalize_reduce<4, 8>(S.fin_part + (int64_t)hl * S.fin_chunks * RL, RL, B * NF_BASE + 1, S.fin_chunks, tab);
+    // 11 chunks per batch: the 21-22 chunk records of C5 / H = 256 in two L2 round trips (8: three;
+    // the same order and bits, 1.1897 -> 1.1890 ms at H = 256, tools/r4_ab_slots.sh)
+    finalize_reduce<4, 11>(S.fin_part + (int64_t)hl * S.fin_chunks * RL, RL, B * NF_BASE + 1, S.fin_chunks, tab);
     __syncthreads();
     if (t < B) {
       double* ax = P.binaux + ((int64_t)hl * B + t) * 2;

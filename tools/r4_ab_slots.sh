@@ -4,7 +4,7 @@
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 reps=$1; shift; cfgs=$1
 o=gpurun_out/r4/ab_slots; rm -rf $o; mkdir -p $o
-for H in 32 256; do
+for H in ${HS:-32 256}; do
   for r in $(seq $reps); do
     for c in $cfgs; do
       v=${c%%:*}; sl=${c##*:}
