@@ -33,6 +33,49 @@ GC_DEV void mf_bin_row(double sN, const double* s_dir, double mN, const double* 
 }
 // SVD, det-sign fix, R_mf = U Vᵀ, L = V diag(s1+s2, s0+s2, s0+s1) Vᵀ, δ = log(R_predᵀ R_mf),
 // PSD(L), h = L δ (matrix_fisher_evidence.py:206-262).
+// The two halves of mf_finalize, so the planar rows (which need only R_mf) can start while the
+// information half runs on another wave: mf_rotation writes R_mf to out[0:9], the singular values to
+// out[24:27] and V to Vout (9); mf_information reads them and writes the rest of the record.
+GC_DEV void mf_rotation(const double* acc, double* out, double* Vout) {
+  double U[9], s3[3], V[9];
+  svd3(acc, U, s3, V);
+  double UVt[9];
+  mat3_mul_nt(U, V, UVt);
+  const double dsg = det3(UVt);
+  const double sgn = (dsg > 0.0) ? 1.0 : ((dsg < 0.0) ? -1.0 : 0.0);
+  for (int k = 0; k < 3; ++k) U[3 * k + 2] *= sgn;
+  double Rmf[9];
+  mat3_mul_nt(U, V, Rmf);
+  for (int k = 0; k < 9; ++k) { out[k] = Rmf[k]; Vout[k] = V[k]; }
+  for (int k = 0; k < 3; ++k) out[24 + k] = s3[k];
+}
+GC_DEV void mf_information(const double* acc, const double* Rp, const double* Vin, double eps, double eps_psd,
+                           double* out) {
+  double s3[3], V[9], Rmf[9];
+  for (int k = 0; k < 9; ++k) { V[k] = Vin[k]; Rmf[k] = out[k]; }
+  for (int k = 0; k < 3; ++k) s3[k] = out[24 + k];
+  const double ld[3] = {s3[1] + s3[2], s3[0] + s3[2], s3[0] + s3[1]};
+  double Lr[9];
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j)
+      Lr[3 * i + j] = V[3 * i] * ld[0] * V[3 * j] + V[3 * i + 1] * ld[1] * V[3 * j + 1] +
+                      V[3 * i + 2] * ld[2] * V[3 * j + 2];
+  double Rerr[9], dl[3], Lrot[9], cc[6];
+  mat3_mul_tn(Rp, Rmf, Rerr);
+  so3_log(Rerr, dl);
+  psd_project3_fast(Lr, eps_psd, Lrot, cc);
+  double hr[3];
+  mat3_vec(Lrot, dl, hr);
+  const double Neff = acc[9];
+  const double nll = 0.5 * (dl[0] * hr[0] + dl[1] * hr[1] + dl[2] * hr[2]);
+  for (int k = 0; k < 9; ++k) out[9 + k] = Lrot[k];
+  for (int k = 0; k < 3; ++k) { out[18 + k] = hr[k]; out[21 + k] = dl[k]; }
+  out[27] = Neff;
+  out[28] = nll / (Neff + eps);
+  out[29] = cc[0];
+  out[30] = cc[0] + eps / (Neff + eps);  // trigger: psd Δ + mass-ε ratio
+  out[31] = nll;
+}
 GC_DEV void mf_finalize(const double* acc, const double* Rp, double eps, double eps_psd, double* out) {
   double U[9], s3[3], V[9];
   svd3(acc, U, s3, V);
