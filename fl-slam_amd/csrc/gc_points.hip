@@ -1701,9 +1701,13 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   // same for every shard size)
   const int64_t U = (P.n_cap + 255) / 256;  // 256-point units per hypothesis
   const int Hg = P.geom_H > 0 ? P.geom_H : H;
-  constexpr int kBinsMinTasks = 3;
+  // >= 2 long tasks per puller: with the late ticket and the tiny tier (below) the tail no longer
+  // needs a third, and fewer, longer tasks amortise each task's set-up and record epilogue: H = 32
+  // 4 -> 8 iterations, 92 -> 62 chunks, 0.2892 -> 0.2800 ms/scan (3 tasks: 0.2892, 1: 0.2848;
+  // profiles/r04/ab_bins_tail.txt); H >= 64 keep 16
+  constexpr int kBinsMinTasks = 2;
   int iters = 16;
-  while (iters > 2 && (int64_t)Hg * U < kBinsMinTasks * (int64_t)pullers * iters) iters >>= 1;  // >= 3 long tasks per puller
+  while (iters > 2 && (int64_t)Hg * U < kBinsMinTasks * (int64_t)pullers * iters) iters >>= 1;
   constexpr int kShortDiv = 2;
   constexpr int kTinyDiv = 4, kTinyPerPuller = 1;
   // short tasks of half a long one, at least 2 iterations: H = 256 8-iteration short tasks (interleaved
