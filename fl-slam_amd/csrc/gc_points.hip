@@ -1706,7 +1706,9 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   // 4 -> 8 iterations, 92 -> 62 chunks, 0.2892 -> 0.2800 ms/scan (3 tasks: 0.2892, 1: 0.2848;
   // profiles/r04/ab_bins_tail.txt); H >= 64 keep 16
   constexpr int kBinsMinTasks = 2;
-  int iters = 16;
+  // at most 32 iterations (8192 points) per long task: H = 256 1.1935 -> 1.1803 ms, H = 128 0.6706 ->
+  // 0.6658 against 16; 64: 1.1872 (profiles/r04/ab_bins_tail.txt)
+  int iters = 32;
   while (iters > 2 && (int64_t)Hg * U < kBinsMinTasks * (int64_t)pullers * iters) iters >>= 1;
   constexpr int kShortDiv = 2;
   constexpr int kTinyDiv = 4, kTinyPerPuller = 1;
