@@ -67,6 +67,10 @@ def parse():
                     help="scan slots in the ingest rotation (the slot staged at step k was last read by scan k - slots + 1)")
     ap.add_argument("--dry-run", action="store_true",
                     help="launch the ranks and exchange the communicator id, then exit (no GPU work)")
+    ap.add_argument("--wait-timeout-s", type=float, default=120.0,
+                    help="fail-fast bound (s) of every host wait: libgcslam's device waits (a timeout aborts "
+                         "the RCCL communicator) and the gloo harness collectives; the bench then exits non-zero")
+    ap.add_argument("--fail-rank", type=int, default=-1, help=argparse.SUPPRESS)  # test: this rank exits early
     return ap.parse_args()
 
 
@@ -115,14 +119,17 @@ class Dist:
     """Host-side barrier / max-over-ranks for the bench harness (gloo); product collectives
     run in libgcslam over RCCL."""
 
-    def __init__(self, n):
+    def __init__(self, n, timeout_s=120.0):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local_rank = int(os.environ.get("LOCAL_RANK", "0"))
         self.pg = None
         if self.world > 1:
+            import datetime
             import torch.distributed as td
-            td.init_process_group("gloo")
+            # bounded: a rank whose peer died leaves its barrier / max with an error (gloo sees the closed
+            # connection at once, or the timeout) instead of waiting out gloo's 30-minute default
+            td.init_process_group("gloo", timeout=datetime.timedelta(seconds=timeout_s))
             self.td = td
 
     def barrier(self):
@@ -195,7 +202,9 @@ def main():
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if world_env != args.gpus:
         raise SystemExit(f"bench.py: --gpus {args.gpus} disagrees with WORLD_SIZE={world_env}")
-    dist = Dist(args.gpus)
+    dist = Dist(args.gpus, args.wait_timeout_s)
+    if args.fail_rank == dist.rank:  # test of the fail-fast path: this rank dies before the id exchange
+        os._exit(3)
     if args.dry_run:
         return dry_run(dist)
     from gcslam import _abi
@@ -205,6 +214,7 @@ def main():
     from gcslam.synth import make_hypotheses, make_scan
 
     ctx = _abi.Context(dist.local_rank)
+    ctx.set_wait_timeout(args.wait_timeout_s)  # every device wait bounded; a timeout aborts the communicator
     H_total = args.hyps
     if args.map_only:
         print(json.dumps({"c5_map_fuse": map_fuse_leg(ctx, _abi, packed=args.map_layout == "packed")}), flush=True)
@@ -752,4 +762,9 @@ def cpu_leg(n_az, H_total, budget_s):
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as e:  # fail fast (backend_node.py:2205-2210: log and re-raise): a non-zero exit
+        print(json.dumps({"error": "%s: %s" % (type(e).__name__, e), "rank": os.environ.get("RANK", "0")}),
+              file=sys.stderr, flush=True)
+        raise

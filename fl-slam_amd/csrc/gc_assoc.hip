@@ -472,7 +472,7 @@ int32_t gc_associate_primitives_ot(gc_ctx* ctx, int64_t N, int32_t n_lobes, cons
   GC_LAUNCH_CHECK(ctx);
   unsigned long long hc[2] = {0, 0};
   GC_HIP(ctx, hipMemcpyAsync(hc, cnt, sizeof(hc), hipMemcpyDeviceToHost, ctx->stream));
-  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc_w = gc::wait_stream(ctx, ctx->stream, "a result download")) return rc_w;
   if (hc[0] == 0 || hc[1] == 0) {
     const size_t nk = (size_t)N * c.K;
     GC_HIP(ctx, hipMemsetAsync(d_resp_out, 0, nk * sizeof(double), ctx->stream));
@@ -493,7 +493,7 @@ int32_t gc_associate_primitives_ot(gc_ctx* ctx, int64_t N, int32_t n_lobes, cons
                      (const double*)kmat, (const double*)d_cost_out, u, d_resp_out, d_row_mass_out, cert);
   GC_LAUNCH_CHECK(ctx);
   GC_HIP(ctx, hipMemcpyAsync(h_cert_out, cert, 12 * sizeof(double), hipMemcpyDeviceToHost, ctx->stream));
-  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc_w = gc::wait_stream(ctx, ctx->stream, "a result download")) return rc_w;
   h_cert_out[12] = (double)hc[1];
   return GC_OK;
 }

@@ -290,16 +290,16 @@ static size_t lds_predict() {
   return sizeof(double) * (5 * N2 + 2 * N2 + 4 * kDZ + 6 * kDZ + 8 + 12 + 64 + 256 * 24);
 }
 
-bool predict_budget_inline(int Hl) { return Hl + kBudgetBlocks <= device_cu_count(); }
+bool predict_budget_inline(const PipeDev& P) { return P.Hl + kBudgetBlocks <= P.cus; }
 
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
   // P.Hl hypothesis workgroups + kBudgetBlocks budget / window workgroups when they all fit one round
   // (they then run beside the hypotheses for free); otherwise the budget scalars were formed when the
   // slot was staged (S.budget, predict_budget_inline) and the hypotheses' workgroups form the window
-  const bool extra = predict_budget_inline(P.Hl);
+  const bool extra = predict_budget_inline(P);
   if (!extra && !S.budget) return hipErrorInvalidValue;
   const unsigned grid = (unsigned)(P.Hl + (extra ? kBudgetBlocks : 0));
-  const int cus = device_cu_count();
+  const int cus = P.cus;
   if ((int)grid > cus) {
     if (hipError_t e = ensure_dyn_lds((const void*)k_predict_imu<2>, lds_predict())) return e;
     hipLaunchKernelGGL(k_predict_imu<2>, dim3(grid), dim3(256), lds_predict(), st, P, S);

@@ -10,6 +10,11 @@ namespace gc {
 
 constexpr int NF_BASE = 19;   // [1, d(3), dd(6: 00 01 02 11 12 22), p(3), pp(6)] x w
 constexpr int REC_EXTRA = 4;  // [entropy_sum, max_resp, sum_w, n_points]
+// k_evidence's per-bin table (64 x 16 doubles) also receives the folded finalize's summed record
+// (B * NF_BASE + REC_EXTRA doubles): the fold is taken only when the record fits it (B <= 53), larger B
+// keep the split finalize kernel (scan_bins_pipeline), so the sums never run into the table's neighbours
+constexpr int kEvidenceTabDoubles = 64 * 16;
+inline constexpr bool fold_record_fits(int B) { return B * NF_BASE + REC_EXTRA <= kEvidenceTabDoubles; }
 
 // Chunk records of one hypothesis summed entry-wise in chunk order (the max entry by fmax), KE
 // entries per thread and KU chunks per batch in flight; a ragged last batch loads zeros past the last

@@ -59,8 +59,8 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
   double* Sx = W3 + NN;      // 2NN + 4*22
   double* vec = Sx + 2 * NN + 4 * kDZ;  // 10 x 22
   double* red = vec + 10 * kDZ;         // 8
-  double* tab = red + 8;                // 64 x 16 per-bin table
-  double* acc = tab + 64 * 16;          // 32
+  double* tab = red + 8;                // 64 x 16 per-bin table (kEvidenceTabDoubles)
+  double* acc = tab + kEvidenceTabDoubles;  // 32
   double* sc = acc + 32;                // 128 scalars
   double* c6 = sc + 128;                // 6
   double* mf = c6 + 6;                  // kMF  Matrix-Fisher record
@@ -91,8 +91,9 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
   const double* st = P.stats + (int64_t)hl * B * 38;
   if constexpr (FOLD) {
     // the a6 finalize of this hypothesis folded in (scan_bins_pipeline, BinsFold): its chunk records
-    // summed in chunk order (the split kernel's sums, bit for bit) into the per-bin table's space,
-    // then one lane per bin; the split kernel's ticket is published here (the bins have completed)
+    // summed in chunk order (the split kernel's sums, bit for bit) into the per-bin table's space
+    // (B * NF_BASE + REC_EXTRA doubles: the host folds only when fold_record_fits(B)), then one lane
+    // per bin; the split kernel's ticket is published here (the bins have completed)
     if (hl == 0 && t == 0 && S.done_word)
       __hip_atomic_store(S.done_word, S.ticket, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     const int RL = B * NF_BASE + REC_EXTRA;
@@ -675,7 +676,7 @@ static hipError_t allow_big_lds(const void* fn, size_t bytes) {
   return bytes > 65536 ? ensure_dyn_lds(fn, bytes) : hipSuccess;
 }
 hipError_t launch_evidence(const PipeDev& P, const ScanArgs& S, hipStream_t st) {
-  const bool two = P.Hl > device_cu_count(), fold = S.fin_part != nullptr;
+  const bool two = P.Hl > P.cus, fold = S.fin_part != nullptr;
 #define GC_EVL(OCC, FOLD)                                                                        \
   do {                                                                                           \
     if (hipError_t e = allow_big_lds((const void*)k_evidence<OCC, FOLD>, lds_evidence())) return e; \

@@ -5,6 +5,8 @@
 #include <string>
 #include "../../include/gcslam.h"
 
+struct gc_comm;
+
 struct gc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -18,6 +20,12 @@ struct gc_ctx {
   void* slot_runs = nullptr;
   int64_t slot_runs_n = 0;
   bool slot_runs_dirty = true;
+  // Fail-fast bound on every host wait for this context's device work (gc_ctx_set_wait_timeout;
+  // GC_WAIT_TIMEOUT_S in the environment, default 300 s). A wait that runs out aborts `comm` (the
+  // RCCL communicator last initialised on this context) so a peer that died cannot hold this rank in
+  // an all-gather, and returns GC_ERR_RUNTIME (backend_node.py:2205-2210: log and re-raise).
+  double wait_timeout_s = 300.0;
+  gc_comm* comm = nullptr;
 };
 
 namespace gc {
@@ -35,8 +43,22 @@ int slot_runs(gc_ctx* ctx, int64_t m_slots, void** out);
 // the table exp's 2048-entry table in device memory (gc_points.hip), enqueued once per context
 hipError_t init_exp_table(hipStream_t st);
 
-// compute units of the current device (queried once per device id, cached)
-int device_cu_count();
+// Bounded host waits (fail fast). Poll the stream / event: ~spin_polls busy polls first (the wake-up
+// latency of a blocking wait can exceed a 0.3 ms scan), then short sleeps, until the device work is
+// done or ctx->wait_timeout_s runs out; the attached communicator's asynchronous error is polled on
+// the way. On a timeout or an RCCL error the communicator is aborted (its kernels see the abort flag
+// and exit) and GC_ERR_RUNTIME is returned with the reason in gc_last_error. ctx may be NULL (the
+// environment's default bound, no communicator). waited_ms (optional) receives the time spent.
+int wait_stream(gc_ctx* ctx, hipStream_t st, const char* what, double* waited_ms = nullptr, long spin_polls = 2000);
+int wait_event(gc_ctx* ctx, hipEvent_t ev, const char* what, double* waited_ms = nullptr, long spin_polls = 2000);
+// the default bound (GC_WAIT_TIMEOUT_S or 300 s)
+double default_wait_timeout_s();
+// RCCL hooks (gc_comm.cpp): the communicator's asynchronous error (false and why set if it failed),
+// abort it (idempotent), and forget the context it was created on
+bool comm_healthy(gc_comm* c, std::string* why);
+void comm_abort(gc_comm* c);
+void comm_detach_ctx(gc_comm* c);
+
 constexpr size_t kSlotRunsBytes = 256;
 
 // hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) only when fn has not yet been allowed that

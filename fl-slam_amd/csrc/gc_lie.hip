@@ -71,3 +71,21 @@ extern "C" int32_t gc_lie_batch(gc_ctx* ctx, int32_t op, int64_t n, const double
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
 }
+
+// Fail-fast test support: one thread that keeps the stream busy for `seconds` of device real time
+// (s_memrealtime, 100 MHz) and then exits by itself, so a host wait with a shorter bound must time out
+// while the kernel always drains (gc_test_device_spin; tests/test_gpu_failfast.py). Writes nothing.
+namespace {
+__global__ void k_test_spin(uint64_t ticks) {
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(127);
+}
+}  // namespace
+
+extern "C" int32_t gc_test_device_spin(gc_ctx* ctx, double seconds) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, seconds >= 0.0 && seconds <= 10.0, "spin time must be in [0, 10] s");
+  hipLaunchKernelGGL(k_test_spin, dim3(1), dim3(1), 0, ctx->stream, (uint64_t)(seconds * 1e8));
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}

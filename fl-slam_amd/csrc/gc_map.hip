@@ -403,7 +403,7 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   if (n_fused_out) {
     std::vector<uint32_t> c(grid);
     GC_HIP(ctx, hipMemcpyAsync(c.data(), cnt, c.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-    GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc_w = gc::wait_stream(ctx, ctx->stream, "the touched-slot counts")) return rc_w;
     int64_t n = 0;
     for (uint32_t v : c) n += v;
     *n_fused_out = n;

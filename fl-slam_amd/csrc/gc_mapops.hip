@@ -353,7 +353,7 @@ int reduce_into(gc_ctx* ctx, int64_t n, double* part, double* out, Launch launch
 
 int download(gc_ctx* ctx, void* h, const void* d, size_t bytes) {
   GC_HIP(ctx, hipMemcpyAsync(h, d, bytes, hipMemcpyDeviceToHost, ctx->stream));
-  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc_w = gc::wait_stream(ctx, ctx->stream, "a result download")) return rc_w;
   return GC_OK;
 }
 

@@ -34,6 +34,8 @@ struct PipeDev {
   int B;         // bins
   int M;         // IMU slots (<= 512)
   int geom_H;    // bins chunk geometry as for this many hypotheses (0: Hl)
+  int cus;       // compute units of the pipeline's device (ctx->device, queried once at create): every
+                 // grid-size decision (predict's budget workgroups, the chain kernels' occupancy) uses it
   int64_t n_in, n_cap;
   double tau, o0, o1, o2;
   double eps_psd, eps_lift, eps_mass, lambda_ou, c_frob, forgetting, weight_floor;
@@ -112,7 +114,7 @@ struct ScanArgs {
 hipError_t launch_predict_imu(const PipeDev& P, const ScanArgs& S, hipStream_t st);
 // the predict launch forms the a1 budget itself (its extra workgroups fit beside Hl hypotheses);
 // otherwise the staging must (S.budget)
-bool predict_budget_inline(int Hl);
+bool predict_budget_inline(const PipeDev& P);
 // a1 budget scalars into out (8) with 3 x 64 partials in part (gc_points.hip)
 hipError_t launch_budget_stats(const double* d_w, int64_t n_in, int64_t n_cap, double* part, double* out,
                                hipStream_t st);

@@ -131,11 +131,11 @@ double now_ms() {
 
 // a stream synchronisation on the host, counted as a host sync and as waiting time
 int sync_counted(gc_pipeline* p) {
-  const double t0 = now_ms();
-  GC_HIP(p->ctx, hipStreamSynchronize(p->ctx->stream));
-  p->wait_acc_ms += now_ms() - t0;
+  double ms = 0.0;
+  const int rc = gc::wait_stream(p->ctx, p->ctx->stream, "the pipeline stream", &ms);
+  p->wait_acc_ms += ms;
   p->hs[GC_HS_HOST_SYNCS] += 1.0;
-  return GC_OK;
+  return rc;
 }
 
 int up(gc_pipeline* p, double* d, const double* h, size_t count) {
@@ -154,26 +154,19 @@ int down(gc_pipeline* p, double* h, const double* d, size_t count) {
 
 // Host wait for a copy-stream event by polling: hipEventSynchronize may sleep on an interrupt and
 // take tens to hundreds of microseconds to wake, enough to make the host, not the device, the
-// bottleneck of a 0.3 ms scan. Falls back to the blocking wait after ~10^5 polls. An event already
-// complete costs one query and is not counted as a sync.
+// bottleneck of a 0.3 ms scan. ~10^5 busy polls, then short sleeps, bounded by the context's wait
+// timeout (fail fast: a stuck device or a dead peer ends in GC_ERR_RUNTIME, never an unbounded wait).
+// An event already complete costs one query and is not counted as a sync.
 int wait_event(gc_pipeline* p, hipEvent_t e) {
   gc_ctx* ctx = p->ctx;
   hipError_t q = hipEventQuery(e);
   if (q == hipSuccess) return GC_OK;
   if (q != hipErrorNotReady) GC_HIP(ctx, q);
-  const double t0 = now_ms();
   p->hs[GC_HS_HOST_SYNCS] += 1.0;
-  for (int spin = 0; spin < 100000; ++spin) {
-    q = hipEventQuery(e);
-    if (q == hipSuccess) {
-      p->wait_acc_ms += now_ms() - t0;
-      return GC_OK;
-    }
-    if (q != hipErrorNotReady) GC_HIP(ctx, q);
-  }
-  GC_HIP(ctx, hipEventSynchronize(e));
-  p->wait_acc_ms += now_ms() - t0;
-  return GC_OK;
+  double ms = 0.0;
+  const int rc = gc::wait_event(ctx, e, "a scan slot's ingest copy", &ms, 100000);
+  p->wait_acc_ms += ms;
+  return rc;
 }
 
 // host time of one entry split into work and waits: sum / max per kind (GC_HS_* layout)
@@ -305,12 +298,18 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   GC_CHECK_ARG(ctx, dims->geom_hyps >= 0 && dims->geom_hyps <= 65536, "geom_hyps must be in [0, 65536]");
   GC_CHECK_ARG(ctx, cfg[GC_PCFG_TAU] >= GC_FUSED_TAU_MIN, "tau must be >= GC_FUSED_TAU_MIN (3e-3)");
   GC_HIP(ctx, hipSetDevice(ctx->device));
+  if (ctx->cu_count == 0) {
+    int cus = 0;
+    GC_HIP(ctx, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, ctx->device));
+    ctx->cu_count = cus > 0 ? cus : 1;
+  }
   gc_pipeline* p = new gc_pipeline();
   p->ctx = ctx;
   gc::PipeDev& P = p->P;
   P.Hl = dims->h_count; P.H = dims->H_total; P.h_begin = dims->h_begin; P.B = dims->B; P.M = dims->M;
   P.n_in = dims->n_in_max; P.n_cap = dims->n_cap; P.G = dims->world_size;
   P.geom_H = dims->geom_hyps;
+  P.cus = ctx->cu_count;
   P.tau = cfg[GC_PCFG_TAU]; P.o0 = cfg[GC_PCFG_ORIGIN]; P.o1 = cfg[GC_PCFG_ORIGIN + 1]; P.o2 = cfg[GC_PCFG_ORIGIN + 2];
   P.eps_psd = cfg[GC_PCFG_EPS_PSD]; P.eps_lift = cfg[GC_PCFG_EPS_LIFT]; P.eps_mass = cfg[GC_PCFG_EPS_MASS];
   P.lambda_ou = cfg[GC_PCFG_LAMBDA_OU]; P.c_frob = cfg[GC_PCFG_C_FROB]; P.forgetting = cfg[GC_PCFG_FORGETTING];
@@ -352,7 +351,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   double* ticket = nullptr;
   if (rc == GC_OK) rc = dalloc(p, 1, &ticket);  // zeroed: the predict grid's budget arrival counter
   P.budget_ticket = reinterpret_cast<unsigned*>(ticket);
-  p->stage_budget = !gc::predict_budget_inline(Hl);
+  p->stage_budget = !gc::predict_budget_inline(P);
   double* ctr = nullptr;
   if (rc == GC_OK) rc = dalloc(p, 1, &ctr);  // zeroed: k_bins_io's task counter + finished pullers
   P.task_ctr = reinterpret_cast<unsigned*>(ctr);
@@ -370,7 +369,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
     gc::set_error(ctx, "hipStreamCreateWithFlags failed for the ingest stream");
     rc = GC_ERR_RUNTIME;
   }
-  if (rc == GC_OK) GC_HIP(ctx, hipStreamSynchronize(ctx->stream));  // the zero fills land before any launch
+  if (rc == GC_OK) rc = gc::wait_stream(ctx, ctx->stream, "the pipeline's zero fills");  // before any launch
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
     return rc;
@@ -381,8 +380,9 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
 
 int32_t gc_pipeline_destroy(gc_pipeline* p) {
   if (!p) return GC_OK;
-  (void)hipStreamSynchronize(p->ctx->stream);
-  if (p->cstream) (void)hipStreamSynchronize(p->cstream);
+  // bounded (a stream stuck behind a failed peer's all-gather is still torn down)
+  (void)gc::wait_stream(p->ctx, p->ctx->stream, "the pipeline stream at destruction");
+  if (p->cstream) (void)gc::wait_stream(p->ctx, p->cstream, "the ingest stream at destruction");
   for (void* a : p->allocs) (void)hipFree(a);
   for (auto& s : p->slots) {
     for (void* d : {(void*)s.dev, (void*)s.bytes, (void*)s.ring, (void*)s.tag, (void*)s.flag})
@@ -708,12 +708,16 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
   // every kBindEvery-th scan's combine_final carries a completion event for the slot staging
   // (fin_ev; with a map attached the slots order on the map update instead)
   hipEvent_t fin = nullptr;
+  int fin_e = -1;
   if (kBindEvery > 0 && !p->smap_on && p->pending_ticket > 0 && p->pending_ticket % kBindEvery == 0) {
-    const int e = (int)((p->pending_ticket / kBindEvery) & 1);
-    fin = p->fin_ev[e];
-    p->fin_ticket[e] = p->pending_ticket;
+    fin_e = (int)((p->pending_ticket / kBindEvery) & 1);
+    fin = p->fin_ev[fin_e];
+    p->fin_ticket[fin_e] = 0;  // the event is re-armed by this launch: unusable until it succeeds
   }
   GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream, fin));
+  // only a launch that carries the event makes it cover this ticket (a failed launch leaves it
+  // cleared, so slot_wait_consumed falls back to an event recorded on the compute stream)
+  if (fin_e >= 0) p->fin_ticket[fin_e] = p->pending_ticket;
   GC_TRY(stage_event(p, 6));
   if (p->smap_on) {
     auto& s = p->slots[p->pending_slot];
@@ -910,7 +914,7 @@ int32_t gc_pipeline_set_exchange_timing(gc_pipeline* p, int32_t on) {
 int32_t gc_pipeline_exchange_ms(gc_pipeline* p, float* ms) {
   GC_CHECK_ARG(nullptr, p && ms, "NULL argument");
   GC_CHECK_ARG(p->ctx, p->x_rec, "no timed exchange has run (timing off, or one rank without a communicator)");
-  GC_HIP(p->ctx, hipEventSynchronize(p->x1));
+  if (int rc = gc::wait_event(p->ctx, p->x1, "the timed exchange")) return rc;
   GC_HIP(p->ctx, hipEventElapsedTime(ms, p->x0, p->x1));
   return GC_OK;
 }
@@ -982,9 +986,9 @@ int32_t gc_pipeline_set_stage_timing(gc_pipeline* p, int32_t on) {
 int32_t gc_pipeline_stage_ms(gc_pipeline* p, float* h_ms) {
   GC_CHECK_ARG(nullptr, p && h_ms, "NULL argument");
   GC_CHECK_ARG(p->ctx, p->st_rec, "no scan has finished with stage timing on (gc_pipeline_set_stage_timing)");
-  const double t0 = now_ms();
-  GC_HIP(p->ctx, hipEventSynchronize(p->st_ev[GC_STAGE_N - 1]));
-  p->wait_acc_ms += now_ms() - t0;
+  double wms = 0.0;
+  if (int rc = gc::wait_event(p->ctx, p->st_ev[GC_STAGE_N - 1], "the stage-timing events", &wms)) return rc;
+  p->wait_acc_ms += wms;
   p->hs[GC_HS_HOST_SYNCS] += 1.0;
   for (int i = 0; i + 1 < GC_STAGE_N; ++i)
     GC_HIP(p->ctx, hipEventElapsedTime(&h_ms[i], p->st_ev[i], p->st_ev[i + 1]));

@@ -1759,7 +1759,7 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   }
 #undef GC_BIO
   GC_LAUNCH_CHECK(ctx);
-  if (fold && chunks <= kFoldChunks) {  // the evidence kernel reduces the records (gc_evidence.hip)
+  if (fold && chunks <= kFoldChunks && fold_record_fits(B)) {  // k_evidence reduces the records (gc_evidence.hip)
     fold->part = (const double*)scr;
     fold->chunks = chunks;
     return GC_OK;

@@ -1,9 +1,12 @@
 // gc_runtime.cpp — context, device buffers, events and error plumbing of libgcslam.
 #include <hip/hip_runtime.h>
+#include <chrono>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <mutex>
 #include <map>
+#include <thread>
 #include "gc_internal.h"
 
 struct gc_event {
@@ -55,7 +58,7 @@ int ensure_no_static_lds(gc_ctx* ctx, const void* fn) {
 
 int scratch(gc_ctx* ctx, size_t bytes, void** out) {
   if (bytes > ctx->scratch_bytes) {
-    GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = wait_stream(ctx, ctx->stream, "the stream before growing the scratch")) return rc;
     if (ctx->scratch) GC_HIP(ctx, hipFree(ctx->scratch));
     ctx->scratch = nullptr;
     ctx->scratch_bytes = 0;
@@ -67,20 +70,76 @@ int scratch(gc_ctx* ctx, size_t bytes, void** out) {
   return GC_OK;
 }
 
-int device_cu_count() {
-  static int cache[64] = {0};
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-  if (cache[dev] == 0) {
-    int cus = 0;
-    cache[dev] = (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && cus > 0) ? cus : 256;
+double default_wait_timeout_s() {
+  static const double v = [] {
+    const char* e = std::getenv("GC_WAIT_TIMEOUT_S");
+    const double x = e ? std::atof(e) : 0.0;
+    return x > 0.0 ? x : 300.0;
+  }();
+  return v;
+}
+
+namespace {
+// The poll loop behind wait_stream / wait_event: query() until hipSuccess, busy for spin_polls polls,
+// then in 20 us sleeps; the deadline and the communicator's asynchronous error are checked every 64
+// polls. Any other HIP status is returned as the error it is.
+template <typename Query>
+int bounded_poll(gc_ctx* ctx, const Query& query, const char* what, double* waited_ms, long spin_polls,
+                 double limit_s) {
+  using clk = std::chrono::steady_clock;
+  const auto t0 = clk::now();
+  const auto done = [&](int rc) {
+    if (waited_ms) *waited_ms = 1e-6 * (double)std::chrono::duration_cast<std::chrono::nanoseconds>(clk::now() - t0).count();
+    return rc;
+  };
+  for (long i = 0;; ++i) {
+    const hipError_t q = query();
+    if (q == hipSuccess) return done(GC_OK);
+    if (q != hipErrorNotReady) {
+      set_error(ctx, std::string("HIP error ") + hipGetErrorString(q) + " while waiting for " + what);
+      return done(GC_ERR_RUNTIME);
+    }
+    if ((i & 63) == 0) {
+      std::string why;
+      if (ctx && ctx->comm && !comm_healthy(ctx->comm, &why)) {
+        comm_abort(ctx->comm);
+        set_error(ctx, std::string("RCCL communicator failed while waiting for ") + what + ": " + why +
+                           " (communicator aborted)");
+        return done(GC_ERR_RUNTIME);
+      }
+      const double el = std::chrono::duration<double>(clk::now() - t0).count();
+      if (el >= limit_s) {
+        if (ctx && ctx->comm) comm_abort(ctx->comm);
+        set_error(ctx, std::string("timed out after ") + std::to_string(el) + " s waiting for " + what +
+                           (ctx && ctx->comm ? " (a peer rank may have failed; the RCCL communicator was aborted)"
+                                             : " (device work did not complete)"));
+        return done(GC_ERR_RUNTIME);
+      }
+    }
+    if (i >= spin_polls) std::this_thread::sleep_for(std::chrono::microseconds(20));
   }
-  return cache[dev];
+}
+}  // namespace
+
+// gc_test_bounded_wait's entry into the poll loop (no HIP call: the query is the caller's)
+template <typename Query>
+int bounded_poll_for_test(gc_ctx* ctx, const Query& query, double* waited_ms) {
+  return bounded_poll(ctx, query, "a test condition that never completes", waited_ms, 100, ctx->wait_timeout_s);
+}
+
+int wait_stream(gc_ctx* ctx, hipStream_t st, const char* what, double* waited_ms, long spin_polls) {
+  const double lim = ctx ? ctx->wait_timeout_s : default_wait_timeout_s();
+  return bounded_poll(ctx, [&] { return hipStreamQuery(st); }, what, waited_ms, spin_polls, lim);
+}
+
+int wait_event(gc_ctx* ctx, hipEvent_t ev, const char* what, double* waited_ms, long spin_polls) {
+  const double lim = ctx ? ctx->wait_timeout_s : default_wait_timeout_s();
+  return bounded_poll(ctx, [&] { return hipEventQuery(ev); }, what, waited_ms, spin_polls, lim);
 }
 
 int slot_runs(gc_ctx* ctx, int64_t m_slots, void** out) {
   if (m_slots > ctx->slot_runs_n) {
-    GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+    if (int rc = wait_stream(ctx, ctx->stream, "the stream before growing the run table")) return rc;
     if (ctx->slot_runs) GC_HIP(ctx, hipFree(ctx->slot_runs));
     ctx->slot_runs = nullptr;
     ctx->slot_runs_n = 0;
@@ -127,6 +186,7 @@ int32_t gc_ctx_create(int32_t device, gc_ctx** out) {
   GC_HIP(nullptr, hipSetDevice(device));
   gc_ctx* c = new gc_ctx();
   c->device = device;
+  c->wait_timeout_s = gc::default_wait_timeout_s();
   hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
   if (e != hipSuccess) {
     gc::set_error(nullptr, std::string("hipStreamCreate: ") + hipGetErrorString(e));
@@ -147,7 +207,9 @@ int32_t gc_ctx_create(int32_t device, gc_ctx** out) {
 int32_t gc_ctx_destroy(gc_ctx* ctx) {
   if (!ctx) return GC_OK;
   (void)hipSetDevice(ctx->device);
-  (void)hipStreamSynchronize(ctx->stream);
+  if (ctx->comm) gc::comm_detach_ctx(ctx->comm);
+  // bounded: a context whose stream is stuck (a failed peer) is still torn down
+  (void)gc::wait_stream(ctx, ctx->stream, "the stream at context destruction");
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->slot_runs) (void)hipFree(ctx->slot_runs);
   (void)hipStreamDestroy(ctx->stream);
@@ -158,8 +220,26 @@ int32_t gc_ctx_destroy(gc_ctx* ctx) {
 int32_t gc_ctx_synchronize(gc_ctx* ctx) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   GC_HIP(ctx, hipSetDevice(ctx->device));
-  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  return gc::wait_stream(ctx, ctx->stream, "the context's stream (gc_ctx_synchronize)");
+}
+
+int32_t gc_ctx_set_wait_timeout(gc_ctx* ctx, double seconds) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, seconds > 0.0, "the wait timeout must be positive");
+  ctx->wait_timeout_s = seconds;
   return GC_OK;
+}
+
+int32_t gc_test_bounded_wait(double timeout_s, int64_t ready_after_polls, double* h_waited_ms) {
+  GC_CHECK_ARG(nullptr, timeout_s > 0.0 && h_waited_ms, "bad arguments");
+  int64_t polls = 0;
+  gc_ctx tmp;  // no device, no stream, no communicator: only the timeout bound
+  tmp.wait_timeout_s = timeout_s;
+  const int rc = gc::bounded_poll_for_test(&tmp, [&] {
+    return (ready_after_polls >= 0 && ++polls > ready_after_polls) ? hipSuccess : hipErrorNotReady;
+  }, h_waited_ms);
+  if (rc != GC_OK) gc::set_error(nullptr, tmp.err);
+  return rc;
 }
 
 int32_t gc_buffer_alloc(gc_ctx* ctx, uint64_t bytes, void** d_ptr) {
@@ -173,7 +253,7 @@ int32_t gc_buffer_free(gc_ctx* ctx, void* d_ptr) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   if (!d_ptr) return GC_OK;
   GC_HIP(ctx, hipSetDevice(ctx->device));
-  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc = gc::wait_stream(ctx, ctx->stream, "the stream before a buffer free")) return rc;
   GC_HIP(ctx, hipFree(d_ptr));
   return GC_OK;
 }
@@ -182,16 +262,14 @@ int32_t gc_buffer_upload(gc_ctx* ctx, void* d_dst, const void* h_src, uint64_t b
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   if (bytes == 0) return GC_OK;
   GC_HIP(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
-  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return GC_OK;
+  return gc::wait_stream(ctx, ctx->stream, "an upload");
 }
 
 int32_t gc_buffer_download(gc_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   if (bytes == 0) return GC_OK;
   GC_HIP(ctx, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
-  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
-  return GC_OK;
+  return gc::wait_stream(ctx, ctx->stream, "a download");
 }
 
 int32_t gc_buffer_copy(gc_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes) {
@@ -236,7 +314,7 @@ int32_t gc_event_record(gc_ctx* ctx, gc_event* ev) {
 
 int32_t gc_event_elapsed_ms(gc_event* start, gc_event* stop, float* ms) {
   GC_CHECK_ARG(nullptr, start && stop && ms, "NULL argument");
-  GC_HIP(nullptr, hipEventSynchronize(stop->ev));
+  if (int rc = gc::wait_event(nullptr, stop->ev, "a timing event")) return rc;
   GC_HIP(nullptr, hipEventElapsedTime(ms, start->ev, stop->ev));
   return GC_OK;
 }

@@ -45,7 +45,7 @@ struct ScanMapArgs {
   const double* h0;                       // reduced record: [z_t 6, Σ_pose 36, ξ 6] of hypothesis 0
   const double* lidar_iw;                 // [ν_2, Ψ_2] of the scan, before its measurement-IW apply
   int64_t n_cap;
-  double t0, t1, o0, o1, o2, voxel, timestamp, eps_mass;
+  double t0, t1, o0, o1, o2, voxel, timestamp, eps_mass, eps_psd;
   int64_t scan_seq;
 };
 
@@ -161,9 +161,13 @@ __global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, SlotRuns
   // the scan's constants: Σ_pose and Σ_lidar by lanes of wave 0, R, tt and Rᵀ t by lane 0 of wave 1
   if (t < 36) {
     C[21 + t] = A.h0[6 + t];
-  } else if (t < 45) {
-    const double den = A.lidar_iw[0] + 3.0 + 1.0;  // measurement_noise_mean_jax, LiDAR block
-    C[12 + (t - 36)] = A.lidar_iw[1 + (t - 36)] / den;
+  } else if (t == 36) {
+    // measurement_noise_mean_jax's LiDAR block (operators/measurement_noise_iw_jax.py:50-56):
+    // domain_projection_psd_core(Ψ / (ν + p + 1), eps_psd) (certified shortcut: S_sym when SPD)
+    const double den = A.lidar_iw[0] + 3.0 + 1.0;
+    double Sl[9];
+    for (int q = 0; q < 9; ++q) Sl[q] = A.lidar_iw[1 + q] / den;
+    psd_project3_fast(Sl, A.eps_psd, C + 12, nullptr);
   } else if (t == 64) {
     double R[9], tt[3];
     smap_pose(A, R, tt);
@@ -368,6 +372,9 @@ int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_s
 
 int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_primitive_map& map,
                         const PipeDev& P, const ScanMapInput& in) {
+  // the per-slot run table (ctx->slot_runs) is zeroed and cleared on ctx->stream by every user (this
+  // update and gc_primitive_map_fuse): a caller on another stream would race those fills and clears
+  GC_CHECK_ARG(ctx, st == ctx->stream, "the in-scan map update runs on the context's stream");
   ScanMapArgs A{};
   A.map = map;
   A.pts = in.pts; A.t = in.t; A.w_win = P.w_win; A.bscal = P.budget;
@@ -377,6 +384,7 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
   A.t0 = in.t0; A.t1 = in.t1;
   A.o0 = P.o0; A.o1 = P.o1; A.o2 = P.o2;
   A.voxel = in.voxel; A.timestamp = in.timestamp; A.eps_mass = P.eps_mass;
+  A.eps_psd = P.eps_psd;
   A.scan_seq = in.scan_seq;
   const int64_t n = P.n_cap;
   void* T = nullptr;
@@ -396,7 +404,7 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
 int32_t scan_map_count(gc_ctx* ctx, const ScanMapWork& W, int64_t* out, size_t* d2h_bytes) {
   std::vector<uint32_t> c((size_t)W.n_wg);
   GC_HIP(ctx, hipMemcpyAsync(c.data(), W.wg_count, c.size() * sizeof(uint32_t), hipMemcpyDeviceToHost, ctx->stream));
-  GC_HIP(ctx, hipStreamSynchronize(ctx->stream));
+  if (int rc_w = gc::wait_stream(ctx, ctx->stream, "a result download")) return rc_w;
   int64_t n = 0;
   for (uint32_t v : c) n += v;
   *out = n;

@@ -31,6 +31,9 @@ SIGNATURES = {
     "gc_ctx_create": [_i32, C.POINTER(_vp)],
     "gc_ctx_destroy": [_vp],
     "gc_ctx_synchronize": [_vp],
+    "gc_ctx_set_wait_timeout": [_vp, _f64],
+    "gc_test_bounded_wait": [_f64, _i64, _dptr],
+    "gc_test_device_spin": [_vp, _f64],
     "gc_buffer_alloc": [_vp, _u64, C.POINTER(_vp)],
     "gc_buffer_free": [_vp, _vp],
     "gc_buffer_upload": [_vp, _vp, _vp, _u64],
@@ -97,6 +100,8 @@ SIGNATURES = {
     "gc_comm_unique_id": [_vp],
     "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],
     "gc_comm_destroy": [_vp],
+    "gc_comm_abort": [_vp],
+    "gc_comm_healthy": [_vp, C.POINTER(C.c_int32)],
     "gc_comm_allgather_f64": [_vp, _vp, _vp, _vp, _i64],
     "gc_lie_batch": [_vp, _i32, _i64, _vp, _vp],
     "gc_belief_world_pose_batch": [_vp, _i32, _vp, _vp, _vp, _f64, _vp, _vp],
@@ -222,6 +227,10 @@ class Context:
 
     def sync(self):
         check(lib().gc_ctx_synchronize(self.handle), self)
+
+    def set_wait_timeout(self, seconds: float):
+        """Bound of every host wait on this context (fail fast; include/gcslam.h gc_ctx_synchronize)."""
+        check(lib().gc_ctx_set_wait_timeout(self.handle, float(seconds)), self)
 
     def close(self):
         if self.handle:

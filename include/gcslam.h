@@ -49,7 +49,19 @@ const char* gc_last_error(const gc_ctx* ctx);
 int32_t gc_device_count(int32_t* count);
 int32_t gc_ctx_create(int32_t device, gc_ctx** out);
 int32_t gc_ctx_destroy(gc_ctx* ctx);
+/* Waits for everything enqueued on the ctx stream. Like every host wait in libgcslam it is bounded
+ * (fail fast, backend_node.py:2205-2210 log and re-raise): after the context's wait timeout it returns
+ * GC_ERR_RUNTIME, and an RCCL communicator initialised on this context is aborted first, so a rank whose
+ * peer died does not stay in an all-gather. Its asynchronous error is polled during the wait. */
 int32_t gc_ctx_synchronize(gc_ctx* ctx);
+/* The bound of every host wait on this context, seconds (default: $GC_WAIT_TIMEOUT_S, else 300). */
+int32_t gc_ctx_set_wait_timeout(gc_ctx* ctx, double seconds);
+/* Test entries of the bounded wait. gc_test_bounded_wait runs the wait loop on a condition that
+ * completes after ready_after_polls polls (< 0: never) with no device involved: GC_OK, or
+ * GC_ERR_RUNTIME once timeout_s has passed; h_waited_ms receives the time spent. gc_test_device_spin
+ * enqueues a one-thread kernel that keeps the stream busy for `seconds` (<= 10) and then exits. */
+int32_t gc_test_bounded_wait(double timeout_s, int64_t ready_after_polls, double* h_waited_ms);
+int32_t gc_test_device_spin(gc_ctx* ctx, double seconds);
 int32_t gc_buffer_alloc(gc_ctx* ctx, uint64_t bytes, void** d_ptr);
 int32_t gc_buffer_free(gc_ctx* ctx, void* d_ptr);
 /* Synchronous copies (stream-ordered, then waited). */
@@ -398,6 +410,11 @@ int32_t gc_pipeline_get_scan_map_count(gc_pipeline* p, int64_t* n_slots);
 int32_t gc_comm_unique_id(uint8_t* h_id_out);
 int32_t gc_comm_init(gc_ctx* ctx, int32_t nranks, int32_t rank, const uint8_t* h_id, gc_comm** out);
 int32_t gc_comm_destroy(gc_comm* comm);
+/* Abort the communicator (ncclCommAbort: its kernels exit; every later exchange fails fast). The
+ * bounded waits of the context it was created on call this themselves on a timeout or an RCCL error. */
+int32_t gc_comm_abort(gc_comm* comm);
+/* *ok = 0 when the communicator has an asynchronous error or was aborted (gc_last_error has why). */
+int32_t gc_comm_healthy(gc_comm* comm, int32_t* ok);
 int32_t gc_comm_allgather_f64(gc_ctx* ctx, gc_comm* comm, const double* d_send, double* d_recv, int64_t count);
 
 /* ------------------------------------------------------------------------------------------

@@ -1371,7 +1371,8 @@ def scan_map_rows(scan_points, scan_t, scan_w, n_points_cap, t0, t1, h0, nu_meas
     R = so3_exp(h0[3:6])
     t = np.array([h0[0], h0[1], 0.0])
     mu = np.stack([((R[i, 0] * p0[:, 0] + R[i, 1] * p0[:, 1]) + R[i, 2] * p0[:, 2]) + t[i] for i in range(3)], axis=1)
-    Sl = Psi_meas[2] / (nu_meas[2] + 3.0 + 1.0)
+    # measurement_noise_mean_jax (operators/measurement_noise_iw_jax.py:50-56): PSD-projected mode
+    Sl = psd_project(Psi_meas[2] / (nu_meas[2] + 3.0 + 1.0))[0]
     Sp = np.asarray(h0[6:42]).reshape(6, 6)
     K = p0.shape[0]
     J = np.zeros((K, 3, 6))

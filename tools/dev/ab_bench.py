@@ -1,5 +1,5 @@
 """Dev helper: run bench.py's main against another build of the library (A/B on one box).
-Usage: python3 tools/ab_bench.py <path/to/libgcslam.so> [bench args]"""
+Usage: python3 tools/dev/ab_bench.py <path/to/libgcslam.so> [bench args]"""
 import os
 import sys
 

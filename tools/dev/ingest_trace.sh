@@ -1,6 +1,6 @@
 #!/bin/bash
 # Dev (GPU box): kernel + memory-copy timeline of the batched pipeline with per-step ingest and
-# without, at H hypotheses. Usage: bash tools/ingest_trace.sh <H> [tag]
+# without, at H hypotheses. Usage: bash tools/dev/ingest_trace.sh <H> [tag]
 set -e
 H=${1:-32}; tag=${2:-h$H}
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"

@@ -8,7 +8,7 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-m
 echo "tests rc=$rc $(tail -1 $o/gpu_tests.txt)"
 case $rc in 0|1) ;; *) exit $rc;; esac
 for H in 256 32; do
-  bash tools/ab_run.sh 3 $H fl-slam_amd/build_var/lb1/libgcslam.so fl-slam_amd/build_var/lb2/libgcslam.so fl-slam_amd/build_var/fold/libgcslam.so > $o/ab_h$H.txt 2>&1 || { cat $o/ab_h$H.txt; exit 1; }
+  bash tools/dev/ab_run.sh 3 $H fl-slam_amd/build_var/lb1/libgcslam.so fl-slam_amd/build_var/lb2/libgcslam.so fl-slam_amd/build_var/fold/libgcslam.so > $o/ab_h$H.txt 2>&1 || { cat $o/ab_h$H.txt; exit 1; }
   cat $o/ab_h$H.txt
 done
-bash tools/r4_saprobe.sh 2 sacur sastore f512 && cp gpurun_out/r4/saprobe/ab.txt $o/saprobe.txt
+bash tools/dev/r4_saprobe.sh 2 sacur sastore f512 && cp gpurun_out/r4/saprobe/ab.txt $o/saprobe.txt

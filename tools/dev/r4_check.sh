@@ -8,7 +8,7 @@ timeout -k 10 900 python3 -u -m pytest tests -m gpu -v --timeout 300 --timeout-m
 echo "tests rc=$rc $(tail -1 $o/gpu_tests.txt)"
 case $rc in 0|1) ;; *) exit $rc;; esac
 for H in 32 256; do
-  bash tools/ab_run.sh $reps $H fl-slam_amd/build_var/$a/libgcslam.so fl-slam_amd/build_var/$b/libgcslam.so > $o/ab_h$H.txt 2>&1 || { cat $o/ab_h$H.txt; exit 1; }
+  bash tools/dev/ab_run.sh $reps $H fl-slam_amd/build_var/$a/libgcslam.so fl-slam_amd/build_var/$b/libgcslam.so > $o/ab_h$H.txt 2>&1 || { cat $o/ab_h$H.txt; exit 1; }
   cat $o/ab_h$H.txt
 done
 d=$o/kt_c5

@@ -1,13 +1,13 @@
 #!/bin/bash
 # GPU box (round 4 probe): contract-pair roofline and the standalone C5 fuse of build_var variants
-# (interleaved). Usage: bash tools/r4_saprobe.sh reps v1 v2 ...   Output: gpurun_out/r4/saprobe/.
+# (interleaved). Usage: bash tools/dev/r4_saprobe.sh reps v1 v2 ...   Output: gpurun_out/r4/saprobe/.
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 reps=$1; shift
 o=gpurun_out/r4/saprobe; rm -rf $o; mkdir -p $o
 for r in $(seq $reps); do
   for v in "$@"; do
-    timeout -k 10 120 python3 tools/ab_bench.py fl-slam_amd/build_var/$v/libgcslam.so --roofline-only > $o/roof_${v}_${r}.json 2>/dev/null || exit 1
-    timeout -k 10 120 python3 tools/ab_bench.py fl-slam_amd/build_var/$v/libgcslam.so --map-only > $o/map_${v}_${r}.json 2>/dev/null || exit 1
+    timeout -k 10 120 python3 tools/dev/ab_bench.py fl-slam_amd/build_var/$v/libgcslam.so --roofline-only > $o/roof_${v}_${r}.json 2>/dev/null || exit 1
+    timeout -k 10 120 python3 tools/dev/ab_bench.py fl-slam_amd/build_var/$v/libgcslam.so --map-only > $o/map_${v}_${r}.json 2>/dev/null || exit 1
     python3 -c "
 import json
 d=json.loads(open('$o/roof_${v}_${r}.json').read().strip().splitlines()[-1]); r=d['roofline']; pk=r['per_kernel']

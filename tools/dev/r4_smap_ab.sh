@@ -1,13 +1,13 @@
 #!/bin/bash
 # GPU box (round 4 dev): C5 in-scan map update kernels per build_var variant (rocprofv3 kernel stats of
-# the C5 leg), twice each, interleaved. Usage: bash tools/r4_smap_ab.sh "v1 v2"   Output: gpurun_out/r4/smap_ab/
+# the C5 leg), twice each, interleaved. Usage: bash tools/dev/r4_smap_ab.sh "v1 v2"   Output: gpurun_out/r4/smap_ab/
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 vs=$1
 o=gpurun_out/r4/smap_ab; rm -rf $o; mkdir -p $o
 for r in 1 2; do
   for v in $vs; do
     d=$o/${v}_$r
-    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d -o kt --output-format csv -- python3 tools/ab_bench.py fl-slam_amd/build_var/$v/libgcslam.so --c5-only > $d.json 2> $d.err || exit 1
+    timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $d -o kt --output-format csv -- python3 tools/dev/ab_bench.py fl-slam_amd/build_var/$v/libgcslam.so --c5-only > $d.json 2> $d.err || exit 1
     f=$(find $d -name '*kernel_stats.csv' | head -1)
     python3 - "$f" "$v" "$r" <<'PY' | tee -a $o/ab.txt
 import csv, sys

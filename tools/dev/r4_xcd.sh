@@ -8,7 +8,7 @@ echo "tests rc=$rc $(tail -1 $o/tests.txt)"
 case $rc in 0|1) ;; *) exit $rc;; esac
 for r in 1 2 3; do
   for v in noxcd xcd; do
-    timeout -k 10 120 python3 tools/ab_bench.py fl-slam_amd/build_var/$v/libgcslam.so --map-only > $o/map_${v}_$r.json 2>/dev/null || exit 1
+    timeout -k 10 120 python3 tools/dev/ab_bench.py fl-slam_amd/build_var/$v/libgcslam.so --map-only > $o/map_${v}_$r.json 2>/dev/null || exit 1
     python3 -c "import json; m=json.loads(open('$o/map_${v}_$r.json').read().strip().splitlines()[-1])['c5_map_fuse']; print('rep $r $v fuse %.4f ms %.0f GB/s' % (m['ms'], m['GB/s']))" | tee -a $o/ab.txt
   done
 done

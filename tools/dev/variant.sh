@@ -1,6 +1,6 @@
 #!/bin/bash
 # Dev (CPU): build an A/B variant of libgcslam.so with extra -D flags on one source file.
-# Usage: bash tools/variant.sh <name> <source (.hip or .cpp, no suffix)> <flags...>  ->  fl-slam_amd/build_var/<name>/libgcslam.so
+# Usage: bash tools/dev/variant.sh <name> <source (.hip or .cpp, no suffix)> <flags...>  ->  fl-slam_amd/build_var/<name>/libgcslam.so
 set -e
 name=$1; src=$2; shift 2
 cd "$(dirname "$0")/../fl-slam_amd"
