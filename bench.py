@@ -57,6 +57,8 @@ def parse():
     ap.add_argument("--map-only", action="store_true",
                     help="run only the C5 PrimitiveMap fuse leg (PMC passes, tools/pmc_fuse.sh)")
     ap.add_argument("--c5-only", action="store_true", help="run only the C5 pipeline leg (PMC passes)")
+    ap.add_argument("--no-dropin", action="store_true", help="skip the per-operator drop-in leg")
+    ap.add_argument("--dropin-only", action="store_true", help="run only the per-operator drop-in leg")
     ap.add_argument("--map-layout", choices=("packed", "fields"), default="packed",
                     help="device PrimitiveMap layout of the map legs (fields = the reference's per-field arrays)")
     ap.add_argument("--io-given", action="store_true", help=argparse.SUPPRESS)
@@ -218,6 +220,9 @@ def main():
     H_total = args.hyps
     if args.map_only:
         print(json.dumps({"c5_map_fuse": map_fuse_leg(ctx, _abi, packed=args.map_layout == "packed")}), flush=True)
+        return
+    if args.dropin_only:
+        print(json.dumps({"dropin": dropin_leg(ctx, _abi)}), flush=True)
         return
     if args.c5_only:
         print(json.dumps({"c5": c5_leg(ctx, _abi, args), "c5_dense": c5_leg(ctx, _abi, args, cap=131072)}),
@@ -390,6 +395,8 @@ def main():
         out["fused_roofline"] = fused_roofline_leg(ctx, _abi, scans[0], B, n, H, bins, origin)
     if dist.rank == 0 and not args.no_map:
         out["c5_map_fuse"] = map_fuse_leg(ctx, _abi, packed=args.map_layout == "packed")
+    if dist.rank == 0 and dist.world == 1 and not args.no_dropin:
+        out["dropin"] = dropin_leg(ctx, _abi)
     if dist.rank == 0 and dist.world == 1 and not args.no_c5:
         out["c5"] = c5_leg(ctx, _abi, args)
         out["c5_dense"] = c5_leg(ctx, _abi, args, cap=131072)
@@ -583,6 +590,67 @@ def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5, m_
                                            H, cap, m_slots, voxel),
             "ms_per_scan": 1e3 * dt, "scans_per_s": 1.0 / dt, "steps": steps, "warmup": warmup,
             "map_slots_touched_last_scan": touched}
+
+
+def dropin_leg(ctx, _abi, K=4, cap=8192, n_az=4096, warm=3, scans=10):
+    """The reference node's own configuration through the per-operator drop-ins (gcslam.dropin_node):
+    K_HYP = 4 hypotheses, N_POINTS_CAP = 8192 (common/constants.py:62-64) on the 65,536-point synthetic
+    scan, each hypothesis's operator chain (budget, predict, windows, preintegration, deskew, directions,
+    soft-assign, moment match, Matrix-Fisher, planar, excitation, fusion, recompose, IW statistics, anchor
+    drift) with its point arrays and responsibilities device-resident, then the barycenter and the IW
+    applies (backend_node.py:2036-2119). ms per scan over `scans` scans after `warm`; the arena's hipMalloc /
+    hipFree count over the timed scans (0: every buffer reused)."""
+    import gc as _gc
+    from gcslam.belief import BeliefGaussianInfo
+    from gcslam.constants import GC_B_BINS, GC_CHART_ID, T_BASE_LIDAR
+    from gcslam.dropin_node import BinMap, DropinNode, IOGiven
+    from gcslam.ops import MeasurementNoiseIWState, ProcessNoiseIWState
+    from gcslam.ops.binning import create_fibonacci_atlas
+    from gcslam.pipeline import BatchedScanPipeline, PipelineConfig, iw_meas_prior, iw_process_prior
+    from gcslam.synth import make_hypotheses, make_io_evidence, make_scan
+    B = GC_B_BINS
+    bins = create_fibonacci_atlas(B).dirs
+    sc = [make_scan(k + 1, n_az=n_az) for k in range(2)]
+    n = sc[0]["points"].shape[0]
+    rec = warmup_map_record(ctx, _abi, make_scan(0, n_az=n_az), n, B, bins, np.asarray(T_BASE_LIDAR[:3]))
+    # the map-derived statistics by the device's k_map_derive (a one-hypothesis pipeline used as the tool)
+    p1 = BatchedScanPipeline(1, n, PipelineConfig(n_points_cap=cap), ctx=ctx)
+    p1.set_map(rec)
+    mp = p1.get_map()
+    p1.close()
+    hy = make_hypotheses(K)
+    Lio, hio, cio = make_io_evidence(K)
+    nuP, PsiP = iw_process_prior()
+    nuM, PsiM = iw_meas_prior()
+    pn = ProcessNoiseIWState(np.asarray(nuP, np.float64).reshape(7), np.asarray(PsiP, np.float64).reshape(7, 6, 6))
+    mn = MeasurementNoiseIWState(np.asarray(nuM, np.float64).reshape(3), np.asarray(PsiM, np.float64).reshape(3, 3, 3))
+    from gcslam.ops import process_noise_state_to_Q_jax
+    beliefs = [BeliefGaussianInfo(GC_CHART_ID, "initial", hy["X_anchor"][i], hy["stamp"][i], hy["z_lin"][i], hy["L"][i],
+                                  hy["h"][i]) for i in range(K)]
+    node = DropinNode(beliefs, hy["weights"], bins, BinMap(mp["map"], mp["derived"]), process_noise_state_to_Q_jax(pn),
+                      pn, mn, cap, ctx=ctx)
+    ios = [IOGiven(Lio[i], hio[i], cio[i]) for i in range(K)]
+    for k in range(warm):
+        node.process_scan(sc[k % 2], ios)
+    ctx.sync()
+    _gc.collect()
+    a0 = ctx.alloc_stats()
+    t0 = time.perf_counter()
+    for k in range(scans):
+        node.process_scan(sc[k % 2], ios)
+    ctx.sync()
+    dt = (time.perf_counter() - t0) / scans
+    _gc.collect()
+    a1 = ctx.alloc_stats()
+    return {"workload": "reference node configuration through the per-operator drop-ins: K_HYP = %d, N_POINTS_CAP = "
+                        "%d (stride %d from %d points), legacy bin-path operator chain per hypothesis + barycenter + "
+                        "IW applies (gcslam.dropin_node)" % (K, cap, -(-n // cap), n),
+            "ms_per_scan": 1e3 * dt, "scans_per_s": 1.0 / dt, "scans": scans, "warmup": warm,
+            "hip_mallocs": a1["hip_mallocs"] - a0["hip_mallocs"], "hip_frees": a1["hip_frees"] - a0["hip_frees"],
+            "arena_reuses": a1["reuses"] - a0["reuses"],
+            "note": "host-driven (one ctypes call + the certificate download per operator, as the reference's "
+                    "wrappers sync per cert); the reference publishes ~1-2 s per scan on its JAX GPU path "
+                    "(backend_node.py:1142, SURVEY §6)"}
 
 
 def primitive_map_1m(ctx, M, seed=20261015):

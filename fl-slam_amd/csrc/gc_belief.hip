@@ -129,53 +129,122 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   double* mu_prev = vec + kDZ;
   double* hpred = vec + 2 * kDZ;
   double* mu_inc = vec + 3 * kDZ;
+  double* xrow1 = vec + 4 * kDZ;  // the lift iterations' broadcast rows (waves 1 and 2)
+  double* xrow2 = vec + 5 * kDZ;
+  const double ef = exp(-2.0 * P.lambda_ou * S.dt);
+  const double dc = (1.0 - ef) / (2.0 * P.lambda_ou + kF64Eps);
 
   GC_PHASE(P, 0);
   // this thread's IMU slots, loaded beside the belief (one exposed latency for both) and parked in
   // the preintegration scratch (Bm..V2, 15 doubles per thread, not live before the IMU section)
   if (S.sig_cached) {
-    // the cached Σ / μ of the previous scan's evidence (L and h are not read): e^{-2λdt}Σ + dc Q formed
-    // here in W3 (wg_predict's second work matrix), its loads in flight with the IMU slots'
+    // the cached Σ / μ of the previous scan's evidence (L and h are not read): Σ' = e^{-2λdt}Σ + dc Q
+    // formed here in W3, its loads in flight with the IMU slots'
     const PredictPrefill pf = predict_prefill_load(P.Sig + (int64_t)h * N2, P.Q, P.mu_fin + (int64_t)h * n);
     imu_pair_store(load_imu_pair(P.M, S.imu_t, S.imu_g, S.imu_a), Bm + 15 * t);
     predict_prefill_store(pf, S.dt, P.lambda_ou, W3, mu_prev);
+    __syncthreads();
   } else {
     imu_pair_store(load_imu_pair(P.M, S.imu_t, S.imu_g, S.imu_a), Bm + 15 * t);
     for (int i = t; i < N2; i += kWG) Lp[i] = P.L[(int64_t)h * N2 + i];
     if (t < n) hprev[t] = P.h[(int64_t)h * n + t];
+    __syncthreads();
+    // μ = (L + εI)⁻¹ h and Σ = (L + εI)⁻¹ by the evidence kernel's routines (so the operands are those
+    // a cached scan would read, bit for bit), stored for the bins launch's L_pred workgroup
+    wg_solve_lifted(Lp, hprev, mu_prev, P.eps_lift, n, W1);  // W1 = chol(L + εI)
+    wg_chol_inverse(W1, W3, W2, n);                          // W3 = Σ
+    for (int i = t; i < N2; i += kWG) {
+      P.Sig[(int64_t)h * N2 + i] = W3[i];
+      W3[i] = ef * W3[i] + dc * P.Q[i];
+    }
+    if (t < n) P.mu_fin[(int64_t)h * n + t] = mu_prev[t];
+    __syncthreads();
+  }
+  // --- a2 predict (predict.py:43-98) split at its first projection. L_pred = PSD((Σ'_psd + ε_l I)⁻¹)
+  // and h_pred = L_pred μ are only read after the bins (evidence); the bins need ξ_body, i.e. the
+  // predicted moments μ_inc = (L_pred + ε_l I)⁻¹ h_pred and σ_warp² = (L_pred + ε_l I)⁻¹[15,15]
+  // (pipeline.py:436-453). With Σ'_psd = Σ'_sym certified (Cholesky of Σ'_sym − ε_psd I on wave 0, as
+  // the full chain's first projection), (L_pred + ε_l I)⁻¹ L_pred = (I + ε_l(Σ'_sym + ε_l I))⁻¹ =: K⁻¹
+  // (L_pred's own projection clamp is inactive whenever the lift iteration's bound holds: its
+  // eigenvalues are >= 1/(‖Σ'‖ + ε_l) > 4 ε_l >> ε_psd), so μ_inc = K⁻¹ μ and σ_warp² = (K⁻¹(Σ'_sym +
+  // ε_l I))[15,15], each a well-conditioned solve (wave_lift_iterate, waves 1 and 2) instead of the
+  // chain Cholesky → inverse → projection → Cholesky → solve of the ill-conditioned L_pred (cond ~1e13
+  // at the bench: the two routes agree to ~1e-16, oracle check in tests). L_pred / h_pred / the cert
+  // are then formed by lpred_wg in the bins launch beside the bin tasks (pred_mode 0). Wave 3: pose0
+  // = world pose of belief_prev and R0 = Exp(its rotation vector). If the certificate or the
+  // iteration's bound fails, the whole factorised chain runs here instead (pred_mode 1).
+  for (int idx = t; idx < N2; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    Sx[idx] = 0.5 * (W3[i * n + j] + W3[j * n + i]) - ((i == j) ? P.eps_psd : 0.0);
   }
   __syncthreads();
-  // --- a2 predict (predict.py:43-98): L_pred -> W1, h_pred, mu_prev, cert; and chol(L_pred + εI)
-  // -> W4 for the predicted moments (pipeline.py:436-453), factored on wave 1 beside L_pred's PSD
-  // certificate on wave 0, with pose0 = world pose of belief_prev on wave 3 (one lane; read after
-  // the barrier)
-  const auto pose0_side = [&]() {
-    if (t == 192) compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);
-  };
-  wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,
-             P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2, false,
-             S.sig_cached ? W3 : nullptr, nullptr,
-             W4, pose0_side, P.io_parts);
-  GC_PHASE(P, 1);
-  if (t < n) P.mu_aux[(int64_t)h * kMuAux + t] = mu_prev[t];
-  for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
-  if (t < n) P.hpred[(int64_t)h * n + t] = hpred[t];
-  GC_PHASE(P, 2);
-  GC_PHASE(P, 3);
-  // μ_inc on wave 0; beside it, one lane each of waves 1 and 2: σ_warp from (L_pred+εI)⁻¹[15,15]
-  // and R0 = Exp(rotvec of pose0) (pose0 from phase 1)
   if (t < 64) {
-    wave0_chol_solve<kDZ>(W4, hpred, mu_inc, n);
-  } else if (t == 64) {
-    const double s1515 = inv_diag_from_chol(W4, n, 15);
-    misc[6] = fmax(sqrt(s1515), 0.01);  // sigma_warp
-  } else if (t == 128) {
+    const bool okc = wave0_chol<kDZ, true>(Sx, n);
+    if (t == 0) red[4] = okc ? 0.0 : 1.0;
+  } else if (t < 128) {
+    const int lane = t - 64;
+    double x = 0.0;
+    const bool ok = wave_lift_iterate<kDZ>(W3, lane < n ? mu_prev[lane] : 0.0, P.eps_lift, xrow1, n, x);
+    if (lane < n) mu_inc[lane] = x;
+    if (lane == 0) red[5] = ok ? 0.0 : 1.0;
+  } else if (t < 192) {
+    const int lane = t - 128;
+    const double c = lane < n ? 0.5 * (W3[lane * n + 15] + W3[15 * n + lane]) + (lane == 15 ? P.eps_lift : 0.0) : 0.0;
+    double x = 0.0;
+    const bool ok = wave_lift_iterate<kDZ>(W3, c, P.eps_lift, xrow2, n, x);
+    if (lane == 15) misc[6] = fmax(sqrt(x), 0.01);  // sigma_warp
+    if (lane == 0) red[6] = ok ? 0.0 : 1.0;
+    // dt_imu (pipeline.py:526-535) from the parked IMU stamps: count, min and max over the valid
+    // (stamp > 0) samples, exact in any order; lane l takes the slots of threads l + 64 k
+    double cnt = 0.0, tmn = 1e308, tmx = -1e308;
+    for (int k = 0; k < 4; ++k) {
+      const int tt = lane + 64 * k;
+      const double sa = Bm[15 * tt], sb = Bm[15 * tt + 1];
+      if (2 * tt < P.M && sa > 0.0) { cnt += 1.0; tmn = fmin(tmn, sa); tmx = fmax(tmx, sa); }
+      if (2 * tt + 1 < P.M && sb > 0.0) { cnt += 1.0; tmn = fmin(tmn, sb); tmx = fmax(tmx, sb); }
+    }
+    cnt = wave_sum(cnt);
+    tmn = wave_min(tmn);
+    tmx = wave_max(tmx);
+    if (lane == 0) misc[7] = fmax(cnt >= 2.0 ? (tmx - tmn) / fmax(cnt - 1.0, 1.0) : 0.0, 1e-12);
+  } else if (t == 192) {
+    // pose0 = world pose of belief_prev = X ⊞ μ: with the cached posterior, the previous scan's
+    // k_combine_local already formed exactly this (compose_exp2 of the same X and μ_fin, the same
+    // routine) as the tape's world pose in P.diag[0:6]
+    if (S.sig_cached) {
+      for (int k = 0; k < 6; ++k) misc[k] = P.diag[(int64_t)h * kHypDiag + k];
+    } else {
+      compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);
+    }
     for (int k = 0; k < 6; ++k) P.mu_aux[(int64_t)h * kMuAux + 44 + k] = misc[k];
     double R0[9];
     so3_exp(misc + 3, R0);
     for (int k = 0; k < 9; ++k) misc[16 + k] = R0[k];
   }
   __syncthreads();
+  const bool fast = red[4] == 0.0 && red[5] == 0.0 && red[6] == 0.0 && P.predict_route == 0;
+  __syncthreads();
+  GC_PHASE(P, 1);
+  if (!fast) {
+    // the factorised route (predict.py:43-98 as restated in wg_predict): L_pred -> W1, h_pred, and
+    // chol(L_pred + ε_l I) -> W4 for the predicted moments; Σ' is in W3 (Sig_cached = W2 form)
+    wg_predict(Lp, hprev, P.Q, S.dt, P.eps_psd, P.eps_lift, P.lambda_ou, W1, hpred, mu_prev,
+               P.pred_cert + (int64_t)h * kPredCert, W2, W3, W4, Sx, red, c1, c2, false, W3, nullptr, W4,
+               NoSideWork(), P.io_parts);
+    for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)h * N2 + i] = W1[i];
+    if (t < n) P.hpred[(int64_t)h * n + t] = hpred[t];
+    if (t < 64) {
+      wave0_chol_solve<kDZ>(W4, hpred, mu_inc, n);
+    } else if (t == 64) {
+      const double s1515 = inv_diag_from_chol(W4, n, 15);
+      misc[6] = fmax(sqrt(s1515), 0.01);  // sigma_warp
+    }
+    __syncthreads();
+  }
+  if (t == 0) P.pred_mode[h] = fast ? 0.0 : 1.0;
+  if (t < n) P.mu_aux[(int64_t)h * kMuAux + t] = mu_prev[t];
+  GC_PHASE(P, 2);
+  GC_PHASE(P, 3);
   GC_PHASE(P, 4);
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + 22 + t] = mu_inc[t];
   // ------------------------------------------------------------------ IMU (a3)
@@ -184,15 +253,8 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   const double bg[3] = {mu_inc[9], mu_inc[10], mu_inc[11]};
   const double ba[3] = {mu_inc[12], mu_inc[13], mu_inc[14]};
   const int M = P.M;
-  // dt_imu over valid (stamp > 0) samples (pipeline.py:526-535)
-  double cnt = 0.0, tmin = 1e308, tmax = -1e308;  // over this thread's slots 2t, 2t+1 (exact in any order)
-  if (2 * t < M && q.ta > 0.0) { cnt += 1.0; tmin = fmin(tmin, q.ta); tmax = fmax(tmax, q.ta); }
-  if (2 * t + 1 < M && q.tb > 0.0) { cnt += 1.0; tmin = fmin(tmin, q.tb); tmax = fmax(tmax, q.tb); }
-  double ntmin = -tmin;
-  wg_sum_max2(cnt, ntmin, tmax, A);  // A: preintegration scratch, not yet live
-  const double nvalid = cnt;
-  tmin = -ntmin;
-  const double dt_imu = fmax(nvalid >= 2.0 ? (tmax - tmin) / fmax(nvalid - 1.0, 1.0) : 0.0, 1e-12);
+  // dt_imu over valid (stamp > 0) samples (pipeline.py:526-535), reduced on wave 2 in the first phase
+  const double dt_imu = misc[7];
   // two samples per thread: a = 2t, b = 2t+1
   const int ia = 2 * t, ib = 2 * t + 1;
   const double ta = q.ta, tb = q.tb;
@@ -201,19 +263,19 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   const double* R0 = misc + 16;
   double* pre = misc + 32;  // kPreint
   const double kG[3] = {0.0, 0.0, -9.81 * P.gravity_scale};  // GC_GRAVITY_W · imu_gravity_scale
-  GC_PHASE(P, 5);
-  wg_preintegrate(M, q, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, pre, P.io_parts);
-  GC_PHASE(P, 6);
   const double *ga = q.ga, *gb = q.gb, *aa = q.aa, *ab = q.ab;
   // --- scan-to-scan window: omega_avg and measurement-noise IW statistics
-  //     (pipeline.py:537-566, measurement_noise_iw_jax.py:130-218)
+  //     (pipeline.py:537-566, measurement_noise_iw_jax.py:130-218); their five sums reduced beside the
+  //     preintegration's p_end (one wg_sum_n, each element in wg_sum's order)
   auto wint = [&](int i, double ti) {
     return (i < M) ? window_weight(ti, S.t_last, S.t_scan, sigma_warp) * (ti > 0.0 ? 1.0 : 0.0) : 0.0;
   };
   const double wia = wint(ia, q.ta), wib = wint(ib, q.tb);
   double om[5] = {wia + wib, 0.0, 0.0, 0.0, wa + wb};
   for (int k = 0; k < 3; ++k) om[1 + k] = wia * (ga[k] - bg[k]) + wib * (gb[k] - bg[k]);
-  wg_sum_n<5>(om, A);  // A: preintegration scratch, free again (om[4]: ess_scan, wg_sum's order)
+  GC_PHASE(P, 5);
+  wg_preintegrate<true, 5>(M, q, wa, wb, R0, bg, ba, kG, A, Bm, V1, V2, pre, P.io_parts, om);
+  GC_PHASE(P, 6);
   const double ess_scan = om[4];
   const double wsum = om[0] + P.eps_mass;
   for (int k = 0; k < 3; ++k) om[k] = om[1 + k] / wsum;
@@ -238,13 +300,6 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   GC_PHASE(P, 7);
   wg_sum_n<12>(rr, A);
   GC_PHASE(P, 8);
-  if (t == 128) {
-    // pose_pred = X ⊕ μ_inc (for MF / planar in the later kernels; nothing here reads it) on wave 2
-    // beside the ξ_body and IW-statistics lanes
-    double pp[6];
-    compose_exp(P.X + (int64_t)h * 6, mu_inc, pp);
-    for (int k = 0; k < 6; ++k) P.pose_pred[(int64_t)h * 6 + k] = pp[k];
-  }
   if (t == 64) {  // ξ_body = se3_log(R0ᵀ Δpose) on wave 1 beside thread 0's IW statistics
     double dR[9], dpose[6], xi[6];
     mat3_mul_tn(R0, pre, dR);

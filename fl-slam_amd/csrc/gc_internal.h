@@ -2,7 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <map>
+#include <mutex>
 #include <string>
+#include <unordered_map>
 #include "../../include/gcslam.h"
 
 struct gc_comm;
@@ -26,6 +29,18 @@ struct gc_ctx {
   // an all-gather, and returns GC_ERR_RUNTIME (backend_node.py:2205-2210: log and re-raise).
   double wait_timeout_s = 300.0;
   gc_comm* comm = nullptr;
+  // Device buffer arena behind gc_buffer_alloc / gc_buffer_free (device buffers are owned
+  // by the context's arena): a freed block goes back to a per-size-class free list and is handed to
+  // the next allocation of its class with no hipMalloc / hipFree and no synchronisation. Every use of
+  // an arena buffer is ordered on this context's stream (the entries, uploads and downloads all run
+  // there), so a block freed while a queued kernel still reads it is only rewritten by work queued
+  // after that kernel. Blocks are returned to HIP at gc_ctx_trim / gc_ctx_destroy, or at once when the
+  // cache would exceed arena_cap bytes.
+  std::mutex arena_mu;
+  std::multimap<size_t, void*> arena_free;     // class size -> cached block
+  std::unordered_map<void*, size_t> arena_live;  // block -> class size
+  size_t arena_cached = 0, arena_live_bytes = 0, arena_cap = (size_t)16 << 30;
+  int64_t arena_hip_allocs = 0, arena_hip_frees = 0, arena_reuses = 0;
 };
 
 namespace gc {

@@ -20,6 +20,69 @@ constexpr int kNFac = 9;  // odom, imu, gyro, preint, planar, vz, odom_vel, odom
 constexpr int kIoU = (256 * 24 > kNFac * (kIoN2 + kDZ)) ? 256 * 24 : kNFac * (kIoN2 + kDZ);
 constexpr int kIoLdsDoubles = kIoU + 1024 + 8 + 64 + kNFac * kIofExtra;
 
+// The predict's L_pred half (predict.py:43-98 after its first projection), for hypothesis hl, in the
+// bins launch beside the bin tasks: the predict kernel certified Σ'_psd = Σ'_sym and formed the
+// predicted moments without L_pred (gc_belief.hip, pred_mode 0); here L_pred = PSD((Σ'_sym + ε_l I)⁻¹),
+// h_pred = L_pred μ and the predict certificate, by the routines and in the order of wg_predict's
+// certified path (wg_psd_fast_lifted_chol's lifted factor, wg_chol_inverse, the projection of L'),
+// so every value is the one the unsplit predict wrote. Only k_evidence reads them. pred_mode 1 (the
+// predict ran the whole chain itself): nothing to do. LDS: kLpredLdsDoubles.
+constexpr int kLpredLdsDoubles = 6 * kIoN2 + 4 * kDZ + 2 * kDZ + 8 + 8 + 4 * (kDZ + 2);
+GC_DEV void pose_pred_lane(const PipeDev& P, int hl) {
+  // pose_pred = X ⊞ μ_inc (for the IMU/odom branch, MF and planar; the predict kernel's bins need only
+  // ξ_body): one lane, beside lpred_wg's loads and factorization (read after its barriers)
+  double e[6], pp[6];
+  se3_exp(P.mu_aux + (int64_t)hl * kMuAux + 22, e);
+  se3_compose(P.X + (int64_t)hl * 6, e, pp);
+  for (int k = 0; k < 6; ++k) P.pose_pred[(int64_t)hl * 6 + k] = pp[k];
+}
+GC_DEV void lpred_wg(const PipeDev& P, const ScanArgs& S, int hl, double* sm) {
+  if (P.pred_mode[hl] != 0.0) {
+    if (threadIdx.x == 192) pose_pred_lane(P, hl);
+    __syncthreads();
+    return;
+  }
+  constexpr int n = kDZ, N2 = kIoN2;
+  double* W2 = sm;             // Σ', then L' raw
+  double* Cl = W2 + N2;        // chol(Σ'_sym + ε_l I)
+  double* Ws = Cl + N2;        // inverse scratch
+  double* Lo = Ws + N2;        // Σ'_psd, then L_pred
+  double* Sx = Lo + N2;        // 2 N2 + 4n (projection scratch)
+  double* mu = Sx + 2 * N2 + 4 * n;
+  double* ho = mu + n;
+  double* red = ho + n;        // 8
+  double* c2 = red + 8;        // 6 (+2)
+  double* cb = c2 + 8;         // 4 x (kDZ + 2): lane_chol's broadcast rows (no static LDS in k_bins_io)
+  const int t = threadIdx.x;
+  const PredictPrefill pf = predict_prefill_load(P.Sig + (int64_t)hl * N2, P.Q, P.mu_fin + (int64_t)hl * n);
+  predict_prefill_store(pf, S.dt, P.lambda_ou, W2, mu);
+  __syncthreads();
+  for (int idx = t; idx < N2; idx += kWG) {
+    const int i = idx / n, j = idx % n;
+    const double sym = 0.5 * (W2[i * n + j] + W2[j * n + i]);
+    Lo[idx] = sym;
+    Cl[idx] = sym + ((i == j) ? P.eps_lift : 0.0);
+  }
+  __syncthreads();
+  const double trace_cov = wg_sum(t < n ? Lo[t * n + t] : 0.0, red);
+  if (t == 192) pose_pred_lane(P, hl);  // wave 3, beside wave 0's factorization
+  wg_chol<true>(Cl, n, cb);
+  wg_chol_inverse(Cl, W2, Ws, n);  // L' raw
+  wg_psd_project_fast<NoSideWork, true>(W2, Lo, P.eps_psd, n, Sx, red, c2, NoSideWork(), cb);
+  wg_matvec(Lo, mu, ho, n);
+  for (int i = t; i < N2; i += kWG) P.Lpred[(int64_t)hl * N2 + i] = Lo[i];
+  if (t < n) P.hpred[(int64_t)hl * n + t] = ho[t];
+  if (t == 0) {
+    double* cert = P.pred_cert + (int64_t)hl * kPredCert;
+    const double lift = 2.0 * P.eps_lift * n;
+    const double psd = 0.0 + c2[0];  // the first projection's delta is 0 (certified)
+    cert[0] = lift; cert[1] = psd; cert[2] = c2[2]; cert[3] = c2[3]; cert[4] = c2[4]; cert[5] = c2[5];
+    cert[6] = trace_cov;
+    cert[7] = lift + psd + fabs(1.0 - S.dt);
+  }
+  __syncthreads();
+}
+
 GC_DEV void io_branch_wg(const PipeDev& P, const ScanArgs& S, const double* __restrict__ odom, int hl, double* sm) {
   double* FL = sm;                          // factor k: L at FL + k*(N2+22), h after it (after the vMF)
   double* A = sm;                           // preint scratch (aliases FL: dead before FL is zeroed)

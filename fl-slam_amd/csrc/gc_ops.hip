@@ -66,6 +66,22 @@ __global__ void __launch_bounds__(256) k_op_world_pose(const double* X, const do
   }
 }
 
+// ------------------------------------------------------------------ a17 lifted inverse
+// spd_cholesky_inverse_lifted_core (primitives.py:169-192): (L + ε I)⁻¹ by the Cholesky factor and
+// C⁻ᵀ C⁻¹ (the pipeline's routines: wg_inverse_lifted), n <= 22, one workgroup per matrix
+__global__ void __launch_bounds__(256) k_op_inverse_lifted(int n, const double* L, double eps_lift, double* out) {
+  extern __shared__ double sm[];
+  double* Ls = sm;
+  double* W = Ls + n * n;
+  double* W2 = W + n * n;
+  const int k = blockIdx.x, t = threadIdx.x;
+  for (int i = t; i < n * n; i += kWG) Ls[i] = L[(int64_t)k * n * n + i];
+  __syncthreads();
+  double* Linv = W2 + n * n;
+  wg_inverse_lifted(Ls, Linv, eps_lift, n, W, W2);
+  for (int i = t; i < n * n; i += kWG) out[(int64_t)k * n * n + i] = Linv[i];
+}
+
 // --------------------------------------------------------------------------------- a2
 __global__ void __launch_bounds__(256) k_op_predict(const double* L, const double* h, const double* Q, double dt,
                                                     double eps_psd, double eps_lift, double lambda_ou,
@@ -588,6 +604,16 @@ int32_t gc_belief_world_pose_batch(gc_ctx* ctx, int32_t H, const double* d_X, co
   const size_t sh = lds_bytes(2 * kNN + 2 * kDZ);
   hipLaunchKernelGGL(k_op_world_pose, dim3(H), dim3(256), sh, ctx->stream, d_X, d_L, d_h, eps_lift, d_pose_out,
                      d_mean_out);
+  GC_LAUNCH_CHECK(ctx);
+  return GC_OK;
+}
+
+int32_t gc_spd_inverse_lifted_batch(gc_ctx* ctx, int32_t H, int32_t n, const double* d_L, double eps_lift,
+                                    double* d_out) {
+  GC_OP_CTX(ctx);
+  GC_CHECK_ARG(ctx, H > 0 && n >= 1 && n <= kDZ && d_L && d_out, "bad arguments (n in [1, 22])");
+  hipLaunchKernelGGL(k_op_inverse_lifted, dim3(H), dim3(256), lds_bytes(4 * n * n), ctx->stream, n, d_L, eps_lift,
+                     d_out);
   GC_LAUNCH_CHECK(ctx);
   return GC_OK;
 }

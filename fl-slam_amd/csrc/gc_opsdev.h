@@ -395,9 +395,13 @@ GC_DEV ImuPair imu_pair_load(const double* d) {
   for (int k = 0; k < 3; ++k) { q.ga[k] = d[3 + k]; q.gb[k] = d[6 + k]; q.aa[k] = d[9 + k]; q.ab[k] = d[12 + k]; }
   return q;
 }
+// ENDS: only R_end and p_end are formed (out[0:12]; the batched predict's ξ_body needs nothing else),
+// with NX further per-thread values (extra, replaced by their workgroup sums) reduced beside p_end in
+// the same wg_sum_n (the same order per element as their own reduction would give).
+template <bool ENDS = false, int NX = 0>
 GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const double* R0, const double* bg,
                             const double* ba, const double* g, double* A, double* Bm, double* V1, double* V2,
-                            double* out, double* sink = nullptr) {
+                            double* out, double* sink = nullptr, double* extra = nullptr) {
   const int t = threadIdx.x;
   (void)sink;
   const int ia = 2 * t, ib = 2 * t + 1;
@@ -493,6 +497,20 @@ GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const
     const double va = (t > 0) ? vs[(t - 1) * 3 + k] : 0.0;
     const double vb = va + awa[k] * dea;
     pc[k] = va * dea + 0.5 * awa[k] * (dea * dea) + vb * deb + 0.5 * awb[k] * (deb * deb);
+  }
+  if constexpr (ENDS) {
+    double s[3 + NX];
+    for (int k = 0; k < 3; ++k) s[k] = pc[k];
+    for (int i = 0; i < NX; ++i) s[3 + i] = extra[i];
+    GC_MARK(sink, 43);
+    wg_sum_n<3 + NX>(s, Bm);
+    for (int i = 0; i < NX; ++i) extra[i] = s[3 + i];
+    if (t == 0) {
+      mat3_mul(R0, src + (kWG - 1) * 9, out);  // R_end
+      for (int k = 0; k < 3; ++k) out[9 + k] = s[k];  // p_end (world)
+    }
+    __syncthreads();
+    return;
   }
   double sums[13];
   for (int k = 0; k < 3; ++k) {

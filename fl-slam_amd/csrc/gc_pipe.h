@@ -34,6 +34,8 @@ struct PipeDev {
   int B;         // bins
   int M;         // IMU slots (<= 512)
   int geom_H;    // bins chunk geometry as for this many hypotheses (0: Hl)
+  int predict_route;  // 0: split predict (lift solves, L_pred in the bins launch) when certified; 1: always
+                      // the factorised chain in the predict kernel (gc_pipeline_set_predict_route)
   int cus;       // compute units of the pipeline's device (ctx->device, queried once at create): every
                  // grid-size decision (predict's budget workgroups, the chain kernels' occupancy) uses it
   int64_t n_in, n_cap;
@@ -45,6 +47,9 @@ struct PipeDev {
   // per local hypothesis
   double *X, *z, *L, *h, *stamp;           // belief (in/out)
   double *Lpred, *hpred, *pred_cert, *pose_pred, *xi, *imu_out, *dPsiM;
+  double *pred_mode;                       // (Hl) 0: L_pred / h_pred / pred_cert are formed by the bins
+                                           // launch's workgroup of the hypothesis (lpred_wg); 1: by the
+                                           // predict kernel itself (its factorised fallback route)
   double *stats, *bincert;                 // (Hl, B, 38), (Hl, 8)
   double *binaux;                          // (Hl, B, 2) per-bin [projection delta, mass-eps ratio]
   double *io_L, *io_h, *io_cert;           // IMU/odom-branch evidence (computed or given)

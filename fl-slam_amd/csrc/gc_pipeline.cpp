@@ -324,14 +324,15 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   int rc = GC_OK;
   double** fields[] = {&P.X, &P.z, &P.L, &P.h, &P.stamp, &P.Lpred, &P.hpred, &P.pred_cert, &P.pose_pred, &P.xi,
                        &P.imu_out, &P.dPsiM, &P.stats, &P.bincert, &P.io_L, &P.io_h, &P.io_cert, &P.dPsiP,
-                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose, &P.Sig, &P.binaux, &P.hcond};
+                       &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose, &P.Sig, &P.binaux, &P.hcond,
+                       &P.pred_mode};
   const size_t sizes[] = {(size_t)Hl * 6, (size_t)Hl * 22, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl,
                           (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kPredCert, (size_t)Hl * 6,
                           (size_t)Hl * 6, (size_t)Hl * gc::kImuOut, (size_t)Hl * 27, (size_t)Hl * B * 38,
                           (size_t)Hl * 8, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kIoCert,
                           (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag, (size_t)Hl * gc::kMuAux,
                           (size_t)Hl * gc::kIoParts, (size_t)Hl * 36, (size_t)Hl * NN, (size_t)Hl * B * 2,
-                          (size_t)Hl * 8};
+                          (size_t)Hl * 8, (size_t)Hl};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert,
@@ -993,6 +994,14 @@ int32_t gc_pipeline_stage_ms(gc_pipeline* p, float* h_ms) {
   for (int i = 0; i + 1 < GC_STAGE_N; ++i)
     GC_HIP(p->ctx, hipEventElapsedTime(&h_ms[i], p->st_ev[i], p->st_ev[i + 1]));
   GC_HIP(p->ctx, hipEventElapsedTime(&h_ms[GC_STAGE_N - 1], p->st_ev[0], p->st_ev[GC_STAGE_N - 1]));
+  return GC_OK;
+}
+
+int32_t gc_pipeline_set_predict_route(gc_pipeline* p, int32_t route) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  GC_CHECK_ARG(p->ctx, route == 0 || route == 1, "route must be 0 (split) or 1 (factorised)");
+  p->P.predict_route = route;
   return GC_OK;
 }
 

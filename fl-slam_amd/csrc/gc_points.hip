@@ -520,6 +520,10 @@ GC_DEV void sa_store_block(const double* S, double* Rh, int64_t wbase, int64_t n
 // (at 3, the 168-VGPR budget spilled ~12-27 VGPRs per point to scratch: 0.6 GB of extra HBM reads and
 // 0.9 GB of extra writes per C3 launch, tools/probe/probe_sa3.hip; 1.74 -> 1.32 ms)
 constexpr int kSaOcc = 2;
+// the responsibility rows' store kind (A/B builds): 0 non-temporal (default), 1 plain, 2 sc1 write-through
+#ifndef GC_SA_STORE
+#define GC_SA_STORE 0
+#endif
 // dynamic LDS of a soft-assign workgroup (doubles): exp table | bins (x, y, z rows of 64) | reduction |
 // 4 wave slabs (FULL: 32 rows of 16 BPL + 2; ragged: 64 rows of 18)
 __host__ __device__ constexpr bool sa_linear(int BPL, bool full) { return full && BPL <= 3; }  // B = 64: 16-bin blocks (register budget)
@@ -643,7 +647,13 @@ __global__ void __launch_bounds__(256, kSaOcc) k_soft_assign(int64_t n, int B, i
         const int64_t pbase = wbase + 32 * hf;
         double* dst = Rh + pbase * NB;
         const auto put = [&](int o, const dvec2& v) {
+#if GC_SA_STORE == 1
+          *reinterpret_cast<dvec2*>(dst + o) = v;  // plain
+#elif GC_SA_STORE == 2
+          asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(dst + o), "v"(v) : "memory");  // write-through
+#else
           __builtin_nontemporal_store(v, reinterpret_cast<dvec2*>(dst + o));
+#endif
         };
         if (pbase + 32 <= n) {  // wave-uniform: the whole block is in range (every block but the tail's)
 #pragma unroll
@@ -720,6 +730,11 @@ constexpr int kMomFS = 34;
 // PAIR (B >= 32, 16-B aligned rows): bins 0..31 arrive as one 16-B load per lane (bins 2l, 2l+1 of its
 // point: four 256-B row segments per load instead of two loads of four 128-B segments); tile 0 holds
 // the even bins, tile 1 the odd ones (row i of tile j < 2 is bin 2i + j), tiles >= 2 bins 16j + l.
+#ifndef GC_MOM_FORWARD
+constexpr bool kMomReverse = true;
+#else
+constexpr bool kMomReverse = false;
+#endif
 template <int BPL, bool COV, bool LAM, int NACC, bool PAIR>
 __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, int groups,
                                                            const double* __restrict__ pts,
@@ -731,12 +746,16 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
   constexpr int NF = COV ? NF_BASE + NF_COV : NF_BASE;
   constexpr int NT = (NF + 15) / 16;  // feature tiles (zero-padded to 16 NT)
   extern __shared__ double lds[];
-  const int h = blockIdx.y;
+  // workgroups run the (hypothesis, chunk) grid from its end: the soft-assign before this kernel wrote
+  // the responsibilities in ascending block order, so the last-written (still in the Infinity Cache /
+  // L2) are read first (records, and so the sums, are the same in either order)
+  const int bx = kMomReverse ? (int)(gridDim.x - 1 - blockIdx.x) : (int)blockIdx.x;
+  const int h = kMomReverse ? (int)(gridDim.y - 1 - blockIdx.y) : (int)blockIdx.y;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, bl = lane & 15;
   double* F = lds + wv * (16 * NT * kMomFS);
   const double o[3] = {o0, o1, o2};
   const double* Rh = resp + (int64_t)h * n * B;
-  const int64_t wbeg = ((int64_t)blockIdx.x * 4 + wv) * groups * 32;
+  const int64_t wbeg = ((int64_t)bx * 4 + wv) * groups * 32;
   int64_t wend = wbeg + (int64_t)groups * 32;
   wend = wend < n ? wend : n;
   const int ng = wbeg < n ? (int)((wend - wbeg + 31) / 32) : 0;
@@ -863,10 +882,10 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
         if (b < B && k < NF) red[(wv * B + b) * NF + k] = NACC == 2 ? acc[0][j][t][r] + acc[NACC - 1][j][t][r] : acc[0][j][t][r];
       }
   __syncthreads();
-  int64_t npts = n - (int64_t)blockIdx.x * 4 * groups * 32;
+  int64_t npts = n - (int64_t)bx * 4 * groups * 32;
   npts = npts < 0 ? 0 : (npts > (int64_t)4 * groups * 32 ? (int64_t)4 * groups * 32 : npts);
   const int RL = B * NF + REC_EXTRA;
-  double* rec = partials + ((int64_t)h * gridDim.x + blockIdx.x) * RL;
+  double* rec = partials + ((int64_t)h * gridDim.x + bx) * RL;
   for (int i = threadIdx.x; i < B * NF; i += kWG)
     rec[i] = (red[i] + red[B * NF + i]) + (red[2 * B * NF + i] + red[3 * B * NF + i]);
   if (threadIdx.x < REC_EXTRA) rec[B * NF + threadIdx.x] = threadIdx.x == 3 ? (double)npts : 0.0;
@@ -1183,8 +1202,8 @@ __device__ double g_task_trace[4 * 16384];  // per task [start, end, puller, XCD
 #endif
 template <int BPL, bool FULL>
 __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
-                                                             const double* __restrict__ odom, int n_io, int H,
-                                                             int64_t chunks, unsigned* ctr) {
+                                                             const double* __restrict__ odom, int n_io, int io_on,
+                                                             int H, int64_t chunks, unsigned* ctr) {
   extern __shared__ double lds[];
   unsigned& task_s = *reinterpret_cast<unsigned*>(lds + fused_lds_doubles(A.B));  // the launch's extra double
 #ifdef GC_BINS_TIMING
@@ -1193,7 +1212,8 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
   int bt_n = 0;
 #endif
   if ((int)blockIdx.x < n_io) {
-    io_branch_wg(P, S, odom, blockIdx.x, lds);
+    lpred_wg(P, S, blockIdx.x, lds);  // the predict's L_pred half (pred_mode 0), then the IMU/odom branch
+    if (io_on) io_branch_wg(P, S, odom, blockIdx.x, lds);
 #ifdef GC_BINS_TIMING
     if (threadIdx.x == 0 && blockIdx.x < 8192) {
       double* g = g_bins_trace + 4 * blockIdx.x;
@@ -1739,15 +1759,18 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   if (int rc = gc::scratch(ctx, sizeof(double) * RL * chunks * H, &scr)) return rc;
   const FusedArgs FA{P.n_cap, B, iters, d_pts, d_t, d_w, P.budget, S.t0, S.t1, P.xi, P.bins, 1.0 / P.tau,
                      P.o0, P.o1, P.o2, (double*)scr, P.w_win, k1, kItersShort, k2, kItersTiny};
-  const int n_io = io ? H : 0;
+  // one auxiliary workgroup per hypothesis first: the predict's L_pred half (lpred_wg), then, when io,
+  // the IMU/odom branch
+  const int n_io = H, io_on = io ? 1 : 0;
   // + 1: the pullers' task slot after the fused layout (no static LDS in k_bins_io: the dynamic block
   // starts at LDS address 0, so the exp table's addresses need no base add, exp2s_shift_tab_n)
-  const size_t sh = sizeof(double) * (std::max<size_t>(fused_lds_doubles(B), io ? (size_t)kIoLdsDoubles : 0) + 1);
+  const size_t sh = sizeof(double) * (std::max<size_t>(std::max<size_t>(fused_lds_doubles(B), (size_t)kLpredLdsDoubles),
+                                                       io ? (size_t)kIoLdsDoubles : 0) + 1);
   const dim3 grid((unsigned)(n_io + pullers));
 #define GC_BIO(BP, FULL)                                                                                       \
   GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_bins_io<BP, FULL>, sh));                                      \
   if (int rc_ = gc::ensure_no_static_lds(ctx, (const void*)k_bins_io<BP, FULL>)) return rc_;                  \
-  hipLaunchKernelGGL((k_bins_io<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA, P, S, d_odom, n_io, H, chunks, \
+  hipLaunchKernelGGL((k_bins_io<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA, P, S, d_odom, n_io, io_on, H, chunks, \
                      P.task_ctr)
   const int bpl = bpl_for(B);
   const bool full = B == 16 * bpl;

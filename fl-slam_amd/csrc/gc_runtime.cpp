@@ -212,6 +212,8 @@ int32_t gc_ctx_destroy(gc_ctx* ctx) {
   (void)gc::wait_stream(ctx, ctx->stream, "the stream at context destruction");
   if (ctx->scratch) (void)hipFree(ctx->scratch);
   if (ctx->slot_runs) (void)hipFree(ctx->slot_runs);
+  for (auto& kv : ctx->arena_free) (void)hipFree(kv.second);
+  for (auto& kv : ctx->arena_live) (void)hipFree(kv.first);  // buffers not freed before the context
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return GC_OK;
@@ -242,19 +244,90 @@ int32_t gc_test_bounded_wait(double timeout_s, int64_t ready_after_polls, double
   return rc;
 }
 
+// size class of an arena block: 256-B granules up to 4 KiB, then quarter steps of the power of two
+// below (<= 25 % slack), so buffers of one shape always share a class
+static size_t arena_class(uint64_t bytes) {
+  size_t b = bytes ? (size_t)bytes : 16;
+  if (b <= 4096) return (b + 255) & ~(size_t)255;
+  size_t p = (size_t)1 << (63 - __builtin_clzll((unsigned long long)b));
+  const size_t step = p >> 2;
+  return (b + step - 1) / step * step;
+}
+
 int32_t gc_buffer_alloc(gc_ctx* ctx, uint64_t bytes, void** d_ptr) {
   GC_CHECK_ARG(nullptr, ctx && d_ptr, "NULL argument");
+  const size_t c = arena_class(bytes);
+  {
+    std::lock_guard<std::mutex> lock(ctx->arena_mu);
+    auto it = ctx->arena_free.find(c);
+    if (it != ctx->arena_free.end()) {
+      *d_ptr = it->second;
+      ctx->arena_free.erase(it);
+      ctx->arena_cached -= c;
+      ctx->arena_live[*d_ptr] = c;
+      ctx->arena_live_bytes += c;
+      ctx->arena_reuses += 1;
+      return GC_OK;
+    }
+  }
   GC_HIP(ctx, hipSetDevice(ctx->device));
-  GC_HIP(ctx, hipMalloc(d_ptr, bytes ? bytes : 16));
+  GC_HIP(ctx, hipMalloc(d_ptr, c));
+  std::lock_guard<std::mutex> lock(ctx->arena_mu);
+  ctx->arena_live[*d_ptr] = c;
+  ctx->arena_live_bytes += c;
+  ctx->arena_hip_allocs += 1;
   return GC_OK;
 }
 
 int32_t gc_buffer_free(gc_ctx* ctx, void* d_ptr) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   if (!d_ptr) return GC_OK;
+  size_t c = 0;
+  {
+    std::lock_guard<std::mutex> lock(ctx->arena_mu);
+    auto it = ctx->arena_live.find(d_ptr);
+    GC_CHECK_ARG(ctx, it != ctx->arena_live.end(), "not a live buffer of this context (gc_buffer_alloc)");
+    c = it->second;
+    ctx->arena_live.erase(it);
+    ctx->arena_live_bytes -= c;
+    if (ctx->arena_cached + c <= ctx->arena_cap) {  // cached for the next allocation of its class
+      ctx->arena_free.emplace(c, d_ptr);
+      ctx->arena_cached += c;
+      return GC_OK;
+    }
+  }
+  // over the cap: returned to HIP after the stream's queued work (which may still read it)
   GC_HIP(ctx, hipSetDevice(ctx->device));
   if (int rc = gc::wait_stream(ctx, ctx->stream, "the stream before a buffer free")) return rc;
   GC_HIP(ctx, hipFree(d_ptr));
+  std::lock_guard<std::mutex> lock(ctx->arena_mu);
+  ctx->arena_hip_frees += 1;
+  return GC_OK;
+}
+
+int32_t gc_ctx_trim(gc_ctx* ctx) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_HIP(ctx, hipSetDevice(ctx->device));
+  if (int rc = gc::wait_stream(ctx, ctx->stream, "the stream before an arena trim")) return rc;
+  std::lock_guard<std::mutex> lock(ctx->arena_mu);
+  for (auto& kv : ctx->arena_free) {
+    GC_HIP(ctx, hipFree(kv.second));
+    ctx->arena_hip_frees += 1;
+  }
+  ctx->arena_free.clear();
+  ctx->arena_cached = 0;
+  return GC_OK;
+}
+
+int32_t gc_ctx_alloc_stats(gc_ctx* ctx, int64_t* h_out6) {
+  GC_CHECK_ARG(nullptr, ctx && h_out6, "NULL argument");
+  std::lock_guard<std::mutex> lock(ctx->arena_mu);
+  h_out6[0] = ctx->arena_hip_allocs;
+  h_out6[1] = ctx->arena_hip_frees;
+  h_out6[2] = ctx->arena_reuses;
+  h_out6[3] = (int64_t)ctx->arena_live.size();
+  h_out6[4] = (int64_t)ctx->arena_live_bytes;
+  h_out6[5] = (int64_t)ctx->arena_cached;
   return GC_OK;
 }
 

@@ -148,11 +148,18 @@ GC_DEV void wg_copy(double* dst, const double* src, int count) {
 // readlane (it feeds the next pivot), L[k+2..][k] through a 22-double LDS row of the calling wave
 // (one ds_write per lane, then same-address broadcast reads, no readlane hazard NOPs). One wave, in
 // program order, so the LDS row needs no barrier.
-template <int NM, bool CHECKED>
-GC_DEV void lane_chol(double (&a)[NM], int lane, bool& ok) {
+// DYN: the broadcast rows live in the caller's dynamic LDS (dyn, 4 x (NM + 2) doubles) instead of a
+// static block, for kernels whose dynamic LDS must start at address 0 (k_bins_io's lpred_wg)
+template <int NM, bool CHECKED, bool DYN = false>
+GC_DEV void lane_chol(double (&a)[NM], int lane, bool& ok, double* dyn = nullptr) {
   // one broadcast row per wave: two waves may factor two matrices at once
-  __shared__ __attribute__((aligned(16))) double colbufs[4][NM + 2];
-  double* colbuf = colbufs[threadIdx.x >> 6];
+  double* colbuf;
+  if constexpr (DYN) {
+    colbuf = dyn + (threadIdx.x >> 6) * (NM + 2);
+  } else {
+    __shared__ __attribute__((aligned(16))) double colbufs[4][NM + 2];
+    colbuf = colbufs[threadIdx.x >> 6];
+  }
 #pragma unroll
   for (int k = 0; k < NM; ++k) {
     double piv = readlane_f64(a[k], k);
@@ -193,22 +200,23 @@ GC_DEV void lane_store_lower(double* A, int n, int lane, const double (&a)[NM]) 
 
 // wave-0 factorization padded to NM = 8 (the 6x6 / 3x3 blocks of IW, Q, pose-6) or kDZ = 22:
 // the padded identity costs full columns, so small blocks take the short form
-template <int NM, bool CHECKED>
-GC_DEV bool wave0_chol(double* A, int n) {
+template <int NM, bool CHECKED, bool DYN = false>
+GC_DEV bool wave0_chol(double* A, int n, double* dyn = nullptr) {
   const int lane = threadIdx.x & 63;  // any single wave (wave 0, or wave 1 beside a wave-0 factorization)
   double a[NM];
   lane_load_rows<NM>(A, n, lane, a);
   bool ok = true;
-  lane_chol<NM, CHECKED>(a, lane, ok);
+  lane_chol<NM, CHECKED, DYN>(a, lane, ok, dyn);
   lane_store_lower<NM>(A, n, lane, a);
   return ok;
 }
 
 // In-place lower Cholesky of the n x n (row-major) A; upper triangle zeroed.
-GC_DEV void wg_chol(double* A, int n) {
+template <bool DYN = false>
+GC_DEV void wg_chol(double* A, int n, double* dyn = nullptr) {
   if (threadIdx.x < 64) {
-    if (n <= 8) (void)wave0_chol<8, false>(A, n);
-    else (void)wave0_chol<kDZ, false>(A, n);
+    if (n <= 8) (void)wave0_chol<8, false, DYN>(A, n, dyn);
+    else (void)wave0_chol<kDZ, false, DYN>(A, n, dyn);
   }
   __syncthreads();
 }
@@ -507,9 +515,9 @@ struct NoSideWork {
   GC_DEV void operator()() const {}
 };
 // side(): optional wave-level work for wave 2, run beside the Cholesky (no barrier inside)
-template <typename Side = NoSideWork>
+template <typename Side = NoSideWork, bool DYN = false>
 GC_DEV void wg_psd_project_fast(const double* M, double* Mp, double eps, int n, double* scratch,
-                                double* red, double* cert6, const Side& side = Side()) {
+                                double* red, double* cert6, const Side& side = Side(), double* dyn = nullptr) {
   for (int idx = threadIdx.x; idx < n * n; idx += kWG) {
     const int i = idx / n, j = idx % n;
     scratch[idx] = 0.5 * (M[i * n + j] + M[j * n + i]) - ((i == j) ? eps : 0.0);
@@ -517,7 +525,7 @@ GC_DEV void wg_psd_project_fast(const double* M, double* Mp, double eps, int n, 
   __syncthreads();
   // Cholesky on wave 0; the symmetry deviation (cert field 1) on wave 1 meanwhile
   if (threadIdx.x < 64) {
-    const bool okc = n <= 8 ? wave0_chol<8, true>(scratch, n) : wave0_chol<kDZ, true>(scratch, n);
+    const bool okc = n <= 8 ? wave0_chol<8, true, DYN>(scratch, n, dyn) : wave0_chol<kDZ, true, DYN>(scratch, n, dyn);
     if (threadIdx.x == 0) red[4] = okc ? 0.0 : 1.0;
   } else if (threadIdx.x < 128) {
     double symloc = 0.0;
@@ -610,6 +618,45 @@ GC_DEV void wg_psd_fast_lifted_chol(const double* M, double* Mp, double eps, dou
 GC_DEV void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
   __builtin_amdgcn_wave_barrier();
+}
+
+// x = (I + B)⁻¹ b with B = ε (S_sym + ε I), S an n x n LDS matrix (row-major, symmetrised here), on one
+// wave: lane i < n owns row i of B and b_i (b_lane), and returns x_i. This is (L' + εI)⁻¹ L' applied
+// in the predict when L' = (S + εI)⁻¹ (a lifted inverse): (L' + εI)⁻¹ L' = (I + ε(S + εI))⁻¹, whose
+// matrix is within ‖B‖ of the identity, so a Richardson iteration x ← b − B x (from x = b) converges
+// by a factor ‖B‖∞ per step and its rounding is that of one well-conditioned product; the step count
+// is the one that takes ‖B‖∞^k below 2^-56 (uniform over the wave). Returns false (x = b) when
+// ‖B‖∞ > 1/4: the caller then takes the factorised route. xrow: an n-double LDS row of this wave.
+template <int NM>
+GC_DEV bool wave_lift_iterate(const double* S, double b_lane, double eps, double* xrow, int n, double& x_out) {
+  const int lane = threadIdx.x & 63;
+  const bool live = lane < n;
+  double br[NM];
+  double rs = 0.0;
+#pragma unroll
+  for (int j = 0; j < NM; ++j) {
+    const bool in = live && j < n;
+    br[j] = in ? eps * (0.5 * (S[lane * n + j] + S[j * n + lane]) + (j == lane ? eps : 0.0)) : 0.0;
+    rs += fabs(br[j]);
+  }
+  const double r = wave_max(rs);
+  const double bi = live ? b_lane : 0.0;
+  x_out = bi;
+  if (!(r <= 0.25)) return false;
+  const int iters = r > 0.0 ? (int)ceil(38.816242111356935 / -log(r)) : 1;  // 56 ln 2 / -ln r
+  double xi = bi;
+  for (int it = 0; it < iters; ++it) {
+    if (live) xrow[lane] = xi;
+    wave_lds_sync();
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int j = 0; j < NM; ++j)
+      if (j < n) s[j & 3] = fma(br[j], xrow[j], s[j & 3]);
+    wave_lds_sync();  // every lane's reads of the row are done before the next step rewrites it
+    xi = bi - ((s[0] + s[1]) + (s[2] + s[3]));
+  }
+  x_out = xi;
+  return true;
 }
 
 // The parallel cyclic Jacobi of wg_jacobi_eigh (eigenvalues only) on wave 0 for n <= 16: the

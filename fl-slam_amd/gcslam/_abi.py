@@ -36,6 +36,8 @@ SIGNATURES = {
     "gc_test_device_spin": [_vp, _f64],
     "gc_buffer_alloc": [_vp, _u64, C.POINTER(_vp)],
     "gc_buffer_free": [_vp, _vp],
+    "gc_ctx_trim": [_vp],
+    "gc_ctx_alloc_stats": [_vp, _vp],
     "gc_buffer_upload": [_vp, _vp, _vp, _u64],
     "gc_buffer_download": [_vp, _vp, _vp, _u64],
     "gc_buffer_copy": [_vp, _vp, _vp, _u64],
@@ -97,6 +99,7 @@ SIGNATURES = {
     "gc_pipeline_stage_ms": [_vp, _vp],
     "gc_pipeline_host_stats": [_vp, _vp, _i32],
     "gc_pipeline_set_inscan_certs": [_vp, _i32],
+    "gc_pipeline_set_predict_route": [_vp, _i32],
     "gc_comm_unique_id": [_vp],
     "gc_comm_init": [_vp, _i32, _i32, _vp, C.POINTER(_vp)],
     "gc_comm_destroy": [_vp],
@@ -105,6 +108,7 @@ SIGNATURES = {
     "gc_comm_allgather_f64": [_vp, _vp, _vp, _vp, _i64],
     "gc_lie_batch": [_vp, _i32, _i64, _vp, _vp],
     "gc_belief_world_pose_batch": [_vp, _i32, _vp, _vp, _vp, _f64, _vp, _vp],
+    "gc_spd_inverse_lifted_batch": [_vp, _i32, _i32, _vp, _f64, _vp],
     "gc_predict_diffusion_batch": [_vp, _i32, _vp, _vp, _vp, _f64, _f64, _f64, _f64, _vp, _vp, _vp],
     "gc_smooth_window_weights": [_vp, _i32, _vp, _f64, _f64, _f64, _vp],
     "gc_preintegrate_imu_batch": [_vp, _i32, _i32, _vp, _vp, _vp, _vp, _i64, _vp, _vp, _vp, _dptr, _vp],
@@ -228,6 +232,17 @@ class Context:
     def sync(self):
         check(lib().gc_ctx_synchronize(self.handle), self)
 
+    def alloc_stats(self) -> dict:
+        """The device-buffer arena's counters (include/gcslam.h gc_ctx_alloc_stats)."""
+        out = np.zeros(6, np.int64)
+        check(lib().gc_ctx_alloc_stats(self.handle, out.ctypes.data), self)
+        return dict(zip(("hip_mallocs", "hip_frees", "reuses", "live", "live_bytes", "cached_bytes"),
+                        (int(v) for v in out)))
+
+    def trim(self):
+        """Return the arena's cached blocks to HIP."""
+        check(lib().gc_ctx_trim(self.handle), self)
+
     def set_wait_timeout(self, seconds: float):
         """Bound of every host wait on this context (fail fast; include/gcslam.h gc_ctx_synchronize)."""
         check(lib().gc_ctx_set_wait_timeout(self.handle, float(seconds)), self)
@@ -245,16 +260,43 @@ class Context:
 
 
 class DeviceArray:
-    """A device allocation with a NumPy dtype/shape view for staging."""
+    """A device allocation (the context's arena, include/gcslam.h gc_buffer_alloc) with a NumPy
+    dtype/shape view. The device-resident drop-ins accept one wherever an array goes and return one
+    with device_out=True, so a chain of operators keeps its point arrays and responsibilities in HBM
+    (as the reference's jnp arrays stay on the JAX device, backend_node.py:1679-1690);
+    np.asarray(d) downloads it."""
 
-    def __init__(self, ctx: Context, shape, dtype=np.float64):
+    def __init__(self, ctx: Context, shape, dtype=np.float64, _base=None, _ptr=None):
         self.ctx = ctx
         self.shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
         self.dtype = np.dtype(dtype)
         self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        self._base = _base  # a view keeps its base alive and never frees
+        if _ptr is not None:
+            self.ptr = _ptr
+            return
         p = _vp()
         check(lib().gc_buffer_alloc(ctx.handle, max(self.nbytes, 16), C.byref(p)), ctx)
         self.ptr = p.value
+
+    def view(self, shape, offset_elems: int = 0) -> "DeviceArray":
+        """A non-owning view of (part of) this buffer with another shape (no copy)."""
+        shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
+        nb = int(np.prod(shape, dtype=np.int64)) * self.dtype.itemsize
+        if offset_elems < 0 or offset_elems * self.dtype.itemsize + nb > self.nbytes:
+            raise ValueError(f"view {shape} at {offset_elems} exceeds the buffer {self.shape}")
+        return DeviceArray(self.ctx, shape, self.dtype, _base=self, _ptr=self.ptr + offset_elems * self.dtype.itemsize)
+
+    @property
+    def ndim(self) -> int:
+        return len(self.shape)
+
+    def __len__(self):
+        return self.shape[0]
+
+    def __array__(self, dtype=None, copy=None):
+        a = self.download()
+        return a if dtype is None else a.astype(dtype)
 
     @classmethod
     def from_host(cls, ctx: Context, arr, dtype=np.float64):
@@ -278,9 +320,9 @@ class DeviceArray:
         check(lib().gc_buffer_memset(self.ctx.handle, self.ptr, 0, self.nbytes), self.ctx)
 
     def free(self):
-        if self.ptr:
+        if self.ptr and self._base is None and self.ctx.handle:
             lib().gc_buffer_free(self.ctx.handle, self.ptr)
-            self.ptr = None
+        self.ptr = None
 
     def __del__(self):
         try:
@@ -308,6 +350,28 @@ class Event:
             lib().gc_event_destroy(self.handle)
         except Exception:
             pass
+
+
+def device_input(ctx: Context, x, dtype=np.float64, shape=None) -> DeviceArray:
+    """x as a device array of dtype (and shape, if given): a DeviceArray is used in place (a reshaped
+    view when only the shape differs), anything else is uploaded into an arena buffer."""
+    if isinstance(x, DeviceArray):
+        if x.dtype != np.dtype(dtype):
+            raise ValueError(f"device array of dtype {x.dtype}, expected {np.dtype(dtype)}")
+        if shape is not None and tuple(shape) != x.shape:
+            if int(np.prod(shape)) != int(np.prod(x.shape)):
+                raise ValueError(f"device array of shape {x.shape}, expected {tuple(shape)}")
+            return x.view(shape)
+        return x
+    a = np.ascontiguousarray(x, dtype=dtype)
+    if shape is not None:
+        a = a.reshape(shape)
+    return DeviceArray.from_host(ctx, a, dtype)
+
+
+def host(x):
+    """A host NumPy view of x (downloads a DeviceArray)."""
+    return x.download() if isinstance(x, DeviceArray) else np.asarray(x)
 
 
 _tls = threading.local()

@@ -5,9 +5,9 @@ result dataclasses and (Result, CertBundle, ExpectedEffect) returns; compute run
 from .point_budget import PointBudgetResult, point_budget_resample
 from .deskew_constant_twist import DeskewConstantTwistResult, deskew_constant_twist
 from .binning import (BinAtlas, BinSoftAssignResult, ScanBinStats, bin_soft_assign,
-                      create_fibonacci_atlas, scan_bin_moment_match)
+                      create_fibonacci_atlas, point_directions, scan_bin_moment_match)
 from .kappa import kappa_from_resultant_batch
-from .primitives import domain_projection_psd, domain_projection_psd_batch
+from .primitives import domain_projection_psd, domain_projection_psd_batch, spd_cholesky_inverse_lifted
 from .predict import predict_diffusion
 from .imu_preintegration import (imu_accel_meas_iw_suffstats_from_gravity_dir_jax,
                                  imu_gyro_meas_iw_suffstats_from_avg_rate_jax,
@@ -36,8 +36,8 @@ from .imu_odom_evidence import (ImuDependenceInflationResult, ImuGyroEvidenceRes
 __all__ = [
     "PointBudgetResult", "point_budget_resample", "DeskewConstantTwistResult",
     "deskew_constant_twist", "BinAtlas", "BinSoftAssignResult", "ScanBinStats",
-    "bin_soft_assign", "create_fibonacci_atlas", "scan_bin_moment_match",
-    "kappa_from_resultant_batch", "domain_projection_psd", "domain_projection_psd_batch",
+    "bin_soft_assign", "create_fibonacci_atlas", "point_directions", "scan_bin_moment_match",
+    "kappa_from_resultant_batch", "domain_projection_psd", "domain_projection_psd_batch", "spd_cholesky_inverse_lifted",
     "predict_diffusion", "smooth_window_weights", "preintegrate_imu_relative_pose_jax",
     "imu_gyro_meas_iw_suffstats_from_avg_rate_jax", "imu_accel_meas_iw_suffstats_from_gravity_dir_jax",
     "MatrixFisherResult", "PlanarTranslationResult", "ScatterMetrics", "matrix_fisher_rotation_evidence",

@@ -27,24 +27,33 @@ class PointBudgetResult:
     indices: np.ndarray = None  # selected source rows (-1 padded): the integer contract
 
 
+def _rows(x, width=None) -> int:
+    sh = x.shape if isinstance(x, _abi.DeviceArray) else np.shape(x)
+    n = int(np.prod(sh)) if sh else 1
+    return n // width if width else n
+
+
 def point_budget_resample(points, timestamps, weights, ring=None, tag=None,
                           n_points_cap: int = GC_N_POINTS_CAP, chart_id: str = GC_CHART_ID,
-                          anchor_id: str = "initial", ctx=None
+                          anchor_id: str = "initial", ctx=None, device_out: bool = False
                           ) -> Tuple[PointBudgetResult, CertBundle, ExpectedEffect]:
+    """Host arrays or DeviceArrays in; with device_out the result's arrays stay in HBM (DeviceArray)."""
     ctx = ctx or _abi.default_context()
-    P = np.ascontiguousarray(points, dtype=np.float64).reshape(-1, 3)
-    n = P.shape[0]
-    T = np.ascontiguousarray(timestamps, dtype=np.float64).reshape(-1)
-    W = np.ascontiguousarray(weights, dtype=np.float64).reshape(-1)
-    if T.shape[0] != n or W.shape[0] != n:
-        raise ValueError(f"timestamps/weights must be ({n},), got {T.shape}, {W.shape}")
+    n = _rows(points, 3)
+    if _rows(timestamps) != n or _rows(weights) != n:
+        raise ValueError(f"timestamps/weights must be ({n},), got {np.shape(timestamps)}, {np.shape(weights)}")
     if n == 0 or n_points_cap <= 0:
         raise ValueError("point_budget_resample needs n_input > 0 and n_points_cap > 0")
-    RG = np.zeros(n, np.uint8) if ring is None else np.ascontiguousarray(ring, np.uint8).reshape(-1)
-    TG = np.zeros(n, np.uint8) if tag is None else np.ascontiguousarray(tag, np.uint8).reshape(-1)
     cap = int(n_points_cap)
-    dev = {k: _abi.DeviceArray.from_host(ctx, v, v.dtype) for k, v in
-           dict(p=P, t=T, w=W, r=RG, g=TG).items()}
+    dev = dict(p=_abi.device_input(ctx, points, np.float64, (n, 3)),
+               t=_abi.device_input(ctx, timestamps, np.float64, (n,)),
+               w=_abi.device_input(ctx, weights, np.float64, (n,)))
+    for k, v in (("r", ring), ("g", tag)):
+        if v is None:
+            dev[k] = _abi.DeviceArray(ctx, n, np.uint8)
+            dev[k].zero()
+        else:
+            dev[k] = _abi.device_input(ctx, v, np.uint8, (n,))
     out_p = _abi.DeviceArray(ctx, (cap, 3)); out_t = _abi.DeviceArray(ctx, cap)
     out_w = _abi.DeviceArray(ctx, cap); out_r = _abi.DeviceArray(ctx, cap, np.uint8)
     out_g = _abi.DeviceArray(ctx, cap, np.uint8); out_i = _abi.DeviceArray(ctx, cap, np.int64)
@@ -54,9 +63,10 @@ def point_budget_resample(points, timestamps, weights, ring=None, tag=None,
               out_g.ptr, out_i.ptr, scal.ptr, ctx=ctx)
     s = scal.download()
     mass_in = float(s[0])
-    res = PointBudgetResult(points=out_p.download(), timestamps=out_t.download(), weights=out_w.download(),
-                            ring=out_r.download(), tag=out_g.download(), n_input=n, n_output=int(s[5]),
-                            total_mass_in=mass_in, total_mass_out=mass_in, indices=out_i.download())
+    get = (lambda d: d) if device_out else (lambda d: d.download())
+    res = PointBudgetResult(points=get(out_p), timestamps=get(out_t), weights=get(out_w),
+                            ring=get(out_r), tag=get(out_g), n_input=n, n_output=int(s[5]),
+                            total_mass_in=mass_in, total_mass_out=mass_in, indices=get(out_i))
     support_frac = min(1.0, cap / (n + GC_EPS_MASS))
     cert = CertBundle.create_approx(
         chart_id=chart_id, anchor_id=anchor_id, triggers=["PointBudgetResample"],

@@ -7,7 +7,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from .. import _abi
-from ..constants import GC_EPS_PSD
+from ..constants import GC_EPS_LIFT, GC_EPS_PSD
 
 
 @dataclass
@@ -37,6 +37,20 @@ def domain_projection_psd_batch(M, eps_psd: float = GC_EPS_PSD, ctx=None):
     do = _abi.DeviceArray(ctx, A.shape); dc = _abi.DeviceArray(ctx, (b, 6))
     _abi.call("gc_domain_projection_psd_batch", ctx.handle, b, d, dm.ptr, float(eps_psd), do.ptr, dc.ptr, ctx=ctx)
     return do.download(), dc.download()
+
+
+def spd_cholesky_inverse_lifted(L, eps_lift: float = GC_EPS_LIFT, ctx=None, device_out: bool = False):
+    """spd_cholesky_inverse_lifted_core (common/primitives.py:169-192): ((L + eps_lift I)⁻¹, lift) for
+    an n x n (or a batch (b, n, n)) SPD matrix, n <= 22, host or DeviceArray in."""
+    ctx = ctx or _abi.default_context()
+    sh = L.shape if isinstance(L, _abi.DeviceArray) else np.shape(L)
+    n = sh[-1]
+    b = int(np.prod(sh[:-2])) if len(sh) > 2 else 1
+    dL = _abi.device_input(ctx, L, np.float64, (b, n, n))
+    out = _abi.DeviceArray(ctx, (b, n, n))
+    _abi.call("gc_spd_inverse_lifted_batch", ctx.handle, b, n, dL.ptr, float(eps_lift), out.ptr, ctx=ctx)
+    res = out.view(sh) if device_out else out.download().reshape(sh)
+    return res, float(eps_lift) * n
 
 
 def domain_projection_psd(M, eps_psd: float = GC_EPS_PSD, ctx=None) -> DomainProjectionPSDResult:

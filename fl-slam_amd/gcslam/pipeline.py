@@ -231,6 +231,11 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_get_hyp_diag", _p(o))
         return o
 
+    def set_predict_route(self, factorised: bool) -> None:
+        """a2 predict route: the split route (default; predicted moments solved from Σ' directly, L_pred
+        formed beside the bins) or the factorised chain in the predict kernel (include/gcslam.h)."""
+        self._call("gc_pipeline_set_predict_route", 1 if factorised else 0)
+
     def set_inscan_certs(self, on: bool = True) -> None:
         """Compute the per-hypothesis predict / fusion ConditioningCerts inside every later scan
         (right after its evidence kernel), as the reference emits them on every call."""

@@ -62,8 +62,16 @@ int32_t gc_ctx_set_wait_timeout(gc_ctx* ctx, double seconds);
  * enqueues a one-thread kernel that keeps the stream busy for `seconds` (<= 10) and then exits. */
 int32_t gc_test_bounded_wait(double timeout_s, int64_t ready_after_polls, double* h_waited_ms);
 int32_t gc_test_device_spin(gc_ctx* ctx, double seconds);
+/* Device buffers from the context's arena (SURVEY §8b ownership): gc_buffer_free returns a block to a
+ * per-size-class cache and the next allocation of that class takes it back, so a steady-state chain of
+ * per-operator calls performs no hipMalloc / hipFree and no synchronisation. All work on arena buffers
+ * must be ordered on the context's stream (as every libgcslam entry is). gc_ctx_trim returns the cached
+ * blocks to HIP; gc_ctx_alloc_stats: [hipMalloc calls, hipFree calls, arena reuses, live buffers,
+ * live bytes, cached bytes]. */
 int32_t gc_buffer_alloc(gc_ctx* ctx, uint64_t bytes, void** d_ptr);
 int32_t gc_buffer_free(gc_ctx* ctx, void* d_ptr);
+int32_t gc_ctx_trim(gc_ctx* ctx);
+int32_t gc_ctx_alloc_stats(gc_ctx* ctx, int64_t* h_out6);
 /* Synchronous copies (stream-ordered, then waited). */
 int32_t gc_buffer_upload(gc_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes);
 int32_t gc_buffer_download(gc_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes);
@@ -327,6 +335,12 @@ int32_t gc_pipeline_get_hyp_conditioning(gc_pipeline* p, double* h_out);
 /* In-scan ConditioningCerts (off by default): on != 0 makes every later scan emit the certificates
  * gc_pipeline_get_hyp_conditioning reads, as the reference emits them on every predict / fusion call. */
 int32_t gc_pipeline_set_inscan_certs(gc_pipeline* p, int32_t on);
+/* The a2 predict's route (predict.py:43-98). 0 (default): split at its first projection — when
+ * Σ'_psd = Σ'_sym is certified, the predicted moments the bins need (μ_inc, σ_warp) are solved from Σ'
+ * directly, (L_pred + ε_l I)⁻¹ L_pred = (I + ε_l(Σ' + ε_l I))⁻¹, and L_pred / h_pred / the predict cert
+ * are formed in the bins launch beside the bin tasks; otherwise the factorised chain runs. 1: always the
+ * factorised chain in the predict kernel (tests compare the two routes). */
+int32_t gc_pipeline_set_predict_route(gc_pipeline* p, int32_t route);
 /* L_evidence[pose, pose] (Hl, 6, 6) of the last scan, as the reference's MinimalScanTape.L_pose6
    (pipeline.py:1537). */
 int32_t gc_pipeline_get_lpose6(gc_pipeline* p, double* h_lpose);
@@ -511,6 +525,10 @@ int32_t gc_imu_vmf_gravity_tr_batch(gc_ctx* ctx, int32_t H, int32_t M, const dou
 #define GC_LIE_NOPS 8
 int32_t gc_lie_batch(gc_ctx* ctx, int32_t op, int64_t n, const double* d_in, double* d_out);
 
+/* spd_cholesky_inverse_lifted_core (common/primitives.py:169-192): d_out = (L + eps_lift I)⁻¹ for H
+ * n x n SPD matrices (n <= 22), by the Cholesky factor and C⁻ᵀ C⁻¹ as in the batched pipeline. */
+int32_t gc_spd_inverse_lifted_batch(gc_ctx* ctx, int32_t H, int32_t n, const double* d_L, double eps_lift,
+                                    double* d_out);
 /* BeliefGaussianInfo.mean_increment + world pose X ∘ Exp(δz) (common/belief.py:373-425). */
 int32_t gc_belief_world_pose_batch(gc_ctx* ctx, int32_t H, const double* d_X, const double* d_L, const double* d_h,
                                    double eps_lift, double* d_pose_out, double* d_mean_out);

@@ -101,3 +101,33 @@ def test_predict_reuses_posterior_factorisation_bit_exactly(ctx):
         outs.append((b["L"], b["h"], b["z_lin"], b["X_anchor"], pipe.combined()["L"], pipe.get_iw()["Psi_proc"]))
     for a, b in zip(*outs):
         assert np.array_equal(a, b)
+
+
+def test_split_predict_matches_factorised_route(ctx):
+    """The split predict (μ_inc, σ_warp solved from Σ' by the lift iteration, L_pred / h_pred / the
+    predict cert formed in the bins launch: gc_belief.hip, gc_iobranch_wg.h lpred_wg) against the
+    factorised chain (gc_pipeline_set_predict_route(1), the unsplit wg_predict) on the same inputs over
+    three scans: L_pred-side outputs bit for bit at the first scan (same routines, same operands),
+    everything within the rounding of the two routes afterwards."""
+    case = cases.build(H=4, n_az=256, n_scans=3)
+    outs = []
+    for route in (0, 1):
+        pipe = _gpu_pipeline(case, ctx)
+        pipe.set_predict_route(bool(route))
+        st = case["state"]
+        per = []
+        for k, s in enumerate(case["scans"]):
+            pipe.stage_scan(0, s)
+            pipe.run_scan(0, s, st.scan_count + k)
+            ctx.sync()
+            stats, bcert, xi = pipe.bin_stats()
+            per.append((pipe.get_beliefs(), xi, pipe.hyp_diag(), pipe.combined()))
+        outs.append(per)
+    for k, (a, b) in enumerate(zip(*outs)):
+        (ba, xa, da, ca), (bb, xb, db, cb) = a, b
+        _close(xa, xb, 1e-12, 1e-15, f"scan{k} xi_body")
+        _close(ba["L"], bb["L"], 1e-12, 0.0, f"scan{k} L")
+        _close(ba["X_anchor"], bb["X_anchor"], 0.0, 1e-12, f"scan{k} X_anchor")
+        _close(ba["z_lin"], bb["z_lin"], 1e-9, 1e-14, f"scan{k} z_lin")
+        _close(da[:, 0:6], db[:, 0:6], 0.0, 1e-12, f"scan{k} world pose")
+        _close(ca["L"], cb["L"], 1e-12, 0.0, f"scan{k} combined L")

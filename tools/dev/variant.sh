@@ -3,7 +3,7 @@
 # Usage: bash tools/dev/variant.sh <name> <source (.hip or .cpp, no suffix)> <flags...>  ->  fl-slam_amd/build_var/<name>/libgcslam.so
 set -e
 name=$1; src=$2; shift 2
-cd "$(dirname "$0")/../fl-slam_amd"
+cd "$(dirname "$0")/../../fl-slam_amd"
 d=build_var/$name; mkdir -p $d
 f=csrc/$src.hip; [ -f $f ] || f=csrc/$src.cpp
 /opt/rocm/bin/hipcc -O3 -std=c++17 -fPIC --offload-arch=gfx950 -Wall -Wno-unused-function -I../include "$@" -c $f -o $d/$src.o
