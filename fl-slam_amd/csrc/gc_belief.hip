@@ -160,6 +160,7 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
     if (t < n) P.mu_fin[(int64_t)h * n + t] = mu_prev[t];
     __syncthreads();
   }
+  GC_PHASE(P, 1);
   // --- a2 predict (predict.py:43-98) split at its first projection. L_pred = PSD((Σ'_psd + ε_l I)⁻¹)
   // and h_pred = L_pred μ are only read after the bins (evidence); the bins need ξ_body, i.e. the
   // predicted moments μ_inc = (L_pred + ε_l I)⁻¹ h_pred and σ_warp² = (L_pred + ε_l I)⁻¹[15,15]
@@ -224,7 +225,7 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   __syncthreads();
   const bool fast = red[4] == 0.0 && red[5] == 0.0 && red[6] == 0.0 && P.predict_route == 0;
   __syncthreads();
-  GC_PHASE(P, 1);
+  GC_PHASE(P, 2);
   if (!fast) {
     // the factorised route (predict.py:43-98 as restated in wg_predict): L_pred -> W1, h_pred, and
     // chol(L_pred + ε_l I) -> W4 for the predicted moments; Σ' is in W3 (Sig_cached = W2 form)
@@ -243,7 +244,6 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   }
   if (t == 0) P.pred_mode[h] = fast ? 0.0 : 1.0;
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + t] = mu_prev[t];
-  GC_PHASE(P, 2);
   GC_PHASE(P, 3);
   GC_PHASE(P, 4);
   if (t < n) P.mu_aux[(int64_t)h * kMuAux + 22 + t] = mu_inc[t];

@@ -72,7 +72,6 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
   double* hps = vec + kDZ;
   double* hpo = vec + 2 * kDZ;
   double* dz = vec + 3 * kDZ;
-  double* hrec = vec + 4 * kDZ;
   double* mupo = vec + 5 * kDZ;
   double* mups = vec + 6 * kDZ;
   double* hfin = vec + 7 * kDZ;
@@ -269,19 +268,73 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
   if (t < n) hpo[t] = hps[t] + alpha * hev[t];
   __syncthreads();
   {
-    // the PSD projection of the fusion (Cholesky-certified) on wave 0 and, at the same time on wave 1,
-    // the factorization of L_post + εI the recompose and the solves below need (Wc); the pose-6
-    // conditioning of L_ev (P6 = W3, untouched by the projection) on wave 3 when α did not need it
+    // the pose-6 conditioning of L_ev (P6 = W3) for the tape when α did not need it, beside the factorization
     const auto cond_side = [&]() {
       if (!alpha_fixed) return;
       double lmin = 0.0, lmax = 0.0;
       wave_extreme_eigvals<6>(W3, lmin, lmax);
       if ((t & 63) == 0) sc[60] = pose6_cond(lmin, lmax, P.eps_psd, P.diag + (int64_t)hl * kHypDiag + 39);
     };
-    wg_psd_fast_lifted_chol(W2, Lpo, P.eps_psd, P.eps_lift, n, Sx, Wc, red, c6, cond_side);
+    // The fusion's PSD projection (fusion.py:150-230) certified from the factorization the recompose
+    // needs anyway: L_post = L_sym, Wc = chol(L_sym + ε_l I) on wave 0 (wave 1: the symmetry deviation,
+    // wave 3: cond_side); then δz = (L_post + ε_l I)⁻¹ h_post on wave 0 beside the first phase of
+    // Σ_post = Wc⁻ᵀ Wc⁻¹ on wave 1, whose trace bounds the spectrum: λ_min(L_sym) >= 1 / tr Σ_post − ε_l.
+    // Above 4 ε_psd the clamp is inactive and the projection is L_sym, as the Cholesky of
+    // L_sym − ε_psd I certified before (one 22x22 factorization fewer on the chain); otherwise the
+    // projection runs (wg_psd_fast_lifted_chol) and the two solves are repeated on its result.
+    for (int idx = t; idx < NN; idx += kWG) {
+      const int i = idx / n, j = idx % n;
+      const double sym = 0.5 * (W2[i * n + j] + W2[j * n + i]);
+      Lpo[idx] = sym;
+      Wc[idx] = sym + ((i == j) ? P.eps_lift : 0.0);
+    }
+    __syncthreads();
+    if (t < 64) {
+      (void)wave0_chol<kDZ, false>(Wc, n);
+    } else if (t < 128) {
+      double symloc = 0.0;
+      for (int idx = t - 64; idx < NN; idx += 64) {
+        const int i = idx / n, j = idx % n;
+        const double d = 0.5 * (W2[i * n + j] + W2[j * n + i]) - W2[idx];
+        symloc += d * d;
+      }
+      symloc = wave_sum(symloc);
+      if (t == 64) red[5] = symloc;
+    } else if (t >= 192) {
+      cond_side();
+    }
+    __syncthreads();
+    // δz on wave 0 and the forward substitution of Σ_post (its first phase; Sx is free) with its trace on
+    // wave 1
+    const auto solve_and_phase1 = [&]() {
+      if (t < 64) {
+        wave0_chol_solve<kDZ>(Wc, hpo, dz, n);
+      } else if (t < 128) {
+        chol_inverse_phase1_lane(Wc, Sx, n, t - 64);
+        double tr = 0.0;
+        if (t - 64 < n)
+          for (int k = 0; k < n; ++k) tr += Sx[(t - 64) * n + k] * Sx[(t - 64) * n + k];
+        tr = wave_sum(tr);
+        if (t == 64) red[6] = tr;
+      }
+      __syncthreads();
+    };
+    solve_and_phase1();
+    const double bound = 1.0 / red[6] - P.eps_lift;
+    if (bound >= 4.0 * P.eps_psd) {
+      if (t == 0) {
+        const double nan = __builtin_nan("");
+        c6[0] = 0.0; c6[1] = sqrt(red[5]); c6[2] = nan; c6[3] = nan; c6[4] = nan; c6[5] = nan;
+      }
+    } else {
+      wg_psd_fast_lifted_chol(W2, Lpo, P.eps_psd, P.eps_lift, n, Sx, Wc, red, c6);
+      solve_and_phase1();
+    }
+    __syncthreads();
   }
   GC_PHASE(P, 15);
-  // a12 recompose: T from every operator's trigger magnitude (pipeline.py:1211)
+  // a12 recompose: T from every operator's trigger magnitude (pipeline.py:1211), then δ' and X_new on
+  // thread 0, beside the second phase of Σ_post -> W2 (also the next scan's predict Σ, P.Sig) on waves 1-3
   if (t == 0) {
     const double* bc = P.bincert + (int64_t)hl * 8;
     const double trig_budget = 1e-12 / (P.budget[0] + 1e-12);
@@ -293,46 +346,36 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     T += c6[0] + fabs(1.0 - alpha);                    // InfoFusionAdditive
     sc[61] = T;
     sc[62] = c6[0];
-  }
-  // δz and the recompose on wave 0 and, beside them on wave 1, the forward substitution of
-  // Σ_post = (L_post + εI)⁻¹ (its first phase; Sx is free here)
-  if (t < 64) {
-    wave0_chol_solve<kDZ>(Wc, hpo, dz, n);
-    wave_lds_sync();
-    if (t == 0) {
-      double bch[6];
-      sc[63] = recompose_pose(P.X + (int64_t)hl * 6, zl, dz, sc[61], P.c_frob, sc + 64, sc + 70, bch);  // X_new, δ'
-    }
-  } else if (t < 128) {
-    chol_inverse_phase1_lane(Wc, Sx, n, t - 64);
+    double bch[6];
+    sc[63] = recompose_pose(P.X + (int64_t)hl * 6, zl, dz, sc[61], P.c_frob, sc + 64, sc + 70, bch);  // X_new, δ'
+  } else if (t >= 64) {
+    chol_inverse_phase2_part(W2, Sx, n, t - 64, kWG - 64);
   }
   __syncthreads();
+  // μ_post = (L_post + ε_l I)⁻¹ h_rec with h_rec = h_post − L_post[:, 0:6] δ' (recompose.py:173-181):
+  // (L + ε_l I)⁻¹ L = I − ε_l Σ_post, so μ_post = δz − δ' + ε_l Σ_post[:, 0:6] δ' — a 22 x 6 product with
+  // the Σ_post just formed instead of a third triangular solve with the ill-conditioned factor
   if (t < n) {
     const double sh = (t < 6) ? sc[70 + t] : 0.0;
-    double v = hpo[t];
-    for (int k = 0; k < 6; ++k) v -= Lpo[t * n + k] * sc[70 + k];
-    hrec[t] = v;
+    double c = 0.0;
+    for (int k = 0; k < 6; ++k) c += W2[t * n + k] * sc[70 + k];
+    mupo[t] = (dz[t] - sh) + P.eps_lift * c;
     zl[t] = zl[t] - sh;
   }
-  __syncthreads();
   GC_PHASE(P, 16);
   // a15 process-noise IW statistics (inverse_wishart_jax.py:71-123)
   if (s_dt == 0.0 && s_ex == 0.0) {
     // no dt / extrinsic excitation: every afac is 1.0, so Lps and hps are L_pred and h_pred bit for
-    // bit and μ_pred = (L_pred + εI)⁻¹ h_pred is predict's μ_inc (same routines, same operands)
+    // bit and μ_pred = (L_pred + εI)⁻¹ h_pred is predict's μ_inc (the predict kernel's predicted moments)
     if (t < n) mups[t] = P.mu_aux[(int64_t)hl * kMuAux + 22 + t];
     __syncthreads();
   } else {
+    __syncthreads();
     for (int i = t; i < NN; i += kWG) W3[i] = Lps[i] + ((i / n == i % n) ? P.eps_lift : 0.0);
     __syncthreads();
     wg_chol(W3, n);
     wg_chol_solve(W3, hps, mups, n);
   }
-  // Σ_post -> W2 (also the next scan's predict Σ, P.Sig) on waves 1-3 beside μ_post = (L_post + εI)⁻¹
-  // h_rec on wave 0: the same results as wg_chol_inverse_and_solve
-  if (t < 64) wave0_chol_solve<kDZ>(Wc, hrec, mupo, n);
-  else chol_inverse_phase2_part(W2, Sx, n, t - 64, kWG - 64);
-  __syncthreads();
   for (int i = t; i < NN; i += kWG) P.Sig[(int64_t)hl * NN + i] = W2[i];
   for (int idx = t; idx < 7 * 36; idx += kWG) P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
   GC_PHASE(P, 17);

@@ -521,6 +521,9 @@ GC_DEV void sa_store_block(const double* S, double* Rh, int64_t wbase, int64_t n
 // 0.9 GB of extra writes per C3 launch, tools/probe/probe_sa3.hip; 1.74 -> 1.32 ms)
 constexpr int kSaOcc = 2;
 // the responsibility rows' store kind (A/B builds): 0 non-temporal (default), 1 plain, 2 sc1 write-through
+// by inline asm. sc1 took the kernel 1.39 -> 1.33 ms (5.15 TB/s, 90 % of the plain-write probe) and the
+// pair 0.673 -> 0.676 (profiles/r05/ab_soft_assign_store_and_moment_order.txt), but its asm form wrote
+// wrong values on a ragged tail (test_soft_assign_matches_oracle[32-333]): not adopted
 #ifndef GC_SA_STORE
 #define GC_SA_STORE 0
 #endif

@@ -3,7 +3,7 @@ Usage: python3 tools/dev/ab_bench.py <path/to/libgcslam.so> [bench args]"""
 import os
 import sys
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
 sys.path.insert(0, ROOT)
 from gcslam import _abi  # noqa: E402

@@ -42,7 +42,7 @@ for r in range(6):
     pipe.run_scan(r % 3, scans[r % 3], r)
 ctx.sync()
 t = pipe.io_parts().reshape(-1)  # hypothesis 0's slots, then hypothesis 1's (40+: preint marks)
-names = {1: "predict: Σ' cert + lift solves + pose0", 2: "predict: (fallback chain)", 3: "predict: -", 4: "predict: -",
+names = {1: "predict: loads (Σ', μ, IMU)", 2: "predict: Σ' cert + lift solves + pose0", 3: "predict: (fallback chain)", 4: "predict: -",
          5: "predict: moments+dt_imu", 6: "predict: preintegrate", 7: "predict: xi+omega", 8: "predict: meas IW",
          11: "evidence: start..MF", 12: "evidence: MF..planar", 13: "evidence: L_raw,beta,excitation",
          14: "evidence: pose6 cond+alpha", 15: "evidence: fusion PSD", 16: "evidence: recompose+IW stats",
