@@ -10,6 +10,15 @@
 
 struct gc_comm;
 
+namespace gc {
+// a device run hash (gc_runs.h RunTable): 2^bits 8-B entries, all empty between uses
+struct RunTableBuf {
+  void* ptr = nullptr;
+  uint32_t bits = 0;
+  bool dirty = true;  // a fill is due (new, grown, or a call that failed between its two passes)
+};
+}  // namespace gc
+
 struct gc_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
@@ -17,12 +26,8 @@ struct gc_ctx {
   void* scratch = nullptr;  // growable device scratch (per ctx, stream-ordered use only)
   size_t scratch_bytes = 0;
   int cu_count = 0;  // compute units of the device (queried on first use)
-  // per-slot run entries of the map reduce-by-key (gc_runs.h SlotRuns, 256 B per slot; gc_map.hip,
-  // gc_scanmap.hip): all zero between calls (each call's owners clear the entries they used);
-  // re-zeroed when grown or after a failed call
-  void* slot_runs = nullptr;
-  int64_t slot_runs_n = 0;
-  bool slot_runs_dirty = true;
+  // the run hash of gc_primitive_map_fuse's reduce-by-key (gc_runs.h RunTable)
+  gc::RunTableBuf runs;
   // Fail-fast bound on every host wait for this context's device work (gc_ctx_set_wait_timeout;
   // GC_WAIT_TIMEOUT_S in the environment, default 300 s). A wait that runs out aborts `comm` (the
   // RCCL communicator last initialised on this context) so a peer that died cannot hold this rank in
@@ -51,9 +56,9 @@ void set_error(gc_ctx* ctx, const std::string& msg);
 // device scratch of at least `bytes` (synchronises the stream before growing)
 int scratch(gc_ctx* ctx, size_t bytes, void** out);
 
-// the context's per-slot run table (gc_runs.h SlotRuns) for a map of m_slots slots, every entry zero on
-// return (stream-ordered: a fill is enqueued on ctx->stream when the table is new, grown or dirty)
-int slot_runs(gc_ctx* ctx, int64_t m_slots, void** out);
+// a run hash (gc_runs.h RunTable) of at least 2 x rows entries, every entry empty on return
+// (stream-ordered: a fill is enqueued on st when the table is new, grown or dirty)
+int run_table(gc_ctx* ctx, hipStream_t st, RunTableBuf* T, int64_t rows);
 
 // the table exp's 2048-entry table in device memory (gc_points.hip), enqueued once per context
 hipError_t init_exp_table(hipStream_t st);
@@ -73,8 +78,6 @@ double default_wait_timeout_s();
 bool comm_healthy(gc_comm* c, std::string* why);
 void comm_abort(gc_comm* c);
 void comm_detach_ctx(gc_comm* c);
-
-constexpr size_t kSlotRunsBytes = 256;
 
 // hipFuncSetAttribute(fn, MaxDynamicSharedMemorySize, bytes) only when fn has not yet been allowed that
 // much: the runtime call is not free (it waited for an in-flight ingest copy on another stream,

@@ -114,7 +114,7 @@ GC_DEV void slot_colour(const gc_primitive_map& m, int64_t s, double cam, const 
 // all-LDS network, 256- and 512-row blocks alike (profiles/r04/ab_fuse_regsort.txt)
 constexpr int kFuseBlk = 512;
 __global__ void __launch_bounds__(kFuseBlk) k_fuse_runs(const int32_t* __restrict__ target, int64_t K, int64_t M,
-                                                   SlotRuns* T, uint32_t* sslot, uint32_t* order,
+                                                   RunTable T, uint32_t* sslot, uint32_t* order,
                                                    uint32_t* run_len, uint32_t* run_next, uint32_t* rank) {
   __shared__ uint64_t a[kFuseBlk];
   const int64_t base = (int64_t)blockIdx.x * kFuseBlk;
@@ -223,7 +223,7 @@ GC_DEV void fuse_apply_slot32(const FuseArgs& A, int64_t s, const double* d) {
 
 // one thread per sorted position; the owner of each slot (the run its list ends on) fuses the slot
 template <int LT, bool R32>  // R32: the packed 3-lobe record (A.rec32)
-__global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, SlotRuns* T,
+__global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, RunTable T,
                                                     const uint32_t* __restrict__ sslot,
                                                     const uint32_t* __restrict__ order,
                                                     const uint32_t* __restrict__ run_len,
@@ -239,7 +239,7 @@ __global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, 
   uint32_t s = 0;
   if (p < K) {
     s = sslot[p];
-    own = (int64_t)s < A.map.m_slots && rank[p] == 0u;
+    own = (int64_t)s < A.map.m_slots && rank[p] != kNoRun;  // the slot's entry index for its owner
   }
   if (own) {
     const int L = LT > 0 ? LT : A.map.n_lobes;
@@ -257,10 +257,12 @@ __global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, 
     };
     __shared__ uint32_t slices[kApplyWG * kRunCap];
     SlotRunList<kRunCap> rl(slices + threadIdx.x * kRunCap);
-    if (T[s].cnt == 1u) {  // the slot's rows all lie in one block (the common case)
+    const uint32_t ent = rank[p];
+    const uint32_t head = (uint32_t)T.e[ent];
+    if (head == (uint32_t)p + 1u) {  // the owner's run is the slot's only one (the common case)
       add_run((uint32_t)p);
     } else {
-      rl.collect(T, s, run_next, (int)((K + kFuseBlk - 1) / kFuseBlk));
+      rl.collect(head, run_next, (int)((K + kFuseBlk - 1) / kFuseBlk));
       uint32_t prev = 0;
       for (int i = 0; i < rl.n; ++i) {  // runs in block order
         const uint32_t r = rl.at(i, prev);
@@ -271,7 +273,7 @@ __global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, 
     }
     if constexpr (R32) fuse_apply_slot32(A, s, d);
     else fuse_apply_slot<LT>(A, s, d);
-    rl.clear(T, s);  // the entry is zero for the next call
+    T.e[ent] = kEmptyEntry;  // empty for the next call
   }
   // the distinct-slot count per workgroup (an LDS sum: one global counter for every wave serialised
   // the kernel's end)
@@ -362,7 +364,7 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   }
   A.timestamp = timestamp;
   A.scan_seq = scan_seq;
-  // scratch: the sorted slot, row order, run length, run rank and overflow link of every position, the
+  // scratch: the sorted slot, row order, run length, owner's entry and run link of every position, the
   // apply launch's per-workgroup distinct-slot counts
   const size_t kv = ((size_t)K * sizeof(uint32_t) + 255) / 256 * 256;
   const unsigned grid = (unsigned)((K + kApplyWG - 1) / kApplyWG);
@@ -375,11 +377,10 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   uint32_t* run_next = (uint32_t*)(base + 3 * kv);
   uint32_t* rank = (uint32_t*)(base + 4 * kv);
   uint32_t* cnt = (uint32_t*)(base + 5 * kv);
-  void* Tv = nullptr;
-  if (int rc = gc::slot_runs(ctx, map->m_slots, &Tv)) return rc;
-  SlotRuns* T = (SlotRuns*)Tv;
-  // from here a failed launch may leave entries set: the next call re-zeroes them
-  ctx->slot_runs_dirty = true;
+  if (int rc = gc::run_table(ctx, ctx->stream, &ctx->runs, K)) return rc;
+  const RunTable T{(unsigned long long*)ctx->runs.ptr, ctx->runs.bits};
+  // from here a failed launch may leave entries set: the next call empties them
+  ctx->runs.dirty = true;
   hipLaunchKernelGGL(k_fuse_runs, dim3((unsigned)((K + kFuseBlk - 1) / kFuseBlk)), dim3(kFuseBlk), 0, ctx->stream,
                      (const int32_t*)meas->target_slots, K, map->m_slots, T, sslot, order, run_len, run_next, rank);
   GC_LAUNCH_CHECK(ctx);
@@ -394,7 +395,7 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
     hipLaunchKernelGGL((k_fuse_apply<0, false>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, sslot, order,
                        run_len, run_next, rank, cnt);
   GC_LAUNCH_CHECK(ctx);
-  ctx->slot_runs_dirty = false;  // every entry the runs pass set, its owner cleared
+  ctx->runs.dirty = false;  // every entry the runs pass set, its owner cleared
   if (color && !map->colors_current) {
     hipLaunchKernelGGL(k_fuse_colors, dim3((unsigned)((map->m_slots + 255) / 256)), dim3(256), 0, ctx->stream, *map,
                        eps_mass);

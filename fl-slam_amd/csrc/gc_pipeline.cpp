@@ -398,6 +398,7 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
   for (hipEvent_t e : p->st_ev)
     if (e) (void)hipEventDestroy(e);
   if (p->smapW.buf) (void)hipFree(p->smapW.buf);
+  if (p->smapW.runs.ptr) (void)hipFree(p->smapW.runs.ptr);
   if (p->cstream) (void)hipStreamDestroy(p->cstream);
   if (p->done_word) (void)hipHostFree(p->done_word);
   delete p;

@@ -3,15 +3,16 @@
 // K rows each target one of M map slots; the rows of a slot must be summed in a fixed order and the
 // slot read-modify-written once. Instead of a global radix sort of (slot, row):
 //  1. each workgroup sorts its own block of rows by (slot, local row) (bitonic, reg_bitonic_sort), so a slot's
-//     rows in the block form one contiguous run, and registers the run with its slot's entry of the
-//     per-slot table (register_run): rank = atomicAdd(&cnt, 1), the run's position stored inline at
-//     that rank (the first kInlRuns runs) or linked into the entry's overflow list;
-//  2. the run of rank 0 belongs to the slot's owner thread, which reads the slot's runs from the
-//     entry (no list walk for up to kInlRuns runs), orders them by position (= block
-//     order), sums them in that order, applies the slot and clears the entry.
-// The order of the atomics only decides ranks and ownership, never the order of the sums: results
-// are bit-reproducible. Entries stay zero between calls (gc_ctx::slot_runs), so no pass over the M
-// slots is needed.
+//     rows in the block form one contiguous run, and registers the run in a row-sized open-addressing
+//     hash of the touched slots (RunTable, register_run): one 8-B entry per touched slot holds the slot
+//     and the head of the list of its runs, pushed by one 64-bit compare-and-swap per run; the run that
+//     finds the entry empty owns the slot;
+//  2. the owner thread walks the slot's list (reverse arrival order), orders the runs by position
+//     (= block order), sums them in that order, applies the slot and empties the entry.
+// The order of the atomics only decides ownership and list order, never the order of the sums: results
+// are bit-reproducible. The table holds 2^bits >= 2 x rows entries (load factor <= 1/2: a few probes),
+// 2 MB for a 131k-row call, so it stays in the caches instead of the 256 B per map slot the previous
+// per-slot table took (32 MB for the C5 map); entries are empty between calls, so no pass over it is needed.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -50,53 +51,74 @@ __device__ __forceinline__ uint64_t reg_bitonic_sort(uint64_t x, uint64_t* a) {
   return x;
 }
 
-constexpr int kInlRuns = 62;
-// a slot's entry: two 128-B lines, all zero between calls. 62 inline runs hold every slot of the C5
-// scans (at most one run per 256-row block: ~45 at the busiest voxel of a dense 131k-point scan), so
-// the overflow list is a correctness path only.
-struct alignas(256) SlotRuns {
-  uint32_t cnt;             // runs registered this call
-  uint32_t ovf;             // overflow list head, as position + 1 (0 = none)
-  uint32_t inl[kInlRuns];   // the positions of the first kInlRuns runs, in arrival order
+// a touched slot's entry: slot << 32 | (position of the last registered run + 1); all ones when empty
+constexpr unsigned long long kEmptyEntry = ~0ull;
+struct RunTable {
+  unsigned long long* e;  // 2^bits entries
+  uint32_t bits;
 };
-static_assert(sizeof(SlotRuns) == 256, "two lines per slot");
 
-// pass 1: register the run at position p with slot s; returns its rank (0: p's thread will own the slot)
-__device__ __forceinline__ uint32_t register_run(SlotRuns* T, uint32_t s, uint32_t p, uint32_t* ovf_next) {
-  const uint32_t r = atomicAdd(&T[s].cnt, 1u);
-  if (r < (uint32_t)kInlRuns) T[s].inl[r] = p;
-  else ovf_next[p] = atomicExch(&T[s].ovf, p + 1u);
-  return r;
+__device__ __forceinline__ uint32_t run_hash(uint32_t s, uint32_t bits) {
+  return (uint32_t)(s * 2654435761u) >> (32u - bits);  // multiplicative (Fibonacci) hashing, top bits
+}
+
+// pass 1: register the run at position p with slot s (s < 2^32 - 1). Pushes p on the slot's list
+// (next[p] = the previous head, position + 1, 0 ends) and returns the entry index when this run is the
+// slot's first (its thread owns the slot), kNoRun otherwise.
+__device__ __forceinline__ uint32_t register_run(RunTable T, uint32_t s, uint32_t p, uint32_t* next) {
+  const uint32_t mask = (1u << T.bits) - 1u;
+  const unsigned long long mine = ((unsigned long long)s << 32) | (p + 1u);
+  uint32_t e = run_hash(s, T.bits);
+  unsigned long long cur = kEmptyEntry;
+  for (uint32_t probes = 0; probes <= mask;) {
+    const unsigned long long old = atomicCAS(&T.e[e], cur, mine);
+    if (old == cur) {  // installed: the list continues with the previous head
+      next[p] = cur == kEmptyEntry ? 0u : (uint32_t)cur;
+      return cur == kEmptyEntry ? e : kNoRun;
+    }
+    if ((uint32_t)(old >> 32) == s) {  // the slot's entry, pushed to by another run meanwhile: again
+      cur = old;
+      continue;
+    }
+    e = (e + 1u) & mask;  // another slot's entry: linear probing
+    cur = kEmptyEntry;
+    ++probes;
+  }
+  return kNoRun;  // unreachable: the table has twice as many entries as runs
 }
 
 // pass 2, the owner: the slot's runs in ascending position order in a thread's LDS slice buf[0..CAP)
-// (a register array indexed at run time would live in scratch memory). The inline runs are in arrival
-// order and the overflow list in reverse arrival order; arrival order is close to block order (blocks
-// are dispatched in order and register their runs as they finish), so after reversing the overflow
-// part the insertion sort sees an almost ascending sequence. More than CAP runs (never at the C5
-// sizes: at most one run per block, ~45 at the busiest voxel of a dense scan) fall back to a
-// selection over the entry and its list, correct for any count. Clears the entry.
+// (a register array indexed at run time would live in scratch memory). The list is in reverse arrival
+// order, and arrival order is close to block order (blocks are dispatched in order and register their
+// runs as they finish), so the collected positions are reversed and an insertion sort finishes an
+// almost ascending sequence. More than CAP runs (never at the C5 sizes: at most one run per block,
+// ~45 at the busiest voxel of a dense scan) fall back to a selection over the list, correct for any count.
 template <int CAP>
 struct SlotRunList {
   uint32_t* buf;
-  const SlotRuns* e = nullptr;
+  uint32_t head = 0;
   const uint32_t* next = nullptr;
   int n = 0;
   bool spill = false;
 
   __device__ explicit SlotRunList(uint32_t* slice) : buf(slice) {}
 
-  __device__ void collect(SlotRuns* T, uint32_t s, const uint32_t* __restrict__ ovf_next, int max_runs) {
-    e = T + s;
-    next = ovf_next;
-    const uint32_t cnt = e->cnt;
-    n = (int)(cnt < (uint32_t)max_runs ? cnt : (uint32_t)max_runs);
+  // head: the entry's low word; at most max_runs list nodes are visited (a bound for a corrupt list)
+  __device__ void collect(uint32_t head_, const uint32_t* __restrict__ nxt, int max_runs) {
+    head = head_;
+    next = nxt;
+    n = 0;
+    for (uint32_t r = head; r != 0u && n < max_runs; r = nxt[r - 1]) {
+      if (n < CAP) buf[n] = r - 1;
+      ++n;
+    }
     spill = n > CAP;
     if (!spill) {
-      const int ni = n < kInlRuns ? n : kInlRuns;
-      for (int i = 0; i < ni; ++i) buf[i] = e->inl[i];
-      int m = n;
-      for (uint32_t r = e->ovf; r != 0u && m > ni; r = ovf_next[r - 1]) buf[--m] = r - 1;  // reversed
+      for (int i = 0, j = n - 1; i < j; ++i, --j) {  // arrival order
+        const uint32_t x = buf[i];
+        buf[i] = buf[j];
+        buf[j] = x;
+      }
       for (int i = 1; i < n; ++i) {
         const uint32_t v = buf[i];
         int j = i - 1;
@@ -109,26 +131,16 @@ struct SlotRunList {
     }
   }
 
-  // the i-th smallest run; with spill the i-th call in ascending i scans the entry and its list once
+  // the i-th smallest run; with spill the i-th call in ascending i walks the list once
   __device__ uint32_t at(int i, uint32_t prev) const {
     if (!spill) return buf[i];
     uint32_t best = kNoRun;
-    for (int k = 0; k < kInlRuns && k < n; ++k) {
-      const uint32_t r = e->inl[k];
-      if ((i == 0 || r > prev) && r < best) best = r;
-    }
-    int m = kInlRuns;
-    for (uint32_t r1 = e->ovf; r1 != 0u && m < n; r1 = next[r1 - 1], ++m) {
+    int m = 0;
+    for (uint32_t r1 = head; r1 != 0u && m < n; r1 = next[r1 - 1], ++m) {
       const uint32_t r = r1 - 1;
       if ((i == 0 || r > prev) && r < best) best = r;
     }
     return best;
-  }
-
-  // after the last at(): the entry is zero for the next call
-  __device__ void clear(SlotRuns* T, uint32_t s) const {
-    T[s].cnt = 0u;
-    T[s].ovf = 0u;
   }
 };
 

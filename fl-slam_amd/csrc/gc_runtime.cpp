@@ -137,21 +137,23 @@ int wait_event(gc_ctx* ctx, hipEvent_t ev, const char* what, double* waited_ms, 
   return bounded_poll(ctx, [&] { return hipEventQuery(ev); }, what, waited_ms, spin_polls, lim);
 }
 
-int slot_runs(gc_ctx* ctx, int64_t m_slots, void** out) {
-  if (m_slots > ctx->slot_runs_n) {
-    if (int rc = wait_stream(ctx, ctx->stream, "the stream before growing the run table")) return rc;
-    if (ctx->slot_runs) GC_HIP(ctx, hipFree(ctx->slot_runs));
-    ctx->slot_runs = nullptr;
-    ctx->slot_runs_n = 0;
-    GC_HIP(ctx, hipMalloc(&ctx->slot_runs, (size_t)m_slots * kSlotRunsBytes));
-    ctx->slot_runs_n = m_slots;
-    ctx->slot_runs_dirty = true;
+int run_table(gc_ctx* ctx, hipStream_t st, RunTableBuf* T, int64_t rows) {
+  uint32_t bits = 8;
+  while (bits < 31 && ((int64_t)1 << bits) < 2 * rows) ++bits;
+  const size_t bytes = ((size_t)1 << bits) * sizeof(unsigned long long);
+  if (bits > T->bits) {
+    if (int rc = wait_stream(ctx, st, "the stream before growing a run table")) return rc;
+    if (T->ptr) GC_HIP(ctx, hipFree(T->ptr));
+    T->ptr = nullptr;
+    T->bits = 0;
+    GC_HIP(ctx, hipMalloc(&T->ptr, bytes));
+    T->bits = bits;
+    T->dirty = true;
   }
-  if (ctx->slot_runs_dirty) {
-    GC_HIP(ctx, hipMemsetAsync(ctx->slot_runs, 0, (size_t)ctx->slot_runs_n * kSlotRunsBytes, ctx->stream));
-    ctx->slot_runs_dirty = false;
+  if (T->dirty) {  // all ones: every entry empty (gc_runs.h kEmptyEntry)
+    GC_HIP(ctx, hipMemsetAsync(T->ptr, 0xFF, ((size_t)1 << T->bits) * sizeof(unsigned long long), st));
+    T->dirty = false;
   }
-  *out = ctx->slot_runs;
   return GC_OK;
 }
 
@@ -211,7 +213,7 @@ int32_t gc_ctx_destroy(gc_ctx* ctx) {
   // bounded: a context whose stream is stuck (a failed peer) is still torn down
   (void)gc::wait_stream(ctx, ctx->stream, "the stream at context destruction");
   if (ctx->scratch) (void)hipFree(ctx->scratch);
-  if (ctx->slot_runs) (void)hipFree(ctx->slot_runs);
+  if (ctx->runs.ptr) (void)hipFree(ctx->runs.ptr);
   for (auto& kv : ctx->arena_free) (void)hipFree(kv.second);
   for (auto& kv : ctx->arena_live) (void)hipFree(kv.first);  // buffers not freed before the context
   (void)hipStreamDestroy(ctx->stream);

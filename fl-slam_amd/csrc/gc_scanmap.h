@@ -2,18 +2,18 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include "gc_internal.h"
 #include "gc_pipe.h"
 #include "../../include/gcslam.h"
-
-struct gc_ctx;
 
 namespace gc {
 
 // device work buffers of one pipeline's update (sized for n_cap rows): the sorted key of every block
-// position, each run's rank and overflow link, the run-piece sums (gc_runs.h), the apply launch's
-// per-workgroup touched-slot counts (summed on request); the per-slot run table is the context's
-// (gc_ctx::slot_runs)
+// position, each run's owner entry and list link, the run-piece sums and the run hash (gc_runs.h), the
+// apply launch's per-workgroup touched-slot counts (summed on request). The pipeline's own run hash
+// (not the context's) lets the update run on a stream of its own.
 struct ScanMapWork {
+  RunTableBuf runs;
   void* buf = nullptr;
   size_t bytes = 0;
   uint32_t *sslot = nullptr, *run_next = nullptr, *rank = nullptr;

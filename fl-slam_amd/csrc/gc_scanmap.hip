@@ -150,7 +150,7 @@ GC_DEV void smap_row(const double* C, const double* o, double eps_mass, const do
 // piece and registered with its slot's entry. A scan's points crowd into few voxels (~65k rows into
 // ~5k slots), so most of the work is this in-block reduction; a slot gets at most one piece per block.
 constexpr int kSmapBlk = 256;
-__global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, SlotRuns* T, uint32_t* sslot,
+__global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, RunTable T, uint32_t* sslot,
                                                          uint32_t* run_next, uint32_t* rank, SmapRow* pieces) {
   __shared__ double C[kSmapC + 3];
   __shared__ double v[kSmapRow][kSmapBlk];
@@ -247,7 +247,7 @@ __global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, SlotRuns
 
 // Pass 2, one thread per position: the owner of each slot (its run of rank 0) adds the slot's pieces
 // in block order and read-modify-writes the slot (the fuse with responsibility 1, source LiDAR)
-__global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t n, SlotRuns* T,
+__global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t n, RunTable T,
                                                          const uint32_t* __restrict__ sslot,
                                                          const uint32_t* __restrict__ run_next,
                                                          const uint32_t* __restrict__ rank,
@@ -258,7 +258,7 @@ __global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t 
   __shared__ double wave_sums[(kApplyWG / 64) * kSmapRow];
   const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const uint32_t key = e < n ? sslot[e] : kNoRun;
-  const bool own = (int64_t)key < A.map.m_slots && rank[e] == 0u;  // not dropped, the owner
+  const bool own = (int64_t)key < A.map.m_slots && rank[e] != kNoRun;  // not dropped, the owner (its entry)
   // the touched-slot count per workgroup (an LDS sum; thousands of global atomics on one counter
   // serialised the kernel: ~20-40 us)
   __shared__ uint32_t owned;
@@ -277,10 +277,12 @@ __global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t 
   SlotRunList<kRunCap> rl(slices + threadIdx.x * kRunCap);
   bool heavy = false;
   if (own) {
-    if (T[key].cnt == 1u) {  // the slot's rows all lie in one block (the common case)
+    const uint32_t head = (uint32_t)T.e[rank[e]];
+    T.e[rank[e]] = kEmptyEntry;  // empty for the next call (nothing probes the table in this pass)
+    if (head == (uint32_t)e + 1u) {  // the owner's run is the slot's only one (the common case)
       add((uint32_t)e);
     } else {
-      rl.collect(T, key, run_next, (int)((n + kSmapBlk - 1) / kSmapBlk));
+      rl.collect(head, run_next, (int)((n + kSmapBlk - 1) / kSmapBlk));
       if (rl.spill) {  // more runs than a slice holds: correctness path, never at the C5 sizes
         uint32_t prev = 0;
         for (int i = 0; i < rl.n; ++i) {
@@ -341,7 +343,6 @@ __global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t 
   mSup(A.map, s) = A.scan_seq;
   mUpd(A.map, s) = A.scan_seq;
   if (A.map.lidar_mass) mLid(A.map, s) = mLid(A.map, s) + d.v[15];
-  rl.clear(T, key);  // the entry is zero for the next call
 }
 
 }  // namespace
@@ -366,15 +367,11 @@ int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_s
   W->rank = (uint32_t*)(base + 2 * kv);
   W->pieces = (double*)(base + 3 * kv);
   W->wg_count = (uint32_t*)(base + 3 * kv + rv);
-  void* T = nullptr;
-  return slot_runs(ctx, m_slots, &T);  // allocated (and zeroed) now, outside any scan
+  return run_table(ctx, ctx->stream, &W->runs, n_cap);  // allocated (and emptied) now, outside any scan
 }
 
 int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_primitive_map& map,
                         const PipeDev& P, const ScanMapInput& in) {
-  // the per-slot run table (ctx->slot_runs) is zeroed and cleared on ctx->stream by every user (this
-  // update and gc_primitive_map_fuse): a caller on another stream would race those fills and clears
-  GC_CHECK_ARG(ctx, st == ctx->stream, "the in-scan map update runs on the context's stream");
   ScanMapArgs A{};
   A.map = map;
   A.pts = in.pts; A.t = in.t; A.w_win = P.w_win; A.bscal = P.budget;
@@ -387,17 +384,17 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
   A.eps_psd = P.eps_psd;
   A.scan_seq = in.scan_seq;
   const int64_t n = P.n_cap;
-  void* T = nullptr;
-  if (int rc = slot_runs(ctx, map.m_slots, &T)) return rc;
-  ctx->slot_runs_dirty = true;  // until both passes are enqueued
+  if (int rc = run_table(ctx, st, &W->runs, n)) return rc;
+  const RunTable T{(unsigned long long*)W->runs.ptr, W->runs.bits};
+  W->runs.dirty = true;  // until both passes are enqueued
   hipLaunchKernelGGL(k_smap_block, dim3((unsigned)((n + kSmapBlk - 1) / kSmapBlk)), dim3(kSmapBlk), 0, st, A,
-                     (SlotRuns*)T, W->sslot, W->run_next, W->rank, (SmapRow*)W->pieces);
+                     T, W->sslot, W->run_next, W->rank, (SmapRow*)W->pieces);
   GC_LAUNCH_CHECK(ctx);
   hipLaunchKernelGGL(k_smap_apply, dim3((unsigned)((n + kApplyWG - 1) / kApplyWG)), dim3(kApplyWG), 0, st, A, n,
-                     (SlotRuns*)T, (const uint32_t*)W->sslot, (const uint32_t*)W->run_next,
+                     T, (const uint32_t*)W->sslot, (const uint32_t*)W->run_next,
                      (const uint32_t*)W->rank, (const SmapRow*)W->pieces, W->wg_count);
   GC_LAUNCH_CHECK(ctx);
-  ctx->slot_runs_dirty = false;
+  W->runs.dirty = false;
   return GC_OK;
 }
 
