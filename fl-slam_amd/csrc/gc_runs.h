@@ -4,15 +4,17 @@
 // slot read-modify-written once. Instead of a global radix sort of (slot, row):
 //  1. each workgroup sorts its own block of rows by (slot, local row) (bitonic, reg_bitonic_sort), so a slot's
 //     rows in the block form one contiguous run, and registers the run in a row-sized open-addressing
-//     hash of the touched slots (RunTable, register_run): one 8-B entry per touched slot holds the slot
-//     and the head of the list of its runs, pushed by one 64-bit compare-and-swap per run; the run that
-//     finds the entry empty owns the slot;
-//  2. the owner thread walks the slot's list (reverse arrival order), orders the runs by position
-//     (= block order), sums them in that order, applies the slot and empties the entry.
-// The order of the atomics only decides ownership and list order, never the order of the sums: results
-// are bit-reproducible. The table holds 2^bits >= 2 x rows entries (load factor <= 1/2: a few probes),
-// 2 MB for a 131k-row call, so it stays in the caches instead of the 256 B per map slot the previous
-// per-slot table took (32 MB for the C5 map); entries are empty between calls, so no pass over it is needed.
+//     hash of the touched slots (RunTable, register_run): an 8-B entry per touched slot, its slot claimed
+//     by a compare-and-swap on the key word (one per slot and probe: no retry loop), the run pushed on
+//     the slot's list by an exchange on the head word;
+//  2. one thread per table entry (a coalesced sweep of the table, 4 B of key + 4 B of head per entry):
+//     each occupied entry's thread walks the slot's list, orders the runs by position (= block order),
+//     sums them in that order, applies the slot and empties the entry.
+// The order of the atomics only decides the list order, never the order of the sums: results are
+// bit-reproducible. The table holds 2^bits >= 4 x rows entries (load factor <= 1/4: ~1.2 probes per
+// claim), 4 MB for a 131k-row call and all zero between calls: the 256 B per map slot of the previous
+// direct-indexed run table (256 MB at the C5 map's 2^20 slots) and the per-position slot / rank arrays
+// its owners were found by are gone.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -51,8 +53,8 @@ __device__ __forceinline__ uint64_t reg_bitonic_sort(uint64_t x, uint64_t* a) {
   return x;
 }
 
-// a touched slot's entry: slot << 32 | (position of the last registered run + 1); all ones when empty
-constexpr unsigned long long kEmptyEntry = ~0ull;
+// a touched slot's entry: low word slot + 1 (0 = empty), high word the head of its run list
+// (position + 1 of the last registered run, 0 = none); all zero when empty
 struct RunTable {
   unsigned long long* e;  // 2^bits entries
   uint32_t bits;
@@ -62,32 +64,21 @@ __device__ __forceinline__ uint32_t run_hash(uint32_t s, uint32_t bits) {
   return (uint32_t)(s * 2654435761u) >> (32u - bits);  // multiplicative (Fibonacci) hashing, top bits
 }
 
-// pass 1: register the run at position p with slot s (s < 2^32 - 1). Pushes p on the slot's list
-// (next[p] = the previous head, position + 1, 0 ends) and returns the entry index when this run is the
-// slot's first (its thread owns the slot), kNoRun otherwise.
-__device__ __forceinline__ uint32_t register_run(RunTable T, uint32_t s, uint32_t p, uint32_t* next) {
-  const uint32_t mask = (1u << T.bits) - 1u;
-  const unsigned long long mine = ((unsigned long long)s << 32) | (p + 1u);
+// pass 1: register the run at position p with slot s (s < 2^32 - 1): claims (or finds) the slot's entry
+// and pushes p on its list (next[p] = the previous head, position + 1; 0 ends the list)
+__device__ __forceinline__ void register_run(RunTable T, uint32_t s, uint32_t p, uint32_t* next) {
+  uint32_t* w = reinterpret_cast<uint32_t*>(T.e);
+  const uint32_t mask = (1u << T.bits) - 1u, key = s + 1u;
   uint32_t e = run_hash(s, T.bits);
-  unsigned long long cur = kEmptyEntry;
-  for (uint32_t probes = 0; probes <= mask;) {
-    const unsigned long long old = atomicCAS(&T.e[e], cur, mine);
-    if (old == cur) {  // installed: the list continues with the previous head
-      next[p] = cur == kEmptyEntry ? 0u : (uint32_t)cur;
-      return cur == kEmptyEntry ? e : kNoRun;
-    }
-    if ((uint32_t)(old >> 32) == s) {  // the slot's entry, pushed to by another run meanwhile: again
-      cur = old;
-      continue;
-    }
-    e = (e + 1u) & mask;  // another slot's entry: linear probing
-    cur = kEmptyEntry;
-    ++probes;
+  for (uint32_t probes = 0; probes <= mask; ++probes) {
+    const uint32_t k = atomicCAS(&w[2 * e], 0u, key);
+    if (k == 0u || k == key) break;
+    e = (e + 1u) & mask;  // another slot's entry: linear probing (never full: 4 x as many entries as runs)
   }
-  return kNoRun;  // unreachable: the table has twice as many entries as runs
+  next[p] = atomicExch(&w[2 * e + 1], p + 1u);
 }
 
-// pass 2, the owner: the slot's runs in ascending position order in a thread's LDS slice buf[0..CAP)
+// pass 2, an occupied entry's thread: the slot's runs in ascending position order in a thread's LDS slice buf[0..CAP)
 // (a register array indexed at run time would live in scratch memory). The list is in reverse arrival
 // order, and arrival order is close to block order (blocks are dispatched in order and register their
 // runs as they finish), so the collected positions are reversed and an insertion sort finishes an
@@ -143,18 +134,6 @@ struct SlotRunList {
     return best;
   }
 };
-
-// XCD-aware workgroup order: workgroups are dispatched round-robin over the 8 XCDs (each with its own
-// L2), so consecutive workgroup ids land on different XCDs. The apply kernels' workgroups that cover
-// one sort block read the same block's rows (in sorted, i.e. random row order): mapping the ids so
-// that the consecutive logical workgroups of one XCD take consecutive positions keeps a block's row
-// lines in one L2. A bijection on [0, 8 floor(n / 8)); the tail keeps its id.
-__device__ __forceinline__ int64_t xcd_block(int64_t b, int64_t n) {
-  constexpr int kXcd = 8;
-  const int64_t full = n / kXcd * kXcd;
-  if (b >= full) return b;
-  return (b % kXcd) * (full / kXcd) + b / kXcd;
-}
 
 // the apply kernels' workgroup and per-thread slice capacity: 128 x 64 x 4 B = 32 KB of LDS
 constexpr int kApplyWG = 128;

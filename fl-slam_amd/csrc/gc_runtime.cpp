@@ -138,8 +138,8 @@ int wait_event(gc_ctx* ctx, hipEvent_t ev, const char* what, double* waited_ms, 
 }
 
 int run_table(gc_ctx* ctx, hipStream_t st, RunTableBuf* T, int64_t rows) {
-  uint32_t bits = 8;
-  while (bits < 31 && ((int64_t)1 << bits) < 2 * rows) ++bits;
+  uint32_t bits = 8;  // >= 4 x rows entries (gc_runs.h), at least two apply workgroups' worth
+  while (bits < 31 && ((int64_t)1 << bits) < 4 * rows) ++bits;
   const size_t bytes = ((size_t)1 << bits) * sizeof(unsigned long long);
   if (bits > T->bits) {
     if (int rc = wait_stream(ctx, st, "the stream before growing a run table")) return rc;
@@ -150,8 +150,8 @@ int run_table(gc_ctx* ctx, hipStream_t st, RunTableBuf* T, int64_t rows) {
     T->bits = bits;
     T->dirty = true;
   }
-  if (T->dirty) {  // all ones: every entry empty (gc_runs.h kEmptyEntry)
-    GC_HIP(ctx, hipMemsetAsync(T->ptr, 0xFF, ((size_t)1 << T->bits) * sizeof(unsigned long long), st));
+  if (T->dirty) {  // zero: every entry empty (gc_runs.h RunTable)
+    GC_HIP(ctx, hipMemsetAsync(T->ptr, 0, ((size_t)1 << T->bits) * sizeof(unsigned long long), st));
     T->dirty = false;
   }
   return GC_OK;
