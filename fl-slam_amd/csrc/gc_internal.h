@@ -11,10 +11,13 @@
 struct gc_comm;
 
 namespace gc {
-// a device run hash (gc_runs.h RunTable): 2^bits 8-B entries, all empty between uses
+// a device run hash (gc_runs.h RunTable): 2^bits 8-B entries and the 2^bits / 4 successor links
+// after them, all zero between uses
 struct RunTableBuf {
   void* ptr = nullptr;
   uint32_t bits = 0;
+  unsigned long long* entries() const { return (unsigned long long*)ptr; }
+  uint32_t* succ() const { return (uint32_t*)((char*)ptr + ((size_t)8 << bits)); }
   bool dirty = true;  // a fill is due (new, grown, or a call that failed between its two passes)
 };
 }  // namespace gc

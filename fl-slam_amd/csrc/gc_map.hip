@@ -114,8 +114,8 @@ GC_DEV void slot_colour(const gc_primitive_map& m, int64_t s, double cam, const 
 // all-LDS network, 256- and 512-row blocks alike (profiles/r04/ab_fuse_regsort.txt)
 constexpr int kFuseBlk = 512;
 __global__ void __launch_bounds__(kFuseBlk) k_fuse_runs(const int32_t* __restrict__ target, int64_t K, int64_t M,
-                                                   RunTable T, uint32_t* order, uint32_t* run_len,
-                                                   uint32_t* run_next) {
+                                                   RunTable T, uint32_t* sslot, uint32_t* order,
+                                                   uint32_t* run_len, uint32_t* rank) {
   __shared__ uint64_t a[kFuseBlk];
   const int64_t base = (int64_t)blockIdx.x * kFuseBlk;
   {
@@ -135,12 +135,15 @@ __global__ void __launch_bounds__(kFuseBlk) k_fuse_runs(const int32_t* __restric
     if (p >= K) break;
     const uint32_t key = (uint32_t)(a[i] >> 32);
     order[p] = (uint32_t)(base + (uint32_t)a[i]);
+    sslot[p] = key;
+    uint32_t rk = kNoRun;
     if ((int64_t)key < M && (i == 0 || (uint32_t)(a[i - 1] >> 32) != key)) {
       int len = 1;
       while (i + len < kFuseBlk && (uint32_t)(a[i + len] >> 32) == key) ++len;
       run_len[p] = (uint32_t)len;
-      register_run(T, key, (uint32_t)p, run_next);
+      rk = register_run(T, key, (uint32_t)p);
     }
+    rank[p] = rk;
   }
 }
 
@@ -218,20 +221,25 @@ GC_DEV void fuse_apply_slot32(const FuseArgs& A, int64_t s, const double* d) {
   if (m.cam_mass && m.colors_current) slot_colour(m, s, rec[16], rec + 18, rec[21], A.eps_mass);
 }
 
-// one thread per run-table entry (gc_runs.h): each occupied entry's thread fuses its slot
+// one thread per sorted position; the owner of each slot (the run its list ends on) fuses the slot
 template <int LT, bool R32>  // R32: the packed 3-lobe record (A.rec32)
 __global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, RunTable T,
+                                                    const uint32_t* __restrict__ sslot,
                                                     const uint32_t* __restrict__ order,
                                                     const uint32_t* __restrict__ run_len,
-                                                    const uint32_t* __restrict__ run_next,
+                                                    const uint32_t* __restrict__ rank,
                                                     uint32_t* wg_count) {
 #pragma clang fp contract(off)
   constexpr int LM = LT > 0 ? LT : kMaxLobes;
   constexpr int NT = row_terms_len(LM);
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // grid = the table's entries
-  const unsigned long long v = T.e[i];
-  const bool own = (uint32_t)v != 0u;
-  const uint32_t s = (uint32_t)v - 1u, head = (uint32_t)(v >> 32);
+  const int64_t wgid = xcd_block(blockIdx.x, gridDim.x);  // a sort block's workgroups on one XCD
+  const int64_t p = wgid * blockDim.x + threadIdx.x;
+  bool own = false;
+  uint32_t s = 0;
+  if (p < K) {
+    s = sslot[p];
+    own = (int64_t)s < A.map.m_slots && rank[p] != kNoRun;  // the slot's entry index for its owner
+  }
   if (own) {
     const int L = LT > 0 ? LT : A.map.n_lobes;
     const int nt = row_terms_len(L);
@@ -248,21 +256,23 @@ __global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, 
     };
     __shared__ uint32_t slices[kApplyWG * kRunCap];
     SlotRunList<kRunCap> rl(slices + threadIdx.x * kRunCap);
-    T.e[i] = 0ull;  // empty for the next call (nothing probes the table in this pass)
-    if (run_next[head - 1] == 0u) {  // the slot's rows all lie in one block (the common case)
-      add_run(head - 1);
+    const uint32_t s1 = T.succ[p];
+    if (s1 == 0u) {  // the slot's rows all lie in one block (the common case)
+      add_run((uint32_t)p);
     } else {
-      rl.collect(head, run_next, (int)((K + kFuseBlk - 1) / kFuseBlk));
+      rl.collect((uint32_t)p, s1, T.succ, (int)((K + kFuseBlk - 1) / kFuseBlk));
       uint32_t prev = 0;
-      for (int k = 0; k < rl.n; ++k) {  // runs in block order
-        const uint32_t r = rl.at(k, prev);
-        if (r == kNoRun) break;  // only a corrupt list: never index past the runs
+      for (int i = 0; i < rl.n; ++i) {  // runs in block order
+        const uint32_t r = rl.at(i, prev);
+        if (r == kNoRun) break;  // only a corrupt entry: never index past the runs
         prev = r;
         add_run(r);
       }
     }
     if constexpr (R32) fuse_apply_slot32(A, s, d);
     else fuse_apply_slot<LT>(A, s, d);
+    if (s1 != 0u) rl.clear();
+    T.e[rank[p]] = 0ull;  // the entry and the chain empty for the next call
   }
   // the distinct-slot count per workgroup (an LDS sum: one global counter for every wave serialised
   // the kernel's end)
@@ -353,34 +363,35 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   }
   A.timestamp = timestamp;
   A.scan_seq = scan_seq;
-  // scratch: the row order, run length and run link of every position, the apply launch's
-  // per-workgroup distinct-slot counts; the run hash (4 x K entries) is the context's
-  if (int rc = gc::run_table(ctx, ctx->stream, &ctx->runs, K)) return rc;
-  const RunTable T{(unsigned long long*)ctx->runs.ptr, ctx->runs.bits};
+  // scratch: the sorted slot, row order, run length and owner's entry of every position, the apply
+  // launch's per-workgroup distinct-slot counts (the run hash and its links are the context's)
   const size_t kv = ((size_t)K * sizeof(uint32_t) + 255) / 256 * 256;
-  const unsigned grid = (unsigned)(((size_t)1 << T.bits) / kApplyWG);
+  const unsigned grid = (unsigned)((K + kApplyWG - 1) / kApplyWG);
   void* scr;
-  if (int rc = gc::scratch(ctx, 3 * kv + (size_t)grid * sizeof(uint32_t), &scr)) return rc;
+  if (int rc = gc::scratch(ctx, 4 * kv + (size_t)grid * sizeof(uint32_t), &scr)) return rc;
   char* base = (char*)scr;
-  uint32_t* order = (uint32_t*)base;
-  uint32_t* run_len = (uint32_t*)(base + kv);
-  uint32_t* run_next = (uint32_t*)(base + 2 * kv);
-  uint32_t* cnt = (uint32_t*)(base + 3 * kv);
+  uint32_t* sslot = (uint32_t*)base;
+  uint32_t* order = (uint32_t*)(base + kv);
+  uint32_t* run_len = (uint32_t*)(base + 2 * kv);
+  uint32_t* rank = (uint32_t*)(base + 3 * kv);
+  uint32_t* cnt = (uint32_t*)(base + 4 * kv);
+  if (int rc = gc::run_table(ctx, ctx->stream, &ctx->runs, K)) return rc;
+  const RunTable T{ctx->runs.entries(), ctx->runs.succ(), ctx->runs.bits};
   // from here a failed launch may leave entries set: the next call empties them
   ctx->runs.dirty = true;
   hipLaunchKernelGGL(k_fuse_runs, dim3((unsigned)((K + kFuseBlk - 1) / kFuseBlk)), dim3(kFuseBlk), 0, ctx->stream,
-                     (const int32_t*)meas->target_slots, K, map->m_slots, T, order, run_len, run_next);
+                     (const int32_t*)meas->target_slots, K, map->m_slots, T, sslot, order, run_len, rank);
   GC_LAUNCH_CHECK(ctx);
   const bool l3 = map->n_lobes == 3;  // GC_VMF_N_LOBES: the compile-time lobe count
   if (A.rec32)
-    hipLaunchKernelGGL((k_fuse_apply<3, true>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, order, run_len,
-                       run_next, cnt);
+    hipLaunchKernelGGL((k_fuse_apply<3, true>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, sslot, order,
+                       run_len, rank, cnt);
   else if (l3)
-    hipLaunchKernelGGL((k_fuse_apply<3, false>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, order, run_len,
-                       run_next, cnt);
+    hipLaunchKernelGGL((k_fuse_apply<3, false>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, sslot, order,
+                       run_len, rank, cnt);
   else
-    hipLaunchKernelGGL((k_fuse_apply<0, false>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, order, run_len,
-                       run_next, cnt);
+    hipLaunchKernelGGL((k_fuse_apply<0, false>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, sslot, order,
+                       run_len, rank, cnt);
   GC_LAUNCH_CHECK(ctx);
   ctx->runs.dirty = false;  // every entry the runs pass set, its owner cleared
   if (color && !map->colors_current) {

@@ -8,18 +8,18 @@
 
 namespace gc {
 
-// device work buffers of one pipeline's update (sized for n_cap rows): each run's list link, the
-// run-piece sums and the run hash (gc_runs.h), the apply launch's per-workgroup touched-slot counts
-// (summed on request). The pipeline's own run hash (not the context's) lets the update run on a
-// stream of its own.
+// device work buffers of one pipeline's update (sized for n_cap rows): the sorted key of every block
+// position and the owner's run-hash entry, the run-piece sums and the run hash with its links
+// (gc_runs.h), the apply launch's per-workgroup touched-slot counts (summed on request). The
+// pipeline's own run hash (not the context's) lets the update run on a stream of its own.
 struct ScanMapWork {
   RunTableBuf runs;
   void* buf = nullptr;
   size_t bytes = 0;
-  uint32_t* run_next = nullptr;
+  uint32_t *sslot = nullptr, *rank = nullptr;
   double* pieces = nullptr;  // (n_cap, 16) the run sums, at each run's last block position
   uint32_t* wg_count = nullptr;
-  int64_t n_wg = 0;  // the apply launch's workgroups (one thread per run-hash entry)
+  int64_t n_wg = 0;  // the apply launch's workgroups
   int64_t n_cap = 0, m_slots = 0;
 };
 

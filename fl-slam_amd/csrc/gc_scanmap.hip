@@ -16,7 +16,7 @@
 // deskewed point weight (a4). Its slot is the spatial hash of the world voxel of μ_w. The rows are
 // fused with responsibility 1 and source LiDAR by a deterministic reduce-by-key (gc_runs.h): each
 // 256-row block sorts its rows by slot in LDS and sums every run of one slot by a segmented scan
-// (k_smap_block), the runs are registered in a run hash, and one thread per touched slot sums its runs
+// (k_smap_block), the runs are registered per slot, and one owner thread per distinct slot sums its runs
 // in block order and applies the sum (k_smap_apply): bit-reproducible, within 1e-12 of np.add.at's
 // sequential order. A scan's points crowd into few voxels
 // (~65k rows into ~5k slots, runs of thousands near the sensor), so rows are computed one per
@@ -150,8 +150,8 @@ GC_DEV void smap_row(const double* C, const double* o, double eps_mass, const do
 // piece and registered with its slot's entry. A scan's points crowd into few voxels (~65k rows into
 // ~5k slots), so most of the work is this in-block reduction; a slot gets at most one piece per block.
 constexpr int kSmapBlk = 256;
-__global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, RunTable T, uint32_t* run_next,
-                                                         SmapRow* pieces) {
+__global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, RunTable T, uint32_t* sslot,
+                                                         uint32_t* rank, SmapRow* pieces) {
   __shared__ double C[kSmapC + 3];
   __shared__ double v[kSmapRow][kSmapBlk];
   __shared__ uint64_t a[kSmapBlk];
@@ -232,27 +232,32 @@ __global__ void __launch_bounds__(kSmapBlk) k_smap_block(ScanMapArgs A, RunTable
   }
   const int64_t p = (int64_t)blockIdx.x * kSmapBlk + t;
   const bool tail = (int64_t)k_t < M && (t == kSmapBlk - 1 || (uint32_t)(a[t + 1] >> 32) != k_t);
+  uint32_t rk = kNoRun;
   if (tail) {
     SmapRow o;
     for (int q = 0; q < kSmapRow; ++q) o.v[q] = x[q];
     pieces[p] = o;
-    register_run(T, k_t, (uint32_t)p, run_next);
+    rk = register_run(T, k_t, (uint32_t)p);
+  }
+  if (p < A.n_cap) {
+    sslot[p] = k_t;
+    rank[p] = rk;
   }
 }
 
-// Pass 2, one thread per run-table entry: each occupied entry's thread adds its slot's pieces in block
-// order and read-modify-writes the slot (the fuse with responsibility 1, source LiDAR)
+// Pass 2, one thread per position: the owner of each slot (its run of rank 0) adds the slot's pieces
+// in block order and read-modify-writes the slot (the fuse with responsibility 1, source LiDAR)
 __global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t n, RunTable T,
-                                                         const uint32_t* __restrict__ run_next,
+                                                         const uint32_t* __restrict__ sslot,
+                                                         const uint32_t* __restrict__ rank,
                                                          const SmapRow* __restrict__ pieces,
                                                          uint32_t* wg_count) {
 #pragma clang fp contract(off)
   __shared__ uint32_t slices[kApplyWG * kRunCap];
   __shared__ double wave_sums[(kApplyWG / 64) * kSmapRow];
-  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;  // grid = the table's entries
-  const unsigned long long ev = T.e[e];
-  const bool own = (uint32_t)ev != 0u;
-  const uint32_t key = (uint32_t)ev - 1u, head = (uint32_t)(ev >> 32);
+  const int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const uint32_t key = e < n ? sslot[e] : kNoRun;
+  const bool own = (int64_t)key < A.map.m_slots && rank[e] != kNoRun;  // not dropped, the owner (its entry)
   // the touched-slot count per workgroup (an LDS sum; thousands of global atomics on one counter
   // serialised the kernel: ~20-40 us)
   __shared__ uint32_t owned;
@@ -270,12 +275,14 @@ __global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t 
   };
   SlotRunList<kRunCap> rl(slices + threadIdx.x * kRunCap);
   bool heavy = false;
+  uint32_t s1 = 0u;
   if (own) {
-    T.e[e] = 0ull;  // empty for the next call (nothing probes the table in this pass)
-    if (run_next[head - 1] == 0u) {  // the slot's rows all lie in one block (the common case)
-      add(head - 1);
+    T.e[rank[e]] = 0ull;  // empty for the next call (nothing probes the table in this pass)
+    s1 = T.succ[e];
+    if (s1 == 0u) {  // the slot's rows all lie in one block (the common case)
+      add((uint32_t)e);
     } else {
-      rl.collect(head, run_next, (int)((n + kSmapBlk - 1) / kSmapBlk));
+      rl.collect((uint32_t)e, s1, T.succ, (int)((n + kSmapBlk - 1) / kSmapBlk));
       if (rl.spill) {  // more runs than a slice holds: correctness path, never at the C5 sizes
         uint32_t prev = 0;
         for (int i = 0; i < rl.n; ++i) {
@@ -324,6 +331,7 @@ __global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t 
     __builtin_amdgcn_wave_barrier();
   }
   if (!own) return;
+  if (s1 != 0u) rl.clear();  // the chain's links zero for the next call
   const int64_t s = key;
   const int L = A.map.n_lobes;
   for (int q = 0; q < 9; ++q) mLam(A.map, s)[q] = mLam(A.map, s)[q] + d.v[q];
@@ -343,12 +351,10 @@ __global__ void __launch_bounds__(kApplyWG) k_smap_apply(ScanMapArgs A, int64_t 
 int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_slots) {
   W->n_cap = n_cap;
   W->m_slots = m_slots;
-  // the run hash first (allocated and emptied now, outside any scan): its size sets the apply grid
-  if (int rc = run_table(ctx, ctx->stream, &W->runs, n_cap)) return rc;
   auto up = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t kv = up((size_t)n_cap * sizeof(uint32_t)), rv = up((size_t)n_cap * sizeof(SmapRow));
-  W->n_wg = (int64_t)(((size_t)1 << W->runs.bits) / kApplyWG);
-  const size_t bytes = kv + rv + up((size_t)W->n_wg * sizeof(uint32_t));
+  W->n_wg = (n_cap + kApplyWG - 1) / kApplyWG;
+  const size_t bytes = 2 * kv + rv + up((size_t)W->n_wg * sizeof(uint32_t));
   if (bytes > W->bytes) {
     if (W->buf) GC_HIP(ctx, hipFree(W->buf));
     W->buf = nullptr;
@@ -357,10 +363,11 @@ int32_t scan_map_prepare(gc_ctx* ctx, ScanMapWork* W, int64_t n_cap, int64_t m_s
     W->bytes = bytes;
   }
   char* base = (char*)W->buf;
-  W->run_next = (uint32_t*)base;
-  W->pieces = (double*)(base + kv);
-  W->wg_count = (uint32_t*)(base + kv + rv);
-  return GC_OK;
+  W->sslot = (uint32_t*)base;
+  W->rank = (uint32_t*)(base + kv);
+  W->pieces = (double*)(base + 2 * kv);
+  W->wg_count = (uint32_t*)(base + 2 * kv + rv);
+  return run_table(ctx, ctx->stream, &W->runs, n_cap);  // allocated (and emptied) now, outside any scan
 }
 
 int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_primitive_map& map,
@@ -378,13 +385,13 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
   A.scan_seq = in.scan_seq;
   const int64_t n = P.n_cap;
   if (int rc = run_table(ctx, st, &W->runs, n)) return rc;
-  const RunTable T{(unsigned long long*)W->runs.ptr, W->runs.bits};
+  const RunTable T{W->runs.entries(), W->runs.succ(), W->runs.bits};
   W->runs.dirty = true;  // until both passes are enqueued
   hipLaunchKernelGGL(k_smap_block, dim3((unsigned)((n + kSmapBlk - 1) / kSmapBlk)), dim3(kSmapBlk), 0, st, A,
-                     T, W->run_next, (SmapRow*)W->pieces);
+                     T, W->sslot, W->rank, (SmapRow*)W->pieces);
   GC_LAUNCH_CHECK(ctx);
-  hipLaunchKernelGGL(k_smap_apply, dim3((unsigned)W->n_wg), dim3(kApplyWG), 0, st, A, n, T,
-                     (const uint32_t*)W->run_next, (const SmapRow*)W->pieces, W->wg_count);
+  hipLaunchKernelGGL(k_smap_apply, dim3((unsigned)((n + kApplyWG - 1) / kApplyWG)), dim3(kApplyWG), 0, st, A, n,
+                     T, (const uint32_t*)W->sslot, (const uint32_t*)W->rank, (const SmapRow*)W->pieces, W->wg_count);
   GC_LAUNCH_CHECK(ctx);
   W->runs.dirty = false;
   return GC_OK;
