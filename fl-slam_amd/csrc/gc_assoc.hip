@@ -365,6 +365,7 @@ extern "C" {
 int32_t gc_extract_map_view(gc_ctx* ctx, const gc_primitive_map* map, int64_t m_tile, const int64_t* h_dense_tiles,
                             const int64_t* h_tile_ids, double eps_lift, double eps_mass, const gc_map_view* view) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   GC_CHECK_ARG(ctx, map && view && h_dense_tiles && h_tile_ids, "NULL argument");
   {
     const char* lay_ = gc::map_layout_error(*map);
@@ -425,6 +426,7 @@ int32_t gc_associate_primitives_ot(gc_ctx* ctx, int64_t N, int32_t n_lobes, cons
                                    int64_t* d_cand_slot_out, double* d_row_mass_out, double* d_cost_out,
                                    double* h_cert_out) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   GC_CHECK_ARG(ctx, view && h_cfg && h_cert_out, "NULL argument");
   GC_CHECK_ARG(ctx, N >= 1 && n_lobes >= 1 && n_lobes <= kMaxLobesA, "bad N or n_lobes");
   GC_CHECK_ARG(ctx, d_Lambdas && d_thetas && d_etas && d_valid && d_resp_out && d_cand_out && d_cand_tile_out &&

@@ -639,7 +639,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     }
     // the LiDAR block as this scan saw it (the in-scan map update's Σ_lidar: the reference builds the
     // scan's measurement covariances from the IW state before the scan's own apply)
-    if (t < 10) P.lidar_iw[t] = t == 0 ? P.nu_meas[2] : P.Psi_meas[18 + t - 1];
+    if (t < 10) P.smap_snap[kSnapIW + t] = t == 0 ? P.nu_meas[2] : P.Psi_meas[18 + t - 1];
     __syncthreads();
     wg_iw_meas_apply(P.nu_meas, P.Psi_meas, Ri, Ri + (kPDNUM - kPDPSIM), P.eps_psd, P.nu_max, P.nu_meas, P.Psi_meas,
                      P.iw_cert + 2, tab);
@@ -674,7 +674,9 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     double s = 0.0;
     for (int g = 0; g < P.G; ++g) s += P.gather[(int64_t)g * PLn + e];
     P.send[e] = s;  // reuse send as the reduced record
+    if (e >= rec_h0(P.B)) P.smap_snap[e - rec_h0(P.B)] = s;
   }
+  if (t < 8) P.smap_snap[kSnapBudget + t] = P.budget[t];
   __syncthreads();
   const double* R = P.send;
   for (int i = t; i < NN; i += kWG) Lr[i] = R[kPL + i];

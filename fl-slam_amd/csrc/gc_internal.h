@@ -31,6 +31,11 @@ struct gc_ctx {
   int cu_count = 0;  // compute units of the device (queried on first use)
   // the run hash of gc_primitive_map_fuse's reduce-by-key (gc_runs.h RunTable)
   gc::RunTableBuf runs;
+  // device work of this context left running on a stream of its own (a pipeline's in-scan map
+  // update, gc_pipeline.cpp): every entry point that may touch its data orders ctx->stream after it
+  // first (gc::join_side); the event belongs to the pipeline, which clears it before destroying it
+  hipEvent_t side_ev = nullptr;
+  bool side_pending = false;
   // Fail-fast bound on every host wait for this context's device work (gc_ctx_set_wait_timeout;
   // GC_WAIT_TIMEOUT_S in the environment, default 300 s). A wait that runs out aborts `comm` (the
   // RCCL communicator last initialised on this context) so a peer that died cannot hold this rank in
@@ -55,6 +60,9 @@ namespace gc {
 
 // thread-local fallback message for errors raised before a ctx exists
 void set_error(gc_ctx* ctx, const std::string& msg);
+
+// orders ctx->stream after the context's pending side-stream work (side_ev), once
+int join_side(gc_ctx* ctx);
 
 // device scratch of at least `bytes` (synchronises the stream before growing)
 int scratch(gc_ctx* ctx, size_t bytes, void** out);

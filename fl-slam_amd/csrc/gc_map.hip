@@ -320,6 +320,7 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
                               const double* h_pose6, double eps_lift, double eps_mass, double timestamp,
                               int64_t scan_seq, int64_t* n_fused_out) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   GC_CHECK_ARG(ctx, map && meas, "NULL map or measurement batch");
   GC_CHECK_ARG(ctx, map->m_slots > 0 && map->m_slots < (int64_t)kDropped, "m_slots out of range");
   GC_CHECK_ARG(ctx, map->n_lobes >= 1 && map->n_lobes <= kMaxLobes, "n_lobes must be in [1, 8]");
@@ -420,6 +421,7 @@ int32_t gc_primitive_map_record_layout(int32_t n_lobes, int64_t* offsets_out, in
 int32_t gc_copy_strided(gc_ctx* ctx, void* d_dst, int64_t dst_pitch, const void* d_src, int64_t src_pitch,
                         int64_t elem_bytes, int64_t rows) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   GC_CHECK_ARG(ctx, elem_bytes >= 1 && rows >= 0 && dst_pitch >= elem_bytes && src_pitch >= elem_bytes,
                "bad element size, pitch or row count");
   if (rows == 0) return GC_OK;

@@ -322,6 +322,7 @@ unsigned part_blocks(int64_t n) {
 
 int check_tile(gc_ctx* ctx, const gc_primitive_map* map, int64_t slot0, int64_t n_slots, bool need_valid) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;  // a pipeline's in-scan update may still write the map
   GC_CHECK_ARG(ctx, map != nullptr, "NULL map");
   GC_CHECK_ARG(ctx, map->m_slots > 0 && slot0 >= 0 && n_slots >= 0 && slot0 + n_slots <= map->m_slots,
                "tile range outside the map");

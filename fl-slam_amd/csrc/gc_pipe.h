@@ -24,6 +24,9 @@ constexpr int kPL = 0, kPH = 484, kPZ = 506, kPMU = 528, kPMU2 = 550, kPDPSIP = 
 // after the map increments: hypothesis 0's [z_t 6 (recomposed world pose), Σ_post pose block 36,
 // ξ_body 6] for the in-scan PrimitiveMap update every rank runs (gc_scanmap.hip)
 constexpr int kH0Len = 48;
+// the in-scan map update's snapshot (PipeDev::smap_snap): [reduced h0 record 48 | the measurement-IW
+// LiDAR block [ν_2, Ψ_2 (9)] before the scan's IW apply 10 | the scan's 8 a1 budget scalars]
+constexpr int kSnapIW = kH0Len, kSnapBudget = kSnapIW + 10, kSnapLen = 72;
 __host__ __device__ inline int rec_h0(int B) { return kPMAP + B * kMapRec; }
 __host__ __device__ inline int partial_len(int B) { return rec_h0(B) + kH0Len; }
 
@@ -66,8 +69,9 @@ struct PipeDev {
   double *map_inc;                         // (B, 26) written by hypothesis 0's owner
   double *h0rec;                           // (kH0Len) hypothesis 0's pose block (its owner's k_evidence)
   double *nu_proc, *Psi_proc, *nu_meas, *Psi_meas;  // (7), (7,36), (3), (3,9)
-  double *lidar_iw;                        // [ν_2, Ψ_2 (9)]: the scan's measurement-IW LiDAR block before its
-                                           // IW apply (k_combine_final wg 3), read by the in-scan map update
+  double *smap_snap;                       // (kSnapLen) the in-scan map update's inputs of the scan, written by
+                                           // k_combine_final (gc_scanmap.hip); the host alternates two blocks
+                                           // per scan so the update can run on a stream of its own
   double *budget;                          // the scan's 8 a1 budget scalars: formed by the predict launch's
                                            // extra workgroups, or copied there from S.budget
   double *budget_part;                     // (64, 3) a1 partials of those workgroups

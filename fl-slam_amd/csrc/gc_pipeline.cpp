@@ -28,6 +28,13 @@ int32_t cloud_parse_on(gc_ctx* ctx, hipStream_t st, int32_t* flag, const uint8_t
 #endif
 constexpr int64_t kBindEvery = GC_BIND_EVERY;
 
+// the in-scan map update on a stream of its own (1), beside the next scan, or on the compute stream
+// after the combine (0)
+#ifndef GC_SMAP_SIDE
+#define GC_SMAP_SIDE 1
+#endif
+constexpr bool kSmapSide = GC_SMAP_SIDE != 0;
+
 struct gc_pipeline {
   gc_ctx* ctx = nullptr;
   gc::PipeDev P{};
@@ -94,6 +101,18 @@ struct gc_pipeline {
   double smap_voxel = 0.0;
   bool smap_colors = false;  // the colour pass is due (first update after attaching a map with colours not current)
   gc::ScanMapWork smapW;
+  // With kSmapSide the update runs on mstream, started by combine_final's completion signal
+  // (smap_go, the launch's own: no packet of its own), from the scan's snapshot block of
+  // P.smap_snap (snap_base + (ticket & 1) x kSnapLen: the inputs the next scan rewrites, copied by
+  // combine_final) and the slot (its restaging waits on `consumed`, recorded after the update). The
+  // next scan's predict, bins and evidence run beside it; the compute stream waits for the update only
+  // before the combine_final that rewrites its snapshot block, two scans later (smap_done), and
+  // host access to the map through the context joins it first (gc::join_side).
+  hipStream_t mstream = nullptr;
+  hipEvent_t smap_go = nullptr;
+  hipEvent_t smap_done[2] = {nullptr, nullptr};
+  bool smap_done_rec[2] = {false, false};
+  double* snap_base = nullptr;
   int pending_slot = -1;
   int64_t pending_seq = 0;
   // Host-side accounting (gc_pipeline_host_stats): the reference's RuntimeCounters
@@ -336,10 +355,10 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert,
-                       &P.h0rec, &P.lidar_iw};
+                       &P.h0rec, &P.smap_snap};
   const size_t ssz[] = {(size_t)P.H, (size_t)NN, (size_t)B * 3, (size_t)B * gc::kMapRec, (size_t)B * gc::kMapDer, 8,
                         (size_t)B * gc::kMapRec, 7, 7 * 36, 3, 27, 8, (size_t)PL, (size_t)PL * P.G,
-                        GC_COMB_LEN, 4, gc::kH0Len, 10};
+                        GC_COMB_LEN, 4, gc::kH0Len, 2 * gc::kSnapLen};
   for (size_t i = 0; i < sizeof(ssz) / sizeof(ssz[0]) && rc == GC_OK; ++i) rc = dalloc(p, ssz[i], shared[i]);
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
@@ -370,6 +389,7 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
     gc::set_error(ctx, "hipStreamCreateWithFlags failed for the ingest stream");
     rc = GC_ERR_RUNTIME;
   }
+  p->snap_base = P.smap_snap;
   if (rc == GC_OK) rc = gc::wait_stream(ctx, ctx->stream, "the pipeline's zero fills");  // before any launch
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
@@ -384,6 +404,12 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
   // bounded (a stream stuck behind a failed peer's all-gather is still torn down)
   (void)gc::wait_stream(p->ctx, p->ctx->stream, "the pipeline stream at destruction");
   if (p->cstream) (void)gc::wait_stream(p->ctx, p->cstream, "the ingest stream at destruction");
+  if (p->mstream) (void)gc::wait_stream(p->ctx, p->mstream, "the map-update stream at destruction");
+  for (hipEvent_t e : p->smap_done)
+    if (e && p->ctx->side_ev == e) {
+      p->ctx->side_ev = nullptr;
+      p->ctx->side_pending = false;
+    }
   for (void* a : p->allocs) (void)hipFree(a);
   for (auto& s : p->slots) {
     for (void* d : {(void*)s.dev, (void*)s.bytes, (void*)s.ring, (void*)s.tag, (void*)s.flag})
@@ -393,13 +419,14 @@ int32_t gc_pipeline_destroy(gc_pipeline* p) {
     for (hipEvent_t e : {s.ready, s.odom_done, s.consumed})
       if (e) (void)hipEventDestroy(e);
   }
-  for (hipEvent_t e : {p->x0, p->x1, p->fin_ev[0], p->fin_ev[1]})
+  for (hipEvent_t e : {p->x0, p->x1, p->fin_ev[0], p->fin_ev[1], p->smap_go, p->smap_done[0], p->smap_done[1]})
     if (e) (void)hipEventDestroy(e);
   for (hipEvent_t e : p->st_ev)
     if (e) (void)hipEventDestroy(e);
   if (p->smapW.buf) (void)hipFree(p->smapW.buf);
   if (p->smapW.runs.ptr) (void)hipFree(p->smapW.runs.ptr);
   if (p->cstream) (void)hipStreamDestroy(p->cstream);
+  if (p->mstream) (void)hipStreamDestroy(p->mstream);
   if (p->done_word) (void)hipHostFree(p->done_word);
   delete p;
   return GC_OK;
@@ -716,6 +743,16 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
     fin = p->fin_ev[fin_e];
     p->fin_ticket[fin_e] = 0;  // the event is re-armed by this launch: unusable until it succeeds
   }
+  const int par = (int)(p->pending_ticket & 1);
+  P.smap_snap = p->snap_base + par * gc::kSnapLen;
+  if (p->smap_on && p->smap_done_rec[par]) {
+    // the map update two scans back read this snapshot block: rewritten only after it (long done
+    // by now, the wait costs the stream a barrier)
+    GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, p->smap_done[par], 0));
+    p->smap_done_rec[par] = false;
+  }
+  const bool side = p->smap_on && p->mstream;
+  if (side) fin = p->smap_go;
   GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream, fin));
   // only a launch that carries the event makes it cover this ticket (a failed launch leaves it
   // cleared, so slot_wait_consumed falls back to an event recorded on the compute stream)
@@ -724,14 +761,16 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
   if (p->smap_on) {
     auto& s = p->slots[p->pending_slot];
     const gc::ScanArgs& S = p->pending_S;
-    const gc::ScanMapInput in{s.pts, s.t, S.t0, S.t1, p->smap_voxel, S.t1, p->pending_seq};
-    int rc = gc::scan_map_update(ctx, ctx->stream, &p->smapW, p->smap, P, in);
+    const gc::ScanMapInput in{s.pts, s.t, s.w, S.t0, S.t1, p->smap_voxel, S.t1, p->pending_seq};
+    hipStream_t ms = side ? p->mstream : ctx->stream;
+    if (side) GC_HIP(ctx, hipStreamWaitEvent(ms, p->smap_go, 0));
+    int rc = gc::scan_map_update(ctx, ms, &p->smapW, p->smap, P, in);
     if (rc == GC_OK && p->smap_colors) {
       // primitive_map_fuse ends with colors = rgb = the estimate from the camera accumulators on
       // every slot (primitive_map.py:1090-1098); LiDAR rows leave those inputs unchanged, so the
       // assignment is idempotent until a host operation (insert, merge, a colour upload) writes the
       // colour fields and marks them stale again (gc_pipeline_map_colors_stale)
-      const hipError_t e = gc::launch_fuse_colors(p->smap, P.eps_mass, ctx->stream);
+      const hipError_t e = gc::launch_fuse_colors(p->smap, P.eps_mass, ms);
       if (e != hipSuccess) {
         gc::set_error(ctx, std::string("HIP error ") + hipGetErrorString(e) + " in the map colour pass");
         rc = GC_ERR_RUNTIME;
@@ -741,9 +780,15 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
     }
     // the map update was the slot's last reader: the next staging into the slot orders after this
     // event on every path, a failed launch of the update included (its earlier kernels may be queued)
-    const hipError_t er = hipEventRecord(s.consumed, ctx->stream);
+    hipError_t er = hipEventRecord(s.consumed, ms);
     s.consumed_rec = er == hipSuccess;
     s.consumed_ticket = 0;
+    if (side && er == hipSuccess) {
+      er = hipEventRecord(p->smap_done[par], ms);
+      p->smap_done_rec[par] = er == hipSuccess;
+      ctx->side_ev = p->smap_done[par];
+      ctx->side_pending = er == hipSuccess;
+    }
     if (rc != GC_OK) return rc;
     GC_HIP(ctx, er);
   }
@@ -795,7 +840,16 @@ int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const gc_primitive_map*
                            map->last_supported_scan_seq && map->last_update_scan_seq,
                "NULL map field");
   GC_CHECK_ARG(p->ctx, voxel_m > 0.0, "voxel_m must be positive");
+  if (p->mstream) GC_TRY(gc::wait_stream(p->ctx, p->mstream, "the map-update stream before re-attaching"));
   GC_TRY(gc::scan_map_prepare(p->ctx, &p->smapW, p->P.n_cap, map->m_slots));
+  if (kSmapSide && !p->mstream) {
+    // the start signal orders device work only; the done events keep the system-scope release (a
+    // host copy of the map joined after them reads memory the update wrote)
+    GC_HIP(p->ctx, hipEventCreateWithFlags(&p->smap_go, hipEventDisableTiming | hipEventDisableSystemFence));
+    for (hipEvent_t* e : {&p->smap_done[0], &p->smap_done[1]})
+      GC_HIP(p->ctx, hipEventCreateWithFlags(e, hipEventDisableTiming));
+    GC_HIP(p->ctx, hipStreamCreateWithFlags(&p->mstream, hipStreamNonBlocking));
+  }
   p->smap = *map;
   p->smap_voxel = voxel_m;
   p->smap_colors = map->cam_mass != nullptr && !map->colors_current;
@@ -815,6 +869,7 @@ int32_t gc_pipeline_get_scan_map_count(gc_pipeline* p, int64_t* n_slots) {
   GC_CHECK_ARG(nullptr, p && n_slots, "NULL argument");
   GC_CHECK_ARG(p->ctx, p->smap_on, "no PrimitiveMap attached");
   GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  GC_TRY(gc::join_side(p->ctx));  // the counts of the last update (its stream)
   size_t bytes = 0;
   const int32_t rc = gc::scan_map_count(p->ctx, p->smapW, n_slots, &bytes);
   p->hs[GC_HS_HOST_SYNCS] += 1.0;

@@ -137,6 +137,13 @@ int wait_event(gc_ctx* ctx, hipEvent_t ev, const char* what, double* waited_ms, 
   return bounded_poll(ctx, [&] { return hipEventQuery(ev); }, what, waited_ms, spin_polls, lim);
 }
 
+int join_side(gc_ctx* ctx) {
+  if (!ctx || !ctx->side_pending) return GC_OK;
+  ctx->side_pending = false;
+  GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev, 0));
+  return GC_OK;
+}
+
 int run_table(gc_ctx* ctx, hipStream_t st, RunTableBuf* T, int64_t rows) {
   uint32_t bits = 8;  // >= 4 x rows entries (gc_runs.h); the links: rows <= 2^bits / 4
   while (bits < 31 && ((int64_t)1 << bits) < 4 * rows) ++bits;
@@ -210,6 +217,7 @@ int32_t gc_ctx_destroy(gc_ctx* ctx) {
   if (!ctx) return GC_OK;
   (void)hipSetDevice(ctx->device);
   if (ctx->comm) gc::comm_detach_ctx(ctx->comm);
+  (void)gc::join_side(ctx);
   // bounded: a context whose stream is stuck (a failed peer) is still torn down
   (void)gc::wait_stream(ctx, ctx->stream, "the stream at context destruction");
   if (ctx->scratch) (void)hipFree(ctx->scratch);
@@ -223,6 +231,7 @@ int32_t gc_ctx_destroy(gc_ctx* ctx) {
 
 int32_t gc_ctx_synchronize(gc_ctx* ctx) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   GC_HIP(ctx, hipSetDevice(ctx->device));
   return gc::wait_stream(ctx, ctx->stream, "the context's stream (gc_ctx_synchronize)");
 }
@@ -283,6 +292,7 @@ int32_t gc_buffer_alloc(gc_ctx* ctx, uint64_t bytes, void** d_ptr) {
 
 int32_t gc_buffer_free(gc_ctx* ctx, void* d_ptr) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   if (!d_ptr) return GC_OK;
   size_t c = 0;
   {
@@ -309,6 +319,7 @@ int32_t gc_buffer_free(gc_ctx* ctx, void* d_ptr) {
 
 int32_t gc_ctx_trim(gc_ctx* ctx) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   GC_HIP(ctx, hipSetDevice(ctx->device));
   if (int rc = gc::wait_stream(ctx, ctx->stream, "the stream before an arena trim")) return rc;
   std::lock_guard<std::mutex> lock(ctx->arena_mu);
@@ -335,6 +346,7 @@ int32_t gc_ctx_alloc_stats(gc_ctx* ctx, int64_t* h_out6) {
 
 int32_t gc_buffer_upload(gc_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   if (bytes == 0) return GC_OK;
   GC_HIP(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
   return gc::wait_stream(ctx, ctx->stream, "an upload");
@@ -342,6 +354,7 @@ int32_t gc_buffer_upload(gc_ctx* ctx, void* d_dst, const void* h_src, uint64_t b
 
 int32_t gc_buffer_download(gc_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   if (bytes == 0) return GC_OK;
   GC_HIP(ctx, hipMemcpyAsync(h_dst, d_src, bytes, hipMemcpyDeviceToHost, ctx->stream));
   return gc::wait_stream(ctx, ctx->stream, "a download");
@@ -349,6 +362,7 @@ int32_t gc_buffer_download(gc_ctx* ctx, void* h_dst, const void* d_src, uint64_t
 
 int32_t gc_buffer_copy(gc_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   if (bytes == 0) return GC_OK;
   GC_HIP(ctx, hipMemcpyAsync(d_dst, d_src, bytes, hipMemcpyDeviceToDevice, ctx->stream));
   return GC_OK;
@@ -356,6 +370,7 @@ int32_t gc_buffer_copy(gc_ctx* ctx, void* d_dst, const void* d_src, uint64_t byt
 
 int32_t gc_buffer_memset(gc_ctx* ctx, void* d_dst, int32_t value, uint64_t bytes) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   if (bytes == 0) return GC_OK;
   GC_HIP(ctx, hipMemsetAsync(d_dst, value, bytes, ctx->stream));
   return GC_OK;
@@ -383,6 +398,7 @@ int32_t gc_event_destroy(gc_event* ev) {
 
 int32_t gc_event_record(gc_ctx* ctx, gc_event* ev) {
   GC_CHECK_ARG(nullptr, ctx && ev, "NULL argument");
+  if (int rc_j = gc::join_side(ctx)) return rc_j;
   GC_HIP(ctx, hipEventRecord(ev->ev, ctx->stream));
   return GC_OK;
 }

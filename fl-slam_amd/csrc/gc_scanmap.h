@@ -24,7 +24,7 @@ struct ScanMapWork {
 };
 
 struct ScanMapInput {
-  const double *pts, *t;  // the scan slot's raw points (n_in, 3) and times
+  const double *pts, *t, *w;  // the scan slot's raw points (n_in, 3), times and weights
   double t0, t1;          // scan window (a4)
   double voxel;           // world voxel edge of the slot hash (m)
   double timestamp;       // scan_end (primitive_map.py:1109)

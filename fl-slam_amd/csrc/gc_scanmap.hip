@@ -41,9 +41,10 @@ namespace {
 
 struct ScanMapArgs {
   gc_primitive_map map;
-  const double *pts, *t, *w_win, *bscal;  // the scan slot and predict's per-point w x window, budget
-  const double* h0;                       // reduced record: [z_t 6, Σ_pose 36, ξ 6] of hypothesis 0
-  const double* lidar_iw;                 // [ν_2, Ψ_2] of the scan, before its measurement-IW apply
+  const double *pts, *t, *w;  // the scan slot's raw points, times and weights
+  const double* bscal;        // the scan's a1 budget scalars       } the scan's snapshot
+  const double* h0;           // reduced record: [z_t 6, Σ_pose 36, ξ 6] of hypothesis 0 } (PipeDev::smap_snap,
+  const double* lidar_iw;     // [ν_2, Ψ_2] before the scan's measurement-IW apply     } k_combine_final)
   int64_t n_cap;
   double t0, t1, o0, o1, o2, voxel, timestamp, eps_mass, eps_psd;
   int64_t scan_seq;
@@ -62,7 +63,10 @@ GC_DEV bool smap_point(const ScanMapArgs& A, int64_t j, double* p0, double* w) {
   const double p[3] = {A.pts[3 * i], A.pts[3 * i + 1], A.pts[3 * i + 2]};
   const double alpha = (A.t[i] - A.t0) / fmax(A.t1 - A.t0, 1e-12);
   deskew_point(p, alpha, A.h0 + 42, p0);
-  *w = A.w_win[j] * A.bscal[2];
+  // the point's w x time window as the predict launch forms it (window_points, gc_belief.hip), then
+  // the budget's mass scale: from the slot, so the update reads nothing the next scan rewrites
+  const double denom = fmax(A.t1 - A.t0, 1e-12);
+  *w = (A.w[i] * window_weight(A.t[i], A.t0, A.t1, 0.1 * denom)) * A.bscal[2];
   return *w > 0.0;
 }
 
@@ -374,9 +378,11 @@ int32_t scan_map_update(gc_ctx* ctx, hipStream_t st, ScanMapWork* W, const gc_pr
                         const PipeDev& P, const ScanMapInput& in) {
   ScanMapArgs A{};
   A.map = map;
-  A.pts = in.pts; A.t = in.t; A.w_win = P.w_win; A.bscal = P.budget;
-  A.h0 = P.send + rec_h0(P.B);  // the reduced record (k_combine_final, earlier on this stream)
-  A.lidar_iw = P.lidar_iw;  // written by k_combine_final, earlier on this stream
+  A.pts = in.pts; A.t = in.t; A.w = in.w;
+  // the scan's snapshot, written by k_combine_final (ordered before this update by the caller)
+  A.h0 = P.smap_snap;
+  A.lidar_iw = P.smap_snap + kSnapIW;
+  A.bscal = P.smap_snap + kSnapBudget;
   A.n_cap = P.n_cap;
   A.t0 = in.t0; A.t1 = in.t1;
   A.o0 = P.o0; A.o1 = P.o1; A.o2 = P.o2;
