@@ -15,6 +15,7 @@
 #include "gc_internal.h"
 #include "gc_pipe.h"
 #include "gc_wgla.h"
+#include "gc_opsdev.h"
 
 namespace gc {
 namespace {
@@ -143,10 +144,100 @@ __global__ void __launch_bounds__(256) k_hyp_certs(PipeDev P) {
   wave_conditioning<kDZ>(M, P.eps_psd, buf[wv], P.hcond + ((int64_t)h * 2 + m) * 4);
 }
 
+// ------------------------------------------------------------------ full projection certificates
+// The reference's cert_vec [projection_delta, sym_delta, eig_min, eig_max, cond, near_null_count] of
+// every remaining PSD projection of a scan (domain_projection_psd_core, primitives.py:80-123), from
+// the unprojected operands by a full eigen-decomposition (the scan itself certifies these projections
+// by Cholesky and keeps only their deltas):
+//   per hypothesis, one thread per 3x3 (psd_project3: cyclic Jacobi): the B bins' Σ_p re-formed from
+//   the bin row's raw sums exactly as finalize_bin forms it (binning.py:175-187), then the MF L_rot and
+//   planar L_trans that k_evidence stored unprojected (P.praw);
+//   per scan, one workgroup each (wg_psd_project: parallel Jacobi): the barycenter L (the reduced
+//   record in P.send, hypothesis.py:99), the 7 process-IW blocks padded to 6x6 (P.iwraw,
+//   k_combine_final) and Q assembled from the updated IW state (inverse_wishart_jax.py:35-68); the 3
+//   measurement blocks (3x3) by psd_project3 on one lane.
+constexpr int kScanCertLds = 2 * kDZ * kDZ + 2 * kDZ * kDZ + 4 * kDZ + 8 + 8;
+
+GC_DEV void bin_sigma_raw(const double* o, double eps_mass, double* Sr) {
+  // finalize_bin's Σ_raw (gc_binfin.h) from its stats row: N = o[0], Σ p = o[26:29], Σ p pᵀ = o[29:38]
+  const double invN = 1.0 / (o[0] + eps_mass + kF64Eps);
+  const double pb[3] = {o[26] * invN, o[27] * invN, o[28] * invN};
+  for (int i = 0; i < 3; ++i)
+    for (int j = 0; j < 3; ++j) Sr[3 * i + j] = o[29 + 3 * i + j] * invN - pb[i] * pb[j];
+}
+
+__global__ void __launch_bounds__(256) k_proj_certs(PipeDev P) {
+  const int B = P.B, per = B + 2;
+  const int nh = (P.Hl * per + kWG - 1) / kWG;
+  if ((int)blockIdx.x < nh) {
+    const int item = blockIdx.x * kWG + threadIdx.x;
+    if (item >= P.Hl * per) return;
+    const int h = item / per, k = item % per;
+    double A[9], Mp[9], c[6];
+    if (k < B) {
+      bin_sigma_raw(P.stats + ((int64_t)h * B + k) * GC_BIN_STATS, P.eps_mass, A);
+    } else {
+      const double* r = P.praw + (int64_t)h * 18 + (k - B) * 9;
+      for (int q = 0; q < 9; ++q) A[q] = r[q];
+    }
+    psd_project3(A, P.eps_psd, Mp, c);
+    for (int q = 0; q < 6; ++q) P.pcert[(int64_t)item * 6 + q] = c[q];
+    return;
+  }
+  __shared__ double sm[kScanCertLds];
+  const int s = (int)blockIdx.x - nh, t = threadIdx.x, n22 = kDZ;
+  double* M = sm;
+  double* Mp = M + kDZ * kDZ;
+  double* scr = Mp + kDZ * kDZ;
+  double* red = scr + 2 * kDZ * kDZ + 4 * kDZ;
+  double* c6 = red + 8;
+  int n;
+  if (s == GC_PCERT_BARY) {
+    n = n22;
+    for (int i = t; i < kDZ * kDZ; i += kWG) M[i] = P.send[kPL + i];
+  } else if (s < GC_PCERT_MEAS0) {
+    n = 6;
+    for (int i = t; i < 36; i += kWG) M[i] = P.iwraw[(s - GC_PCERT_PROC0) * 36 + i];
+  } else if (s < GC_PCERT_Q) {
+    // a 3x3 block: psd_project3 on one lane (the per-operator entries route d <= 3 there as well)
+    if (t == 0) {
+      double A[9], Ap[9], c[6];
+      for (int i = 0; i < 9; ++i) A[i] = P.iwraw[7 * 36 + (s - GC_PCERT_MEAS0) * 9 + i];
+      psd_project3(A, P.eps_psd, Ap, c);
+      for (int q = 0; q < 6; ++q) P.pcert[((int64_t)P.Hl * per + s) * 6 + q] = c[q];
+    }
+    return;
+  } else {
+    // Q = ⊕ Ψ_b / den_b over the masked blocks (block diagonal; wg_iw_Q's den)
+    n = n22;
+    for (int i = t; i < kDZ * kDZ; i += kWG) {
+      const int r = i / kDZ, q = i % kDZ;
+      double v = 0.0;
+      for (int b = 0; b < 7; ++b) {
+        const int s0 = kIwBlockStart[b], d = kIwBlockDim[b];
+        if (r >= s0 && r < s0 + d && q >= s0 && q < s0 + d) {
+          const double den = softplus(50.0 * (P.nu_proc[b] - d - 1.0)) / 50.0 + 1e-12;
+          v = P.Psi_proc[b * 36 + 6 * (r - s0) + (q - s0)] / den;
+        }
+      }
+      M[i] = v;
+    }
+  }
+  __syncthreads();
+  wg_psd_project(M, Mp, P.eps_psd, n, scr, red, c6);
+  if (t < 6) P.pcert[((int64_t)P.Hl * per + s) * 6 + t] = c6[t];
+}
+
 }  // namespace
 
 hipError_t launch_hyp_certs(const PipeDev& P, hipStream_t st) {
   hipLaunchKernelGGL(k_hyp_certs, dim3((unsigned)((2 * P.Hl + kCertWaves - 1) / kCertWaves)), dim3(256), 0, st, P);
+  return hipGetLastError();
+}
+
+hipError_t launch_proj_certs(const PipeDev& P, hipStream_t st) {
+  const int nh = (P.Hl * (P.B + 2) + kWG - 1) / kWG;
+  hipLaunchKernelGGL(k_proj_certs, dim3((unsigned)(nh + kScanCerts)), dim3(256), 0, st, P);
   return hipGetLastError();
 }
 

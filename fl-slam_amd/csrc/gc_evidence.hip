@@ -176,6 +176,16 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     const int i = t / 3, j = t % 3;
     Lev[i * n + j] += pt[3 + t];                  // translation block [0:3, 0:3]
     Lev[(3 + i) * n + (3 + j)] += mf[9 + t];      // rotation block [3:6, 3:6]
+    // the two 3x3 information matrices before their PSD projections, for the projection certificates
+    // (gc_certs.hip): L_rot = V diag(s1+s2, s0+s2, s0+s1) Vᵀ as mf_information forms it, L_trans =
+    // the summed WLS information masked by the z-scale as planar_finalize forms it
+    const double* V = sc + 116;
+    const double* s3 = mf + 24;
+    const double msk[3] = {1.0, 1.0, P.map_misc[0]};
+    double* raw = P.praw + (int64_t)hl * 18;
+    raw[t] = V[3 * i] * (s3[1] + s3[2]) * V[3 * j] + V[3 * i + 1] * (s3[0] + s3[2]) * V[3 * j + 1] +
+             V[3 * i + 2] * (s3[0] + s3[1]) * V[3 * j + 2];
+    raw[9 + t] = acc[t] * msk[i] * msk[j];
   }
   if (t < 3) { hev[t] += pt[12 + t]; hev[3 + t] += mf[18 + t]; }
   __syncthreads();
@@ -642,7 +652,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     if (t < 10) P.smap_snap[kSnapIW + t] = t == 0 ? P.nu_meas[2] : P.Psi_meas[18 + t - 1];
     __syncthreads();
     wg_iw_meas_apply(P.nu_meas, P.Psi_meas, Ri, Ri + (kPDNUM - kPDPSIM), P.eps_psd, P.nu_max, P.nu_meas, P.Psi_meas,
-                     P.iw_cert + 2, tab);
+                     P.iw_cert + 2, tab, P.iwraw + 7 * 36);
     GC_PHASE_WG(P, 47, 3);
     return;
   }
@@ -661,7 +671,7 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     GC_PHASE_WG(P, 22, 2);
     // process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
     wg_iw_proc_apply(P.nu_proc, P.Psi_proc, Ri, Ri + (kPDNUP - kPDPSIP), S.w_process, P.eps_psd, P.nu_max, P.nu_proc,
-                     P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab);
+                     P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab, P.iwraw);
     GC_PHASE_WG(P, 23, 2);
     GC_PHASE_WG(P, 24, 2);
     iw_Q_wg(P, Qs, Qp, Sx, red);

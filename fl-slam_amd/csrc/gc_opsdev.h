@@ -555,7 +555,7 @@ GC_DEV double nu_project(double nu_raw, double dim, double nu_max) {
 GC_DEV void wg_iw_proc_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double w,
                              double eps_psd, double nu_max, double* nu_out, double* Psi_out, double* cert,
                              double* Qs, double* blk, double* blkp, double* Sx, double* red, double* c6,
-                             double* tab) {
+                             double* tab, double* raw_out = nullptr) {
   const int t = threadIdx.x;
   if (t < 7) {
     const double nr = kIwRhoProc[t] * nu[t] + w * dnu[t];
@@ -576,12 +576,16 @@ GC_DEV void wg_iw_proc_apply(const double* nu, const double* Psi, const double* 
       const double a = rho * Ps[0] + w * dP[0], pv = fmax(a, eps_psd);
       for (int k = 0; k < 9; ++k) Pp[k] = (k == 0) ? pv : ((k % 4 == 0) ? eps_psd : 0.0);
       d2 = 5.0 * eps_psd * eps_psd + (pv - a) * (pv - a);
+      if (raw_out)
+        for (int k = 0; k < 36; ++k) raw_out[t * 36 + k] = k == 0 ? a : 0.0;
     } else {
       double A[9], c[6];
       for (int i = 0; i < 3; ++i)
         for (int j = 0; j < 3; ++j) A[3 * i + j] = rho * Ps[6 * i + j] + w * dP[6 * i + j];
       psd_project3_fast(A, eps_psd, Pp, c);
       d2 = 3.0 * eps_psd * eps_psd + c[0] * c[0];
+      if (raw_out)  // the masked block, padded to 6x6 (the reference's projection operand)
+        for (int k = 0; k < 36; ++k) raw_out[t * 36 + k] = (k / 6 < 3 && k % 6 < 3) ? A[3 * (k / 6) + k % 6] : 0.0;
     }
     tab[8 + t] = sqrt(d2);
     for (int k = 0; k < 36; ++k) {
@@ -589,7 +593,10 @@ GC_DEV void wg_iw_proc_apply(const double* nu, const double* Psi, const double* 
       Qs[t * 36 + k] = (i < 3 && j < 3) ? Pp[3 * i + j] : ((i == j) ? eps_psd : 0.0);
     }
   }
-  if (t < 36) blk[t] = kIwRhoProc[6] * Psi[6 * 36 + t] + w * dPsi[6 * 36 + t];
+  if (t < 36) {
+    blk[t] = kIwRhoProc[6] * Psi[6 * 36 + t] + w * dPsi[6 * 36 + t];
+    if (raw_out) raw_out[6 * 36 + t] = blk[t];
+  }
   __syncthreads();
   wg_psd_project_fast(blk, blkp, eps_psd, 6, Sx, red, c6);
   for (int k = t; k < 6 * 36; k += kWG) Psi_out[k] = Qs[k];
@@ -610,7 +617,7 @@ GC_DEV void wg_iw_proc_apply(const double* nu, const double* Psi, const double* 
 // Ψ' = PSD(sym(ρ Ψ + dΨ)), ν' = proj(ρ ν + dν). tab: 6 doubles; cert (thread 0) = [Σ psd Δ, Σ |Δν|].
 GC_DEV void wg_iw_meas_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu,
                              double eps_psd, double nu_max, double* nu_out, double* Psi_out, double* cert,
-                             double* tab) {
+                             double* tab, double* raw_out = nullptr) {
   const int t = threadIdx.x;
   if (t < 3) {
     double Mr[9], Mp[9], cc[6], Ms[9];
@@ -618,6 +625,8 @@ GC_DEV void wg_iw_meas_apply(const double* nu, const double* Psi, const double* 
     for (int i = 0; i < 3; ++i)
       for (int j = 0; j < 3; ++j) Ms[3 * i + j] = 0.5 * (Mr[3 * i + j] + Mr[3 * j + i]);
     psd_project3_fast(Ms, eps_psd, Mp, cc);
+    if (raw_out)
+      for (int k = 0; k < 9; ++k) raw_out[t * 9 + k] = Ms[k];
     const double nr = kIwRhoMeas[t] * nu[t] + dnu[t];
     const double nn = nu_project(nr, 3.0, nu_max);
     tab[t] = cc[0];

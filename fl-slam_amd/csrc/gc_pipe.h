@@ -61,6 +61,10 @@ struct PipeDev {
   double *lpose;                           // (Hl, 36) pose block of L_evidence (diagnostics tape)
   double *Sig;                             // (Hl, 22, 22) Σ_post = (L_post + εI)⁻¹ of the last scan
   double *hcond;                           // (Hl, 2, 4) in-scan ConditioningCerts [L_pred, L_post] (gc_certs.hip)
+  double *praw;                            // (Hl, 18) the unprojected MF L_rot and planar L_trans of the last
+                                           // scan (k_evidence), for their projection certificates
+  double *pcert;                           // (Hl (B + 2) + kScanCerts, 6) full projection certificates
+                                           // (gc_certs.hip, layout GC_PCERT_* in include/gcslam.h)
   // shared
   double *weights;                         // (H)
   double *Q;                               // (22, 22)
@@ -83,7 +87,14 @@ struct PipeDev {
   int G;                                   // ranks
   double *comb;                            // combined belief: L 484, h 22, z 22, X 6, stamp, cert 16
   double *iw_cert;                         // [proc psd, proc nu, meas psd, meas nu]
+  double *iwraw;                           // (kIwRawLen) the scan's unprojected IW blocks (k_combine_final):
+                                           // process 7 x 6x6 masked, measurement 3 x 3x3 symmetrised
 };
+
+constexpr int kIwRawLen = 7 * 36 + 3 * 9;
+// scan-level projection certificates after the per-hypothesis ones: the barycenter L, the 7 process-IW
+// blocks, the 3 measurement-IW blocks, Q
+constexpr int kScanCerts = 12;
 
 struct ScanArgs {
   const double *imu_t, *imu_g, *imu_a;     // (M), (M,3), (M,3)
@@ -135,6 +146,8 @@ hipError_t launch_map_derive(const PipeDev& P, hipStream_t st);
 hipError_t launch_iw_Q(const PipeDev& P, hipStream_t st);
 // the per-hypothesis ConditioningCerts of L_pred and L_post into P.hcond (gc_certs.hip)
 hipError_t launch_hyp_certs(const PipeDev& P, hipStream_t st);
+// the full projection certificates of the last scan into P.pcert (gc_certs.hip)
+hipError_t launch_proj_certs(const PipeDev& P, hipStream_t st);
 }  // namespace gc
 
 struct gc_ctx;

@@ -127,6 +127,8 @@ struct gc_pipeline {
   // in-scan ConditioningCerts (gc_pipeline_set_inscan_certs): launched after every scan's evidence;
   // hcond_scan: P.hcond holds the certificates of the current L_pred / L (cleared by a belief upload)
   bool inscan_certs = false, hcond_scan = false;
+  // P.pcert holds the projection certificates of the last finished scan (computed inside it)
+  bool pcert_scan = false;
   // getter workspace (conditioning certificates), allocated with the pipeline: no hipMalloc / hipFree
   // (device-synchronising) on a getter a live node calls every scan
   double* ws = nullptr;
@@ -344,21 +346,22 @@ int32_t gc_pipeline_create(gc_ctx* ctx, const gc_pipeline_dims* dims, const doub
   double** fields[] = {&P.X, &P.z, &P.L, &P.h, &P.stamp, &P.Lpred, &P.hpred, &P.pred_cert, &P.pose_pred, &P.xi,
                        &P.imu_out, &P.dPsiM, &P.stats, &P.bincert, &P.io_L, &P.io_h, &P.io_cert, &P.dPsiP,
                        &P.mu_fin, &P.diag, &P.mu_aux, &P.io_parts, &P.lpose, &P.Sig, &P.binaux, &P.hcond,
-                       &P.pred_mode};
+                       &P.pred_mode, &P.praw, &P.pcert};
   const size_t sizes[] = {(size_t)Hl * 6, (size_t)Hl * 22, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl,
                           (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kPredCert, (size_t)Hl * 6,
                           (size_t)Hl * 6, (size_t)Hl * gc::kImuOut, (size_t)Hl * 27, (size_t)Hl * B * 38,
                           (size_t)Hl * 8, (size_t)Hl * NN, (size_t)Hl * 22, (size_t)Hl * gc::kIoCert,
                           (size_t)Hl * 252, (size_t)Hl * 22, (size_t)Hl * gc::kHypDiag, (size_t)Hl * gc::kMuAux,
                           (size_t)Hl * gc::kIoParts, (size_t)Hl * 36, (size_t)Hl * NN, (size_t)Hl * B * 2,
-                          (size_t)Hl * 8, (size_t)Hl};
+                          (size_t)Hl * 8, (size_t)Hl, (size_t)Hl * 18,
+                          ((size_t)Hl * (B + 2) + gc::kScanCerts) * 6};
   for (size_t i = 0; i < sizeof(sizes) / sizeof(sizes[0]) && rc == GC_OK; ++i) rc = dalloc(p, sizes[i], fields[i]);
   double** shared[] = {&P.weights, &P.Q, &P.bins, &P.map, &P.map_der, &P.map_misc, &P.map_inc, &P.nu_proc,
                        &P.Psi_proc, &P.nu_meas, &P.Psi_meas, &P.budget, &P.send, &P.gather, &P.comb, &P.iw_cert,
-                       &P.h0rec, &P.smap_snap};
+                       &P.h0rec, &P.smap_snap, &P.iwraw};
   const size_t ssz[] = {(size_t)P.H, (size_t)NN, (size_t)B * 3, (size_t)B * gc::kMapRec, (size_t)B * gc::kMapDer, 8,
                         (size_t)B * gc::kMapRec, 7, 7 * 36, 3, 27, 8, (size_t)PL, (size_t)PL * P.G,
-                        GC_COMB_LEN, 4, gc::kH0Len, 2 * gc::kSnapLen};
+                        GC_COMB_LEN, 4, gc::kH0Len, 2 * gc::kSnapLen, gc::kIwRawLen};
   for (size_t i = 0; i < sizeof(ssz) / sizeof(ssz[0]) && rc == GC_OK; ++i) rc = dalloc(p, ssz[i], shared[i]);
   if (rc != GC_OK) {
     gc_pipeline_destroy(p);
@@ -757,6 +760,9 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
   // only a launch that carries the event makes it cover this ticket (a failed launch leaves it
   // cleared, so slot_wait_consumed falls back to an event recorded on the compute stream)
   if (fin_e >= 0) p->fin_ticket[fin_e] = p->pending_ticket;
+  // the scan's remaining projection certificates (the record and IW blocks combine_final just used)
+  if (p->inscan_certs) GC_HIP(ctx, gc::launch_proj_certs(P, ctx->stream));
+  p->pcert_scan = p->inscan_certs;
   GC_TRY(stage_event(p, 6));
   if (p->smap_on) {
     auto& s = p->slots[p->pending_slot];
@@ -1002,6 +1008,18 @@ int32_t gc_pipeline_get_hyp_conditioning(gc_pipeline* p, double* h_out) {
     for (int m = 0; m < 2; ++m)
       for (int k = 0; k < 4; ++k) h_out[((size_t)h * 2 + m) * 4 + k] = c6[((size_t)m * Hl + h) * 6 + 2 + k];
   return GC_OK;
+}
+
+int32_t gc_pipeline_get_projection_certs(gc_pipeline* p, double* h_hyp, double* h_scan) {
+  GC_CHECK_ARG(nullptr, p && h_hyp && h_scan, "NULL argument");
+  GC_CHECK_ARG(p->ctx, p->sig_cached, "no scan has run since the beliefs were set");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  const gc::PipeDev& P = p->P;
+  // computed inside the scan (in-scan certificates), or now from the last scan's stored operands
+  if (!p->pcert_scan) GC_HIP(p->ctx, gc::launch_proj_certs(P, p->ctx->stream));
+  const size_t nh = (size_t)P.Hl * (P.B + 2) * 6;
+  GC_TRY(down(p, h_hyp, P.pcert, nh));
+  return down(p, h_scan, P.pcert + nh, (size_t)gc::kScanCerts * 6);
 }
 
 int32_t gc_pipeline_get_hyp_diag(gc_pipeline* p, double* h_diag) {

@@ -84,6 +84,7 @@ SIGNATURES = {
     "gc_pipeline_get_combined": [_vp, _vp],
     "gc_pipeline_get_hyp_diag": [_vp, _vp],
     "gc_pipeline_get_hyp_conditioning": [_vp, _vp],
+    "gc_pipeline_get_projection_certs": [_vp, _vp, _vp],
     "gc_pipeline_get_lpose6": [_vp, _vp],
     "gc_pipeline_get_bin_stats": [_vp, _vp, _vp, _vp],
     "gc_pipeline_get_hyp_stats": [_vp, _vp, _vp, _vp],
@@ -159,6 +160,9 @@ GC_HS_NAMES = ("scans", "scan_enqueue_ms", "scan_enqueue_max_ms", "scan_wait_ms"
                "stage_work_ms", "stage_work_max_ms", "stage_wait_ms", "stage_wait_max_ms", "host_syncs", "h2d_bytes",
                "d2h_bytes", "jit_recompiles")
 GC_COMB_LEN = 484 + 22 + 22 + 6 + 16
+# gc_pipeline_get_projection_certs layout (include/gcslam.h GC_PCERT_*)
+GC_PCERT_SCAN = 12
+GC_PCERT_BARY, GC_PCERT_PROC0, GC_PCERT_MEAS0, GC_PCERT_Q = 0, 1, 8, 11
 GC_COMM_ID_BYTES = 128
 GC_PRED_CERT = 8
 GC_PREINT_OUT = 32

@@ -250,6 +250,20 @@ class BatchedScanPipeline:
         self._call("gc_pipeline_get_hyp_conditioning", _p(o))
         return o
 
+    def projection_certs(self):
+        """The reference's cert_vec [projection_delta, sym_delta, eig_min, eig_max, cond,
+        near_null_count] (primitives.py:80-123) of the last scan's other PSD projections:
+        hyp (Hl, B + 2, 6) = per hypothesis the B bins' Σ_p (binning.py:175-187), the MF L_rot and
+        the planar L_trans (matrix_fisher_evidence.py:330, :609); scan (12, 6) = the barycenter L
+        (hypothesis.py:99), the 7 process-IW blocks, the 3 measurement-IW blocks and Q
+        (inverse_wishart_jax.py:67,168; measurement_noise_iw_jax.py:82). Computed inside the scan with
+        set_inscan_certs, else on demand from the last scan's stored operands."""
+        hyp, scan = np.empty((self.Hl, self.B + 2, 6)), np.empty((_abi.GC_PCERT_SCAN, 6))
+        self._call("gc_pipeline_get_projection_certs", _p(hyp), _p(scan))
+        return dict(bins=hyp[:, :self.B], mf=hyp[:, self.B], planar=hyp[:, self.B + 1],
+                    barycenter=scan[_abi.GC_PCERT_BARY], iw_proc=scan[_abi.GC_PCERT_PROC0:_abi.GC_PCERT_MEAS0],
+                    iw_meas=scan[_abi.GC_PCERT_MEAS0:_abi.GC_PCERT_Q], Q=scan[_abi.GC_PCERT_Q])
+
     def lpose6(self):
         """L_evidence[pose, pose] per hypothesis of the last scan (Hl, 6, 6)."""
         o = np.empty((self.Hl, 6, 6))

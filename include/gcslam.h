@@ -335,6 +335,28 @@ int32_t gc_pipeline_get_hyp_conditioning(gc_pipeline* p, double* h_out);
 /* In-scan ConditioningCerts (off by default): on != 0 makes every later scan emit the certificates
  * gc_pipeline_get_hyp_conditioning reads, as the reference emits them on every predict / fusion call. */
 int32_t gc_pipeline_set_inscan_certs(gc_pipeline* p, int32_t on);
+/* The full certificate vector of every other PSD projection of the last scan, in the reference's
+ * cert_vec layout [projection_delta, sym_delta, eig_min, eig_max, cond, near_null_count]
+ * (domain_projection_psd_core, primitives.py:80-123; eigenvalues clamped at eps_psd, near-null =
+ * clamped eigenvalues below 10 eps_psd), recomputed from the unprojected matrices by a full
+ * eigen-decomposition (the scan certifies these projections by Cholesky and keeps only their deltas):
+ *   h_hyp  (Hl, B + 2, 6): per hypothesis, GC_PCERT_BIN0 + b = the a6 Σ_p of bin b (binning.py:175-187),
+ *          GC_PCERT_MF(B) = the a7 L_rot (matrix_fisher_evidence.py:330-331), GC_PCERT_PLANAR(B) = the
+ *          a8 L_trans (matrix_fisher_evidence.py:609-610);
+ *   h_scan (GC_PCERT_SCAN, 6): the a16 barycenter L (hypothesis.py:99), the 7 process-IW blocks
+ *          (inverse_wishart_jax.py:168-172, each padded 6x6 block), the 3 measurement-IW blocks
+ *          (measurement_noise_iw_jax.py:82-86) and Q (inverse_wishart_jax.py:67).
+ * With in-scan certificates on, every scan computes them after its combine; otherwise this getter
+ * does, from the last scan's stored matrices (call it before the next scan). Synchronises the stream. */
+#define GC_PCERT_BIN0 0
+#define GC_PCERT_MF(B) (B)
+#define GC_PCERT_PLANAR(B) ((B) + 1)
+#define GC_PCERT_SCAN 12
+#define GC_PCERT_BARY 0
+#define GC_PCERT_PROC0 1
+#define GC_PCERT_MEAS0 8
+#define GC_PCERT_Q 11
+int32_t gc_pipeline_get_projection_certs(gc_pipeline* p, double* h_hyp, double* h_scan);
 /* The a2 predict's route (predict.py:43-98). 0 (default): split at its first projection — when
  * Σ'_psd = Σ'_sym is certified, the predicted moments the bins need (μ_inc, σ_warp) are solved from Σ'
  * directly, (L_pred + ε_l I)⁻¹ L_pred = (I + ε_l(Σ' + ε_l I))⁻¹, and L_pred / h_pred / the predict cert

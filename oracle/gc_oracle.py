@@ -517,10 +517,11 @@ def moments_finalize(N, s_dir, S_sc, sum_p, sum_ppT, sum_cov, eps_psd=EPS_PSD, e
     p_bar = sum_p * inv_N[:, None]
     Sig_raw = sum_ppT * inv_N[:, None, None] - np.einsum("bi,bj->bij", p_bar, p_bar) + sum_cov * inv_N[:, None, None]
     Sig = np.empty_like(Sig_raw)
+    certs = np.empty((N.shape[0], 6))
     psd_total = 0.0
     for b in range(N.shape[0]):
-        Sig[b], c = psd_project(Sig_raw[b], eps_psd)
-        psd_total += c[0]
+        Sig[b], certs[b] = psd_project(Sig_raw[b], eps_psd)
+        psd_total += certs[b, 0]
     Rbar = np.linalg.norm(s_dir, axis=1) * inv_N
     kap = kappa_batch(Rbar)
     tm = np.sum(N)
@@ -528,7 +529,7 @@ def moments_finalize(N, s_dir, S_sc, sum_p, sum_ppT, sum_cov, eps_psd=EPS_PSD, e
     sf = float(np.mean(N / (N + eps_mass)))
     return dict(N=N, s_dir=s_dir, S_dir_scatter=S_sc, p_bar=p_bar, Sigma_p=Sig, kappa=kap,
                 sum_p=sum_p, sum_ppT=sum_ppT, ess=float(ess), support_frac=sf,
-                psd_delta=float(psd_total), max_eps_ratio=float(np.max(eps_ratio)),
+                psd_delta=float(psd_total), psd_certs=certs, max_eps_ratio=float(np.max(eps_ratio)),
                 trig=trigger(psd=float(psd_total), mass=float(np.max(eps_ratio))))
 
 
@@ -635,7 +636,7 @@ def matrix_fisher(R_pred, scan_s, scan_S, scan_N, map_s, map_S, map_N, eps_psd=E
     N_eff = float(np.sum(wf))
     nll = 0.5 * float(delta @ L_rot @ delta)
     return dict(R_mf=R_mf, L_rot=L_rot, h_rot=h_rot, delta_rot=delta, svd=s, N_eff=N_eff,
-                nll_per_ess=nll / (N_eff + eps), psd_delta=float(pc[0]),
+                nll_per_ess=nll / (N_eff + eps), psd_delta=float(pc[0]), psd_cert=pc,
                 scan_metrics=scatter_metrics(scan_S.sum(0), float(scan_N.sum()), eps),
                 map_metrics=scatter_metrics(map_S.sum(0), float(map_N.sum()), eps),
                 trig=trigger(psd=float(pc[0]), mass=eps / (N_eff + eps)))
@@ -664,7 +665,7 @@ def planar_translation(t_pred, scan_p, scan_Sig, scan_N, map_c, map_Sig, map_Np,
     N_eff = float(np.sum(wb))
     nll = 0.5 * float(delta @ L_t @ delta)
     return dict(t_wls=t_wls, L_trans=L_t, h_trans=h_t, delta_trans=delta, z_scale=zs, N_eff=N_eff,
-                nll_per_ess=nll / (N_eff + eps), psd_delta=float(pc[0]),
+                nll_per_ess=nll / (N_eff + eps), psd_delta=float(pc[0]), psd_cert=pc,
                 xy_info_scale=0.5 * (L_t[0, 0] + L_t[1, 1]), z_info_scale=L_t[2, 2],
                 trig=trigger(psd=float(pc[0]), mass=eps / (N_eff + eps)))
 
@@ -1113,6 +1114,33 @@ def iw_meas_apply(nu, Psi, dPsi, dnu, eps_psd=EPS_PSD):
     nr = IW_RHO_MEAS * nu + dnu
     n2 = _nu_project(nr, np.array([3.0, 3.0, 3.0]))
     return n2, out, np.array([pd, np.sum(np.abs(n2 - nr))])
+
+
+def iw_process_block_certs(Psi, dPsi, eps_psd=EPS_PSD):
+    """The cert_vec of each padded process-IW block projection of iw_process_apply
+    (inverse_wishart_jax.py:163-172), (7, 6)."""
+    raw = (IW_RHO_PROC[:, None, None] * Psi + dPsi) * PROC_BLOCK_MASKS
+    return np.stack([psd_project(raw[i], eps_psd)[1] for i in range(7)])
+
+
+def iw_meas_block_certs(Psi, dPsi, eps_psd=EPS_PSD):
+    """The cert_vec of each measurement-IW block projection of iw_meas_apply
+    (measurement_noise_iw_jax.py:78-86), (3, 6)."""
+    raw = IW_RHO_MEAS[:, None, None] * Psi + dPsi
+    raw = 0.5 * (raw + np.swapaxes(raw, -1, -2))
+    return np.stack([psd_project(raw[i], eps_psd)[1] for i in range(3)])
+
+
+def iw_process_Q_cert(nu, Psi, eps_psd=EPS_PSD):
+    """The cert_vec of Q's projection in process_noise_state_to_Q_jax (inverse_wishart_jax.py:67)."""
+    den = softplus_pos(nu - PROC_BLOCK_DIMS - 1.0)
+    Qb = Psi / den[:, None, None] * PROC_BLOCK_MASKS
+    Q = np.zeros((D_Z, D_Z))
+    for i in range(7):
+        s = PROC_BLOCK_STARTS[i]
+        e = min(s + 6, D_Z)
+        Q[s:e, s:e] = Qb[i][: e - s, : e - s]
+    return psd_project(Q, eps_psd)[1]
 
 
 def iw_meas_mode(nu, Psi, idx):

@@ -50,6 +50,24 @@ def _report():
     assert not _FAILS, "\n".join(_FAILS[:60])
 
 
+def _cert6(dev, ref, what):
+    """The reference's cert_vec [projection_delta, sym_delta, eig_min, eig_max, cond, nnc]
+    (primitives.py:80-123) of one projection: both deltas within the rounding of the two
+    V diag(λ) Vᵀ reconstructions (~1e-16 of the spectrum's scale per entry), the clamped eigenvalue
+    extremes at the absolute accuracy of eigh (~1e-12 of the largest), cond = eig_max / eig_min of the
+    device's own extremes and within 1e-6 of the reference's where eig_min is resolved to that
+    relative accuracy, near-null count exact."""
+    dev, ref = np.asarray(dev), np.asarray(ref)
+    sc = max(abs(ref[3]), 1e-300)
+    _close(dev[0:2], ref[0:2], 0.0, 1e-12 * sc, f"{what} deltas")
+    _close(dev[3], ref[3], 1e-10, 0.0, f"{what} eig_max")
+    _close(dev[2], ref[2], 0.0, 1e-12 * sc, f"{what} eig_min")
+    _close(dev[4], dev[3] / dev[2], 1e-15, 0.0, f"{what} cond (own extremes)")
+    if ref[2] > 1e-5 * ref[3]:
+        _close(dev[4], ref[4], 1e-6, 0.0, f"{what} cond")
+    _close(dev[5], ref[5], 0.0, 0.0, f"{what} near-null count")
+
+
 def _cov(L):
     return np.linalg.inv(L + EPS_LIFT * np.eye(L.shape[-1]))
 
@@ -106,6 +124,7 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None,
         stats, bcert, xi = pipe.bin_stats()
         bel = pipe.get_beliefs()
         dPp, dPm, Sig = pipe.hyp_stats()
+        pcert = pipe.projection_certs()
         res0 = None
         for i in sample:
             b_prev = O.Belief(bel0["X_anchor"][i].copy(), bel0["z_lin"][i].copy(), bel0["L"][i].copy(),
@@ -154,6 +173,11 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None,
                 _close(hcond[i, m, 0], ref[0], 0.0, 1e-12 * ref[1], f"{tag} {name} eig_min")
                 _close(hcond[i, m, 2], hcond[i, m, 1] / hcond[i, m, 0], 1e-15, 0.0, f"{tag} {name} cond")
                 _close(hcond[i, m, 3], ref[3], 0.0, 0.0, f"{tag} {name} near-null count")
+            # the full cert_vec of the bin, MF and planar projections (primitives.py:80-123)
+            for b in range(stats.shape[1]):
+                _cert6(pcert["bins"][i, b], r["moments"]["psd_certs"][b], f"{tag} bin {b} Sigma_p cert")
+            _cert6(pcert["mf"][i], r["mf"]["psd_cert"], f"{tag} MF L_rot cert")
+            _cert6(pcert["planar"][i], r["planar"]["psd_cert"], f"{tag} planar L_trans cert")
             _close(dPp[i], r["dPsi_proc"], 1e-8, 1e-18, f"{tag} dPsi_proc")
             _close(dPm[i], r["dPsi_meas"], 1e-8, 1e-18, f"{tag} dPsi_meas")
         # every hypothesis: the device covariance is the inverse of the device information matrix
@@ -174,6 +198,7 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None,
         _close(c["near_null"], pc[5], 0.0, 0.0, f"scan{k} combined near-null count")
         Sc = _cov(comb["L"])
         _close(_cov(c["L"])[0:6, 0:6], Sc[0:6, 0:6], 0.0, 1e-6, f"scan{k} combined pose covariance")
+        _cert6(pcert["barycenter"], pc, f"scan{k} barycenter projection cert")
         # IW apply from the GPU's per-hypothesis statistics of ALL hypotheses
         aP = np.einsum("k,kabc->abc", weights, dPp)
         aM = np.einsum("k,kabc->abc", weights, dPm)
@@ -186,6 +211,13 @@ def _run_and_compare(ctx, case, H, cap, sample, n_scans, io_computed, pipe=None,
         _close(iw["nu_meas"], nu_m, 1e-12, 0, f"scan{k} nu_meas")
         _close(iw["Psi_meas"], Psi_m, 1e-9, 1e-20, f"scan{k} Psi_meas")
         _close(iw["Q"], O.iw_process_Q(nu_p, Psi_p), 1e-9, 1e-20, f"scan{k} Q")
+        cp = O.iw_process_block_certs(iw0["Psi_proc"], wp * aP)
+        cm = O.iw_meas_block_certs(iw0["Psi_meas"], aM)
+        for b in range(7):
+            _cert6(pcert["iw_proc"][b], cp[b], f"scan{k} process-IW block {b} cert")
+        for b in range(3):
+            _cert6(pcert["iw_meas"][b], cm[b], f"scan{k} measurement-IW block {b} cert")
+        _cert6(pcert["Q"], O.iw_process_Q_cert(nu_p, Psi_p), f"scan{k} Q projection cert")
         # map: hypothesis 0's pushforward increment on the forgotten map (backend_node.py:2081-2083)
         if res0 is not None:
             mp = pipe.get_map()

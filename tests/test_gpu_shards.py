@@ -133,6 +133,13 @@ class ShardSet:
     def hyp_stats(self):
         return self._cat(lambda p: p.hyp_stats())
 
+    def projection_certs(self):
+        outs = [p.projection_certs() for p in self.shards]
+        d = dict(outs[0])  # the scan-level certificates: every rank's combine forms the same ones
+        for k in ("bins", "mf", "planar"):
+            d[k] = np.concatenate([o[k] for o in outs])
+        return d
+
     def get_iw(self):
         return self.shards[0].get_iw()
 
