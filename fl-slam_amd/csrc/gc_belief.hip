@@ -182,12 +182,14 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
   if (t < 64) {
     const bool okc = wave0_chol<kDZ, true>(Sx, n);
     if (t == 0) red[4] = okc ? 0.0 : 1.0;
+    if (t == 0) GC_STAMP(P.io_parts, 26);
   } else if (t < 128) {
     const int lane = t - 64;
     double x = 0.0;
     const bool ok = wave_lift_iterate<kDZ>(W3, lane < n ? mu_prev[lane] : 0.0, P.eps_lift, xrow1, n, x);
     if (lane < n) mu_inc[lane] = x;
     if (lane == 0) red[5] = ok ? 0.0 : 1.0;
+    if (lane == 0) GC_STAMP(P.io_parts, 27);
   } else if (t < 192) {
     const int lane = t - 128;
     const double c = lane < n ? 0.5 * (W3[lane * n + 15] + W3[15 * n + lane]) + (lane == 15 ? P.eps_lift : 0.0) : 0.0;
@@ -195,8 +197,27 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
     const bool ok = wave_lift_iterate<kDZ>(W3, c, P.eps_lift, xrow2, n, x);
     if (lane == 15) misc[6] = fmax(sqrt(x), 0.01);  // sigma_warp
     if (lane == 0) red[6] = ok ? 0.0 : 1.0;
-    // dt_imu (pipeline.py:526-535) from the parked IMU stamps: count, min and max over the valid
+    if (lane == 0) GC_STAMP(P.io_parts, 28);
+  } else {
+    if (t == 192) {
+      // pose0 = world pose of belief_prev = X ⊞ μ: with the cached posterior, the previous scan's
+      // k_combine_local already formed exactly this (compose_exp2 of the same X and μ_fin, the same
+      // routine) as the tape's world pose in P.diag[0:6]
+      if (S.sig_cached) {
+        for (int k = 0; k < 6; ++k) misc[k] = P.diag[(int64_t)h * kHypDiag + k];
+      } else {
+        compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);
+      }
+      for (int k = 0; k < 6; ++k) P.mu_aux[(int64_t)h * kMuAux + 44 + k] = misc[k];
+      double R0[9];
+      so3_exp(misc + 3, R0);
+      for (int k = 0; k < 9; ++k) misc[16 + k] = R0[k];
+      GC_STAMP(P.io_parts, 29);
+    }
+    // dt_imu (pipeline.py:526-535) from the parked IMU stamps on wave 3 after lane 192's pose0 (the
+    // lift waves 1-2 and the certificate on wave 0 are longer): count, min and max over the valid
     // (stamp > 0) samples, exact in any order; lane l takes the slots of threads l + 64 k
+    const int lane = t - 192;
     double cnt = 0.0, tmn = 1e308, tmx = -1e308;
     for (int k = 0; k < 4; ++k) {
       const int tt = lane + 64 * k;
@@ -208,19 +229,6 @@ GC_DEV void predict_imu_body(const PipeDev& P, const ScanArgs& S) {
     tmn = wave_min(tmn);
     tmx = wave_max(tmx);
     if (lane == 0) misc[7] = fmax(cnt >= 2.0 ? (tmx - tmn) / fmax(cnt - 1.0, 1.0) : 0.0, 1e-12);
-  } else if (t == 192) {
-    // pose0 = world pose of belief_prev = X ⊞ μ: with the cached posterior, the previous scan's
-    // k_combine_local already formed exactly this (compose_exp2 of the same X and μ_fin, the same
-    // routine) as the tape's world pose in P.diag[0:6]
-    if (S.sig_cached) {
-      for (int k = 0; k < 6; ++k) misc[k] = P.diag[(int64_t)h * kHypDiag + k];
-    } else {
-      compose_exp(P.X + (int64_t)h * 6, mu_prev, misc);
-    }
-    for (int k = 0; k < 6; ++k) P.mu_aux[(int64_t)h * kMuAux + 44 + k] = misc[k];
-    double R0[9];
-    so3_exp(misc + 3, R0);
-    for (int k = 0; k < 9; ++k) misc[16 + k] = R0[k];
   }
   __syncthreads();
   const bool fast = red[4] == 0.0 && red[5] == 0.0 && red[6] == 0.0 && P.predict_route == 0;

@@ -301,6 +301,7 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     __syncthreads();
     if (t < 64) {
       (void)wave0_chol<kDZ, false>(Wc, n);
+      if (t == 0) GC_STAMP(P.io_parts, 9);
     } else if (t < 128) {
       double symloc = 0.0;
       for (int idx = t - 64; idx < NN; idx += 64) {
@@ -312,6 +313,8 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
       if (t == 64) red[5] = symloc;
     } else if (t >= 192) {
       cond_side();
+    } else if (t == 128) {
+      so3_exp(P.X + (int64_t)hl * 6 + 3, sc + 24);  // R_X for the recompose (recompose_pose_R)
     }
     __syncthreads();
     // δz on wave 0 and the forward substitution of Σ_post (its first phase; Sx is free) with its trace on
@@ -319,6 +322,7 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     const auto solve_and_phase1 = [&]() {
       if (t < 64) {
         wave0_chol_solve<kDZ>(Wc, hpo, dz, n);
+        if (t == 0) GC_STAMP(P.io_parts, 38);
       } else if (t < 128) {
         chol_inverse_phase1_lane(Wc, Sx, n, t - 64);
         double tr = 0.0;
@@ -326,6 +330,7 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
           for (int k = 0; k < n; ++k) tr += Sx[(t - 64) * n + k] * Sx[(t - 64) * n + k];
         tr = wave_sum(tr);
         if (t == 64) red[6] = tr;
+        if (t == 64) GC_STAMP(P.io_parts, 39);
       }
       __syncthreads();
     };
@@ -357,9 +362,11 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     sc[61] = T;
     sc[62] = c6[0];
     double bch[6];
-    sc[63] = recompose_pose(P.X + (int64_t)hl * 6, zl, dz, sc[61], P.c_frob, sc + 64, sc + 70, bch);  // X_new, δ'
+    sc[63] = recompose_pose_R(P.X + (int64_t)hl * 6, sc + 24, zl, dz, sc[61], P.c_frob, sc + 64, sc + 70, bch);  // X_new, δ'
+    GC_STAMP(P.io_parts, 51);
   } else if (t >= 64) {
     chol_inverse_phase2_part(W2, Sx, n, t - 64, kWG - 64);
+    if (t == 64) GC_STAMP(P.io_parts, 52);
   }
   __syncthreads();
   // μ_post = (L_post + ε_l I)⁻¹ h_rec with h_rec = h_post − L_post[:, 0:6] δ' (recompose.py:173-181):
@@ -386,24 +393,34 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     wg_chol(W3, n);
     wg_chol_solve(W3, hps, mups, n);
   }
-  for (int i = t; i < NN; i += kWG) P.Sig[(int64_t)hl * NN + i] = W2[i];
-  for (int idx = t; idx < 7 * 36; idx += kWG) P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
   GC_PHASE(P, 17);
-  // a14 anchor drift (anchor_drift.py:93-191) on wave 0 and, beside it on wave 1, the a13 map
-  // increment from hypothesis 0 only (backend_node.py:2081-2083, build-defined pushforward): both
-  // read μ_post, X_new and Σ_post, neither writes what the other reads
+  // a14 anchor drift (anchor_drift.py:93-191) and, for hypothesis 0 only, the a13 map increment
+  // (backend_node.py:2081-2083, build-defined pushforward), beside the a15 process-noise statistics
+  // (inverse_wishart_jax.py:71-123) and Σ_post's store. Every SE(3) map of the two compositions with
+  // X_new, Exp(μ) and Exp(ρ μ) (compose_exp2: se3_exp, both rotations' so3_exp, the product's so3_log)
+  // is split over waves, each piece the same routine on the same operands (bit-identical):
+  //   step 1: ρ (wave 0), se3_exp(μ_post) (wave 1, hypothesis 0), so3_exp(μ_post rot) (wave 2,
+  //           hypothesis 0), R_Xnew = so3_exp(X_new rot) (wave 3);
+  //   step 2: h_fin, μ_fin (wave 0); z_t = X_new ∘ Exp(μ_post), R = Exp(z_t rot), the pushforward
+  //           (wave 1, hypothesis 0); X_fin = X_new ∘ Exp(ρ μ_post) (wave 2, lane 128); the statistics
+  //           and Σ_post's store on the rest of waves 2-3.
+  // Neither step writes what the other waves read.
+  double* e_zt = sc;        // 6
+  double* R_ezt = sc + 6;   // 9
+  double* R_xn = sc + 15;   // 9
+  if (t == 0) {
+    sc[98] = drift_rho(mupo, nullptr, nullptr);
+  } else if (t == 64 && P.h_begin + hl == 0) {
+    se3_exp(mupo, e_zt);
+  } else if (t == 128 && P.h_begin + hl == 0) {
+    so3_exp(mupo + 3, R_ezt);
+  } else if (t == 192) {
+    so3_exp(sc + 64 + 3, R_xn);
+  }
+  __syncthreads();
   if (t < 64) {
-    // δz = μ_post of the recomposed belief
-    if (t == 0) {
-      const double rho = drift_rho(mupo, nullptr, nullptr);
-      double d6[6];
-      for (int k = 0; k < 6; ++k) d6[k] = rho * mupo[k];
-      compose_exp2(sc + 64, d6, sc + 92);  // X_fin
-      sc[98] = rho;
-      GC_STAMP(P.io_parts, 36);
-    }
-    wave_lds_sync();
     const double rho = sc[98];
+    if (t == 0) GC_STAMP(P.io_parts, 36);
     if (t < n) zl[t] = (1.0 - rho) * mupo[t];
     wave_lds_sync();
     if (t < n) {  // h_fin = L_post z (wg_matvec's row order)
@@ -414,22 +431,36 @@ GC_DEV void evidence_body(const PipeDev& P, const ScanArgs& S) {
     wave_lds_sync();
     wave0_chol_solve<kDZ>(Wc, hfin, mufin, n);
     if (t == 0) GC_STAMP(P.io_parts, 37);
-  } else if (t < 128 && P.h_begin + hl == 0) {
-    if (t == 64) {
-      double zt[6], R[9];
-      compose_exp2(sc + 64, mupo, zt);
-      so3_exp(zt + 3, R);
-      for (int k = 0; k < 9; ++k) sc[80 + k] = R[k];
-      sc[89] = zt[0]; sc[90] = zt[1]; sc[91] = 0.0;  // planar map: t[2] = 0 (CHANGELOG.md:575-578)
-      for (int k = 0; k < 6; ++k) P.h0rec[k] = zt[k];
-      GC_STAMP(P.io_parts, 34);
+  } else if (t < 128) {
+    if (P.h_begin + hl == 0) {
+      if (t == 64) {
+        double zt[6], R[9];
+        se3_compose_R(sc + 64, R_xn, e_zt, R_ezt, zt);
+        so3_exp(zt + 3, R);
+        for (int k = 0; k < 9; ++k) sc[80 + k] = R[k];
+        sc[89] = zt[0]; sc[90] = zt[1]; sc[91] = 0.0;  // planar map: t[2] = 0 (CHANGELOG.md:575-578)
+        for (int k = 0; k < 6; ++k) P.h0rec[k] = zt[k];
+        GC_STAMP(P.io_parts, 34);
+      }
+      // hypothesis 0's pose covariance and deskew twist for the in-scan PrimitiveMap update
+      if (t - 64 < 36) P.h0rec[6 + (t - 64)] = W2[((t - 64) / 6) * n + (t - 64) % 6];
+      else if (t - 64 < 42) P.h0rec[42 + (t - 100)] = P.xi[(int64_t)hl * 6 + (t - 100)];
+      wave_lds_sync();
+      for (int b = t - 64; b < B; b += 64) pushforward_bin(st + b * 38, sc + 80, sc + 89, W2, n, P.map_inc + b * kMapRec);
+      if (t == 64) GC_STAMP(P.io_parts, 35);
     }
-    // hypothesis 0's pose covariance and deskew twist for the in-scan PrimitiveMap update
-    if (t - 64 < 36) P.h0rec[6 + (t - 64)] = W2[((t - 64) / 6) * n + (t - 64) % 6];
-    else if (t - 64 < 42) P.h0rec[42 + (t - 100)] = P.xi[(int64_t)hl * 6 + (t - 100)];
-    wave_lds_sync();
-    for (int b = t - 64; b < B; b += 64) pushforward_bin(st + b * 38, sc + 80, sc + 89, W2, n, P.map_inc + b * kMapRec);
-    if (t == 64) GC_STAMP(P.io_parts, 35);
+  } else {
+    if (t == 128) {  // X_fin = X_new ∘ Exp(ρ μ_post) (compose_exp2's pieces)
+      const double rho = sc[98];
+      double d6[6], e[6], Re[9];
+      for (int k = 0; k < 6; ++k) d6[k] = rho * mupo[k];
+      se3_exp(d6, e);
+      so3_exp(e + 3, Re);
+      se3_compose_R(sc + 64, R_xn, e, Re, sc + 92);
+    }
+    for (int i = t - 128; i < NN; i += kWG - 128) P.Sig[(int64_t)hl * NN + i] = W2[i];
+    for (int idx = t - 128; idx < 7 * 36; idx += kWG - 128)
+      P.dPsiP[(int64_t)hl * 252 + idx] = iw_proc_stat(idx, mupo, mups, W2);
   }
   __syncthreads();
   const double rho = sc[98];

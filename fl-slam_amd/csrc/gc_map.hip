@@ -23,6 +23,12 @@ namespace {
 
 constexpr uint32_t kDropped = 0xFFFFFFFFu;
 
+// the packed record's apply with the sort block's rows staged in LDS (k_fuse_apply_blk), or gathered
+// from HBM by 128-position workgroups (k_fuse_apply)
+#ifndef GC_FUSE_STAGED
+#define GC_FUSE_STAGED 1
+#endif
+
 struct FuseArgs {
   gc_primitive_map map;
   gc_fuse_batch meas;
@@ -31,16 +37,16 @@ struct FuseArgs {
   double eps_lift, eps_mass, timestamp;
   int64_t scan_seq;
   int rec32;  // the map is the packed record of gc_primitive_map_record_layout with 3 lobes (fuse_slot32)
+  int col32;  // rgb (and colors) at their layout offsets: written as whole 32-B sectors (slot_colour32)
 };
 
 // One measurement row in the world frame (pipeline.py:1248-1256): Λ_w = R Λ Rᵀ,
-// μ_b = (Λ + ε I)⁻¹ θ, μ_w = R μ_b + t, θ_w = Λ_w μ_w, η_w = R η (each lobe).
+// μ_b = (Λ + ε I)⁻¹ θ, μ_w = R μ_b + t, θ_w = Λ_w μ_w, η_w = R η (each lobe). Lb / tb / eb: the row's
+// Λ (9), θ (3) and η (3L), in HBM or staged in LDS.
 template <int LT>  // LT > 0: the lobe count at compile time (registers, no scratch); 0: A.map.n_lobes
-GC_DEV void meas_world(const FuseArgs& A, const double* R, int64_t k, double* Lw, double* th, double* et) {
+GC_DEV void meas_world(const FuseArgs& A, const double* R, const double* Lb, const double* tb, const double* eb,
+                       double* Lw, double* th, double* et) {
   const int L = LT > 0 ? LT : A.map.n_lobes;
-  const double* Lb = A.meas.Lambdas + 9 * k;
-  const double* tb = A.meas.thetas + 3 * k;
-  const double* eb = A.meas.etas + (int64_t)3 * L * k;
   if (!A.world) {
     for (int q = 0; q < 9; ++q) Lw[q] = Lb[q];
     for (int q = 0; q < 3; ++q) th[q] = tb[q];
@@ -63,34 +69,44 @@ constexpr int kMaxLobes = 8;
 // A measurement row's contribution, formed exactly as the reference forms it before its scatter-add
 // (r * X, primitive_map.py:1074-1095): [r Λ_w 9 | r θ_w 3 | r η_w 3L | r w | r | w_cam | w_lidar |
 // clip(c) w_cam 3]. The owner of a slot adds these rounded terms in row order, so the slot's sums are
-// bit-identical to a sequential scatter-add of them.
+// bit-identical to a sequential scatter-add of them. r = responsibility x (valid ? 1 : 0), src < 0:
+// no source column, col: the row's colour or NULL.
 __host__ __device__ constexpr int row_terms_len(int L) { return 19 + 3 * L; }
 template <int LT>
-GC_DEV void row_terms(const FuseArgs& A, const double* R, int64_t k, double* o) {
+GC_DEV void row_terms_at(const FuseArgs& A, const double* R, const double* Lb, const double* tb, const double* eb,
+                         double r, double wm, int src, const double* col, double* o) {
 #pragma clang fp contract(off)  // the products rounded as the reference's r * X
   constexpr int LM = LT > 0 ? LT : kMaxLobes;
   const int L = LT > 0 ? LT : A.map.n_lobes;
-  const double r = A.meas.responsibilities[k] * ((A.meas.valid_mask && !A.meas.valid_mask[k]) ? 0.0 : 1.0);
   double Lw[9], th[3], et[3 * LM];
-  meas_world<LT>(A, R, k, Lw, th, et);
+  meas_world<LT>(A, R, Lb, tb, eb, Lw, th, et);
   for (int q = 0; q < 9; ++q) o[q] = r * Lw[q];
   for (int q = 0; q < 3; ++q) o[9 + q] = r * th[q];
   for (int q = 0; q < 3 * L; ++q) o[12 + q] = r * et[q];
   double* t = o + 12 + 3 * L;
-  const double wm = A.meas.weights[k];
   t[0] = r * wm;
   t[1] = r;
   double wc = 0.0, wl = 0.0, ca[3] = {0.0, 0.0, 0.0};
-  if (A.meas.sources) {
-    const int src = A.meas.sources[k];
+  if (src >= 0) {
     wc = r * wm * (src == 0 ? 1.0 : 0.0);
     wl = r * wm * (src == 1 ? 1.0 : 0.0);
-    if (A.meas.colors)
-      for (int q = 0; q < 3; ++q) ca[q] = clampd(A.meas.colors[3 * k + q], 0.0, 1.0) * wc;
+    if (col)
+      for (int q = 0; q < 3; ++q) ca[q] = clampd(col[q], 0.0, 1.0) * wc;
   }
   t[2] = wc;
   t[3] = wl;
   for (int q = 0; q < 3; ++q) t[4 + q] = ca[q];
+}
+GC_DEV double row_r(const FuseArgs& A, int64_t k) {
+  return A.meas.responsibilities[k] * ((A.meas.valid_mask && !A.meas.valid_mask[k]) ? 0.0 : 1.0);
+}
+// row k read from HBM
+template <int LT>
+GC_DEV void row_terms(const FuseArgs& A, const double* R, int64_t k, double* o) {
+  const int L = LT > 0 ? LT : A.map.n_lobes;
+  const int src = A.meas.sources ? A.meas.sources[k] : -1;
+  row_terms_at<LT>(A, R, A.meas.Lambdas + 9 * k, A.meas.thetas + 3 * k, A.meas.etas + (int64_t)3 * L * k,
+                   row_r(A, k), A.meas.weights[k], src, A.meas.colors ? A.meas.colors + 3 * k : nullptr, o);
 }
 
 // rgb of one slot from its camera accumulators (primitive_map.py:1090-1098): clip(accum / max(denom,
@@ -112,7 +128,10 @@ GC_DEV void slot_colour(const gc_primitive_map& m, int64_t s, double cam, const 
 // idle (C5 fuse 0.081 -> 0.065 ms, profiles/r04/probe_soft_assign_store_only_and_fuse512.txt). The
 // sort keeps one key per thread in a register (reg_bitonic_sort): 0.062 -> 0.054 ms against the
 // all-LDS network, 256- and 512-row blocks alike (profiles/r04/ab_fuse_regsort.txt)
-constexpr int kFuseBlk = 512;
+#ifndef GC_FUSE_BLK
+#define GC_FUSE_BLK 256
+#endif
+constexpr int kFuseBlk = GC_FUSE_BLK;
 __global__ void __launch_bounds__(kFuseBlk) k_fuse_runs(const int32_t* __restrict__ target, int64_t K, int64_t M,
                                                    RunTable T, uint32_t* sslot, uint32_t* order,
                                                    uint32_t* run_len, uint32_t* rank) {
@@ -182,21 +201,34 @@ GC_DEV void fuse_apply_slot(const FuseArgs& A, int64_t s, const double* d) {
   }
 }
 
+// slot_colour for the packed record: rgb and colors each as one 32-B sector (the value and a pad
+// double), whole sectors for the memory controller (gc_mapslot.h)
+GC_DEV void slot_colour32(const gc_primitive_map& m, int64_t s, double cam, const double* acc, double denom,
+                          double eps_mass) {
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
+  const bool on = cam > 0.0;
+  const double den = fmax(denom, eps_mass);
+  double v[3];
+  for (int q = 0; q < 3; ++q) v[q] = on ? clampd(acc[q] / den, 0.0, 1.0) : 0.5;
+  dvec2* rgb = reinterpret_cast<dvec2*>(mRgb(m, s));
+  rgb[0] = dvec2{v[0], v[1]};
+  rgb[1] = dvec2{v[2], 0.0};
+  if (m.colors) {
+    dvec2* col = reinterpret_cast<dvec2*>(mCol(m, s));
+    col[0] = dvec2{v[0], v[1]};
+    col[1] = dvec2{v[2], 0.0};
+  }
+}
+
 // The packed 3-lobe record (gc_mapslot.h): doubles [Λ 0-8 | θ 9-11 | w 12 | stamp 13 | supported seq 14 |
 // update seq 15 | cam 16 | lidar 17 | accum 18-20 | denom 21 | η 22-30 | pad 31] in the record's first two
 // lines, read and written as 16 16-B vectors (whole lines instead of 31 separate 8-B accesses).
-GC_DEV void fuse_apply_slot32(const FuseArgs& A, int64_t s, const double* d) {
+// the record rec (its first two lines, loaded) updated with the row sums d and stored back
+GC_DEV void fuse_apply_rec32(const FuseArgs& A, int64_t s, double* rec, const double* d) {
 #pragma clang fp contract(off)
   typedef double dvec2 __attribute__((ext_vector_type(2)));
   const gc_primitive_map& m = A.map;
   dvec2* rp = reinterpret_cast<dvec2*>((char*)m.Lambdas + s * m.slot_bytes);
-  double rec[32];
-#pragma unroll
-  for (int v = 0; v < 16; ++v) {
-    const dvec2 x = rp[v];
-    rec[2 * v] = x.x;
-    rec[2 * v + 1] = x.y;
-  }
   // d: [r Λ 0-8 | r θ 9-11 | r η 12-20 | r w 21 | r 22 | w_cam 23 | w_lidar 24 | c w_cam 25-27]
   const bool src = A.meas.sources != nullptr, col = src && A.meas.colors;
 #pragma unroll
@@ -218,7 +250,22 @@ GC_DEV void fuse_apply_slot32(const FuseArgs& A, int64_t s, const double* d) {
   }
 #pragma unroll
   for (int v = 0; v < 16; ++v) rp[v] = dvec2{rec[2 * v], rec[2 * v + 1]};
-  if (m.cam_mass && m.colors_current) slot_colour(m, s, rec[16], rec + 18, rec[21], A.eps_mass);
+  if (m.cam_mass && m.colors_current) {
+    if (A.col32) slot_colour32(m, s, rec[16], rec + 18, rec[21], A.eps_mass);
+    else slot_colour(m, s, rec[16], rec + 18, rec[21], A.eps_mass);
+  }
+}
+GC_DEV void fuse_apply_slot32(const FuseArgs& A, int64_t s, const double* d) {
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
+  const dvec2* rp = reinterpret_cast<const dvec2*>((const char*)A.map.Lambdas + s * A.map.slot_bytes);
+  double rec[32];
+#pragma unroll
+  for (int v = 0; v < 16; ++v) {
+    const dvec2 x = rp[v];
+    rec[2 * v] = x.x;
+    rec[2 * v + 1] = x.y;
+  }
+  fuse_apply_rec32(A, s, rec, d);
 }
 
 // one thread per sorted position; the owner of each slot (the run its list ends on) fuses the slot
@@ -283,6 +330,147 @@ __global__ void __launch_bounds__(kApplyWG) k_fuse_apply(FuseArgs A, int64_t K, 
   if ((threadIdx.x & 63) == 0 && b) atomicAdd(&owned, (uint32_t)__popcll(b));
   __syncthreads();
   if (threadIdx.x == 0) wg_count[blockIdx.x] = owned;
+}
+
+// The packed 3-lobe record's apply with the rows staged: one workgroup per sort block (kFuseBlk
+// positions = the block's rows, sorted by slot), whose rows are first read into LDS as coalesced
+// field slices, so each owner takes its own block's rows from LDS instead of gathering them from HBM in
+// sorted (random) order: with 128-position workgroups a block's row lines were fetched by four
+// workgroups beside every other block's slot records in the same L2 and re-read (k_fuse_apply read
+// ~1.5x the rows' and records' bytes). Runs in other blocks (a slot hit by several blocks) are read from
+// HBM. Every term is formed by row_terms_at in the same order: bit-identical to k_fuse_apply.
+constexpr int kBlkRunCap = 8;  // a position's run slice (more runs: SlotRunList's walk over the chain)
+constexpr int kStageDoubles = (9 + 3 + 9 + 1 + 1 + 3) * kFuseBlk;
+constexpr size_t kStageLds = sizeof(double) * kStageDoubles + sizeof(int32_t) * kFuseBlk +
+                             sizeof(uint32_t) * kFuseBlk * kBlkRunCap;
+__global__ void __launch_bounds__(kFuseBlk) k_fuse_apply_blk(FuseArgs A, int64_t K, RunTable T,
+                                                         const uint32_t* __restrict__ sslot,
+                                                         const uint32_t* __restrict__ order,
+                                                         const uint32_t* __restrict__ run_len,
+                                                         const uint32_t* __restrict__ rank, uint32_t* wg_count) {
+#pragma clang fp contract(off)
+  constexpr int L = 3, NT = row_terms_len(L), NB = kFuseBlk;
+  extern __shared__ double stg[];
+  double* sL = stg;            // Λ   NB x 9
+  double* sT = sL + 9 * NB;    // θ   NB x 3
+  double* sE = sT + 3 * NB;    // η   NB x 9
+  double* sR = sE + 9 * NB;    // r (masked)
+  double* sW = sR + NB;        // w
+  double* sC = sW + NB;        // colour NB x 3
+  int32_t* sS = reinterpret_cast<int32_t*>(sC + 3 * NB);             // source
+  uint32_t* slices = reinterpret_cast<uint32_t*>(sS + NB);           // NB x kBlkRunCap
+  __shared__ double Rs[9];
+  __shared__ uint32_t owned;
+  const int64_t base = (int64_t)blockIdx.x * NB;
+  const int nrow = (int)min<int64_t>(NB, K - base);
+  const int t = threadIdx.x;
+  // the position's slot and, for its owner, the slot's record (the first two lines) and chain link,
+  // loaded before the staging so the record's HBM round trip overlaps it
+  const int64_t p = base + t;
+  bool own = false;
+  uint32_t s = 0, s1 = 0;
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
+  dvec2 rv[16];
+  if (p < K) {
+    s = sslot[p];
+    own = (int64_t)s < A.map.m_slots && rank[p] != kNoRun;
+  }
+  if (own) {
+    const dvec2* rp = reinterpret_cast<const dvec2*>((const char*)A.map.Lambdas + (int64_t)s * A.map.slot_bytes);
+#pragma unroll
+    for (int v = 0; v < 16; ++v) rv[v] = rp[v];
+    s1 = T.succ[p];
+  }
+  // the block's rows as coalesced field slices, every load of a thread in flight at once
+  {
+    double vL[9], vE[9], vT[3], vC[3];
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      const int i = t + j * NB;
+      vL[j] = i < 9 * nrow ? A.meas.Lambdas[9 * base + i] : 0.0;
+      vE[j] = i < 9 * nrow ? A.meas.etas[9 * base + i] : 0.0;
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int i = t + j * NB;
+      vT[j] = i < 3 * nrow ? A.meas.thetas[3 * base + i] : 0.0;
+      vC[j] = (A.meas.colors && i < 3 * nrow) ? A.meas.colors[3 * base + i] : 0.0;
+    }
+    const bool in = t < nrow;
+    const double vR = in ? row_r(A, base + t) : 0.0, vW = in ? A.meas.weights[base + t] : 0.0;
+    const int32_t vS = (in && A.meas.sources) ? A.meas.sources[base + t] : -1;
+#pragma unroll
+    for (int j = 0; j < 9; ++j) {
+      sL[t + j * NB] = vL[j];
+      sE[t + j * NB] = vE[j];
+    }
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      sT[t + j * NB] = vT[j];
+      sC[t + j * NB] = vC[j];
+    }
+    sR[t] = vR;
+    sW[t] = vW;
+    sS[t] = vS;
+  }
+  if (t == 0) {
+    owned = 0u;
+    if (A.world) so3_exp(A.pose + 3, Rs);
+  }
+  // the run hash is not read past the runs pass (owners follow the position-indexed links): the
+  // grid zeroes it for the next call in coalesced 16-B stores, whole lines instead of one 8-B store
+  // per owner at a random entry (each a partial-sector write the memory controller reads back)
+  {
+    typedef unsigned long long u64v2 __attribute__((ext_vector_type(2)));
+    const int64_t n2 = ((int64_t)1 << T.bits) / 2;
+    u64v2* e2 = reinterpret_cast<u64v2*>(T.e);
+    for (int64_t i = (int64_t)blockIdx.x * NB + t; i < n2; i += (int64_t)gridDim.x * NB) e2[i] = u64v2{0ull, 0ull};
+  }
+  __syncthreads();
+  if (own) {
+    double R[9];
+    for (int q = 0; q < 9; ++q) R[q] = Rs[q];
+    double d[NT], tt[NT];
+    for (int q = 0; q < NT; ++q) d[q] = 0.0;
+    const auto add_run = [&](uint32_t r) {  // a run's rows in row order
+      const uint32_t len = run_len[r];
+      for (uint32_t q = 0; q < len; ++q) {
+        const int64_t k = (int64_t)order[r + q];
+        const int64_t i = k - base;
+        if (i >= 0 && i < NB)
+          row_terms_at<L>(A, R, sL + 9 * i, sT + 3 * i, sE + 9 * i, sR[i], sW[i], sS[i],
+                          A.meas.colors ? sC + 3 * i : nullptr, tt);
+        else
+          row_terms<L>(A, R, k, tt);
+        for (int e = 0; e < NT; ++e) d[e] += tt[e];
+      }
+    };
+    SlotRunList<kBlkRunCap> rl(slices + t * kBlkRunCap);
+    if (s1 == 0u) {
+      add_run((uint32_t)p);
+    } else {
+      rl.collect((uint32_t)p, s1, T.succ, (int)((K + NB - 1) / NB));
+      uint32_t prev = 0;
+      for (int i = 0; i < rl.n; ++i) {
+        const uint32_t r = rl.at(i, prev);
+        if (r == kNoRun) break;
+        prev = r;
+        add_run(r);
+      }
+    }
+    double rec[32];
+#pragma unroll
+    for (int v = 0; v < 16; ++v) {
+      rec[2 * v] = rv[v].x;
+      rec[2 * v + 1] = rv[v].y;
+    }
+    fuse_apply_rec32(A, s, rec, d);
+    if (s1 != 0u) rl.clear();
+  }
+  const unsigned long long b = __ballot(own);
+  if ((t & 63) == 0 && b) atomicAdd(&owned, (uint32_t)__popcll(b));
+  __syncthreads();
+  if (t == 0) wg_count[blockIdx.x] = owned;
 }
 
 // every slot's colour estimate (primitive_map.py:1090-1098)
@@ -361,13 +549,16 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
     for (int q = 0; q < 7 && ok; ++q) ok = (const char*)f[q] - b0 == off[q];  // the fuse's fields
     for (int q = 7; q < 11 && ok; ++q) ok = f[q] == nullptr || (const char*)f[q] - b0 == off[q];
     A.rec32 = ok ? 1 : 0;
+    A.col32 = ok && (const char*)map->rgb - b0 == off[11] && (!map->colors || (const char*)map->colors - b0 == off[12]);
   }
   A.timestamp = timestamp;
   A.scan_seq = scan_seq;
   // scratch: the sorted slot, row order, run length and owner's entry of every position, the apply
   // launch's per-workgroup distinct-slot counts (the run hash and its links are the context's)
   const size_t kv = ((size_t)K * sizeof(uint32_t) + 255) / 256 * 256;
-  const unsigned grid = (unsigned)((K + kApplyWG - 1) / kApplyWG);
+  const bool staged = A.rec32 && GC_FUSE_STAGED;  // k_fuse_apply_blk: one workgroup per sort block
+  const unsigned nblk = (unsigned)((K + kFuseBlk - 1) / kFuseBlk);
+  const unsigned grid = staged ? nblk : (unsigned)((K + kApplyWG - 1) / kApplyWG);
   void* scr;
   if (int rc = gc::scratch(ctx, 4 * kv + (size_t)grid * sizeof(uint32_t), &scr)) return rc;
   char* base = (char*)scr;
@@ -380,11 +571,15 @@ int32_t gc_primitive_map_fuse(gc_ctx* ctx, const gc_primitive_map* map, const gc
   const RunTable T{ctx->runs.entries(), ctx->runs.succ(), ctx->runs.bits};
   // from here a failed launch may leave entries set: the next call empties them
   ctx->runs.dirty = true;
-  hipLaunchKernelGGL(k_fuse_runs, dim3((unsigned)((K + kFuseBlk - 1) / kFuseBlk)), dim3(kFuseBlk), 0, ctx->stream,
+  hipLaunchKernelGGL(k_fuse_runs, dim3(nblk), dim3(kFuseBlk), 0, ctx->stream,
                      (const int32_t*)meas->target_slots, K, map->m_slots, T, sslot, order, run_len, rank);
   GC_LAUNCH_CHECK(ctx);
   const bool l3 = map->n_lobes == 3;  // GC_VMF_N_LOBES: the compile-time lobe count
-  if (A.rec32)
+  if (staged) {
+    GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_fuse_apply_blk, kStageLds));
+    hipLaunchKernelGGL(k_fuse_apply_blk, dim3(grid), dim3(kFuseBlk), kStageLds, ctx->stream, A, K, T, sslot, order,
+                       run_len, rank, cnt);
+  } else if (A.rec32)
     hipLaunchKernelGGL((k_fuse_apply<3, true>), dim3(grid), dim3(kApplyWG), 0, ctx->stream, A, K, T, sslot, order,
                        run_len, rank, cnt);
   else if (l3)

@@ -196,16 +196,21 @@ GC_DEV void se3_log(const double* T, double* xi) {
 }
 
 // se3_jax.py:420-438
-GC_DEV void se3_compose(const double* a, const double* b, double* out) {
-  double Ra[9], Rb[9], Rab[9], t[3];
-  so3_exp(a + 3, Ra);
-  so3_exp(b + 3, Rb);
+// se3_compose given Ra = so3_exp(a rot) and Rb = so3_exp(b rot) (formed elsewhere, e.g. on other waves)
+GC_DEV void se3_compose_R(const double* a, const double* Ra, const double* b, const double* Rb, double* out) {
+  double Rab[9], t[3];
   mat3_vec(Ra, b, t);
   mat3_mul(Ra, Rb, Rab);
   double o[6];
   o[0] = a[0] + t[0]; o[1] = a[1] + t[1]; o[2] = a[2] + t[2];
   so3_log(Rab, o + 3);
   for (int i = 0; i < 6; ++i) out[i] = o[i];
+}
+GC_DEV void se3_compose(const double* a, const double* b, double* out) {
+  double Ra[9], Rb[9];
+  so3_exp(a + 3, Ra);
+  so3_exp(b + 3, Rb);
+  se3_compose_R(a, Ra, b, Rb, out);
 }
 
 // se3_jax.py:442-453 : [-Rᵀ t, log(Rᵀ)]

@@ -172,8 +172,8 @@ GC_DEV double planar_z_scale(const double* Ssum, double Ntot, double eps) {
 // Frobenius recompose given δz = (L + εI)⁻¹h (recompose.py:50-205): s = T/(T + c_frob),
 // δ' = δ + s·½[z_lin, δ] (BCH3 on the pose slice), X_new = X ∘ Exp(δ'). Writes X_new (6),
 // δ' (6) and the bch term (6); returns s.
-GC_DEV double recompose_pose(const double* X, const double* zl, const double* dz, double T, double c_frob,
-                             double* X_new, double* dpc, double* bch) {
+GC_DEV double recompose_pose_R(const double* X, const double* RX, const double* zl, const double* dz, double T,
+                               double c_frob, double* X_new, double* dpc, double* bch) {
   const double s = T / (T + c_frob);
   double c1[3], c2[3], c3[3];
   cross3(zl + 3, dz, c1);
@@ -185,10 +185,18 @@ GC_DEV double recompose_pose(const double* X, const double* zl, const double* dz
     dpc[k] = dz[k] + s * bch[k];
     dpc[3 + k] = dz[3 + k] + s * bch[3 + k];
   }
-  double e[6];
+  double e[6], Re[9];
   se3_exp(dpc, e);
-  se3_compose(X, e, X_new);
+  so3_exp(e + 3, Re);
+  se3_compose_R(X, RX, e, Re, X_new);
   return s;
+}
+// with RX = so3_exp(X rot) formed here (recompose_pose_R takes it formed elsewhere: the same bits)
+GC_DEV double recompose_pose(const double* X, const double* zl, const double* dz, double T, double c_frob,
+                             double* X_new, double* dpc, double* bch) {
+  double RX[9];
+  so3_exp(X + 3, RX);
+  return recompose_pose_R(X, RX, zl, dz, T, c_frob, X_new, dpc, bch);
 }
 
 // ------------------------------------------------------------------------------------ a14

@@ -1338,6 +1338,10 @@ __global__ void __launch_bounds__(kFinWG) k_bins_finalize(int B, int NF, int64_t
 // per-bin projection delta and mass-epsilon ratio go to aux (H, B, 2) and k_evidence reduces them
 // (finalize_cert), in k_bins_finalize's wave_sum order.
 constexpr int kFinBins = 6;
+// chunk records in flight per lane in the split finalize (one L2 round trip per batch)
+#ifndef GC_FIN_KU
+#define GC_FIN_KU 16
+#endif
 constexpr int kFinSplitWG = 128;
 // up to this many chunk records per hypothesis (H = 256: 18, C5's 1024: 17) the evidence workgroup of
 // each hypothesis sums its own records (one more L2 round trip per 8 chunks at its start) in place of
@@ -1366,7 +1370,7 @@ __global__ void __launch_bounds__(kFinSplitWG) k_bins_finalize_split(int B, int 
   const int t = threadIdx.x;
   if (t < ne) {
     const int e = e0 + t;
-    constexpr int KU = 16;
+    constexpr int KU = GC_FIN_KU;
     double v = 0.0;
     for (int64_t c = 0; c < chunks; c += KU) {
       double x[KU];

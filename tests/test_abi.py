@@ -63,6 +63,9 @@ def test_packed_map_record_layout():
         assert sb.value % 128 == 0 and spans[-1][1] <= sb.value
         if L <= 3:  # Λ θ η w stamp seqs cam lidar accum denom: the first two lines
             assert max(int(off[k]) + w[k] for k in range(11)) <= 256
+        # rgb and colors each own a whole 32-B sector (the fuse writes them as such)
+        assert off[11] % 32 == 0 and off[12] % 32 == 0 and off[12] - off[11] >= 32
+        assert all(not (off[11] < o < off[11] + 32 or off[12] < o < off[12] + 32) for o in off)
     with pytest.raises(ValueError):
         _abi.call("gc_primitive_map_record_layout", 9, off.ctypes.data, ctypes.byref(sb))
     # int64 m_slots, int32 n_lobes, int32 colors_current, 16 pointers, int64 slot_bytes

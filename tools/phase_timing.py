@@ -49,11 +49,7 @@ names = {1: "predict: loads (Σ', μ, IMU)", 2: "predict: Σ' cert + lift solves
          17: "evidence: IW solves/inverse", 18: "evidence: map increment", 19: "evidence: drift+final solves",
          21: "combine wg0: reduce + 22x22 PSD", 23: "combine wg2: process IW apply",
          24: "combine wg2: meas IW apply", 25: "combine wg2: Q rebuild"}
-inner = {26: "predict: load Sig/Q, W2", 27: "predict: PSD Σ' + chol", 28: "predict: chol inverse",
-         29: "predict: PSD L' + lifted chol"}
-for i in sorted(inner):
-    if t[i] and t[i - 1 if i > 26 else 0]:
-        print(f"{inner[i]:36s} {t[i] - t[i - 1 if i > 26 else 0]:10.0f} cycles")
+
 for a, b, nm in ((10, 30, "evidence: MF rows"), (30, 31, "evidence: MF sum_bins"), (31, 11, "evidence: mf_finalize"),
                  (11, 32, "evidence: planar rows"), (32, 33, "evidence: planar sum_bins"),
                  (33, 12, "evidence: planar_finalize")):
@@ -66,6 +62,14 @@ for a, b, nm in ((5, 40, "predict: preint: 2 x so3_exp"), (40, 41, "predict: pre
         print(f"{nm:36s} {t[b] - t[a]:10.0f} cycles")
 for a, b, nm in ((17, 34, "evidence: map inc: zt, R (lane 64)"), (34, 35, "evidence: map inc: pushforward"),
                  (17, 36, "evidence: drift: X_fin (lane 0)"), (36, 37, "evidence: drift: h_fin, μ_fin")):
+    if t[a] and t[b]:
+        print(f"{nm:36s} {t[b] - t[a]:10.0f} cycles")
+# per-wave marks inside two phases (slots free on the split-predict route; 51-52 in hypothesis 1's area)
+for a, b, nm in ((1, 26, "predict: Σ' chol cert (wave 0)"), (1, 27, "predict: lift μ_inc (wave 1)"),
+                 (1, 28, "predict: lift σ_warp + dt_imu (wave 2)"), (1, 29, "predict: pose0, R0 (lane 192)"),
+                 (14, 9, "evidence: fusion chol (wave 0)"), (9, 38, "evidence: δz solve (wave 0)"),
+                 (9, 39, "evidence: Σ phase 1 + trace (wave 1)"), (15, 51, "evidence: recompose (lane 0)"),
+                 (15, 52, "evidence: Σ phase 2 (waves 1-3)")):
     if t[a] and t[b]:
         print(f"{nm:36s} {t[b] - t[a]:10.0f} cycles")
 for i in sorted(names):
