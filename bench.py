@@ -29,7 +29,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md: 8.0 TB/s)
-PROFILE_ROUNDS = ("r04", "r03", "r02", "r01")  # committed rocprofv3 summaries (profiles/<round>/), newest first
+PROFILE_ROUNDS = ("r05", "r04", "r03", "r02", "r01")  # committed rocprofv3 summaries (profiles/<round>/), newest first
 
 
 def parse():
@@ -704,7 +704,7 @@ def map_fuse_leg(ctx, _abi, m_slots=1 << 20, rows=1 << 17, reps=5, packed=True):
     return {"slots": M, "rows": K, "distinct_slots": n_unique, "ms": ms, "bytes": b,
             "GB/s": b / (ms * 1e-3) / 1e9, "bytes_all_slot_colour": b_all,
             "GB/s_all_slot_colour": b_all / (ms * 1e-3) / 1e9, "layout": "packed" if packed else "fields",
-            "kernel": "k_fuse_runs + k_fuse_apply (per-block LDS sort, per-slot run entries; colour estimate of the touched slots)"}
+            "kernel": "k_fuse_runs + k_fuse_apply_blk (per-block register sort, run hash of the touched slots; the sort block's rows staged in LDS; colour estimate of the touched slots)"}
 
 
 def cpu_info():
