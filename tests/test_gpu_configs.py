@@ -329,17 +329,17 @@ def test_c3_is_bit_reproducible(ctx):
         assert np.array_equal(a, b)
 
 
-def test_c3_every_hypothesis_matches_fixture(ctx):
-    """C3's first scan for ALL 256 hypotheses (the bench workload; the other C3 tests run the oracle on 4
-    samples per scan) against tests/golden/c3_all.npz, the oracle's result for every hypothesis from the
-    case's initial state (tests/golden/make_c3_all.py; tests/test_c3_fixture.py pins the fixture to the
-    inputs and the current oracle). The C3 test's bars: world pose, anchor and the pose block of Σ
-    within 1e-6 abs (north star), z_lin 1e-6 rel, ξ_body 1e-9 rel, α and the excitation-free β exact
-    to 1e-12 / 1e-10, T 1e-7 rel, cond_pose6 1e-6 rel."""
+def _every_hypothesis(ctx, name, H, n_az, cap):
+    """The first scan of a config for ALL its hypotheses against tests/golden/<name>_all.npz, the oracle's
+    result for every hypothesis from the case's initial state (tests/golden/make_c3_all.py;
+    tests/test_c3_fixture.py pins the fixtures to the inputs and the current oracle). The C3 test's bars:
+    world pose, anchor and the pose block of Σ within 1e-6 abs (north star), z_lin 1e-6 rel, ξ_body
+    1e-9 rel, α and the excitation-free β to 1e-12 / 1e-10 abs, T 1e-7 rel, cond_pose6 1e-6 rel."""
     import os
-    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "c3_all.npz"))
-    case = cases.build(H=256, n_az=4096, n_scans=1, io="computed")
-    pipe = _pipeline(case, ctx, 256, case["n"], True)
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", f"{name}_all.npz"))
+    case = cases.build(H=H, n_az=n_az, n_scans=1, io="computed", cap=cap)
+    n_cap = case["n"]
+    pipe = _pipeline(case, ctx, H, n_cap, True)
     s = case["scans"][0]
     pipe.stage_scan(0, s)
     pipe.run_scan(0, s, 0)
@@ -347,16 +347,26 @@ def test_c3_every_hypothesis_matches_fixture(ctx):
     diag, bel = pipe.hyp_diag(), pipe.get_beliefs()
     _, _, Sig = pipe.hyp_stats()
     _, _, xi = pipe.bin_stats()
-    _close(diag[:, 0:6], g["pose"], 0.0, 1e-6, "every hypothesis: world pose")
-    _close(bel["X_anchor"], g["X_anchor"], 0.0, 1e-6, "every hypothesis: X_anchor")
-    _close(Sig[:, 0:6, 0:6], g["Sigma_pose"], 0.0, 1e-6, "every hypothesis: pose covariance")
-    for i in range(256):
-        _close(bel["z_lin"][i], g["z_lin"][i], 1e-6, 1e-9, f"hyp{i} z_lin")
-        _close(xi[i], g["xi_body"][i], 1e-9, 1e-12, f"hyp{i} xi_body")
+    _close(diag[:, 0:6], g["pose"], 0.0, 1e-6, f"{name} every hypothesis: world pose")
+    _close(bel["X_anchor"], g["X_anchor"], 0.0, 1e-6, f"{name} every hypothesis: X_anchor")
+    _close(Sig[:, 0:6, 0:6], g["Sigma_pose"], 0.0, 1e-6, f"{name} every hypothesis: pose covariance")
     sc = g["scalars"]  # [alpha, beta, T, cond6]
-    _close(diag[:, 8], sc[:, 0], 0.0, 1e-12, "every hypothesis: alpha")
-    _close(diag[:, 7], sc[:, 1], 0.0, 1e-10, "every hypothesis: beta")
-    for i in range(256):
-        _close(diag[i, 6], sc[i, 2], 1e-7, 1e-10, f"hyp{i} T")
-        _close(diag[i, 13], sc[i, 3], 1e-6, 0.0, f"hyp{i} cond_pose6")
+    _close(diag[:, 8], sc[:, 0], 0.0, 1e-12, f"{name} every hypothesis: alpha")
+    _close(diag[:, 7], sc[:, 1], 0.0, 1e-10, f"{name} every hypothesis: beta")
+    for i in range(H):
+        _close(bel["z_lin"][i], g["z_lin"][i], 1e-6, 1e-9, f"{name} hyp{i} z_lin")
+        _close(xi[i], g["xi_body"][i], 1e-9, 1e-12, f"{name} hyp{i} xi_body")
+        _close(diag[i, 6], sc[i, 2], 1e-7, 1e-10, f"{name} hyp{i} T")
+        _close(diag[i, 13], sc[i, 3], 1e-6, 0.0, f"{name} hyp{i} cond_pose6")
     pipe.close()
+
+
+def test_c3_every_hypothesis_matches_fixture(ctx):
+    """C3 (the bench workload): all 256 hypotheses of the first scan (the other C3 tests run the oracle
+    on 4-5 samples per scan)."""
+    _every_hypothesis(ctx, "c3", 256, 4096, None)
+
+
+def test_c5_every_hypothesis_matches_fixture(ctx):
+    """C5 shape (131,072 points budgeted to 65,536, stride 2): all 1024 hypotheses of the first scan."""
+    _every_hypothesis(ctx, "c5", 1024, 8192, 65536)
