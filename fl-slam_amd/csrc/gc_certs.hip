@@ -41,7 +41,8 @@ GC_DEV int sturm_count(const double* d, const double* e2, double sig, double piv
 // One wave: the ConditioningCert of the symmetrised N x N row-major M (global) into out4.
 // buf: 3 N + 8 doubles of wave-private LDS.
 template <int N>
-GC_DEV void wave_conditioning(const double* __restrict__ M, double eps, double* buf, double* out4) {
+GC_DEV void wave_conditioning(const double* __restrict__ M, double eps, double* buf, double* out4,
+                              int* below_eps = nullptr) {
   const int lane = threadIdx.x & 63;
   const bool row = lane < N;
   double a[N];  // row `lane` of the symmetrised matrix (zeros on idle lanes)
@@ -124,6 +125,7 @@ GC_DEV void wave_conditioning(const double* __restrict__ M, double eps, double* 
   const double mid = 0.5 * (lo_b + hi_b);
   const double lmin = readlane_f64(mid, 0), lmax = readlane_f64(mid, 32);
   const int nnc = sturm_count<N>(d, e2, 10.0 * eps, pivmin);  // every lane the same
+  if (below_eps && lane == 0) *below_eps = sturm_count<N>(d, e2, eps, pivmin);  // eigenvalues the clamp moves
   if (lane == 0) {
     const double mn = fmax(lmin, eps), mx = fmax(lmax, eps);
     out4[0] = mn;
@@ -224,8 +226,37 @@ __global__ void __launch_bounds__(256) k_proj_certs(PipeDev P) {
     }
   }
   __syncthreads();
+  double* out = P.pcert + ((int64_t)P.Hl * per + s) * 6;
+  if (n == kDZ) {
+    // the 22x22 barycenter and Q: the extremes and the near-null count by the tridiagonal Sturm
+    // multisection (wave 0, as k_hyp_certs) beside the symmetry deviation (wave 1); when no eigenvalue
+    // lies below eps_psd the clamp moves nothing and the projection delta is 0 (the reference's is the
+    // rounding of V diag(λ) Vᵀ), otherwise the full Jacobi projection below
+    int* below = reinterpret_cast<int*>(red + 6);
+    if (t < 64) {
+      wave_conditioning<kDZ>(M, P.eps_psd, scr, c6 + 2, below);
+    } else if (t < 128) {
+      double sl = 0.0;
+      for (int idx = t - 64; idx < kDZ * kDZ; idx += 64) {
+        const int i = idx / kDZ, j = idx % kDZ;
+        const double dd = 0.5 * (M[i * kDZ + j] + M[j * kDZ + i]) - M[idx];
+        sl += dd * dd;
+      }
+      sl = wave_sum(sl);
+      if (t == 64) c6[1] = sqrt(sl);
+    }
+    __syncthreads();
+    if (*below == 0) {
+      if (t == 0) {
+        out[0] = 0.0; out[1] = c6[1];
+        for (int q = 2; q < 6; ++q) out[q] = c6[q];
+      }
+      return;
+    }
+    __syncthreads();
+  }
   wg_psd_project(M, Mp, P.eps_psd, n, scr, red, c6);
-  if (t < 6) P.pcert[((int64_t)P.Hl * per + s) * 6 + t] = c6[t];
+  if (t < 6) out[t] = c6[t];
 }
 
 }  // namespace

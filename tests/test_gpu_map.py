@@ -34,8 +34,9 @@ def _tile(rng, M, L=3):
                                               (20000, 1 << 16, False, True), (3000, 2000, True, True),
                                               (3000, 2000, True, False), (1, 10, False, True),
                                               (131072, 1 << 20, False, True), (131072, 1 << 20, True, True),
-                                              # every slot in every 512-row block: 40 runs per slot (the
-                                              # sorted slice) and 128 (past the 64-run slice: the list walk)
+                                              # every slot in every 256-row sort block: ~79 runs per slot
+                                              # (past the staged apply's 8-run slice: the chain walk) and
+                                              # 256 (past the gathering apply's 64-run slice)
                                               (20000, 100, False, True), (65536, 16, False, False)])
 def test_primitive_map_fuse_matches_oracle(ctx, K, M, world, packed):
     """Two fuses in a row: the first onto uploaded colours (not current: every slot's colour is
