@@ -901,9 +901,14 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
 // the VALU ones 17.. . It is recovered from the trace of the direction scatter, Σ R w |d|² = N − ε_d
 // with ε_d = Σ R w (1 − |d|²) ≤ 2·1e-12 / range of N (|d| = |r| / (|r| + 1e-12)): d_z² = N − d_x² − d_y²,
 // an absolute error ~1e-12 N in that one scatter entry; N, the resultant and κ stay exact sums.
-template <int BPL, int NX, int DF = -1>
+struct NoHook {
+  GC_DEV void operator()() const {}
+};
+// pre() runs before the first barrier, mid() after it (the persistent bins form's next-task broadcast)
+template <int BPL, int NX, int DF = -1, typename Pre = NoHook, typename Mid = NoHook>
 GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL][NX], double ent, double mxr,
-                                      double sumw, double npts, int B, double* lds, double* rec) {
+                                      double sumw, double npts, int B, double* lds, double* rec,
+                                      const Pre& pre = Pre(), const Mid& mid = Mid()) {
   constexpr int ND = DF >= 0 ? 1 : 0;
   constexpr int NF = ND + 16 + NX;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, bl = lane & 15;
@@ -917,7 +922,9 @@ GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL
       v += __shfl_xor(v, 32, 64);
       accx[j][t] = v;
     }
+  pre();
   __syncthreads();
+  mid();
 #pragma unroll
   for (int j = 0; j < BPL; ++j) {
 #pragma unroll
@@ -1008,11 +1015,52 @@ GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
   __syncthreads();
 }
 
+// the first point index of chunk c (the tiers of FusedArgs) and its iteration count
+GC_DEV int64_t chunk_first(const FusedArgs& A, int64_t c, int* iters_out) {
+  const bool big = c < A.k1, mid = !big && c < A.k1 + A.k2;
+  *iters_out = big ? A.iters : (mid ? A.iters_s : A.iters_t);
+  return big ? c * A.iters * 256
+             : (mid ? (A.k1 * A.iters + (c - A.k1) * A.iters_s) * 256
+                    : (A.k1 * A.iters + A.k2 * A.iters_s + (c - A.k1 - A.k2) * A.iters_t) * 256);
+}
+// A task's operands that its first iteration waits for: the hypothesis's twist and the lane's raw point
+// of iteration 0. The persistent form loads the next task's during the current task's epilogue
+// (TaskAhead::valid), so the HBM round trip overlaps the record's reduction instead of opening the task.
+struct TaskAhead {
+  double xr[6];
+  double np[3], ntt, nww;
+  unsigned t;   // the next task's ticket (all lanes), read back from the workgroup's task slot
+  bool valid;
+};
+template <bool PRE>
+GC_DEV void task_operands(const FusedArgs& A, int h, int64_t c, TaskAhead& ta) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  int it_unused;
+  const int64_t chunk0 = chunk_first(A, c, &it_unused);
+#pragma unroll
+  for (int k = 0; k < 6; ++k) ta.xr[k] = A.xi[6 * h + k];
+  const int64_t n_sel = (int64_t)A.bscal[5], stride = (int64_t)A.bscal[6];
+  const int64_t j = chunk0 + wv * 64 + lane;
+  ta.np[0] = 0.0; ta.np[1] = 0.0; ta.np[2] = 0.0; ta.ntt = 0.0; ta.nww = 0.0;
+  if (j < A.n_cap && j < n_sel) {
+    const int64_t i = j * stride;
+    ta.np[0] = A.pts_raw[3 * i]; ta.np[1] = A.pts_raw[3 * i + 1]; ta.np[2] = A.pts_raw[3 * i + 2];
+    ta.ntt = A.t_raw[i];
+    ta.nww = PRE ? A.w_win[j] : A.w_raw[i];
+  }
+  ta.valid = true;
+}
+
 // One task: hypothesis h, chunk c (its points: the tiers of FusedArgs) of the budgeted scan,
 // its partial record written to rec. Ends with the workgroup synchronised (LDS free for the next task).
+// Persistent form (ctr, task_slot, ahead non-null): the next task's ticket is taken by thread 0 at the
+// start of the task's last iteration, broadcast through task_slot at the epilogue's first barrier, and
+// the next task's operands are loaded into ahead during the rest of the epilogue (T tasks, H_l
+// hypotheses: ticket t = chunk t / H_l, hypothesis t % H_l).
 template <int BPL, bool FULL, bool PRE>
 GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec, unsigned* ctr = nullptr,
-                      unsigned* next = nullptr) {
+                      unsigned* task_slot = nullptr, TaskAhead* ahead = nullptr, unsigned T = 0, int Hl = 1,
+                      unsigned* late_next = nullptr) {
   constexpr int NF = NF_BASE;
   // features 0..8 and 10..16 on the matrix core, 17..18 on the VALU; feature 9 (w d_z²) is the trace
   // complement N − w d_x² − w d_y² (write_partial_record_mfma<.., 9>): one VALU feature fewer per step
@@ -1021,19 +1069,21 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   constexpr int NS = kFusedNS;
   const int64_t n_cap = A.n_cap;
   const int B = A.B;
-  const bool big = c < A.k1, mid = !big && c < A.k1 + A.k2;
-  const int iters = big ? A.iters : (mid ? A.iters_s : A.iters_t);
-  const int64_t chunk0 = big ? c * A.iters * 256
-                             : (mid ? (A.k1 * A.iters + (c - A.k1) * A.iters_s) * 256
-                                    : (A.k1 * A.iters + A.k2 * A.iters_s + (c - A.k1 - A.k2) * A.iters_t) * 256);
+  int iters;
+  const int64_t chunk0 = chunk_first(A, c, &iters);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int g = lane >> 4, bl = lane & 15;
   const int fcol = bl >= DF ? bl + 1 : bl;  // the feature of this lane's MFMA column
   double* F = lds + wv * (NS * kFusedFS);
   const double o[3] = {A.o0, A.o1, A.o2};
+  // the twist and iteration 0's raw point: loaded by the previous task's epilogue (persistent form), or
+  // here
+  TaskAhead ta_local;
+  TaskAhead& ta = ahead ? *ahead : ta_local;
+  if (!ahead || !ahead->valid) task_operands<PRE>(A, h, c, ta);
   double xr[6];
 #pragma unroll
-  for (int k = 0; k < 6; ++k) xr[k] = A.xi[6 * h + k];
+  for (int k = 0; k < 6; ++k) xr[k] = ta.xr[k];
   const double* __restrict__ pts_raw = A.pts_raw;
   const double* __restrict__ t_raw = A.t_raw;
   const double* __restrict__ w_raw = A.w_raw;
@@ -1081,7 +1131,8 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
       nww = PRE ? A.w_win[j] : w_raw[i];  // PRE: the window is already applied (once per scan)
     }
   };
-  fetch(0);
+  np[0] = ta.np[0]; np[1] = ta.np[1]; np[2] = ta.np[2]; ntt = ta.ntt; nww = ta.nww;
+  unsigned next = 0;
   // A chunk without padding points (all of it below n_cap: every chunk but the last) runs with
   // the valid flag folded to 1.0 — the masking multiplies vanish (x·1 = x, fma(Z−1, 1, 1) = Z
   // exactly), bit-identical to the masked form
@@ -1089,6 +1140,9 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
     constexpr bool PAD = decltype(pad_tag)::value;
     for (int it = 0; it < iters; ++it) {
       const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
+      // the next task's ticket, a whole iteration before the epilogue that broadcasts it (its round trip
+      // is long done by then; the ticket is held one iteration, not the whole task)
+      if (ctr && !late_next && it == iters - 1 && threadIdx.x == 0) next = atomicAdd(ctr, 1u);
       {  // phase A
         const int64_t j = wbase + lane;
         const bool inr = j < n_cap;
@@ -1180,10 +1234,20 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
     if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
-  // persistent form: the workgroup's next task ticket, taken here so that its round trip overlaps
-  // the epilogue (and the ticket is held only that long, not for a whole task)
-  if (ctr && threadIdx.x == 0) *next = atomicAdd(ctr, 1u);
-  write_partial_record_mfma<BPL, NX, DF>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec);
+  if (ahead) ahead->valid = false;
+  // without the look-ahead (late_next): the ticket taken here, its round trip overlapping the epilogue,
+  // and broadcast by the caller after it
+  if (ctr && late_next && threadIdx.x == 0) *late_next = atomicAdd(ctr, 1u);
+  const auto pre = [&]() {  // before the epilogue's first barrier: the ticket into the task slot
+    if (ctr && !late_next && threadIdx.x == 0) *task_slot = next;
+  };
+  const auto mid = [&]() {  // after it: every lane reads the ticket and loads the next task's operands
+    if (!ctr || late_next) return;
+    const unsigned tn = *task_slot;
+    ahead->t = tn;
+    if (tn < T) task_operands<PRE>(A, (int)(tn % (unsigned)Hl), (int64_t)(tn / (unsigned)Hl), *ahead);
+  };
+  write_partial_record_mfma<BPL, NX, DF>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec, pre, mid);
   __syncthreads();  // the epilogue's LDS reads are done before the next task writes the slabs
 }
 
@@ -1203,7 +1267,7 @@ __device__ double g_bins_trace[4 * 8192];
 __device__ double g_task_trace[4 * 16384];  // per task [start, end, puller, XCD id]
 #define GC_BT_NOW() ((double)__builtin_amdgcn_s_memrealtime())
 #endif
-template <int BPL, bool FULL>
+template <int BPL, bool FULL, bool AHEAD>
 __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
                                                              const double* __restrict__ odom, int n_io, int io_on,
                                                              int H, int64_t chunks, unsigned* ctr) {
@@ -1236,12 +1300,13 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
   // is rewritten). Taken at the start of the task instead, a ticket was held for the whole task: at
   // the end of the launch a workgroup pairing a long task with another on its CU (each then runs at
   // half speed) started its reserved one ~180 us late (GC_BINS_TIMING task traces)
-  unsigned next = 0;
-  if (threadIdx.x == 0) next = atomicAdd(ctr, 1u);
+  if (threadIdx.x == 0) task_s = atomicAdd(ctr, 1u);
+  __syncthreads();
+  TaskAhead ahead;
+  ahead.valid = false;
+  ahead.t = task_s;
   for (;;) {
-    if (threadIdx.x == 0) task_s = next;
-    __syncthreads();
-    const unsigned t = task_s;
+    const unsigned t = ahead.t;
     if (t >= T) break;
     // chunk-major: the workgroups in flight share a chunk's raw points across hypotheses (L2)
     const int64_t c = t / H;
@@ -1249,7 +1314,16 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
 #ifdef GC_BINS_TIMING
     const double tt0 = GC_BT_NOW();
 #endif
-    bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &next);
+    if constexpr (AHEAD) {
+      bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &task_s, &ahead, T, H);
+    } else {
+      unsigned next = 0;
+      bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &task_s, &ahead, T, H,
+                                 &next);
+      if (threadIdx.x == 0) task_s = next;
+      __syncthreads();
+      ahead.t = task_s;
+    }
 #ifdef GC_BINS_TIMING
     ++bt_n;
     if (threadIdx.x == 0 && t < 16384) {
@@ -1774,11 +1848,23 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   const size_t sh = sizeof(double) * (std::max<size_t>(std::max<size_t>(fused_lds_doubles(B), (size_t)kLpredLdsDoubles),
                                                        io ? (size_t)kIoLdsDoubles : 0) + 1);
   const dim3 grid((unsigned)(n_io + pullers));
-#define GC_BIO(BP, FULL)                                                                                       \
-  GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_bins_io<BP, FULL>, sh));                                      \
-  if (int rc_ = gc::ensure_no_static_lds(ctx, (const void*)k_bins_io<BP, FULL>)) return rc_;                  \
-  hipLaunchKernelGGL((k_bins_io<BP, FULL>), grid, dim3(256), sh, ctx->stream, FA, P, S, d_odom, n_io, io_on, H, chunks, \
-                     P.task_ctr)
+  // the look-ahead instantiation (the next task's operands loaded during the current task's epilogue,
+  // the ticket taken one iteration earlier) for short tasks: H = 32's 8-iteration tasks 0.2597 ->
+  // 0.2582 ms; H = 256's 32-iteration tasks keep the late ticket (holding it an iteration longer cost
+  // as much as the hidden loads gained, 1.1699 -> 1.1709; profiles/r05/ab_bins_ahead.txt). One
+  // instantiation per form: both paths in one kernel raised its spills and cost H = 32 10 us.
+  const bool ahead = iters < 32;
+#define GC_BIO2(BP, FULL, AH)                                                                                  \
+  GC_HIP(ctx, gc::ensure_dyn_lds((const void*)k_bins_io<BP, FULL, AH>, sh));                                  \
+  if (int rc_ = gc::ensure_no_static_lds(ctx, (const void*)k_bins_io<BP, FULL, AH>)) return rc_;              \
+  hipLaunchKernelGGL((k_bins_io<BP, FULL, AH>), grid, dim3(256), sh, ctx->stream, FA, P, S, d_odom, n_io, io_on, H,   \
+                     chunks, P.task_ctr)
+#define GC_BIO(BP, FULL)          \
+  if (ahead) {                    \
+    GC_BIO2(BP, FULL, true);      \
+  } else {                        \
+    GC_BIO2(BP, FULL, false);     \
+  }
   const int bpl = bpl_for(B);
   const bool full = B == 16 * bpl;
   switch (bpl) {
@@ -1788,6 +1874,7 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
     default: if (full) { GC_BIO(4, true); } else { GC_BIO(4, false); } break;
   }
 #undef GC_BIO
+#undef GC_BIO2
   GC_LAUNCH_CHECK(ctx);
   if (fold && chunks <= kFoldChunks && fold_record_fits(B)) {  // k_evidence reduces the records (gc_evidence.hip)
     fold->part = (const double*)scr;
