@@ -11,8 +11,12 @@
 struct gc_comm;
 
 namespace gc {
-// a device run hash (gc_runs.h RunTable): 2^bits 8-B entries and the 2^bits / 4 successor links
-// after them, all zero between uses
+// a device run hash (gc_runs.h RunTable): 2^bits 8-B entries (>= 2^kRunLoadShift x the rows) and
+// the 2^(bits - kRunLoadShift) position-indexed successor links after them, all zero between uses
+#ifndef GC_RUN_LOAD_SHIFT
+#define GC_RUN_LOAD_SHIFT 2
+#endif
+constexpr uint32_t kRunLoadShift = GC_RUN_LOAD_SHIFT;
 struct RunTableBuf {
   void* ptr = nullptr;
   uint32_t bits = 0;

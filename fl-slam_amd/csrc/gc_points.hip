@@ -1420,7 +1420,10 @@ constexpr int kFinSplitWG = 128;
 // up to this many chunk records per hypothesis (H = 256: 18, C5's 1024: 17) the evidence workgroup of
 // each hypothesis sums its own records (one more L2 round trip per 8 chunks at its start) in place of
 // this kernel's launch; more (H = 32: 80) keep the split kernel, which spreads them over 8 CUs
-constexpr int64_t kFoldChunks = 32;
+#ifndef GC_FOLD_CHUNKS
+#define GC_FOLD_CHUNKS 32
+#endif
+constexpr int64_t kFoldChunks = GC_FOLD_CHUNKS;
 static_assert(kFinBins * NF_BASE + REC_EXTRA <= kFinSplitWG, "one lane per record entry");
 __global__ void __launch_bounds__(kFinSplitWG) k_bins_finalize_split(int B, int NF, int64_t chunks,
                                                                      const double* __restrict__ partials,

@@ -145,9 +145,9 @@ int join_side(gc_ctx* ctx) {
 }
 
 int run_table(gc_ctx* ctx, hipStream_t st, RunTableBuf* T, int64_t rows) {
-  uint32_t bits = 8;  // >= 4 x rows entries (gc_runs.h); the links: rows <= 2^bits / 4
-  while (bits < 31 && ((int64_t)1 << bits) < 4 * rows) ++bits;
-  const size_t bytes = ((size_t)8 << bits) + ((size_t)1 << bits);  // entries + 2^bits / 4 links of 4 B
+  uint32_t bits = 8;  // >= 2^kRunLoadShift x rows entries (gc_runs.h); the links: rows <= 2^(bits - shift)
+  while (bits < 31 && ((int64_t)1 << bits) < (rows << kRunLoadShift)) ++bits;
+  const size_t bytes = ((size_t)8 << bits) + ((size_t)4 << (bits - kRunLoadShift));  // entries + links of 4 B
   if (bits > T->bits) {
     if (int rc = wait_stream(ctx, st, "the stream before growing a run table")) return rc;
     if (T->ptr) GC_HIP(ctx, hipFree(T->ptr));
@@ -158,7 +158,7 @@ int run_table(gc_ctx* ctx, hipStream_t st, RunTableBuf* T, int64_t rows) {
     T->dirty = true;
   }
   if (T->dirty) {  // zero: every entry empty, every link none
-    GC_HIP(ctx, hipMemsetAsync(T->ptr, 0, ((size_t)8 << T->bits) + ((size_t)1 << T->bits), st));
+    GC_HIP(ctx, hipMemsetAsync(T->ptr, 0, ((size_t)8 << T->bits) + ((size_t)4 << (T->bits - kRunLoadShift)), st));
     T->dirty = false;
   }
   return GC_OK;
