@@ -14,10 +14,10 @@
 // Sinkhorn couples all rows through the column sums, so it runs in one 1024-thread workgroup with
 // fixed-order block reductions (deterministic), the N x K kernel matrix streamed from L2.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include "gc_internal.h"
 #include "gc_math.h"
 #include "gc_mapslot.h"
+#include "gc_sort.h"
 
 namespace gc {
 namespace {
@@ -381,14 +381,7 @@ int32_t gc_extract_map_view(gc_ctx* ctx, const gc_primitive_map* map, int64_t m_
     GC_CHECK_ARG(ctx, h_dense_tiles[t] < 0 || (h_dense_tiles[t] + 1) * m_tile <= map->m_slots, "dense tile outside map");
   const int64_t n = (int64_t)T * m_tile;
   GC_CHECK_ARG(ctx, n < (int64_t)INT32_MAX, "view too large");
-  size_t temp = 0;
-  if (hipcub::DeviceSegmentedRadixSort::SortPairs(nullptr, temp, (const double*)nullptr, (double*)nullptr,
-                                                  (const int32_t*)nullptr, (int32_t*)nullptr, (int)n, T,
-                                                  (const int*)nullptr, (const int*)nullptr, 0, 64,
-                                                  ctx->stream) != hipSuccess) {
-    gc::set_error(ctx, "segmented sort sizing failed");
-    return GC_ERR_RUNTIME;
-  }
+  const size_t temp = gc::sort_temp_bytes(T, m_tile, true);
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t bk = al(sizeof(double) * n), bv = al(sizeof(int32_t) * n), bo = al(sizeof(int) * (T + 1)),
                bd = al(sizeof(int64_t) * T);
@@ -407,8 +400,8 @@ int32_t gc_extract_map_view(gc_ctx* ctx, const gc_primitive_map* map, int64_t m_
   hipLaunchKernelGGL(k_view_keys, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, ctx->stream, *map, m_tile,
                      (const int64_t*)dense, T, keys_in, vals_in, offs);
   GC_LAUNCH_CHECK(ctx);
-  if (hipcub::DeviceSegmentedRadixSort::SortPairs(tmp, temp, keys_in, keys, vals_in, vals, (int)n, T, offs, offs + 1,
-                                                  0, 64, ctx->stream) != hipSuccess) {
+  if (gc::radix_sort_pairs(ctx->stream, keys_in, keys, (const uint32_t*)vals_in, (uint32_t*)vals, T, m_tile, false,
+                           tmp) != hipSuccess) {
     gc::set_error(ctx, "segmented sort failed");
     return GC_ERR_RUNTIME;
   }

@@ -15,10 +15,10 @@
 // inherently sequential and runs on one lane over the sorted candidates, stopping at the first
 // distance >= threshold.
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 #include "gc_internal.h"
 #include "gc_math.h"
 #include "gc_mapslot.h"
+#include "gc_sort.h"
 
 namespace gc {
 namespace {
@@ -394,18 +394,27 @@ int32_t gc_primitive_map_recency_inflate(gc_ctx* ctx, const gc_primitive_map* ma
   return h_stats3 ? download(ctx, h_stats3, out, 3 * sizeof(double)) : GC_OK;
 }
 
+int32_t gc_test_radix_sort(gc_ctx* ctx, const double* d_keys_in, const uint32_t* d_vals_in, int64_t n_seg, int64_t L,
+                           int32_t descending, double* d_keys_out, uint32_t* d_vals_out) {
+  GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
+  GC_CHECK_ARG(ctx, n_seg >= 0 && L >= 0 && n_seg * L < ((int64_t)1 << 32), "n_seg * L must be in [0, 2^32)");
+  GC_CHECK_ARG(ctx, n_seg * L == 0 || (d_keys_in && d_keys_out), "NULL key buffer");
+  GC_CHECK_ARG(ctx, !d_vals_in || d_vals_out, "NULL value output");
+  if (n_seg * L == 0) return GC_OK;
+  void* scr;
+  if (int rc = gc::scratch(ctx, gc::sort_temp_bytes(n_seg, L, d_vals_in != nullptr), &scr)) return rc;
+  GC_HIP(ctx, gc::radix_sort_pairs(ctx->stream, d_keys_in, d_keys_out, d_vals_in, d_vals_out, n_seg, L, descending != 0,
+                                   scr));
+  return GC_OK;
+}
+
 int32_t gc_primitive_map_cull(gc_ctx* ctx, const gc_primitive_map* map, int64_t slot0, int64_t n_slots,
                               double weight_threshold, int64_t max_primitives, double* h_out4) {
   if (int rc = check_tile(ctx, map, slot0, n_slots, true)) return rc;
   GC_CHECK_ARG(ctx, h_out4 != nullptr, "h_out4 is NULL");
   for (int q = 0; q < 4; ++q) h_out4[q] = 0.0;
   if (n_slots == 0) return GC_OK;
-  size_t temp = 0;
-  if (hipcub::DeviceRadixSort::SortKeysDescending(nullptr, temp, (const double*)nullptr, (double*)nullptr,
-                                                  (int)n_slots, 0, 64, ctx->stream) != hipSuccess) {
-    gc::set_error(ctx, "radix sort sizing failed");
-    return GC_ERR_RUNTIME;
-  }
+  const size_t temp = gc::sort_temp_bytes(1, n_slots, false);
   const size_t kb = ((size_t)n_slots * sizeof(double) + 255) / 256 * 256;
   void* scr;
   if (int rc = gc::scratch(ctx, sizeof(double) * (4 * kPartBlocks + 8) + 2 * kb + temp, &scr)) return rc;
@@ -430,8 +439,7 @@ int32_t gc_primitive_map_cull(gc_ctx* ctx, const gc_primitive_map* map, int64_t 
   if (max_primitives >= 0 && n_valid - c[1] > (double)max_primitives && max_primitives < n_slots) {
     hipLaunchKernelGGL(k_cull_keys, dim3(blocks_for(n_slots)), dim3(256), 0, ctx->stream, T, keys_in);
     GC_LAUNCH_CHECK(ctx);
-    if (hipcub::DeviceRadixSort::SortKeysDescending(tmp, temp, keys_in, keys, (int)n_slots, 0, 64, ctx->stream) !=
-        hipSuccess) {
+    if (gc::radix_sort_pairs(ctx->stream, keys_in, keys, nullptr, nullptr, 1, n_slots, true, tmp) != hipSuccess) {
       gc::set_error(ctx, "radix sort failed");
       return GC_ERR_RUNTIME;
     }
@@ -459,13 +467,7 @@ int32_t gc_primitive_map_insert_masked(gc_ctx* ctx, const gc_primitive_map* map,
   GC_CHECK_ARG(ctx, n_slots < (int64_t)INT32_MAX, "tile too large");
   GC_CHECK_ARG(ctx, batch->Lambdas && batch->thetas && batch->etas && batch->weights && batch->valid_mask,
                "NULL proposal field");
-  size_t temp = 0;
-  if (hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const double*)nullptr, (double*)nullptr,
-                                         (const int32_t*)nullptr, (int32_t*)nullptr, (int)n_slots, 0, 64,
-                                         ctx->stream) != hipSuccess) {
-    gc::set_error(ctx, "radix sort sizing failed");
-    return GC_ERR_RUNTIME;
-  }
+  const size_t temp = gc::sort_temp_bytes(1, n_slots, true);
   const size_t kb = ((size_t)n_slots * sizeof(double) + 255) / 256 * 256;
   const size_t vb = ((size_t)n_slots * sizeof(int32_t) + 255) / 256 * 256;
   const size_t head = sizeof(double) * (kPartBlocks + 16);
@@ -483,8 +485,8 @@ int32_t gc_primitive_map_insert_masked(gc_ctx* ctx, const gc_primitive_map* map,
   hipLaunchKernelGGL(k_insert_keys, dim3(blocks_for(n_slots)), dim3(256), 0, ctx->stream, T, scan_seq,
                      recency_decay_lambda, keys_in, vals_in);
   GC_LAUNCH_CHECK(ctx);
-  if (hipcub::DeviceRadixSort::SortPairs(tmp, temp, keys_in, keys, vals_in, vals, (int)n_slots, 0, 64,
-                                         ctx->stream) != hipSuccess) {
+  if (gc::radix_sort_pairs(ctx->stream, keys_in, keys, (const uint32_t*)vals_in, (uint32_t*)vals, 1, n_slots, false,
+                           tmp) != hipSuccess) {
     gc::set_error(ctx, "radix sort failed");
     return GC_ERR_RUNTIME;
   }
@@ -512,13 +514,7 @@ int32_t gc_primitive_map_merge_reduce(gc_ctx* ctx, const gc_primitive_map* map, 
   h_out2[1] = 0;
   const Tile T{*map, slot0, n_slots};
   const int64_t P = n_slots * (n_slots - 1) / 2;
-  size_t temp = 0;
-  if (P > 0 && hipcub::DeviceRadixSort::SortPairs(nullptr, temp, (const double*)nullptr, (double*)nullptr,
-                                                  (const uint32_t*)nullptr, (uint32_t*)nullptr, (int)P, 0, 64,
-                                                  ctx->stream) != hipSuccess) {
-    gc::set_error(ctx, "radix sort sizing failed");
-    return GC_ERR_RUNTIME;
-  }
+  const size_t temp = P > 0 ? gc::sort_temp_bytes(1, P, true) : 0;
   auto al = [](size_t b) { return (b + 255) / 256 * 256; };
   const size_t head = sizeof(double) * (kPartBlocks + 16);
   const size_t b_mu = al(sizeof(double) * 3 * n_slots), b_sig = al(sizeof(double) * 9 * n_slots),
@@ -559,8 +555,7 @@ int32_t gc_primitive_map_merge_reduce(gc_ctx* ctx, const gc_primitive_map* map, 
   hipLaunchKernelGGL(k_merge_dist, dim3(blocks_for(P)), dim3(256), 0, ctx->stream, T, P, (const double*)mu,
                      (const double*)Sig, (const double*)dets, eps_lift, keys_in, vals_in);
   GC_LAUNCH_CHECK(ctx);
-  if (hipcub::DeviceRadixSort::SortPairs(tmp, temp, keys_in, keys, vals_in, vals, (int)P, 0, 64, ctx->stream) !=
-      hipSuccess) {
+  if (gc::radix_sort_pairs(ctx->stream, keys_in, keys, vals_in, vals, 1, P, false, tmp) != hipSuccess) {
     gc::set_error(ctx, "radix sort failed");
     return GC_ERR_RUNTIME;
   }

@@ -34,6 +34,7 @@ SIGNATURES = {
     "gc_ctx_set_wait_timeout": [_vp, _f64],
     "gc_test_bounded_wait": [_f64, _i64, _dptr],
     "gc_test_device_spin": [_vp, _f64],
+    "gc_test_radix_sort": [_vp, _vp, _vp, _i64, _i64, _i32, _vp, _vp],
     "gc_buffer_alloc": [_vp, _u64, C.POINTER(_vp)],
     "gc_buffer_free": [_vp, _vp],
     "gc_ctx_trim": [_vp],

@@ -62,6 +62,12 @@ int32_t gc_ctx_set_wait_timeout(gc_ctx* ctx, double seconds);
  * enqueues a one-thread kernel that keeps the stream busy for `seconds` (<= 10) and then exits. */
 int32_t gc_test_bounded_wait(double timeout_s, int64_t ready_after_polls, double* h_waited_ms);
 int32_t gc_test_device_spin(gc_ctx* ctx, double seconds);
+/* Test entry of the library's device radix sort (the PrimitiveMap cull / insert / merge and the map view's
+ * per-tile order): d_keys_in (n_seg x L doubles, n_seg * L < 2^32) sorted within each segment of L keys,
+ * ascending (or descending), stable (equal keys, -0.0 and +0.0 included, in input order), into
+ * d_keys_out, with d_vals_in (32-bit; NULL: keys only) permuted alike into d_vals_out. */
+int32_t gc_test_radix_sort(gc_ctx* ctx, const double* d_keys_in, const uint32_t* d_vals_in, int64_t n_seg, int64_t L,
+                           int32_t descending, double* d_keys_out, uint32_t* d_vals_out);
 /* Device buffers from the context's arena (SURVEY §8b ownership): gc_buffer_free returns a block to a
  * per-size-class cache and the next allocation of that class takes it back, so a steady-state chain of
  * per-operator calls performs no hipMalloc / hipFree and no synchronisation. All work on arena buffers

@@ -85,6 +85,26 @@ def softplus(x):
 # ---------------------------------------------------------------------------------------
 # Numeric primitives — fl_slam_poc/common/primitives.py
 # ---------------------------------------------------------------------------------------
+# Test switch (exact_inactive_deltas below): the projection delta of a clamp that moves no eigenvalue is
+# reported as the exact-arithmetic 0 instead of the rounding of V diag(λ) Vᵀ (the reference's value,
+# ~1e-16 ||M||, LAPACK-dependent). Off by default: the oracle follows the reference.
+EXACT_INACTIVE_DELTA = False
+
+
+class exact_inactive_deltas:
+    """Context manager: psd_project reports 0 for an inactive clamp while it is active."""
+
+    def __enter__(self):
+        global EXACT_INACTIVE_DELTA
+        self._prev, EXACT_INACTIVE_DELTA = EXACT_INACTIVE_DELTA, True
+        return self
+
+    def __exit__(self, *exc):
+        global EXACT_INACTIVE_DELTA
+        EXACT_INACTIVE_DELTA = self._prev
+        return False
+
+
 def psd_project(M, eps_psd=EPS_PSD):
     """domain_projection_psd_core (primitives.py:80-123). Returns (M_psd, cert6)."""
     M = np.asarray(M, dtype=np.float64)
@@ -94,6 +114,8 @@ def psd_project(M, eps_psd=EPS_PSD):
     wc = np.maximum(w, eps_psd)
     M_psd = V @ np.diag(wc) @ V.T
     proj = np.linalg.norm(M_psd - M_sym, "fro")
+    if EXACT_INACTIVE_DELTA and float(np.min(w)) > eps_psd:
+        proj = 0.0
     nnc = float(np.sum(wc < 10.0 * eps_psd))
     emin, emax = float(np.min(wc)), float(np.max(wc))
     return M_psd, np.array([proj, sym_delta, emin, emax, emax / emin, nnc])
