@@ -1809,13 +1809,25 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   // needs a third, and fewer, longer tasks amortise each task's set-up and record epilogue: H = 32
   // 4 -> 8 iterations, 92 -> 62 chunks, 0.2892 -> 0.2800 ms/scan (3 tasks: 0.2892, 1: 0.2848;
   // profiles/r04/ab_bins_tail.txt); H >= 64 keep 16
-  constexpr int kBinsMinTasks = 2;
+#ifndef GC_BINS_MIN_TASKS
+#define GC_BINS_MIN_TASKS 2
+#endif
+  constexpr int kBinsMinTasks = GC_BINS_MIN_TASKS;
   // at most 32 iterations (8192 points) per long task: H = 256 1.1935 -> 1.1803 ms, H = 128 0.6706 ->
   // 0.6658 against 16; 64: 1.1872 (profiles/r04/ab_bins_tail.txt)
   int iters = 32;
   while (iters > 2 && (int64_t)Hg * U < kBinsMinTasks * (int64_t)pullers * iters) iters >>= 1;
-  constexpr int kShortDiv = 2;
-  constexpr int kTinyDiv = 4, kTinyPerPuller = 1;
+#ifndef GC_BINS_SHORT_DIV
+#define GC_BINS_SHORT_DIV 2
+#endif
+  constexpr int kShortDiv = GC_BINS_SHORT_DIV;
+#ifndef GC_BINS_TINY_DIV
+#define GC_BINS_TINY_DIV 4
+#endif
+#ifndef GC_BINS_TINY_PER_PULLER
+#define GC_BINS_TINY_PER_PULLER 1
+#endif
+  constexpr int kTinyDiv = GC_BINS_TINY_DIV, kTinyPerPuller = GC_BINS_TINY_PER_PULLER;
   // short tasks of half a long one, at least 2 iterations: H = 256 8-iteration short tasks (interleaved
   // A/B on one box, 1.2499/1.2463 ms/scan with 4 -> 1.2377/1.2391 with 8); H = 32 (4-iteration long
   // tasks) 2, which stays best there (0.3013/0.3004/0.3003 ms against 0.305-0.313 for 8-iteration long
@@ -1830,7 +1842,15 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   const int kItersTiny = std::max(1, kItersShort / kTinyDiv);
   int64_t Ut = ((int64_t)pullers * kItersTiny * kTinyPerPuller + Hg - 1) / Hg;
   Ut = std::min<int64_t>((Ut + kItersTiny - 1) / kItersTiny * kItersTiny, U);
-  int64_t Us = std::max<int64_t>(iters, ((int64_t)pullers * iters + Hg - 1) / Hg);
+  // the short tier's work: one long task per puller, or half of one when the long tasks are short (below 32
+  // iterations: H = 32's 8, H = 64's 16): there the epilogues of the many short tasks cost more than the
+  // finer tail gains (H = 32 0.2586 -> 0.2548 ms/scan; H = 256 keeps one, 1.1624 against 1.1656 with half;
+  // profiles/r05/ab_bins_short_share.txt)
+#ifndef GC_BINS_SHORT_SHARE
+#define GC_BINS_SHORT_SHARE 0.5
+#endif
+  const double short_share = iters < 32 ? GC_BINS_SHORT_SHARE : 1.0;
+  int64_t Us = std::max<int64_t>(iters, (int64_t)(short_share * (double)pullers * iters + Hg - 1) / Hg);
   Us = std::min(Us, U - Ut);
   const int64_t k1 = (U - Ut - Us) / iters;  // long chunks; the short and tiny tiers take the rest
   const int64_t k2 = (U - Ut - k1 * iters) / kItersShort;
