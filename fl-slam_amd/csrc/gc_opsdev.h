@@ -428,24 +428,29 @@ GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const
     mat3_mul(dRa, dRb, Pl);
   }
   GC_MARK(sink, 40);
-  // inclusive scan of 3x3 products X_t = Pl_0 ... Pl_t: 6 shuffle levels inside each wave, then the
-  // wave totals (left to right) applied on the left; result rows in A for the reads below
+  // inclusive scan of 3x3 products X_t = Pl_0 ... Pl_t: six DPP levels inside each wave (scan_dpp_f64:
+  // lanes without a source take the identity, I X = X exactly), then the wave totals (left to right)
+  // applied on the left; result rows in A for the reads below
   double* src = A;
   {
     const int lane = t & 63, w = t >> 6;
+    (void)lane;
     double X[9];
     for (int k = 0; k < 9; ++k) X[k] = Pl[k];
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
+    const auto level = [&](auto shift) {
       double Y[9], Z[9];
 #pragma unroll
-      for (int k = 0; k < 9; ++k) Y[k] = __shfl_up(X[k], off, 64);
-      if (lane >= off) {
-        mat3_mul(Y, X, Z);
+      for (int k = 0; k < 9; ++k) Y[k] = shift(X[k], (k % 4 == 0) ? 1.0 : 0.0);
+      mat3_mul(Y, X, Z);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) X[k] = Z[k];
-      }
-    }
+      for (int k = 0; k < 9; ++k) X[k] = Z[k];
+    };
+    level([](double v, double o) { return scan_dpp_f64<0x111>(v, o); });
+    level([](double v, double o) { return scan_dpp_f64<0x112>(v, o); });
+    level([](double v, double o) { return scan_dpp_f64<0x114>(v, o); });
+    level([](double v, double o) { return scan_dpp_f64<0x118>(v, o); });
+    level([](double v, double o) { return scan_dpp_f64<0x142, 0xA>(v, o); });
+    level([](double v, double o) { return scan_dpp_f64<0x143, 0xC>(v, o); });
     if (lane == 63)
       for (int k = 0; k < 9; ++k) Bm[w * 9 + k] = X[k];
     __syncthreads();
@@ -483,13 +488,15 @@ GC_DEV void wg_preintegrate(int M, const ImuPair& q, double wa, double wb, const
     const int lane = t & 63, w = t >> 6;
     double v[3];
     for (int k = 0; k < 3; ++k) v[k] = awa[k] * dea + awb[k] * deb;
+    (void)lane;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const double y = __shfl_up(v[k], off, 64);
-        if (lane >= off) v[k] = y + v[k];
-      }
+    for (int k = 0; k < 3; ++k) {  // the same six DPP levels (identity 0.0)
+      v[k] = scan_dpp_f64<0x111>(v[k], 0.0) + v[k];
+      v[k] = scan_dpp_f64<0x112>(v[k], 0.0) + v[k];
+      v[k] = scan_dpp_f64<0x114>(v[k], 0.0) + v[k];
+      v[k] = scan_dpp_f64<0x118>(v[k], 0.0) + v[k];
+      v[k] = scan_dpp_f64<0x142, 0xA>(v[k], 0.0) + v[k];
+      v[k] = scan_dpp_f64<0x143, 0xC>(v[k], 0.0) + v[k];
     }
     if (lane == 63)
       for (int k = 0; k < 3; ++k) V2[w * 3 + k] = v[k];

@@ -58,6 +58,17 @@ GC_DEV double wdpp_f64(double v) {
   const int hi = __builtin_amdgcn_mov_dpp(__double2hiint(v), CTRL, 0xF, 0xF, false);
   return __hiloint2double(hi, lo);
 }
+// DPP lane shift of a wave prefix scan: lane l takes lane l - k of its 16-lane row (row_shr:k, CTRL =
+// 0x110 + k), or the last lane of the row before (row_bcast:15, CTRL 0x142, ROW_MASK 0xA: rows 1 and 3)
+// or of row 1 (row_bcast:31, CTRL 0x143, ROW_MASK 0xC: rows 2 and 3); lanes without a source keep
+// `old` (the scan's identity). Six steps (1, 2, 4, 8 in rows, then the two broadcasts) give an inclusive
+// scan over the wave with VALU moves only (the __shfl_up form: six ds_bpermute round trips per value).
+template <int CTRL, int ROW_MASK = 0xF>
+GC_DEV double scan_dpp_f64(double v, double old) {
+  const int lo = __builtin_amdgcn_update_dpp(__double2loint(old), __double2loint(v), CTRL, ROW_MASK, 0xF, false);
+  const int hi = __builtin_amdgcn_update_dpp(__double2hiint(old), __double2hiint(v), CTRL, ROW_MASK, 0xF, false);
+  return __hiloint2double(hi, lo);
+}
 template <typename Op>
 GC_DEV double wave_reduce(double v, const Op& op) {
   v = op(v, wdpp_f64<0xB1>(v));   // quad_perm [1,0,3,2]
