@@ -1842,14 +1842,19 @@ int32_t scan_bins_pipeline(gc_ctx* ctx, const PipeDev& P, const ScanArgs& S, con
   const int kItersTiny = std::max(1, kItersShort / kTinyDiv);
   int64_t Ut = ((int64_t)pullers * kItersTiny * kTinyPerPuller + Hg - 1) / Hg;
   Ut = std::min<int64_t>((Ut + kItersTiny - 1) / kItersTiny * kItersTiny, U);
-  // the short tier's work: one long task per puller, or half of one when the long tasks are short (below 32
-  // iterations: H = 32's 8, H = 64's 16): there the epilogues of the many short tasks cost more than the
-  // finer tail gains (H = 32 0.2586 -> 0.2548 ms/scan; H = 256 keeps one, 1.1624 against 1.1656 with half;
-  // profiles/r05/ab_bins_short_share.txt)
+  // the short tier's work: one long task per puller when every puller has at least 4 long tasks (H = 256),
+  // three quarters of one with fewer 32-iteration tasks (H = 128: 0.6497 -> 0.6459 ms/scan), half of one when
+  // the long tasks are shorter (H = 32's 8 iterations, H = 64's 16): with few long tasks per puller the
+  // epilogues of the many short tasks cost more than the finer tail gains (H = 32 0.2586 -> 0.2548 ms/scan;
+  // H = 256 1.1624 against 1.1656 with half, 1.1648 with three quarters; profiles/r05/ab_bins_short_share.txt)
 #ifndef GC_BINS_SHORT_SHARE
 #define GC_BINS_SHORT_SHARE 0.5
 #endif
-  const double short_share = iters < 32 ? GC_BINS_SHORT_SHARE : 1.0;
+#ifndef GC_BINS_SHORT_SHARE_32
+#define GC_BINS_SHORT_SHARE_32 0.75
+#endif
+  const bool many_long = (int64_t)Hg * U >= 4 * (int64_t)pullers * iters;
+  const double short_share = many_long ? 1.0 : (iters >= 32 ? GC_BINS_SHORT_SHARE_32 : GC_BINS_SHORT_SHARE);
   int64_t Us = std::max<int64_t>(iters, (int64_t)(short_share * (double)pullers * iters + Hg - 1) / Hg);
   Us = std::min(Us, U - Ut);
   const int64_t k1 = (U - Ut - Us) / iters;  // long chunks; the short and tiny tiers take the rest
