@@ -23,11 +23,12 @@ namespace gc {
 int comm_size(const gc_comm* c) { return c ? c->nranks : 1; }
 
 bool comm_healthy(gc_comm* c, std::string* why) {
-  if (!c || !c->comm) return true;
-  if (c->aborted) {
+  if (!c) return true;
+  if (c->aborted) {  // before the NULL-comm test: an abort clears c->comm
     if (why) *why = "the communicator was aborted by an earlier failure";
     return false;
   }
+  if (!c->comm) return true;
   ncclResult_t a = ncclSuccess;
   const ncclResult_t r = ncclCommGetAsyncError(c->comm, &a);
   if (r != ncclSuccess) {

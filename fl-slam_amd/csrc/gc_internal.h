@@ -17,6 +17,8 @@ namespace gc {
 #define GC_RUN_LOAD_SHIFT 2
 #endif
 constexpr uint32_t kRunLoadShift = GC_RUN_LOAD_SHIFT;
+// the linear probe (gc_runs.h) relies on a table strictly larger than its runs
+static_assert(kRunLoadShift >= 1, "the run hash needs more entries than rows");
 struct RunTableBuf {
   void* ptr = nullptr;
   uint32_t bits = 0;
@@ -71,7 +73,7 @@ int join_side(gc_ctx* ctx);
 // device scratch of at least `bytes` (synchronises the stream before growing)
 int scratch(gc_ctx* ctx, size_t bytes, void** out);
 
-// a run hash (gc_runs.h RunTable) of at least 2 x rows entries, every entry empty on return
+// a run hash (gc_runs.h RunTable) of at least 2^kRunLoadShift x rows entries, every entry empty on return
 // (stream-ordered: a fill is enqueued on st when the table is new, grown or dirty)
 int run_table(gc_ctx* ctx, hipStream_t st, RunTableBuf* T, int64_t rows);
 

@@ -343,6 +343,9 @@ constexpr int kBlkRunCap = 8;  // a position's run slice (more runs: SlotRunList
 constexpr int kStageDoubles = (9 + 3 + 9 + 1 + 1 + 3) * kFuseBlk;
 constexpr size_t kStageLds = sizeof(double) * kStageDoubles + sizeof(int32_t) * kFuseBlk +
                              sizeof(uint32_t) * kFuseBlk * kBlkRunCap;
+// one workgroup's dynamic LDS on gfx950 (160 KiB per CU, all of it addressable by one workgroup once
+// ensure_dyn_lds raises the limit): ~62 KB at GC_FUSE_BLK=256, ~125 KB at 512
+static_assert(kStageLds <= 160 * 1024, "the staged fuse apply's rows do not fit one workgroup's LDS");
 __global__ void __launch_bounds__(kFuseBlk) k_fuse_apply_blk(FuseArgs A, int64_t K, RunTable T,
                                                          const uint32_t* __restrict__ sslot,
                                                          const uint32_t* __restrict__ order,

@@ -770,6 +770,12 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
     const gc::ScanMapInput in{s.pts, s.t, s.w, S.t0, S.t1, p->smap_voxel, S.t1, p->pending_seq};
     hipStream_t ms = side ? p->mstream : ctx->stream;
     if (side) GC_HIP(ctx, hipStreamWaitEvent(ms, p->smap_go, 0));
+    if (side && ctx->side_pending && ctx->side_ev != p->smap_done[0] && ctx->side_ev != p->smap_done[1]) {
+      // the context keeps one side event: another pipeline's update is still pending on it, so this
+      // update orders after it and the event recorded below covers both (join_side then joins every
+      // pipeline's update, not only the last one's)
+      GC_HIP(ctx, hipStreamWaitEvent(ms, ctx->side_ev, 0));
+    }
     int rc = gc::scan_map_update(ctx, ms, &p->smapW, p->smap, P, in);
     if (rc == GC_OK && p->smap_colors) {
       // primitive_map_fuse ends with colors = rgb = the estimate from the camera accumulators on

@@ -139,8 +139,8 @@ int wait_event(gc_ctx* ctx, hipEvent_t ev, const char* what, double* waited_ms, 
 
 int join_side(gc_ctx* ctx) {
   if (!ctx || !ctx->side_pending) return GC_OK;
-  ctx->side_pending = false;
   GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, ctx->side_ev, 0));
+  ctx->side_pending = false;  // only once the wait is enqueued (a failed wait leaves it to the next join)
   return GC_OK;
 }
 

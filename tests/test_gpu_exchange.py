@@ -103,6 +103,13 @@ def test_rccl_single_rank_communicator(ctx):
     _abi.call("gc_comm_allgather_f64", ctx.handle, h.value, ds.ptr, dr.ptr, 1000, ctx=ctx)
     ctx.sync()
     assert np.array_equal(dr.download(), x)
+    ok = C.c_int32(-1)
+    assert _abi.lib().gc_comm_healthy(h.value, C.byref(ok)) == _abi.GC_OK and ok.value == 1
+    # after an abort the communicator reports unhealthy and every exchange is refused with the reason
+    assert _abi.lib().gc_comm_abort(h.value) == _abi.GC_OK
+    assert _abi.lib().gc_comm_healthy(h.value, C.byref(ok)) == _abi.GC_OK and ok.value == 0
+    with pytest.raises(RuntimeError, match="refused.*aborted"):
+        _abi.call("gc_comm_allgather_f64", ctx.handle, h.value, ds.ptr, dr.ptr, 1000, ctx=ctx)
     _abi.lib().gc_comm_destroy(h.value)
 
     case = cases.build(H=4, n_az=256, n_scans=2)

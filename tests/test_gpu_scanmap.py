@@ -141,6 +141,28 @@ def test_scan_map_update_replicated_across_shards(ctx):
                 assert np.array_equal(got[f], ref[f]), f"scan{k} {f}"
 
 
+def test_first_pipelines_map_read_after_a_later_pipelines_finish(ctx):
+    """Several pipelines with attached maps on one context: each scan_finish chains its
+    side-stream update after the context's pending one, so reading the FIRST pipeline's map after a
+    later pipeline's finish (no ctx.sync in between) joins every update, and the map matches the
+    oracle."""
+    voxel, cap, M = 0.1, 16384, 1 << 14
+    case = cases.build(H=4, n_az=1024, n_scans=2, io="computed", cap=cap)
+    pipes = [_pipeline(case, ctx, 4, cap, True) for _ in range(3)]
+    maps = [_map(ctx, M, 21 + i) for i in range(3)]
+    for p, m in zip(pipes, maps):
+        p.attach_primitive_map(m, voxel)
+    for k, s in enumerate(case["scans"]):
+        tiles, iws = [m.download() for m in maps], [p.get_iw() for p in pipes]
+        for p in pipes:
+            p.stage_scan(0, s)
+            p.run_scan(0, s, k)
+        for i in (0, 1):  # the earlier pipelines' maps, read right after the last pipeline's finish
+            _check_scan(pipes[i], maps[i], tiles[i], s, k, cap, M, voxel, iws[i])
+    for p in pipes:
+        p.close()
+
+
 def test_scan_map_attach_rules(ctx):
     from gcslam.primitive_map import DevicePrimitiveMap
     case = cases.build(H=2, n_az=256, n_scans=1, io="computed")
