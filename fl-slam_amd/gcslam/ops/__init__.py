@@ -23,7 +23,7 @@ from .inverse_wishart import (MeasurementNoiseIWState, ProcessNoiseIWState,
                               process_noise_iw_apply_suffstats_jax,
                               process_noise_iw_suffstats_from_info_jax, process_noise_state_to_Q_jax)
 from .hypothesis import HypothesisProjectionResult, hypothesis_barycenter_projection
-from .pointcloud import PointCloud2Msg, PointField, imu_window_padded, parse_pointcloud2_vlp16
+from .pointcloud import PointCloud2Msg, PointField, imu_message_to_base, imu_window_padded, parse_pointcloud2_vlp16
 from .imu_odom_evidence import (ImuDependenceInflationResult, ImuGyroEvidenceResult, ImuPreintegrationFactorResult,
                                 OdomDependenceInflationResult, OdomEvidenceResult, OdomVelocityEvidenceResult,
                                 OdomYawRateEvidenceResult, PlanarPriorResult, PoseTwistConsistencyResult,
@@ -52,5 +52,5 @@ __all__ = [
     "imu_preintegration_factor", "PlanarPriorResult", "planar_z_prior", "VelocityZPriorResult", "velocity_z_prior",
     "OdomVelocityEvidenceResult", "odom_velocity_evidence", "OdomYawRateEvidenceResult", "odom_yawrate_evidence",
     "PoseTwistConsistencyResult", "pose_twist_kinematic_consistency", "OdomDependenceInflationResult",
-    "odom_dependence_inflation", "PointCloud2Msg", "PointField", "parse_pointcloud2_vlp16", "imu_window_padded",
+    "odom_dependence_inflation", "PointCloud2Msg", "PointField", "parse_pointcloud2_vlp16", "imu_window_padded", "imu_message_to_base",
 ]

@@ -97,6 +97,19 @@ def parse_pointcloud2_vlp16(msg, R_base_lidar=None, t_base_lidar=None, ctx=None
     return pts.download(), ts.download(), ws.download(), rg.download(), tg.download()
 
 
+def imu_message_to_base(gyro, accel, R_base_imu, accel_scale: float = 1.0) -> Tuple[np.ndarray, np.ndarray]:
+    """The node's IMU callback transform (on_imu, backend_node.py:1397-1412): accel · imu_accel_scale,
+    then gyro_base = R_base_imu @ gyro and accel_base = R_base_imu @ accel. One message's 3-vectors (or
+    (n, 3) rows of several). The reference keeps this callback CPU-only by design (no device work per
+    message, :1400); the rotated samples feed imu_window_padded."""
+    R = np.asarray(R_base_imu, np.float64).reshape(3, 3)
+    g = np.asarray(gyro, np.float64)
+    a = np.asarray(accel, np.float64) * float(accel_scale)
+    if g.ndim == 1:
+        return R @ g, R @ a
+    return np.einsum("ij,nj->ni", R, g), np.einsum("ij,nj->ni", R, a)
+
+
 def imu_window_padded(imu_buffer, t_last_scan: float, scan_start_time: float, t_scan: float,
                       scan_end_time: float, M: int = GC_MAX_IMU_PREINT_LEN
                       ) -> Tuple[np.ndarray, np.ndarray, np.ndarray]:

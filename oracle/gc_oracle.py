@@ -329,6 +329,43 @@ def to_base(points, R, t):
     return (R @ points.T).T + t[None, :]
 
 
+# The IMU extrinsic of the reference's raw sensor dump (docs/raw_sensor_dump; a Livox IMU reporting
+# accelerations in g): tools/apply_imu_extrinsic_to_csv.py:38-42, GC_IMU_ACCEL_SCALE constants.py:85
+DUMP_T_BASE_IMU = (0.0, 0.0, 0.0, -0.015586, 0.489293, 0.0)
+DUMP_ACCEL_SCALE = 9.81
+ODOM_Z_VARIANCE_PRIOR = 1e6  # GC_ODOM_Z_VARIANCE_PRIOR (constants.py:300)
+
+
+def imu_to_base(gyro, accel, R_base_imu, accel_scale=1.0):
+    """on_imu (backend_node.py:1397-1412): accel = accel_raw · imu_accel_scale, then the no-TF
+    numeric rotation of both into the base frame, gyro_base = R @ gyro, accel_base = R @ accel (per
+    sample; the same math as tools/apply_imu_extrinsic_to_csv.py:85-110). (n, 3) arrays in and out."""
+    R = np.asarray(R_base_imu, np.float64)
+    g = np.asarray(gyro, np.float64)
+    a = np.asarray(accel, np.float64) * float(accel_scale)
+    return np.einsum("ij,nj->ni", R, g), np.einsum("ij,nj->ni", R, a)
+
+
+def odom_pose_from_msg(position, quat_xyzw):
+    """on_odom (backend_node.py:1441-1465): rotvec = Rotation.from_quat([x, y, z, w]).as_rotvec(),
+    pose = se3_from_rotvec_trans(rotvec, position) = [trans, rotvec] (belief.py:93-110)."""
+    from scipy.spatial.transform import Rotation
+    rv = Rotation.from_quat(np.asarray(quat_xyzw, np.float64)).as_rotvec()
+    return np.concatenate([np.asarray(position, np.float64), rv])
+
+
+def odom_relative(first_abs, pose_abs):
+    """first-odom-as-origin (backend_node.py:1512-1514): first⁻¹ ∘ pose."""
+    return se3_compose(se3_inverse(first_abs), pose_abs)
+
+
+def odom_cov_capped(cov, z_prior=ODOM_Z_VARIANCE_PRIOR):
+    """backend_node.py:1518-1523: the pose covariance with its z variance raised to the prior."""
+    c = np.array(cov, np.float64).reshape(6, 6)
+    c[2, 2] = max(c[2, 2], float(z_prior))
+    return c
+
+
 # ---------------------------------------------------------------------------------------
 # a1 PointBudgetResample — backend/operators/point_budget.py:50-221
 # ---------------------------------------------------------------------------------------
