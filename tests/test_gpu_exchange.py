@@ -171,3 +171,77 @@ def test_two_process_gloo_exchange_on_one_gpu(ctx, tmp_path):
     for key in SHARED:
         assert np.array_equal(st[0][key], st[1][key]), key
         _rel_close(st[0][key], ref[key], 1e-12, key)
+
+
+def _dying_peer_rank(rank, world, port, outdir, timeout_s):
+    """Rank 1 completes two scans, then dies (os._exit) before the third scan's exchange; rank 0
+    must leave that exchange with an error within the bound, tear its pipeline down (bounded waits,
+    a scan half still pending) and exit non-zero (backend_node.py:2205-2210: log and re-raise)."""
+    import datetime
+    import json
+    import time
+    sys.path.insert(0, os.path.join(ROOT, "fl-slam_amd"))
+    sys.path.insert(0, ROOT)
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+    from gcslam import _abi
+    from oracle import cases as cs
+    dist.init_process_group("gloo", rank=rank, world_size=world, timeout=datetime.timedelta(seconds=timeout_s))
+    ctx = _abi.Context(0)
+    ctx.set_wait_timeout(timeout_s)
+    case = cs.build(H=6, n_az=256, n_scans=3)
+    pipe = _make(case, ctx, rank, world)
+    t_fail, err = None, None
+    try:
+        for k, s in enumerate(case["scans"]):
+            pipe.stage_scan(0, s)
+            pipe.run_scan_local(0, s, k)
+            if rank == 1 and k == 2:
+                os._exit(0)  # the peer dies mid-run: its third scan's local half done, no exchange
+            rec = torch.from_numpy(pipe.partial())
+            out = [torch.empty_like(rec) for _ in range(world)]
+            t_fail = time.perf_counter()
+            dist.all_gather(out, rec)
+            pipe.finish_scan(torch.stack(out).numpy())
+    except (RuntimeError, ValueError) as e:
+        err = "%s: %s" % (type(e).__name__, str(e)[:300])
+    waited = time.perf_counter() - t_fail if t_fail is not None else None
+    t_close = time.perf_counter()
+    pipe.close()  # the pending scan half is abandoned; destroy's waits are bounded
+    with open(os.path.join(outdir, f"rank{rank}.json"), "w") as f:
+        json.dump({"error": err, "waited_s": waited, "close_s": time.perf_counter() - t_close}, f)
+    os._exit(3 if err else 0)
+
+
+def test_peer_dying_mid_run_fails_the_survivor_within_bound(tmp_path):
+    """Two processes on one GPU (ranks 0, 1 of 3 / 3 hypotheses, gloo exchange of the device partial
+    records): rank 1 exits after its second full scan. Rank 0's third-scan exchange must fail (an
+    error, not a hang) within the 20 s bound, its pipeline must tear down with the scan half pending,
+    and it must exit non-zero."""
+    import json
+    import socket
+    import time
+    import torch.multiprocessing as mp
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        port = so.getsockname()[1]
+    bound = 20.0
+    pctx = mp.get_context("spawn")
+    procs = [pctx.Process(target=_dying_peer_rank, args=(r, 2, port, str(tmp_path), bound)) for r in range(2)]
+    t0 = time.perf_counter()
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(timeout=240)
+    for p in procs:
+        if p.is_alive():
+            p.kill()
+            raise AssertionError("a rank is still running after 240 s")
+    assert procs[1].exitcode == 0
+    assert procs[0].exitcode == 3, procs[0].exitcode
+    r0 = json.load(open(tmp_path / "rank0.json"))
+    assert r0["error"] and r0["error"].startswith("RuntimeError"), r0
+    assert r0["waited_s"] is not None and r0["waited_s"] < bound + 5.0, r0
+    assert r0["close_s"] < 10.0, r0
+    assert time.perf_counter() - t0 < 240.0
