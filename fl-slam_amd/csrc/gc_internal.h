@@ -60,6 +60,19 @@ struct gc_ctx {
   std::unordered_map<void*, size_t> arena_live;  // block -> class size
   size_t arena_cached = 0, arena_live_bytes = 0, arena_cap = (size_t)16 << 30;
   int64_t arena_hip_allocs = 0, arena_hip_frees = 0, arena_reuses = 0;
+  // Pinned staging ring of gc_buffer_upload (uploads of at most kStageSeg bytes): the caller's bytes are
+  // copied into the current segment of a pinned host ring and the DMA is enqueued on the stream with
+  // no wait, so the caller's buffer is free on return and a chain of small uploads and launches
+  // never drains the stream (the per-operator drop-ins upload a few hundred small operands per scan).
+  // A segment is reused only after the event recorded when the ring last left it has completed.
+  static constexpr int kStageSegs = 8;
+  static constexpr size_t kStageSeg = (size_t)512 << 10;
+  char* stage_host = nullptr;
+  hipEvent_t stage_ev[kStageSegs] = {};
+  bool stage_rec[kStageSegs] = {};
+  int stage_seg = 0;
+  size_t stage_off = 0;
+  int64_t stage_uploads = 0;
 };
 
 namespace gc {

@@ -97,6 +97,9 @@ struct gc_pipeline {
   bool x_timing = false;  // gc_pipeline_set_exchange_timing
   // the in-scan PrimitiveMap update (gc_scanmap.hip), run by scan_finish after the combine
   bool smap_on = false;
+  // GC_SMAP_OWNER: only the rank holding hypothesis 0 runs the in-scan update (backend_node.py:2081-2083:
+  // hypothesis 0 writes the map); GC_SMAP_REPLICATED: every rank updates its own replica
+  int32_t smap_mode = GC_SMAP_OWNER;
   gc_primitive_map smap{};
   double smap_voxel = 0.0;
   bool smap_colors = false;  // the colour pass is due (first update after attaching a map with colours not current)
@@ -247,8 +250,13 @@ int slot_alloc(gc_pipeline* p, gc_pipeline::Slot& s) {
 // the copy stream may overwrite the slot's device block only after the last scan that read it
 // with a PrimitiveMap attached the pending scan's last read of its slot (the map update) is only
 // enqueued by scan_finish, so that slot cannot be restaged before then
+// the in-scan map update runs on this rank (a map attached, and this rank its owner or every rank updating)
+bool smap_active(const gc_pipeline* p) {
+  return p->smap_on && (p->smap_mode == GC_SMAP_REPLICATED || p->P.h_begin == 0);
+}
+
 int slot_check_restage(gc_pipeline* p, int slot) {
-  GC_CHECK_ARG(p->ctx, !(p->pending && p->smap_on && slot == p->pending_slot),
+  GC_CHECK_ARG(p->ctx, !(p->pending && smap_active(p) && slot == p->pending_slot),
                "the slot is read by the pending scan's map update (gc_pipeline_scan_finish first)");
   return GC_OK;
 }
@@ -741,20 +749,21 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
   // (fin_ev; with a map attached the slots order on the map update instead)
   hipEvent_t fin = nullptr;
   int fin_e = -1;
-  if (kBindEvery > 0 && !p->smap_on && p->pending_ticket > 0 && p->pending_ticket % kBindEvery == 0) {
+  const bool smap = smap_active(p);
+  if (kBindEvery > 0 && !smap && p->pending_ticket > 0 && p->pending_ticket % kBindEvery == 0) {
     fin_e = (int)((p->pending_ticket / kBindEvery) & 1);
     fin = p->fin_ev[fin_e];
     p->fin_ticket[fin_e] = 0;  // the event is re-armed by this launch: unusable until it succeeds
   }
   const int par = (int)(p->pending_ticket & 1);
   P.smap_snap = p->snap_base + par * gc::kSnapLen;
-  if (p->smap_on && p->smap_done_rec[par]) {
+  if (smap && p->smap_done_rec[par]) {
     // the map update two scans back read this snapshot block: rewritten only after it (long done
     // by now, the wait costs the stream a barrier)
     GC_HIP(ctx, hipStreamWaitEvent(ctx->stream, p->smap_done[par], 0));
     p->smap_done_rec[par] = false;
   }
-  const bool side = p->smap_on && p->mstream;
+  const bool side = smap && p->mstream;
   if (side) fin = p->smap_go;
   GC_HIP(ctx, gc::launch_combine_final(P, p->pending_S, ctx->stream, fin));
   // only a launch that carries the event makes it cover this ticket (a failed launch leaves it
@@ -764,7 +773,7 @@ static int32_t scan_finish_impl(gc_pipeline* p, const double* h_gather) {
   if (p->inscan_certs) GC_HIP(ctx, gc::launch_proj_certs(P, ctx->stream));
   p->pcert_scan = p->inscan_certs;
   GC_TRY(stage_event(p, 6));
-  if (p->smap_on) {
+  if (smap) {
     auto& s = p->slots[p->pending_slot];
     const gc::ScanArgs& S = p->pending_S;
     const gc::ScanMapInput in{s.pts, s.t, s.w, S.t0, S.t1, p->smap_voxel, S.t1, p->pending_seq};
@@ -871,6 +880,14 @@ int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const gc_primitive_map*
   return GC_OK;
 }
 
+int32_t gc_pipeline_set_scan_map_mode(gc_pipeline* p, int32_t mode) {
+  GC_CHECK_ARG(nullptr, p, "NULL pipeline");
+  GC_CHECK_ARG(p->ctx, mode == GC_SMAP_OWNER || mode == GC_SMAP_REPLICATED, "mode must be GC_SMAP_OWNER or GC_SMAP_REPLICATED");
+  GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  p->smap_mode = mode;
+  return GC_OK;
+}
+
 int32_t gc_pipeline_get_scan_map_pose(gc_pipeline* p, double* h_out) {
   GC_CHECK_ARG(nullptr, p && h_out, "NULL argument");
   GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
@@ -881,6 +898,10 @@ int32_t gc_pipeline_get_scan_map_count(gc_pipeline* p, int64_t* n_slots) {
   GC_CHECK_ARG(nullptr, p && n_slots, "NULL argument");
   GC_CHECK_ARG(p->ctx, p->smap_on, "no PrimitiveMap attached");
   GC_CHECK_ARG(p->ctx, !p->pending, "a scan's exchange is pending (gc_pipeline_scan_finish)");
+  if (!smap_active(p)) {  // not this rank's map to update (GC_SMAP_OWNER on a rank without hypothesis 0)
+    *n_slots = 0;
+    return GC_OK;
+  }
   GC_TRY(gc::join_side(p->ctx));  // the counts of the last update (its stream)
   size_t bytes = 0;
   const int32_t rc = gc::scan_map_count(p->ctx, p->smapW, n_slots, &bytes);
@@ -918,14 +939,14 @@ static int32_t scan_local_impl(gc_pipeline* p, int32_t slot, double scan_start, 
   // kernel publishes as this scan's ticket (done_word)
   ++p->ticket;
   gc::BinsFold fold;
-  int64_t* dw = p->smap_on ? nullptr : p->done_word;
+  int64_t* dw = smap_active(p) ? nullptr : p->done_word;
   GC_TRY(gc::scan_bins_pipeline(ctx, P, S, s.odom, io, s.pts, s.t, s.w, s.n_in, dw, p->ticket, &fold));
   gc::ScanArgs Se = S;  // the evidence launch's: with the finalize folded in, its records and the ticket
   Se.fin_part = fold.part;
   Se.fin_chunks = fold.chunks;
   Se.done_word = fold.part ? dw : nullptr;
   Se.ticket = p->ticket;
-  if (!p->smap_on) s.consumed_ticket = p->ticket;
+  if (!smap_active(p)) s.consumed_ticket = p->ticket;
   p->pending_ticket = p->ticket;
   GC_TRY(stage_event(p, 2));
   // a7 .. a15

@@ -224,6 +224,11 @@ int32_t gc_ctx_destroy(gc_ctx* ctx) {
   if (ctx->runs.ptr) (void)hipFree(ctx->runs.ptr);
   for (auto& kv : ctx->arena_free) (void)hipFree(kv.second);
   for (auto& kv : ctx->arena_live) (void)hipFree(kv.first);  // buffers not freed before the context
+  if (ctx->stage_host) {
+    for (hipEvent_t e : ctx->stage_ev)
+      if (e) (void)hipEventDestroy(e);
+    (void)hipHostFree(ctx->stage_host);
+  }
   (void)hipStreamDestroy(ctx->stream);
   delete ctx;
   return GC_OK;
@@ -344,10 +349,56 @@ int32_t gc_ctx_alloc_stats(gc_ctx* ctx, int64_t* h_out6) {
   return GC_OK;
 }
 
+namespace {
+// a pinned staging slot of `bytes` (<= kStageSeg) in ctx's ring (gc_ctx::stage_host)
+int stage_slot(gc_ctx* ctx, uint64_t bytes, char** out) {
+  if (!ctx->stage_host) {
+    void* h = nullptr;
+    GC_HIP(ctx, hipHostMalloc(&h, gc_ctx::kStageSegs * gc_ctx::kStageSeg, hipHostMallocDefault));
+    for (hipEvent_t& e : ctx->stage_ev) {
+      const hipError_t er = hipEventCreateWithFlags(&e, hipEventDisableTiming);
+      if (er != hipSuccess) {
+        (void)hipHostFree(h);
+        gc::set_error(ctx, std::string("HIP error ") + hipGetErrorString(er) + " creating the staging events");
+        return GC_ERR_RUNTIME;
+      }
+    }
+    ctx->stage_host = (char*)h;
+    ctx->stage_seg = 0;
+    ctx->stage_off = 0;
+  }
+  const size_t need = (bytes + 255) & ~(size_t)255;
+  if (ctx->stage_off + need > gc_ctx::kStageSeg) {
+    // leave the segment: its copies are done once this event has completed
+    const int s = ctx->stage_seg;
+    GC_HIP(ctx, hipEventRecord(ctx->stage_ev[s], ctx->stream));
+    ctx->stage_rec[s] = true;
+    const int nx = (s + 1) % gc_ctx::kStageSegs;
+    if (ctx->stage_rec[nx]) {  // recorded kStageSegs - 1 segments ago: normally long complete
+      if (int rc = gc::wait_event(ctx, ctx->stage_ev[nx], "a staging segment's uploads")) return rc;
+      ctx->stage_rec[nx] = false;
+    }
+    ctx->stage_seg = nx;
+    ctx->stage_off = 0;
+  }
+  *out = ctx->stage_host + (size_t)ctx->stage_seg * gc_ctx::kStageSeg + ctx->stage_off;
+  ctx->stage_off += need;
+  return GC_OK;
+}
+}  // namespace
+
 int32_t gc_buffer_upload(gc_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes) {
   GC_CHECK_ARG(nullptr, ctx != nullptr, "ctx is NULL");
   if (int rc_j = gc::join_side(ctx)) return rc_j;
   if (bytes == 0) return GC_OK;
+  if (bytes <= gc_ctx::kStageSeg) {  // staged: no wait (the pinned copy is the caller's buffer's)
+    char* h = nullptr;
+    if (int rc = stage_slot(ctx, bytes, &h)) return rc;
+    std::memcpy(h, h_src, bytes);
+    GC_HIP(ctx, hipMemcpyAsync(d_dst, h, bytes, hipMemcpyHostToDevice, ctx->stream));
+    ++ctx->stage_uploads;
+    return GC_OK;
+  }
   GC_HIP(ctx, hipMemcpyAsync(d_dst, h_src, bytes, hipMemcpyHostToDevice, ctx->stream));
   return gc::wait_stream(ctx, ctx->stream, "an upload");
 }

@@ -95,6 +95,7 @@ SIGNATURES = {
     "gc_pipeline_get_scan_map_pose": [_vp, _vp],
     "gc_pipeline_map_colors_stale": [_vp],
     "gc_pipeline_get_scan_map_count": [_vp, C.POINTER(C.c_int64)],
+    "gc_pipeline_set_scan_map_mode": [_vp, _i32],
     "gc_pipeline_set_exchange_timing": [_vp, _i32],
     "gc_pipeline_exchange_ms": [_vp, C.POINTER(C.c_float)],
     "gc_pipeline_set_stage_timing": [_vp, _i32],
@@ -377,6 +378,70 @@ def device_input(ctx: Context, x, dtype=np.float64, shape=None) -> DeviceArray:
 def host(x):
     """A host NumPy view of x (downloads a DeviceArray)."""
     return x.download() if isinstance(x, DeviceArray) else np.asarray(x)
+
+
+_PACK_ALIGN = 256
+
+
+def _packed_offsets(nbytes):
+    offs, tot = [], 0
+    for nb in nbytes:
+        offs.append(tot)
+        tot += -(-max(int(nb), 1) // _PACK_ALIGN) * _PACK_ALIGN
+    return offs, tot
+
+
+def alloc_many(ctx: Context, specs):
+    """Several device arrays as views of ONE arena block (one gc_buffer_alloc): specs = [(shape, dtype)
+    or shape]. download_many of the views is then one copy and one wait."""
+    specs = [s if (isinstance(s, tuple) and len(s) == 2 and isinstance(s[1], (type, np.dtype))) else (s, np.float64)
+             for s in specs]
+    shapes = [tuple(int(v) for v in (sh if isinstance(sh, (tuple, list)) else (sh,))) for sh, _ in specs]
+    dts = [np.dtype(dt) for _, dt in specs]
+    nbytes = [int(np.prod(sh, dtype=np.int64)) * dt.itemsize for sh, dt in zip(shapes, dts)]
+    offs, tot = _packed_offsets(nbytes)
+    base = DeviceArray(ctx, tot, np.uint8)
+    return [DeviceArray(ctx, sh, dt, _base=base, _ptr=base.ptr + o) for sh, dt, o in zip(shapes, dts, offs)]
+
+
+def upload_many(ctx: Context, arrays, dtype=np.float64):
+    """Host arrays (or DeviceArrays, used in place) as device arrays: every host array is packed into
+    one host buffer and one arena block, so an operator's small operands cost one upload (staged, no
+    wait: gc_buffer_upload) instead of one each. dtype: one dtype for all, or a list."""
+    dts = dtype if isinstance(dtype, (list, tuple)) else [dtype] * len(arrays)
+    out = [None] * len(arrays)
+    host_idx, host_arr = [], []
+    for i, (x, dt) in enumerate(zip(arrays, dts)):
+        if isinstance(x, DeviceArray):
+            out[i] = device_input(ctx, x, dt)
+        else:
+            host_idx.append(i)
+            host_arr.append(np.ascontiguousarray(x, dtype=dt))
+    if host_arr:
+        offs, tot = _packed_offsets([a.nbytes for a in host_arr])
+        buf = np.empty(tot, np.uint8)
+        for a, o in zip(host_arr, offs):
+            buf[o:o + a.nbytes] = a.reshape(-1).view(np.uint8)
+        base = DeviceArray(ctx, tot, np.uint8)
+        base.upload(buf)
+        for i, a, o in zip(host_idx, host_arr, offs):
+            out[i] = DeviceArray(ctx, a.shape, a.dtype, _base=base, _ptr=base.ptr + o)
+    return out
+
+
+def download_many(arrays):
+    """Host copies of device arrays; views of one block (alloc_many) come back with one download."""
+    if not arrays:
+        return []
+    b0 = arrays[0]._base
+    if b0 is not None and all(a._base is b0 for a in arrays):
+        raw = b0.download()
+        out = []
+        for a in arrays:
+            o = a.ptr - b0.ptr
+            out.append(raw[o:o + a.nbytes].view(a.dtype).reshape(a.shape))
+        return out
+    return [a.download() for a in arrays]
 
 
 _tls = threading.local()

@@ -69,8 +69,8 @@ def world_pose_batch(beliefs: List[BeliefGaussianInfo], eps_lift: float = GC_EPS
     ctx = ctx or _abi.default_context()
     X, _, L, h = arrays if arrays is not None else stack(beliefs)
     H = X.shape[0]
-    dX, dL, dh = (_abi.DeviceArray.from_host(ctx, a) for a in (X, L, h))
-    dp, dm = _abi.DeviceArray(ctx, (H, 6)), _abi.DeviceArray(ctx, (H, D_Z))
+    dX, dL, dh = _abi.upload_many(ctx, (X, L, h))
+    dp, dm = _abi.alloc_many(ctx, [(H, 6), (H, D_Z)])
     _abi.call("gc_belief_world_pose_batch", ctx.handle, H, dX.ptr, dL.ptr, dh.ptr, float(eps_lift), dp.ptr, dm.ptr,
               ctx=ctx)
-    return dp.download(), dm.download()
+    return tuple(_abi.download_many([dp, dm]))

@@ -76,14 +76,14 @@ def bin_soft_assign_batch(dirs, bins, tau=GC_TAU_SOFT_ASSIGN, ctx=None, device_o
     B = Bd.shape[0]
     if not 1 <= B <= 64:
         raise ValueError(f"bin count must be in [1, 64], got {B}")
-    dd, db = _abi.device_input(ctx, dirs, np.float64, (H, n, 3)), _abi.DeviceArray.from_host(ctx, Bd)
-    dr = _abi.DeviceArray(ctx, (H, n, B)); di = _abi.DeviceArray(ctx, (H, n), np.int32)
-    dc = _abi.DeviceArray(ctx, (H, 2))
+    dd, db = _abi.upload_many(ctx, (dirs, Bd))
+    dd = _abi.device_input(ctx, dd, np.float64, (H, n, 3))
+    dr, di, dc = _abi.alloc_many(ctx, [(H, n, B), ((H, n), np.int32), (H, 2)])
     _abi.call("gc_bin_soft_assign", ctx.handle, H, n, B, dd.ptr, db.ptr, float(tau), dr.ptr, di.ptr, dc.ptr,
               ctx=ctx)
     if device_out:
         return dr, di, dc.download()
-    return dr.download(), di.download(), dc.download()
+    return tuple(_abi.download_many([dr, di, dc]))
 
 
 def bin_soft_assign(point_directions, bin_directions, tau: float = GC_TAU_SOFT_ASSIGN,
@@ -124,11 +124,11 @@ def scan_bin_moment_match_batch(points, point_covariances, weights, responsibili
            _abi.device_input(ctx, responsibilities, np.float64, (H, n, B)),
            None if point_lambda is None else _abi.device_input(ctx, point_lambda, np.float64, (H, n))]
     ptr = [d.ptr if d is not None else None for d in dev]
-    ds = _abi.DeviceArray(ctx, (H, B, _abi.GC_BIN_STATS)); dc = _abi.DeviceArray(ctx, (H, _abi.GC_BIN_CERT))
+    ds, dc = _abi.alloc_many(ctx, [(H, B, _abi.GC_BIN_STATS), (H, _abi.GC_BIN_CERT)])
     oa, op = _abi.f64p(o)
     _abi.call("gc_scan_bin_moment_match", ctx.handle, H, n, B, ptr[0], ptr[1], ptr[2], ptr[3], ptr[4], op,
               float(eps_psd), float(eps_mass), ds.ptr, dc.ptr, ctx=ctx)
-    return ds.download(), dc.download()
+    return tuple(_abi.download_many([ds, dc]))
 
 
 def scan_bin_moment_match(points, point_covariances, weights, responsibilities, point_lambda=None,

@@ -39,12 +39,12 @@ def deskew_batch(points, timestamps, weights, scan_start_time, scan_end_time, xi
     dt = _abi.device_input(ctx, timestamps, np.float64, (n,))
     dw = _abi.device_input(ctx, weights, np.float64, (n,))
     dx = _abi.DeviceArray.from_host(ctx, X)
-    op = _abi.DeviceArray(ctx, (H, n, 3)); ow = _abi.DeviceArray(ctx, (H, n)); os_ = _abi.DeviceArray(ctx, H)
+    op, ow, os_ = _abi.alloc_many(ctx, [(H, n, 3), (H, n), H])
     _abi.call("gc_deskew_constant_twist", ctx.handle, H, n, dp.ptr, dt.ptr, dw.ptr,
               float(scan_start_time), float(scan_end_time), dx.ptr, op.ptr, ow.ptr, os_.ptr, ctx=ctx)
     if device_out:
         return op, ow, os_.download()
-    return op.download(), ow.download(), os_.download()
+    return tuple(_abi.download_many([op, ow, os_]))
 
 
 def _weight_sum(ctx, weights) -> float:

@@ -15,11 +15,11 @@ def excitation_scaling_batch(L_evidence, L_prior, h_prior, eps=GC_EXC_EPS, ctx=N
     Lp = np.ascontiguousarray(L_prior, np.float64).reshape(-1, D_Z, D_Z)
     hp = np.ascontiguousarray(h_prior, np.float64).reshape(-1, D_Z)
     H = Le.shape[0]
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (Le, Lp, hp)]
-    s, Lo, ho = _abi.DeviceArray(ctx, (H, 2)), _abi.DeviceArray(ctx, Lp.shape), _abi.DeviceArray(ctx, hp.shape)
+    d = _abi.upload_many(ctx, (Le, Lp, hp))
+    s, Lo, ho = _abi.alloc_many(ctx, [(H, 2), Lp.shape, hp.shape])
     _abi.call("gc_excitation_scaling_batch", ctx.handle, H, d[0].ptr, d[1].ptr, d[2].ptr, float(eps), s.ptr, Lo.ptr,
               ho.ptr, ctx=ctx)
-    return s.download(), Lo.download(), ho.download()
+    return tuple(_abi.download_many([s, Lo, ho]))
 
 
 def compute_excitation_scales_jax(L_evidence, L_prior, eps: float = GC_EXC_EPS, ctx=None):
@@ -33,8 +33,9 @@ def apply_excitation_prior_scaling_jax(L_prior, h_prior, s_dt, s_ex, ctx=None):
     ctx = ctx or _abi.default_context()
     Lp = np.ascontiguousarray(L_prior, np.float64).reshape(1, D_Z, D_Z)
     hp = np.ascontiguousarray(h_prior, np.float64).reshape(1, D_Z)
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (Lp, hp, np.array([[float(s_dt), float(s_ex)]]))]
-    Lo, ho = _abi.DeviceArray(ctx, Lp.shape), _abi.DeviceArray(ctx, hp.shape)
+    d = _abi.upload_many(ctx, (Lp, hp, np.array([[float(s_dt), float(s_ex)]])))
+    Lo, ho = _abi.alloc_many(ctx, [Lp.shape, hp.shape])
     _abi.call("gc_excitation_scaling_batch", ctx.handle, 1, None, d[0].ptr, d[1].ptr, GC_EXC_EPS, d[2].ptr, Lo.ptr,
               ho.ptr, ctx=ctx)
-    return Lo.download()[0], ho.download()[0]
+    Lh, hh = _abi.download_many([Lo, ho])
+    return Lh[0], hh[0]

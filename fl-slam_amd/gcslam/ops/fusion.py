@@ -60,11 +60,11 @@ def info_fusion_additive_batch(L_pred, h_pred, L_evidence, h_evidence, alpha, ep
     Le = np.ascontiguousarray(L_evidence, np.float64).reshape(H, D_Z, D_Z)
     he = np.ascontiguousarray(h_evidence, np.float64).reshape(H, D_Z)
     al = np.ascontiguousarray(np.broadcast_to(np.asarray(alpha, np.float64).reshape(-1), (H,)))
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (Lp, hp, Le, he, al)]
-    Lo, ho, co = _abi.DeviceArray(ctx, Lp.shape), _abi.DeviceArray(ctx, hp.shape), _abi.DeviceArray(ctx, (H, 6))
+    d = _abi.upload_many(ctx, (Lp, hp, Le, he, al))
+    Lo, ho, co = _abi.alloc_many(ctx, [Lp.shape, hp.shape, (H, 6)])
     _abi.call("gc_info_fusion_additive_batch", ctx.handle, H, *[x.ptr for x in d], float(eps_psd), Lo.ptr, ho.ptr,
               co.ptr, ctx=ctx)
-    return Lo.download(), ho.download(), co.download()
+    return tuple(_abi.download_many([Lo, ho, co]))
 
 
 def info_fusion_additive(belief_pred: BeliefGaussianInfo, L_evidence, h_evidence, alpha: float,

@@ -24,14 +24,13 @@ def hypothesis_barycenter_batch(L, h, z, weights, floor, eps_psd=GC_EPS_PSD, eps
     ctx = ctx or _abi.default_context()
     Ls = np.ascontiguousarray(L, np.float64).reshape(-1, D_Z, D_Z)
     K = Ls.shape[0]
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (Ls, np.ascontiguousarray(h, np.float64).reshape(K, D_Z),
-                                                      np.ascontiguousarray(z, np.float64).reshape(K, D_Z),
-                                                      np.ascontiguousarray(weights, np.float64).reshape(K))]
-    oL, oh, oz = _abi.DeviceArray(ctx, (D_Z, D_Z)), _abi.DeviceArray(ctx, D_Z), _abi.DeviceArray(ctx, D_Z)
-    oc = _abi.DeviceArray(ctx, _abi.GC_BARY_CERT)
+    d = _abi.upload_many(ctx, (Ls, np.ascontiguousarray(h, np.float64).reshape(K, D_Z),
+                               np.ascontiguousarray(z, np.float64).reshape(K, D_Z),
+                               np.ascontiguousarray(weights, np.float64).reshape(K)))
+    oL, oh, oz, oc = _abi.alloc_many(ctx, [(D_Z, D_Z), D_Z, D_Z, _abi.GC_BARY_CERT])
     _abi.call("gc_hypothesis_barycenter", ctx.handle, K, *[x.ptr for x in d], float(floor), float(eps_psd),
               float(eps_lift), oL.ptr, oh.ptr, oz.ptr, oc.ptr, ctx=ctx)
-    return oL.download(), oh.download(), oz.download(), oc.download()
+    return tuple(_abi.download_many([oL, oh, oz, oc]))
 
 
 def hypothesis_barycenter_projection(hypotheses: List[BeliefGaussianInfo], weights, K_HYP: int = GC_K_HYP,

@@ -124,7 +124,7 @@ def imu_vmf_gravity_evidence_time_resolved_batch(rotvec, imu_accel, imu_gyro, we
     M = acc.shape[0]
     w = np.ascontiguousarray(np.broadcast_to(np.asarray(weights, np.float64), (H, M)))
     ba = np.ascontiguousarray(np.broadcast_to(np.asarray(accel_bias, np.float64), (H, 3)))
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (rv, acc, np.ascontiguousarray(imu_gyro, np.float64), w, ba)]
+    d = _abi.upload_many(ctx, (rv, acc, np.ascontiguousarray(imu_gyro, np.float64), w, ba))
     out = _abi.DeviceArray(ctx, (H, _abi.GC_IOF_OUT))
     g, gp = _abi.f64p(_v(gravity_W, 3))
     _abi.call("gc_imu_vmf_gravity_tr_batch", ctx.handle, H, M, *[x.ptr for x in d], gp, float(dt_imu),

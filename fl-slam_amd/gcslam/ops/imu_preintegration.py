@@ -39,7 +39,7 @@ def preintegrate_imu_batch(imu_stamps, imu_gyro, imu_accel, weights, rotvec_star
     stride = 0 if w.ndim == 1 else M
     if w.reshape(-1).shape[0] not in (M, H * M):
         raise ValueError("weights must be (M,) or (H, M)")
-    dev = [_abi.DeviceArray.from_host(ctx, x) for x in (t, g, a, w, r0, bg, ba)]
+    dev = _abi.upload_many(ctx, (t, g, a, w, r0, bg, ba))
     out = _abi.DeviceArray(ctx, (H, _abi.GC_PREINT_OUT))
     ga, gp = _abi.f64p(gravity_W)
     _abi.call("gc_preintegrate_imu_batch", ctx.handle, H, M, dev[0].ptr, dev[1].ptr, dev[2].ptr, dev[3].ptr, stride,
@@ -69,7 +69,7 @@ def imu_meas_iw_suffstats_batch(imu_gyro, imu_accel, weights, gyro_bias, accel_b
             (gyro_bias, accel_bias, omega_avg, rotvec_start_WB)]
     H = max(r.shape[0] for r in rows)
     rows = [np.ascontiguousarray(np.broadcast_to(r, (H, 3))) for r in rows]
-    dev = [_abi.DeviceArray.from_host(ctx, x) for x in [g, a, w] + rows]
+    dev = _abi.upload_many(ctx, [g, a, w] + rows)
     out = _abi.DeviceArray(ctx, (H, 18))
     _abi.call("gc_imu_meas_iw_suffstats_batch", ctx.handle, H, M, *[d.ptr for d in dev], float(dt_imu),
               float(eps_mass), float(eps_psd), out.ptr, ctx=ctx)

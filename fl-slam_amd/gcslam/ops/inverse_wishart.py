@@ -33,12 +33,11 @@ def process_noise_iw_suffstats_batch(L_pred, h_pred, L_post, h_post, eps_lift=GC
     ctx = ctx or _abi.default_context()
     Lq = _f(L_pred, (-1, D_Z, D_Z))
     H = Lq.shape[0]
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (Lq, _f(h_pred, (H, D_Z)), _f(L_post, (H, D_Z, D_Z)),
-                                                      _f(h_post, (H, D_Z)))]
-    dP, dn = _abi.DeviceArray(ctx, (H, 7, 6, 6)), _abi.DeviceArray(ctx, (H, 7))
+    d = _abi.upload_many(ctx, (Lq, _f(h_pred, (H, D_Z)), _f(L_post, (H, D_Z, D_Z)), _f(h_post, (H, D_Z))))
+    dP, dn = _abi.alloc_many(ctx, [(H, 7, 6, 6), (H, 7)])
     _abi.call("gc_iw_process_suffstats_batch", ctx.handle, H, *[x.ptr for x in d], float(eps_lift), dP.ptr, dn.ptr,
               ctx=ctx)
-    return dP.download(), dn.download()
+    return tuple(_abi.download_many([dP, dn]))
 
 
 def process_noise_iw_suffstats_from_info_jax(L_pred, h_pred, L_post, h_post, eps_lift: float = GC_EPS_LIFT, ctx=None):
@@ -50,18 +49,18 @@ def process_noise_iw_apply_suffstats_jax(pn_state: ProcessNoiseIWState, dPsi, dn
                                          eps_psd: float = GC_EPS_PSD, nu_max: float = 1000.0, ctx=None):
     """-> (ProcessNoiseIWState, cert (2,) = [psd Δ sum, ν projection sum]). dt_sec unused (API compat)."""
     ctx = ctx or _abi.default_context()
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (_f(pn_state.nu, 7), _f(pn_state.Psi, (7, 6, 6)),
-                                                      _f(dPsi, (7, 6, 6)), _f(dnu, 7))]
-    on, oP, oc = _abi.DeviceArray(ctx, 7), _abi.DeviceArray(ctx, (7, 6, 6)), _abi.DeviceArray(ctx, 2)
+    d = _abi.upload_many(ctx, (_f(pn_state.nu, 7), _f(pn_state.Psi, (7, 6, 6)), _f(dPsi, (7, 6, 6)), _f(dnu, 7)))
+    on, oP, oc = _abi.alloc_many(ctx, [7, (7, 6, 6), 2])
     _abi.call("gc_iw_process_apply", ctx.handle, *[x.ptr for x in d], float(eps_psd), float(nu_max), on.ptr, oP.ptr,
               oc.ptr, ctx=ctx)
-    return replace(pn_state, nu=on.download(), Psi=oP.download()), oc.download()
+    nu, Psi, c = _abi.download_many([on, oP, oc])
+    return replace(pn_state, nu=nu, Psi=Psi), c
 
 
 def process_noise_state_to_Q_jax(pn_state: ProcessNoiseIWState, eps_psd: float = GC_EPS_PSD, ctx=None):
     """Q (22,22) = PSD(block-diag(Ψ_b / softplus⁺(ν_b − d_b − 1)))."""
     ctx = ctx or _abi.default_context()
-    dn, dP = _abi.DeviceArray.from_host(ctx, _f(pn_state.nu, 7)), _abi.DeviceArray.from_host(ctx, _f(pn_state.Psi, (7, 6, 6)))
+    dn, dP = _abi.upload_many(ctx, (_f(pn_state.nu, 7), _f(pn_state.Psi, (7, 6, 6))))
     oQ = _abi.DeviceArray(ctx, (D_Z, D_Z))
     _abi.call("gc_iw_process_Q", ctx.handle, dn.ptr, dP.ptr, float(eps_psd), oQ.ptr, ctx=ctx)
     return oQ.download()
@@ -71,9 +70,9 @@ def measurement_noise_apply_suffstats_jax(mn_state: MeasurementNoiseIWState, dPs
                                           nu_max: float = 1000.0, ctx=None):
     """-> (MeasurementNoiseIWState, cert (2,))."""
     ctx = ctx or _abi.default_context()
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (_f(mn_state.nu, 3), _f(mn_state.Psi, (3, 3, 3)),
-                                                      _f(dPsi, (3, 3, 3)), _f(dnu, 3))]
-    on, oP, oc = _abi.DeviceArray(ctx, 3), _abi.DeviceArray(ctx, (3, 3, 3)), _abi.DeviceArray(ctx, 2)
+    d = _abi.upload_many(ctx, (_f(mn_state.nu, 3), _f(mn_state.Psi, (3, 3, 3)), _f(dPsi, (3, 3, 3)), _f(dnu, 3)))
+    on, oP, oc = _abi.alloc_many(ctx, [3, (3, 3, 3), 2])
     _abi.call("gc_iw_meas_apply", ctx.handle, *[x.ptr for x in d], float(eps_psd), float(nu_max), on.ptr, oP.ptr,
               oc.ptr, ctx=ctx)
-    return replace(mn_state, nu=on.download(), Psi=oP.download()), oc.download()
+    nu, Psi, c = _abi.download_many([on, oP, oc])
+    return replace(mn_state, nu=nu, Psi=Psi), c

@@ -53,8 +53,13 @@ def _scatter(v) -> ScatterMetrics:
 
 
 def _dev(ctx, *arrays):
-    return [_abi.DeviceArray.from_host(ctx, np.ascontiguousarray(a, dtype=np.float64)) if a is not None else None
-            for a in arrays]
+    """The operands in one packed upload (None stays None)."""
+    idx = [i for i, a in enumerate(arrays) if a is not None]
+    up = _abi.upload_many(ctx, [arrays[i] for i in idx])
+    out = [None] * len(arrays)
+    for i, d in zip(idx, up):
+        out[i] = d
+    return out
 
 
 def matrix_fisher_batch(pose_pred, scan_s_dir, scan_N, scan_S_dir_scatter, map_S_dir, map_N_dir, map_S_dir_scatter,

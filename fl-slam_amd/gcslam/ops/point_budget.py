@@ -54,19 +54,19 @@ def point_budget_resample(points, timestamps, weights, ring=None, tag=None,
             dev[k].zero()
         else:
             dev[k] = _abi.device_input(ctx, v, np.uint8, (n,))
-    out_p = _abi.DeviceArray(ctx, (cap, 3)); out_t = _abi.DeviceArray(ctx, cap)
-    out_w = _abi.DeviceArray(ctx, cap); out_r = _abi.DeviceArray(ctx, cap, np.uint8)
-    out_g = _abi.DeviceArray(ctx, cap, np.uint8); out_i = _abi.DeviceArray(ctx, cap, np.int64)
-    scal = _abi.DeviceArray(ctx, 8)
+    out_p, out_t, out_w, out_r, out_g, out_i, scal = _abi.alloc_many(
+        ctx, [(cap, 3), cap, cap, (cap, np.uint8), (cap, np.uint8), (cap, np.int64), 8])
     _abi.call("gc_point_budget_resample", ctx.handle, dev["p"].ptr, dev["t"].ptr, dev["w"].ptr,
               dev["r"].ptr, dev["g"].ptr, n, cap, out_p.ptr, out_t.ptr, out_w.ptr, out_r.ptr,
               out_g.ptr, out_i.ptr, scal.ptr, ctx=ctx)
-    s = scal.download()
+    if device_out:
+        s = scal.download()
+        arr = (out_p, out_t, out_w, out_r, out_g, out_i)
+    else:
+        *arr, s = _abi.download_many([out_p, out_t, out_w, out_r, out_g, out_i, scal])
     mass_in = float(s[0])
-    get = (lambda d: d) if device_out else (lambda d: d.download())
-    res = PointBudgetResult(points=get(out_p), timestamps=get(out_t), weights=get(out_w),
-                            ring=get(out_r), tag=get(out_g), n_input=n, n_output=int(s[5]),
-                            total_mass_in=mass_in, total_mass_out=mass_in, indices=get(out_i))
+    res = PointBudgetResult(points=arr[0], timestamps=arr[1], weights=arr[2], ring=arr[3], tag=arr[4], n_input=n,
+                            n_output=int(s[5]), total_mass_in=mass_in, total_mass_out=mass_in, indices=arr[5])
     support_frac = min(1.0, cap / (n + GC_EPS_MASS))
     cert = CertBundle.create_approx(
         chart_id=chart_id, anchor_id=anchor_id, triggers=["PointBudgetResample"],

@@ -23,11 +23,11 @@ def predict_diffusion_batch(L, h, Q, dt_sec, eps_psd=GC_EPS_PSD, eps_lift=GC_EPS
     if Qa.shape != (D_Z, D_Z):
         raise ValueError(f"Q must be ({D_Z}, {D_Z}), got {Qa.shape}")
     H = L.shape[0]
-    dL, dh, dQ = (_abi.DeviceArray.from_host(ctx, a) for a in (L, h, Qa))
-    oL, oh, oc = _abi.DeviceArray(ctx, L.shape), _abi.DeviceArray(ctx, h.shape), _abi.DeviceArray(ctx, (H, 8))
+    dL, dh, dQ = _abi.upload_many(ctx, (L, h, Qa))
+    oL, oh, oc = _abi.alloc_many(ctx, [L.shape, h.shape, (H, 8)])
     _abi.call("gc_predict_diffusion_batch", ctx.handle, H, dL.ptr, dh.ptr, dQ.ptr, float(dt_sec), float(eps_psd),
               float(eps_lift), float(lambda_ou), oL.ptr, oh.ptr, oc.ptr, ctx=ctx)
-    return oL.download(), oh.download(), oc.download()
+    return tuple(_abi.download_many([oL, oh, oc]))
 
 
 def predict_diffusion(belief_prev: BeliefGaussianInfo, Q, dt_sec: float, eps_psd: float = GC_EPS_PSD,

@@ -34,9 +34,9 @@ def domain_projection_psd_batch(M, eps_psd: float = GC_EPS_PSD, ctx=None):
         raise ValueError(f"expected (batch, d, d), got {A.shape}")
     b, d, _ = A.shape
     dm = _abi.DeviceArray.from_host(ctx, A)
-    do = _abi.DeviceArray(ctx, A.shape); dc = _abi.DeviceArray(ctx, (b, 6))
+    do, dc = _abi.alloc_many(ctx, [A.shape, (b, 6)])
     _abi.call("gc_domain_projection_psd_batch", ctx.handle, b, d, dm.ptr, float(eps_psd), do.ptr, dc.ptr, ctx=ctx)
-    return do.download(), dc.download()
+    return tuple(_abi.download_many([do, dc]))
 
 
 def spd_cholesky_inverse_lifted(L, eps_lift: float = GC_EPS_LIFT, ctx=None, device_out: bool = False):

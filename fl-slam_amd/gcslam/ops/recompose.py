@@ -33,16 +33,15 @@ class AnchorDriftResult:
 def _run(name, X, z, L, h, extra, ctx, res_w):
     ctx = ctx or _abi.default_context()
     H = X.shape[0]
-    d = [_abi.DeviceArray.from_host(ctx, a) for a in (X, z, L, h)]
-    oX, oz, oh = _abi.DeviceArray(ctx, (H, 6)), _abi.DeviceArray(ctx, (H, D_Z)), _abi.DeviceArray(ctx, (H, D_Z))
-    res = _abi.DeviceArray(ctx, (H, res_w))
+    d = _abi.upload_many(ctx, (X, z, L, h))
+    oX, oz, oh, res = _abi.alloc_many(ctx, [(H, 6), (H, D_Z), (H, D_Z), (H, res_w)])
     if name == "gc_recompose_batch":
         dT = _abi.DeviceArray.from_host(ctx, np.ascontiguousarray(extra[0], np.float64).reshape(H))
         _abi.call(name, ctx.handle, H, *[x.ptr for x in d], dT.ptr, float(extra[1]), float(extra[2]), oX.ptr, oz.ptr,
                   oh.ptr, res.ptr, ctx=ctx)
     else:
         _abi.call(name, ctx.handle, H, *[x.ptr for x in d], float(extra[0]), oX.ptr, oz.ptr, oh.ptr, res.ptr, ctx=ctx)
-    return oX.download(), oz.download(), oh.download(), res.download()
+    return tuple(_abi.download_many([oX, oz, oh, res]))
 
 
 def recompose_batch(X, z, L, h, T, c_frob=GC_C_FROB, eps_lift=GC_EPS_LIFT, ctx=None):

@@ -294,6 +294,18 @@ class BatchedScanPipeline:
         if dmap is not None:
             dmap._listeners.append(weakref.ref(self))
 
+    def set_scan_map_mode(self, replicated: bool):
+        """Which ranks run the in-scan map update: False (the default, GC_SMAP_OWNER) only the rank
+        holding hypothesis 0, as the reference lets hypothesis 0 alone write the map
+        (backend_node.py:2081-2083), so the other ranks' attached maps stay untouched; True
+        (GC_SMAP_REPLICATED) every rank, each keeping a bit-identical replica."""
+        self._call("gc_pipeline_set_scan_map_mode", 1 if replicated else 0)
+        self._smap_replicated = bool(replicated)
+
+    def scan_map_owner(self) -> bool:
+        """This rank runs the in-scan map update (it holds hypothesis 0, or the mode is replicated)."""
+        return self.h0 == 0 or getattr(self, "_smap_replicated", False)
+
     def _map_colors_stale(self):
         """The attached map's colour fields were written by a host operation (DevicePrimitiveMap
         .colors_stale): the next in-scan update recomputes every slot's colour estimate."""
@@ -303,7 +315,7 @@ class BatchedScanPipeline:
         """After a scan_finish with a map attached the map's colours are the fuse's estimate on every
         slot (the update's colour pass ran if they were stale; LiDAR rows keep them otherwise)."""
         m = getattr(self, "_smap", None)
-        if m is not None and "cam_mass" in m.ptrs:
+        if m is not None and "cam_mass" in m.ptrs and self.scan_map_owner():
             m._tile_cc = [True] * m.n_tiles
 
     def scan_map_pose(self):

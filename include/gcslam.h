@@ -78,7 +78,9 @@ int32_t gc_buffer_alloc(gc_ctx* ctx, uint64_t bytes, void** d_ptr);
 int32_t gc_buffer_free(gc_ctx* ctx, void* d_ptr);
 int32_t gc_ctx_trim(gc_ctx* ctx);
 int32_t gc_ctx_alloc_stats(gc_ctx* ctx, int64_t* h_out6);
-/* Synchronous copies (stream-ordered, then waited). */
+/* Copies on the context's stream. An upload returns once the caller's buffer may be reused: up to
+ * 512 KiB it is copied into the context's pinned staging ring and the DMA is left in flight (later work
+ * on the stream is ordered after it), larger ones are waited for. A download is waited for. */
 int32_t gc_buffer_upload(gc_ctx* ctx, void* d_dst, const void* h_src, uint64_t bytes);
 int32_t gc_buffer_download(gc_ctx* ctx, void* h_dst, const void* d_src, uint64_t bytes);
 int32_t gc_buffer_copy(gc_ctx* ctx, void* d_dst, const void* d_src, uint64_t bytes);
@@ -431,11 +433,17 @@ int32_t gc_pipeline_host_stats(gc_pipeline* p, double* h_out, int32_t reset);
  * world-frame Gaussian row (pose z_t of hypothesis 0 with t_z = 0, covariance Σ_lidar inflated by
  * J Σ_pose Jᵀ) into the slot hashed from its voxel (edge voxel_m), responsibility 1, source
  * LiDAR, timestamp scan_end, scan_seq = scan_count. Σ_lidar is the measurement-IW LiDAR mode of the
- * state the scan started from (before its own IW apply). Every rank runs it from the reduced record,
- * so replicated maps stay bit-identical. The map's device arrays must outlive the attachment;
+ * state the scan started from (before its own IW apply). Which ranks run it is the scan-map mode
+ * (gc_pipeline_set_scan_map_mode): by default only the rank whose shard holds hypothesis 0 (the
+ * reference's owner, backend_node.py:2081-2083); replicated, every rank runs it from the reduced
+ * record and the replicas stay bit-identical. The map's device arrays must outlive the attachment;
  * map == NULL detaches. */
 struct gc_primitive_map; /* defined with the PrimitiveMap entries below */
 int32_t gc_pipeline_attach_primitive_map(gc_pipeline* p, const struct gc_primitive_map* map, double voxel_m);
+#define GC_SMAP_OWNER 0      /* default: the update runs on hypothesis 0's rank only */
+#define GC_SMAP_REPLICATED 1 /* every rank updates its replica of the map */
+/* Not while a scan is pending. A pipeline with world size 1 holds hypothesis 0: both modes update. */
+int32_t gc_pipeline_set_scan_map_mode(gc_pipeline* p, int32_t mode);
 /* The attached map's colour fields were written outside the pipeline (an insert, a merge, a colour
  * upload): the next in-scan update recomputes rgb / colors on every slot, as primitive_map_fuse does
  * on every fuse (primitive_map.py:1097-1105); while they stay current it only touches its rows' slots.
@@ -444,7 +452,8 @@ int32_t gc_pipeline_map_colors_stale(gc_pipeline* p);
 /* Hypothesis 0's [z_t 6, Σ_post pose block 36 (row-major 6x6), ξ_body 6] that the last scan's
  * update used (from the reduced record). */
 int32_t gc_pipeline_get_scan_map_pose(gc_pipeline* p, double* h_out48);
-/* Distinct map slots the last in-scan update touched (synchronises the stream). */
+/* Distinct map slots the last in-scan update touched (synchronises the stream); 0 on a rank that does
+ * not run the update. */
 int32_t gc_pipeline_get_scan_map_count(gc_pipeline* p, int64_t* n_slots);
 
 /* ------------------------------------------------------------------ RCCL communicator */
