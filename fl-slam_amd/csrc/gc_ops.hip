@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 #include "gc_internal.h"
 #include "gc_opsdev.h"
+#include "gc_cond.h"
 
 namespace gc {
 
@@ -104,8 +105,16 @@ __global__ void __launch_bounds__(256) k_op_predict(const double* L, const doubl
   load_mat(Lp, L + (int64_t)k * kNN);
   load_vec(hp, h + (int64_t)k * N, N);
   __syncthreads();
-  wg_predict(Lp, hp, Q, dt, eps_psd, eps_lift, lambda_ou, Lo, ho, mu, cert + (int64_t)k * kPredCertLen, W1, W2,
-             W3, Sx, red, c1, c2, /*full_cert=*/true);
+  // the pipeline's Cholesky-certified projections, then the reference's ConditioningCert of L_pred
+  // (predict.py:183-188) by Sturm counts when the second clamp is inactive (gc_cond.h)
+  double* ck = cert + (int64_t)k * kPredCertLen;
+  wg_predict(Lp, hp, Q, dt, eps_psd, eps_lift, lambda_ou, Lo, ho, mu, ck, W1, W2, W3, Sx, red, c1, c2);
+  if (c2[2] != c2[2]) {  // NaN: the shortcut was taken (wg_predict ends with a barrier)
+    if (t < 64) wave_conditioning<kDZ>(Lo, eps_psd, Sx, c2 + 2);
+    __syncthreads();
+    if (t == 0)
+      for (int q = 2; q < 6; ++q) ck[q] = c2[q];
+  }
   for (int i = t; i < kNN; i += kWG) L_out[(int64_t)k * kNN + i] = Lo[i];
   if (t < N) h_out[(int64_t)k * N + t] = ho[t];
 }
@@ -385,7 +394,7 @@ __global__ void __launch_bounds__(256) k_op_info_fusion(const double* L_pred, co
   const double al = alpha[k];
   for (int i = t; i < kNN; i += kWG) W[i] = L_pred[(int64_t)k * kNN + i] + al * L_ev[(int64_t)k * kNN + i];
   __syncthreads();
-  wg_psd_project(W, Lo, eps_psd, N, Sx, red, c6);
+  wg_psd_project_certified(W, Lo, eps_psd, Sx, red, c6);
   for (int i = t; i < kNN; i += kWG) L_out[(int64_t)k * kNN + i] = Lo[i];
   if (t < N) h_out[(int64_t)k * N + t] = h_pred[(int64_t)k * N + t] + al * h_ev[(int64_t)k * N + t];
   if (t < 6) cert[6 * k + t] = c6[t];
@@ -560,7 +569,7 @@ __global__ void __launch_bounds__(256) k_op_barycenter(int H, const double* L, c
     mom[t] = sm_;
   }
   __syncthreads();
-  wg_psd_project(Lr, Lo, eps_psd, N, Sx, red, c6);
+  wg_psd_project_certified(Lr, Lo, eps_psd, Sx, red, c6);
   for (int i = t; i < kNN; i += kWG) L_out[i] = Lo[i];
   double sp = 0.0, l2 = 0.0, lc = 0.0, la = 0.0;
   for (int k = t; k < H; k += kWG) {

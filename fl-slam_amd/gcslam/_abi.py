@@ -8,6 +8,7 @@ visible, the first call raises — the product path never computes on the CPU.
 from __future__ import annotations
 
 import ctypes as C
+import math
 import os
 import threading
 
@@ -276,7 +277,7 @@ class DeviceArray:
         self.ctx = ctx
         self.shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
         self.dtype = np.dtype(dtype)
-        self.nbytes = int(np.prod(self.shape, dtype=np.int64)) * self.dtype.itemsize
+        self.nbytes = math.prod(self.shape) * self.dtype.itemsize
         self._base = _base  # a view keeps its base alive and never frees
         if _ptr is not None:
             self.ptr = _ptr
@@ -288,7 +289,7 @@ class DeviceArray:
     def view(self, shape, offset_elems: int = 0) -> "DeviceArray":
         """A non-owning view of (part of) this buffer with another shape (no copy)."""
         shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
-        nb = int(np.prod(shape, dtype=np.int64)) * self.dtype.itemsize
+        nb = math.prod(shape) * self.dtype.itemsize
         if offset_elems < 0 or offset_elems * self.dtype.itemsize + nb > self.nbytes:
             raise ValueError(f"view {shape} at {offset_elems} exceeds the buffer {self.shape}")
         return DeviceArray(self.ctx, shape, self.dtype, _base=self, _ptr=self.ptr + offset_elems * self.dtype.itemsize)
@@ -365,7 +366,7 @@ def device_input(ctx: Context, x, dtype=np.float64, shape=None) -> DeviceArray:
         if x.dtype != np.dtype(dtype):
             raise ValueError(f"device array of dtype {x.dtype}, expected {np.dtype(dtype)}")
         if shape is not None and tuple(shape) != x.shape:
-            if int(np.prod(shape)) != int(np.prod(x.shape)):
+            if math.prod(shape) != math.prod(x.shape):
                 raise ValueError(f"device array of shape {x.shape}, expected {tuple(shape)}")
             return x.view(shape)
         return x
@@ -398,7 +399,7 @@ def alloc_many(ctx: Context, specs):
              for s in specs]
     shapes = [tuple(int(v) for v in (sh if isinstance(sh, (tuple, list)) else (sh,))) for sh, _ in specs]
     dts = [np.dtype(dt) for _, dt in specs]
-    nbytes = [int(np.prod(sh, dtype=np.int64)) * dt.itemsize for sh, dt in zip(shapes, dts)]
+    nbytes = [math.prod(sh) * dt.itemsize for sh, dt in zip(shapes, dts)]
     offs, tot = _packed_offsets(nbytes)
     base = DeviceArray(ctx, tot, np.uint8)
     return [DeviceArray(ctx, sh, dt, _base=base, _ptr=base.ptr + o) for sh, dt, o in zip(shapes, dts, offs)]

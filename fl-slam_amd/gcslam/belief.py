@@ -45,13 +45,25 @@ class BeliefGaussianInfo:
         return cls(GC_CHART_ID, anchor_id, np.zeros(6), float(stamp_sec), np.zeros(D_Z),
                    prior_precision * np.eye(D_Z), np.zeros(D_Z), cert)
 
+    def _pose_and_mean(self, eps_lift: float, ctx):
+        """(world pose, mean increment) from one launch, remembered for the belief's current (X, L, h, ε):
+        the node asks a belief for both, several times per scan (the cache key is the arrays' bytes,
+        so an in-place edit of X_anchor / L / h is seen)."""
+        key = (float(eps_lift), self.X_anchor.tobytes(), self.L.tobytes(), self.h.tobytes())
+        c = self.__dict__.get("_pm_cache")
+        if c is None or c[0] != key:
+            p, m = world_pose_batch([self], eps_lift, ctx)
+            c = (key, p[0], m[0])
+            self.__dict__["_pm_cache"] = c
+        return c[1], c[2]
+
     def mean_increment(self, eps_lift: float = GC_EPS_LIFT, ctx=None) -> np.ndarray:
         """δz* = (L + eps_lift I)⁻¹ h (belief.py:373-386)."""
-        return world_pose_batch([self], eps_lift, ctx)[1][0]
+        return self._pose_and_mean(eps_lift, ctx)[1].copy()
 
     def world_pose(self, eps_lift: float = GC_EPS_LIFT, ctx=None) -> np.ndarray:
         """X_anchor ∘ Exp(δz*[0:6]) (belief.py:408-425)."""
-        return world_pose_batch([self], eps_lift, ctx)[0][0]
+        return self._pose_and_mean(eps_lift, ctx)[0].copy()
 
 
 def stack(beliefs: List[BeliefGaussianInfo]) -> Tuple[np.ndarray, np.ndarray, np.ndarray, np.ndarray]:

@@ -24,6 +24,7 @@ import numpy as np
 from . import _abi
 from . import ops
 from .ops import se3 as _se3
+from .ops.imu_preintegration import imu_meas_iw_suffstats_batch
 from .belief import BeliefGaussianInfo
 from .constants import (D_Z, GC_ALPHA_MAX, GC_ALPHA_MIN, GC_CHART_ID, GC_EPS_MASS, GC_GRAVITY_W,
                         GC_TAU_SOFT_ASSIGN, POWER_BETA_EXC_C, POWER_BETA_MIN, POWER_BETA_Z_C, T_BASE_LIDAR)
@@ -130,11 +131,11 @@ class DropinNode:
         wv = w_int * (st > 0.0)
         wnv = wv / (np.sum(wv) + GC_EPS_MASS)
         omega_avg = wnv @ (scan["imu_gyro"] - bg[None, :])
+        # imu_gyro_meas_iw_suffstats_from_avg_rate_jax and imu_accel_meas_iw_suffstats_from_gravity_dir_jax
+        # (measurement_noise_iw_jax.py:131-218) share the window: both from one launch
         dPsi_meas = np.zeros((3, 3, 3))
-        dPsi_meas[0] = ops.imu_gyro_meas_iw_suffstats_from_avg_rate_jax(scan["imu_gyro"], wv, bg, omega_avg, dt_imu,
-                                                                        ctx=ctx)[0, 0]
-        dPsi_meas[1] = ops.imu_accel_meas_iw_suffstats_from_gravity_dir_jax(pose0[3:6], scan["imu_accel"], wv, ba,
-                                                                           dt_imu, ctx=ctx)[0, 1]
+        dPsi_meas[0:2] = imu_meas_iw_suffstats_batch(scan["imu_gyro"], scan["imu_accel"], wv, bg, ba, omega_avg,
+                                                     pose0[3:6], dt_imu, ctx=ctx)[0]
         # a4 -> a6 on the device-resident point arrays
         dsk, c_dsk, _ = ops.deskew_constant_twist(bud.points, bud.timestamps, bud.weights, scan["scan_start"],
                                                   scan["scan_end"], xi, ess_imu, GC_CHART_ID, b_prev.anchor_id,

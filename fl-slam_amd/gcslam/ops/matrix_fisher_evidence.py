@@ -9,7 +9,7 @@ from typing import Tuple
 import numpy as np
 
 from .. import _abi
-from ..belief import BeliefGaussianInfo, world_pose_batch
+from ..belief import BeliefGaussianInfo
 from ..certificates import (CertBundle, ConditioningCert, ExpectedEffect, InfluenceCert, MismatchCert)
 from ..constants import GC_EPS_LIFT, GC_EPS_MASS, GC_EPS_PSD
 
@@ -87,7 +87,7 @@ def matrix_fisher_rotation_evidence(belief_pred: BeliefGaussianInfo, scan_s_dir,
                                     map_S_dir, map_S_dir_scatter, map_N_dir, eps_psd: float = GC_EPS_PSD,
                                     eps_lift: float = GC_EPS_LIFT, eps_mass: float = GC_EPS_MASS, ctx=None
                                     ) -> Tuple[MatrixFisherResult, CertBundle, ExpectedEffect]:
-    pose = world_pose_batch([belief_pred], eps_lift, ctx)[0]
+    pose = belief_pred.world_pose(eps_lift, ctx)[None]
     o = matrix_fisher_batch(pose, np.asarray(scan_s_dir)[None], np.asarray(scan_N)[None],
                             np.asarray(scan_S_dir_scatter)[None], map_S_dir, map_N_dir, map_S_dir_scatter, eps_psd,
                             eps_mass, ctx)[0]
@@ -135,7 +135,7 @@ def planar_translation_evidence(belief_pred: BeliefGaussianInfo, scan_p_bar, sca
                                 eps_psd: float = GC_EPS_PSD, eps_lift: float = GC_EPS_LIFT,
                                 eps_mass: float = GC_EPS_MASS, ctx=None
                                 ) -> Tuple[PlanarTranslationResult, CertBundle, ExpectedEffect]:
-    pose = world_pose_batch([belief_pred], eps_lift, ctx)[0]
+    pose = belief_pred.world_pose(eps_lift, ctx)[None]
     o = planar_translation_batch(pose, np.asarray(R_hat)[None], np.asarray(scan_p_bar)[None],
                                  np.asarray(scan_Sigma_p)[None], np.asarray(scan_N)[None], map_centroid, map_Sigma_c,
                                  map_N_pos, map_S_dir_scatter, map_N_dir, eps_psd, eps_mass, ctx)[0]

@@ -57,6 +57,9 @@ def test_dropin_chain_matches_oracle(ctx):
             assert np.max(np.abs(r["xi"] - o["xi_body"])) <= 1e-9, (k, i)
         assert np.max(np.abs(node.combined.belief_out.L - comb["L"])) <= 1e-8 * np.max(np.abs(comb["L"]))
         assert np.max(np.abs(node.pn.Psi - st.Psi_proc)) <= 1e-7 * np.max(np.abs(st.Psi_proc)) + 1e-18
+        # the measurement-IW state from the gyro / accel window statistics of every hypothesis
+        assert np.max(np.abs(node.mn.Psi - st.Psi_meas)) <= 1e-9 * np.max(np.abs(st.Psi_meas)), k
+        assert np.max(np.abs(node.mn.nu - st.nu_meas)) <= 1e-12 * np.max(np.abs(st.nu_meas)), k
         node.map = _binmap(st.map)
 
 

@@ -270,3 +270,50 @@ def test_hypothesis_barycenter(ctx, K):
     assert abs(cert.support.support_frac - ref["support_frac"]) < 1e-15
     with pytest.raises(ValueError):
         hypothesis_barycenter_projection(bs, w, K_HYP=K + 1, ctx=ctx)
+
+
+def _cond_fields(dev4, ref4, what):
+    """ConditioningCert [eig_min, eig_max, cond, near_null_count] of a projection certified by the
+    Cholesky shortcut + Sturm counts (gc_cond.h) against the oracle's eigh: eig_max 1e-10 relative,
+    eig_min within 1e-12 of eig_max (the absolute accuracy of eigh), cond of the device's own extremes,
+    the near-null count exact."""
+    dev4, ref4 = np.asarray(dev4, np.float64), np.asarray(ref4, np.float64)
+    assert abs(dev4[1] - ref4[1]) <= 1e-10 * ref4[1], (what, dev4, ref4)
+    assert abs(dev4[0] - ref4[0]) <= 1e-12 * ref4[1], (what, dev4, ref4)
+    assert abs(dev4[2] - dev4[1] / dev4[0]) <= 1e-15 * dev4[2], (what, dev4)
+    if ref4[0] > 1e-5 * ref4[1]:
+        assert abs(dev4[2] - ref4[2]) <= 1e-6 * ref4[2], (what, dev4, ref4)
+    assert dev4[3] == ref4[3], (what, dev4, ref4)
+
+
+def test_single_operator_certificates_on_the_shortcut(ctx):
+    """predict_diffusion, info_fusion_additive and hypothesis_barycenter_projection with inactive clamps
+    (SPD operands): the projections take the Cholesky-certified shortcut and the ConditioningCert comes
+    from Sturm counts (no Jacobi sweep); every cert field against the oracle (projection delta 0 here vs
+    the reference's rounding of V diag(λ) Vᵀ, ~1e-16 of the spectrum)."""
+    from gcslam.ops import hypothesis_barycenter_projection, info_fusion_additive, predict_diffusion
+    rng = np.random.default_rng(31)
+    for k in range(3):
+        b = _belief(rng, k)
+        Q = _spd(rng, 1e-3)
+        out, cert, _ = predict_diffusion(b, Q, 0.1, ctx=ctx)
+        ref, rc = O.predict_diffusion(_ob(b), Q, 0.1)
+        c = cert.conditioning
+        _cond_fields([c.eig_min, c.eig_max, c.cond, c.near_null_count], rc["cond"], f"predict {k}")
+        assert abs(cert.influence.psd_projection_delta - rc["psd_delta"]) <= 1e-12 * np.max(np.abs(ref.L))
+        Le, he = _spd(rng, 3.0), rng.normal(size=D)
+        post, cf, _ = info_fusion_additive(b, Le, he, 0.7, ctx=ctx)
+        rL, rh, r6 = O.info_fusion_additive(b.L, b.h, Le, he, 0.7)
+        c = cf.conditioning
+        _cond_fields([c.eig_min, c.eig_max, c.cond, c.near_null_count], r6[2:6], f"fusion {k}")
+        assert cf.influence.psd_projection_delta <= 1e-12 * r6[3] and abs(r6[0]) <= 1e-12 * r6[3]
+        assert _rel(post.L, rL) < 1e-12
+    K = 5
+    bs = [_belief(rng, k) for k in range(K)]
+    w = rng.uniform(0.1, 1, K)
+    res, cb, _ = hypothesis_barycenter_projection(bs, w, K_HYP=K, HYP_WEIGHT_FLOOR=0.01 / K, ctx=ctx)
+    ref = O.hypothesis_barycenter(np.stack([x.L for x in bs]), np.stack([x.h for x in bs]),
+                                  np.stack([x.z_lin for x in bs]), w, 0.01 / K)
+    c = cb.conditioning
+    _cond_fields([c.eig_min, c.eig_max, c.cond, c.near_null_count], ref["psd_cert"][2:6], "barycenter")
+    assert _rel(res.belief_out.L, ref["L"]) < 1e-12

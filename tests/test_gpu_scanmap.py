@@ -124,6 +124,7 @@ def test_scan_map_update_replicated_across_shards(ctx):
     full.attach_primitive_map(maps[0], 0.1)
     for p, m in zip(shards, maps[1:]):
         p.attach_primitive_map(m, 0.1)
+        p.set_scan_map_mode(replicated=True)
     for k, s in enumerate(case["scans"]):
         full.stage_scan(0, s)
         full.run_scan(0, s, k)
@@ -139,6 +140,40 @@ def test_scan_map_update_replicated_across_shards(ctx):
             got = m.download()
             for f in ref:
                 assert np.array_equal(got[f], ref[f]), f"scan{k} {f}"
+
+
+def test_scan_map_update_runs_on_the_owner_rank_only(ctx):
+    """The default scan-map mode (GC_SMAP_OWNER): of two shards (4 + 4 of 8), only hypothesis 0's
+    rank runs the update (backend_node.py:2081-2083); its map ends bit-identical to the unsharded
+    pipeline's, the other rank's map is left exactly as uploaded and reports no touched slots, and the
+    other rank's slot rotation (no map update as the slot's last reader) stays usable."""
+    case = cases.build(H=8, n_az=1024, n_scans=3, io="computed")
+    cap = case["n"]
+    full = _pipeline(case, ctx, 8, cap, True)
+    shards = [_pipeline(case, ctx, 8, cap, True, rank=r, world=2, geometry_hyps=8) for r in range(2)]
+    maps = [_map(ctx, 1 << 14, 3) for _ in range(3)]
+    untouched = maps[2].download()
+    full.attach_primitive_map(maps[0], 0.1)
+    for p, m in zip(shards, maps[1:]):
+        p.attach_primitive_map(m, 0.1)
+    assert shards[0].scan_map_owner() and not shards[1].scan_map_owner()
+    for k, s in enumerate(case["scans"]):
+        full.stage_scan(k % 2, s)
+        full.run_scan(k % 2, s, k)
+        for p in shards:
+            p.stage_scan(k % 2, s)
+            p.run_scan_local(k % 2, s, k)
+        recs = np.stack([p.partial() for p in shards])
+        for p in shards:
+            p.finish_scan(recs)
+        ref, own, other = maps[0].download(), maps[1].download(), maps[2].download()
+        for f in ref:
+            assert np.array_equal(own[f], ref[f]), f"scan{k} owner {f}"
+            assert np.array_equal(other[f], untouched[f]), f"scan{k} non-owner {f} changed"
+        assert shards[0].scan_map_count() == full.scan_map_count() > 0
+        assert shards[1].scan_map_count() == 0
+    for p in [full] + shards:
+        p.close()
 
 
 def test_first_pipelines_map_read_after_a_later_pipelines_finish(ctx):
