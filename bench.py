@@ -56,7 +56,9 @@ def parse():
                     help="run only the contract-pair roofline leg (PMC traffic passes, tools/pmc_traffic.sh)")
     ap.add_argument("--map-only", action="store_true",
                     help="run only the C5 PrimitiveMap fuse leg (PMC passes, tools/pmc_fuse.sh)")
-    ap.add_argument("--c5-only", action="store_true", help="run only the C5 pipeline leg (PMC passes)")
+    ap.add_argument("--c5-only", action="store_true", help="run only the C5 pipeline legs (PMC passes)")
+    ap.add_argument("--c5-shard-only", action="store_true",
+                    help="run only the C5 rank-shard leg (128 of 1024 hypotheses, with / without the map update)")
     ap.add_argument("--no-dropin", action="store_true", help="skip the per-operator drop-in leg")
     ap.add_argument("--dropin-only", action="store_true", help="run only the per-operator drop-in leg")
     ap.add_argument("--map-layout", choices=("packed", "fields"), default="packed",
@@ -227,6 +229,9 @@ def main():
     if args.c5_only:
         print(json.dumps({"c5": c5_leg(ctx, _abi, args), "c5_dense": c5_leg(ctx, _abi, args, cap=131072)}),
               flush=True)
+        return
+    if args.c5_shard_only:
+        print(json.dumps({"c5_shard": c5_shard_leg(ctx, _abi, args)}), flush=True)
         return
     if args.roofline_only:
         from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
@@ -400,6 +405,7 @@ def main():
     if dist.rank == 0 and dist.world == 1 and not args.no_c5:
         out["c5"] = c5_leg(ctx, _abi, args)
         out["c5_dense"] = c5_leg(ctx, _abi, args, cap=131072)
+        out["c5_shard"] = c5_shard_leg(ctx, _abi, args)
     if dist.rank == 0 and dist.world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_leg(args.n_az, H_total, args.cpu_budget_s)
     if dist.rank == 0:
@@ -544,11 +550,14 @@ def fused_roofline_leg(ctx, _abi, s, B, n, H, bins, origin, reps=10, warm=10):
             "kernel": "k_bins_fused + k_bins_finalize (gc_scan_bins_fused)", "hypotheses": H, "points": n, "bins": B}
 
 
-def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5, m_slots=1 << 20, voxel=0.1):
+def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5, m_slots=1 << 20, voxel=0.1,
+           map_update=True):
     """C5 on one GPU: 131,072-point scans budgeted to 65,536 (stride 2) x 1024
     hypotheses through the full batched pipeline, each scan staged from host memory and fused into
     a resident 1M-slot PrimitiveMap by the in-scan map update (csrc/gc_scanmap.hip). BASELINE.json
-    quotes C5 on 8 GPUs; this is one GPU's whole-job throughput at the full 1024 hypotheses."""
+    quotes C5 on 8 GPUs; this is one GPU's whole-job throughput at the full 1024 hypotheses.
+    H=128: one rank's shard of C5 on 8 GPUs; map_update=False times it without the update (the
+    non-owner ranks: only hypothesis 0's rank runs it, include/gcslam.h GC_SMAP_OWNER)."""
     from gcslam.constants import GC_B_BINS, T_BASE_LIDAR
     from gcslam.ops.binning import create_fibonacci_atlas
     from gcslam.pipeline import BatchedScanPipeline, PipelineConfig, iw_meas_prior, iw_process_prior
@@ -564,8 +573,9 @@ def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5, m_
     pipe.set_iw(*iw_process_prior(), *iw_meas_prior())
     pipe.set_map(warmup_map_record(ctx, _abi, make_scan(0, n_az=n_az), n_in, B, create_fibonacci_atlas(B).dirs,
                                    np.asarray(T_BASE_LIDAR[:3])))
-    dm = primitive_map_1m(ctx, m_slots)
-    pipe.attach_primitive_map(dm, voxel)  # the in-scan map update runs inside every timed scan
+    if map_update:
+        dm = primitive_map_1m(ctx, m_slots)
+        pipe.attach_primitive_map(dm, voxel)  # the in-scan map update runs inside every timed scan
 
     pipe.stage_scan(0, scans[0])
 
@@ -581,15 +591,30 @@ def c5_leg(ctx, _abi, args, H=1024, n_az=8192, cap=65536, steps=10, warmup=5, m_
         step(warmup + i)
     ctx.sync()
     dt = (time.perf_counter() - t0) / steps
-    touched = pipe.scan_map_count()
+    touched = pipe.scan_map_count() if map_update else 0
     pipe.close()
     stride = -(-n_in // cap)
+    upd = ("the in-scan PrimitiveMap update (%d rows into a %d-slot map, voxel %.2f m)" % (cap, m_slots, voxel)
+           if map_update else "no map update (a non-owner rank)")
     return {"workload": "C5 shape on 1 GPU: %d-point scans (staged every step), budget cap %d (%s), %d "
-                        "hypotheses, full pipeline + the in-scan PrimitiveMap update (%d rows into a %d-slot map, "
-                        "voxel %.2f m)" % (n_in, cap, "dense: every point" if stride == 1 else "stride %d" % stride,
-                                           H, cap, m_slots, voxel),
+                        "hypotheses, full pipeline + %s" % (n_in, cap, "dense: every point" if stride == 1 else
+                                                            "stride %d" % stride, H, upd),
             "ms_per_scan": 1e3 * dt, "scans_per_s": 1.0 / dt, "steps": steps, "warmup": warmup,
             "map_slots_touched_last_scan": touched}
+
+
+def c5_shard_leg(ctx, _abi, args, H=128):
+    """One rank's shard of C5 on 8 GPUs (1024 / 8 = 128 hypotheses, 131,072-point scans, stride 2): the
+    owner rank's step (hypothesis 0's rank: the in-scan map update on its side stream) and a non-owner
+    rank's (no update, GC_SMAP_OWNER). The exchange is not in it (no communicator on one GPU)."""
+    own = c5_leg(ctx, _abi, args, H=H, steps=20, warmup=10)
+    other = c5_leg(ctx, _abi, args, H=H, steps=20, warmup=10, map_update=False)
+    return {"hypotheses": H, "of": 1024, "owner_ms_per_scan": own["ms_per_scan"],
+            "non_owner_ms_per_scan": other["ms_per_scan"],
+            "update_cost_ms": own["ms_per_scan"] - other["ms_per_scan"],
+            "map_slots_touched_last_scan": own["map_slots_touched_last_scan"],
+            "note": "the scan rate of C5 on 8 GPUs is bounded by the slower of the two (max over ranks) plus the "
+                    "per-scan all-gather"}
 
 
 def dropin_leg(ctx, _abi, K=4, cap=8192, n_az=4096, warm=3, scans=10):
