@@ -700,12 +700,12 @@ __global__ void __launch_bounds__(256) k_combine_final(PipeDev P, ScanArgs S) {
     }
     __syncthreads();
     GC_PHASE_WG(P, 22, 2);
-    // process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count)
-    wg_iw_proc_apply(P.nu_proc, P.Psi_proc, Ri, Ri + (kPDNUP - kPDPSIP), S.w_process, P.eps_psd, P.nu_max, P.nu_proc,
-                     P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab, P.iwraw);
+    // process-noise IW apply (inverse_wishart_jax.py:126-185), weight min(1, scan_count), and Q of the
+    // updated state (:35-68) formed beside it from the apply's own blocks (wg_iw_proc_apply<true>)
+    wg_iw_proc_apply<true>(P.nu_proc, P.Psi_proc, Ri, Ri + (kPDNUP - kPDPSIP), S.w_process, P.eps_psd, P.nu_max,
+                           P.nu_proc, P.Psi_proc, P.iw_cert, Qs, blk, blkp, Sx, red, c6, tab, P.iwraw, P.Q, Qp, Lr);
     GC_PHASE_WG(P, 23, 2);
     GC_PHASE_WG(P, 24, 2);
-    iw_Q_wg(P, Qs, Qp, Sx, red);
     GC_PHASE_WG(P, 25, 2);
     return;
   }

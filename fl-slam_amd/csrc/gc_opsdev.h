@@ -567,16 +567,34 @@ GC_DEV double nu_project(double nu_raw, double dim, double nu_max) {
 // Outputs may alias the inputs (all reads precede the writes). cert (thread 0) =
 // [Σ_b psd Δ_b, Σ_b |ν_b' − ν_b,raw|]. Scratch: Qs 216, blk 36, blkp 36, Sx 2*36+24, red 16,
 // c6 8, tab 32.
+// den_b of process_noise_state_to_Q_jax (inverse_wishart_jax.py:35-68): softplus⁺(ν_b − d_b − 1)
+GC_DEV double iw_q_den(double nu_b, int b) { return softplus(50.0 * (nu_b - kIwBlockDim[b] - 1.0)) / 50.0 + 1e-12; }
+
+// WITH_Q: the apply followed by process_noise_state_to_Q_jax of the updated state (wg_iw_Q's result,
+// bit for bit) with Q's blocks formed from the apply's own results instead of a second pass over the
+// state: each 3x3 / 1x1 block's thread projects Ψ'_b / den_b right after forming Ψ'_b, and the 6x6
+// block's Cholesky certificate of Ψ'_6 / den_6 − εI runs on wave 2 beside the apply's own certificate
+// (wg_psd_project_fast's side slot). That speculation holds when the apply's 6x6 projection takes its
+// shortcut (then Ψ'_6 = sym(M_6) exactly); otherwise, or if its own Cholesky fails, the 6x6 block is
+// projected after the apply as wg_iw_Q does. Q_out: global 22x22; Qp: NN doubles of LDS; X: 2 x 36 + 8.
+template <bool WITH_Q = false>
 GC_DEV void wg_iw_proc_apply(const double* nu, const double* Psi, const double* dPsi, const double* dnu, double w,
                              double eps_psd, double nu_max, double* nu_out, double* Psi_out, double* cert,
                              double* Qs, double* blk, double* blkp, double* Sx, double* red, double* c6,
-                             double* tab, double* raw_out = nullptr) {
+                             double* tab, double* raw_out = nullptr, double* Q_out = nullptr, double* Qp = nullptr,
+                             double* X = nullptr) {
   const int t = threadIdx.x;
+  if constexpr (WITH_Q) {
+    for (int idx = t; idx < kNN; idx += kWG) Qp[idx] = 0.0;
+    __syncthreads();
+  }
+  double nn_t = 0.0;
   if (t < 7) {
     const double nr = kIwRhoProc[t] * nu[t] + w * dnu[t];
     const double nn = nu_project(nr, kIwBlockDim[t], nu_max);
     tab[16 + t] = fabs(nn - nr);
     tab[24 + t] = nn;
+    nn_t = nn;
   }
   if (t < 6) {
     // 3x3 blocks (t < 5) and the 1x1 block (t = 5) in registers. The reference projects each masked
@@ -607,13 +625,61 @@ GC_DEV void wg_iw_proc_apply(const double* nu, const double* Psi, const double* 
       const int i = k / 6, j = k % 6;
       Qs[t * 36 + k] = (i < 3 && j < 3) ? Pp[3 * i + j] : ((i == j) ? eps_psd : 0.0);
     }
+    if constexpr (WITH_Q) {  // Q's block t from Ψ'_t in registers (wg_iw_Q's arithmetic)
+      const int s0 = kIwBlockStart[t];
+      const double dn = iw_q_den(nn_t, t);
+      if (kIwBlockDim[t] == 1) {
+        Qp[s0 * kDZ + s0] = fmax(Pp[0] / dn, eps_psd);
+      } else {
+        double A2[9], P2[9];
+        for (int k = 0; k < 9; ++k) A2[k] = Pp[k] / dn;
+        psd_project3_fast(A2, eps_psd, P2, nullptr);
+        for (int i = 0; i < 3; ++i)
+          for (int j = 0; j < 3; ++j) Qp[(s0 + i) * kDZ + (s0 + j)] = P2[3 * i + j];
+      }
+    }
   }
   if (t < 36) {
     blk[t] = kIwRhoProc[6] * Psi[6 * 36 + t] + w * dPsi[6 * 36 + t];
     if (raw_out) raw_out[6 * 36 + t] = blk[t];
   }
   __syncthreads();
-  wg_psd_project_fast(blk, blkp, eps_psd, 6, Sx, red, c6);
+  if constexpr (WITH_Q) {
+    const double d6 = iw_q_den(tab[24 + 6], 6);
+    // wave 2: X = sym(M_6) / den_6 (= Ψ'_6 / den_6 under the shortcut) and the Cholesky of X − εI formed as
+    // wg_psd_project_fast forms it (X is exactly symmetric, so its symmetrisation is X itself)
+    const auto spec = [&]() {
+      const int l = threadIdx.x & 63;
+      if (l < 36) {
+        const int i = l / 6, j = l % 6;
+        X[l] = (0.5 * (blk[6 * i + j] + blk[6 * j + i])) / d6;
+      }
+      wave_lds_sync();
+      if (l < 36) {
+        const int i = l / 6, j = l % 6;
+        X[36 + l] = 0.5 * (X[6 * i + j] + X[6 * j + i]) - ((i == j) ? eps_psd : 0.0);
+      }
+      wave_lds_sync();
+      const bool ok = wave0_chol<8, true>(X + 36, 6);
+      if (l == 0) X[72] = ok ? 0.0 : 1.0;
+    };
+    wg_psd_project_fast(blk, blkp, eps_psd, 6, Sx, red, c6, spec);
+    const bool shortcut = c6[2] != c6[2];  // the apply's projection is sym(M_6) (eigen fields not computed)
+    const bool q_ok = shortcut && X[72] == 0.0;
+    __syncthreads();
+    if (q_ok) {
+      if (t < 36) Qp[(16 + t / 6) * kDZ + 16 + t % 6] = X[t];
+    } else {  // wg_iw_Q's 6x6 form on the apply's result
+      if (t < 36) X[t] = blkp[t] / d6;
+      __syncthreads();
+      wg_psd_project_fast(X, X + 36, eps_psd, 6, Sx, red, nullptr);
+      if (t < 36) Qp[(16 + t / 6) * kDZ + 16 + t % 6] = X[36 + t];
+    }
+    __syncthreads();
+    for (int idx = t; idx < kNN; idx += kWG) Q_out[idx] = Qp[idx];
+  } else {
+    wg_psd_project_fast(blk, blkp, eps_psd, 6, Sx, red, c6);
+  }
   for (int k = t; k < 6 * 36; k += kWG) Psi_out[k] = Qs[k];
   if (t < 36) Psi_out[6 * 36 + t] = blkp[t];
   if (t < 7) nu_out[t] = tab[24 + t];
@@ -666,7 +732,7 @@ GC_DEV void wg_iw_Q(const double* nu, const double* Psi, double eps_psd, double*
   const int t = threadIdx.x, n = kDZ;
   for (int idx = t; idx < kNN; idx += kWG) Qp[idx] = 0.0;
   __syncthreads();
-  auto den = [&](int b) { return softplus(50.0 * (nu[b] - kIwBlockDim[b] - 1.0)) / 50.0 + 1e-12; };
+  auto den = [&](int b) { return iw_q_den(nu[b], b); };
   if (t < 6) {
     const int b = t, d = kIwBlockDim[b], s0 = kIwBlockStart[b];
     const double dn = den(b);
