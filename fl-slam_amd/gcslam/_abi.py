@@ -217,8 +217,16 @@ def check(rc: int, ctx=None):
     raise RuntimeError(msg)
 
 
+_fns = {}
+
+
 def call(name: str, *args, ctx=None):
-    check(getattr(lib(), name)(*args), ctx)
+    f = _fns.get(name)
+    if f is None:
+        f = _fns[name] = getattr(lib(), name)
+    rc = f(*args)
+    if rc != GC_OK:
+        check(rc, ctx)
 
 
 def device_count() -> int:
@@ -275,15 +283,17 @@ class DeviceArray:
 
     def __init__(self, ctx: Context, shape, dtype=np.float64, _base=None, _ptr=None):
         self.ctx = ctx
-        self.shape = tuple(int(s) for s in (shape if isinstance(shape, (tuple, list)) else (shape,)))
-        self.dtype = np.dtype(dtype)
+        self.shape = tuple(map(int, shape)) if isinstance(shape, (tuple, list)) else (int(shape),)
+        self.dtype = dtype if isinstance(dtype, np.dtype) else np.dtype(dtype)
         self.nbytes = math.prod(self.shape) * self.dtype.itemsize
         self._base = _base  # a view keeps its base alive and never frees
         if _ptr is not None:
             self.ptr = _ptr
             return
         p = _vp()
-        check(lib().gc_buffer_alloc(ctx.handle, max(self.nbytes, 16), C.byref(p)), ctx)
+        rc = lib().gc_buffer_alloc(ctx.handle, max(self.nbytes, 16), C.byref(p))
+        if rc != GC_OK:
+            check(rc, ctx)
         self.ptr = p.value
 
     def view(self, shape, offset_elems: int = 0) -> "DeviceArray":
