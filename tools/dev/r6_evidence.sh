@@ -8,5 +8,5 @@ bash tools/round_profile.sh $tag || exit $?
 o=gpurun_out/$tag
 timeout -k 10 200 python3 bench.py --hyps 32 --steps 400 --warmup 50 --no-cpu --no-roofline --no-map --no-c5 --no-dropin > $o/bench_h32.json 2> $o/bench_h32.err || { tail -5 $o/bench_h32.err; exit 1; }
 python3 tools/summ.py $o/bench_h32.json
-timeout -k 10 200 python3 bench.py --hyps 1 --steps 400 --warmup 50 --no-cpu --no-roofline --no-map --no-c5 --no-dropin > $o/bench_h1.json 2> $o/bench_h1.err || { tail -5 $o/bench_h1.err; exit 1; }
+timeout -k 10 300 python3 bench.py --hyps 1 --steps 400 --warmup 50 --no-roofline --no-map --no-c5 --no-dropin > $o/bench_h1.json 2> $o/bench_h1.err || { tail -5 $o/bench_h1.err; exit 1; }
 python3 tools/summ.py $o/bench_h1.json
