@@ -53,6 +53,39 @@ GC_DEV double group16_sum(double v) {
   v += dpp_f64<kDppMirror>(v);
   return v;
 }
+// The same 16-lane sum for the issue-bound fused bins block, its exchanges on the LDS pipe: each
+// ds_swizzle (bit mode, lane ^ XOR inside 32-lane halves) moves one 32-bit half of the partner's
+// value through the LDS crossbar without touching memory, so a round costs the SIMD one f64 add
+// instead of two DPP moves and an add (the block's VALU slots are its bound; the LDS pipe runs
+// beside them). xor butterfly: lanes a and a ^ k add the same two partials, so all 16 lanes still
+// end with the bit-identical total. GC_ZSUM: 0 = DPP (group16_sum), 1 = four swizzle rounds, 2 = two
+// DPP rounds then two swizzle rounds.
+#ifndef GC_ZSUM
+#define GC_ZSUM 0
+#endif
+template <int XOR>
+GC_DEV double swz_f64(double v) {
+  constexpr int pat = (XOR << 10) | 0x1F;  // and_mask 0x1F, or_mask 0, xor_mask XOR
+  const int lo = __builtin_amdgcn_ds_swizzle(__double2loint(v), pat);
+  const int hi = __builtin_amdgcn_ds_swizzle(__double2hiint(v), pat);
+  return __hiloint2double(hi, lo);
+}
+GC_DEV double group16_sum_bins(double v) {
+#if GC_ZSUM == 0
+  return group16_sum(v);
+#else
+#if GC_ZSUM == 2
+  v += dpp_f64<kDppXor1>(v);
+  v += dpp_f64<kDppXor2>(v);
+#else
+  v += swz_f64<1>(v);
+  v += swz_f64<2>(v);
+#endif
+  v += swz_f64<4>(v);
+  v += swz_f64<8>(v);
+  return v;
+#endif
+}
 GC_DEV double group16_max(double v) {
   v = fmax(v, dpp_f64<kDppXor1>(v));
   v = fmax(v, dpp_f64<kDppXor2>(v));
@@ -994,17 +1027,43 @@ struct FusedArgs {
   int iters_t;
 };
 constexpr int kFusedNS = NF_BASE + 4;  // feature slab rows: 19 features + d(3) + valid flag
-// dynamic LDS of a fused workgroup (doubles): 4 wave slabs | exp table | scaled bins | epilogue
-// reduction (aliases the slabs)
+// Point-major softmax (GC_BINS_LP = 1, B <= 48; off: the A/B in profiles/r06/ab_bins_point_major.txt
+// measured it neutral at H = 256 and 10 % slower at H = 32). The exp / softmax half runs with a quad of
+// lanes per point (12 of its bins per lane, the quad's Z by two DPP rounds instead of the 16-lane
+// butterfly), the responsibilities reach the matrix-core layout through a per-wave LDS slab of 16 points
+// x B, and the moment half is bins_task's. ~14 % fewer VALU slots per block, but a slab round trip and
+// a direction shuffle per 16 points on the chain. Per wave: 18 feature rows (the trace-complement
+// feature DF has no row) of kFusedFS and the 16-row slab of stride 16 BPL + 2; the table after the four
+// waves; no scaled-bins block (each lane holds its 12 bin directions).
+#ifndef GC_BINS_LP
+#define GC_BINS_LP 0
+#endif
+__host__ __device__ constexpr bool bins_lp(int BPL) { return GC_BINS_LP && BPL <= 3; }
+constexpr int kLpFRows = NF_BASE - 1;
+__host__ __device__ constexpr int lp_es(int BPL) { return 16 * BPL + 2; }
+__host__ __device__ constexpr int lp_wave_doubles(int BPL) { return kLpFRows * kFusedFS + 16 * lp_es(BPL); }
+__host__ __device__ constexpr int fused_tab_offset(int BPL) {
+  return bins_lp(BPL) ? 4 * lp_wave_doubles(BPL) : 4 * kFusedFS * kFusedNS;
+}
+// dynamic LDS of a fused workgroup (doubles): 4 wave slabs | exp table | scaled bins (not LP) | epilogue
+// reduction (aliases the slabs). LP at B = 48: 80,000 B, two workgroups per CU.
 __host__ __device__ inline size_t fused_lds_doubles(int B) {
-  const size_t a = 4 * (size_t)kFusedFS * kFusedNS + kExpTab2 + 192, b = 4 * (size_t)B * NF_BASE + 12;
+  const int bpl = (B + 15) / 16;
+  const size_t a = (size_t)fused_tab_offset(bpl) + kExpTab2 + (bins_lp(bpl) ? 0 : 192),
+               b = 4 * (size_t)B * NF_BASE + 12;
   return a > b ? a : b;
 }
+static_assert(4 * lp_wave_doubles(3) + kExpTab2 + 1 <= 81920 / 8, "LP bins workgroup beyond half a CU's LDS");
 
+template <int BPL>
 GC_DEV void bins_prologue(const FusedArgs& A, double* lds) {
-  double* Tx = lds + 4 * kFusedFS * kFusedNS;
-  double* Lb = Tx + kExpTab2;  // bin directions pre-scaled by 2048/(τ ln2) (x, y, z rows of 64)
+  double* Tx = lds + fused_tab_offset(BPL);
   exp_table2_load(Tx);
+  if constexpr (bins_lp(BPL)) {
+    __syncthreads();
+    return;
+  }
+  double* Lb = Tx + kExpTab2;  // bin directions pre-scaled by 2048/(τ ln2) (x, y, z rows of 64)
   const double ysc = A.inv_tau * kTab2OverLn2;
   if (threadIdx.x < 64) {
     const int b = threadIdx.x;
@@ -1051,6 +1110,217 @@ GC_DEV void task_operands(const FusedArgs& A, int h, int64_t c, TaskAhead& ta) {
   ta.valid = true;
 }
 
+// bins_task in the point-major softmax form (bins_lp): the same task, records and ticket protocol.
+// Per iteration of 64 points per wave:
+//  phase A (lane = point): budget selection, deskew, direction, window weight and the 18 features,
+//     as bins_task;
+//  four sub-iterations of 16 points, lane = (point l >> 2, bin quarter l & 3):
+//   B1: the lane's 12 logits against its bin directions (registers), exps (the 2048-entry table), the
+//       quad's Z by two DPP rounds, 1/Z by one Newton step, Σ R x and max R, r = e / Z into the slab;
+//   B2 (lanes = 4 points x 16 bins): the sub-iteration's 4 steps of BPL MFMAs (A = r of point 4s + g,
+//       bin 16 j + l, from the slab; B = feature l of that point) and the two VALU features.
+template <int BPL, bool FULL, bool PRE>
+GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, double* rec, unsigned* ctr,
+                         unsigned* task_slot, TaskAhead* ahead, unsigned T, int Hl, unsigned* late_next) {
+  typedef double dvec2 __attribute__((ext_vector_type(2)));
+  constexpr int NF = NF_BASE;
+  constexpr int DF = 9;
+  constexpr int NX = NF - 16 - 1;
+  constexpr int NB = 16 * BPL, ES = lp_es(BPL), WD = lp_wave_doubles(BPL);
+  constexpr unsigned TAB = 8u * (unsigned)fused_tab_offset(BPL);
+  constexpr int FS = kFusedFS;
+  const int64_t n_cap = A.n_cap;
+  const int B = A.B;
+  int iters;
+  const int64_t chunk0 = chunk_first(A, c, &iters);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int g = lane >> 4, bl = lane & 15;
+  double* F = lds + wv * WD;         // feature rows (row r = feature r, r + 1 past DF) x 64 points
+  double* E = F + kLpFRows * FS;     // exp slab: 16 points x ES
+  const double o[3] = {A.o0, A.o1, A.o2};
+  TaskAhead ta_local;
+  TaskAhead& ta = ahead ? *ahead : ta_local;
+  if (!ahead || !ahead->valid) task_operands<PRE>(A, h, c, ta);
+  double xr[6];  // the hypothesis's twist: wave-uniform, held in SGPRs
+#pragma unroll
+  for (int k = 0; k < 6; ++k) {
+    const double v = ta.xr[k];
+    xr[k] = __hiloint2double(__builtin_amdgcn_readfirstlane(__double2hiint(v)),
+                             __builtin_amdgcn_readfirstlane(__double2loint(v)));
+  }
+  const double* __restrict__ pts_raw = A.pts_raw;
+  const double* __restrict__ t_raw = A.t_raw;
+  const double* __restrict__ w_raw = A.w_raw;
+  const double t0 = A.t0, t1 = A.t1;
+  const double scale = A.bscal[2];
+  const int64_t n_sel = (int64_t)A.bscal[5];
+  const int64_t stride = (int64_t)A.bscal[6];
+  const double denom = fmax(t1 - t0, 1e-12);
+  const double inv_denom = 1.0 / denom;
+  const double inv_sig = 1.0 / fmax(0.1 * denom, 1e-6);
+  double* Tx = lds + fused_tab_offset(BPL);
+  const double ysc = A.inv_tau * kTab2OverLn2;
+  constexpr int NACC = 1;  // BPL independent MFMA chains per step suffice here (the slab round trip paces them)
+  v4d acc4[NACC][BPL];
+  double accx[BPL][NX];
+#pragma unroll
+  for (int j = 0; j < BPL; ++j) {
+    acc4[0][j] = v4d{0.0, 0.0, 0.0, 0.0};
+    acc4[NACC - 1][j] = v4d{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < NX; ++t) accx[j][t] = 0.0;
+  }
+  double sumw = 0.0, entq = 0.0, mxr = 0.0;
+  double zst = 1.0;  // Π Z of the lane's points as mantissa x 2^zex (renormalised every iteration)
+  int zex = 0;
+  // x = (ysc d)·b <= ysc (1 + 1e-16) < ymax: the exp argument x - ymax <= 0, the shift riding in the
+  // rounding constant (exp2s_shift_tab_n) and added back to the entropy below
+  const double ymax = ceil(ysc);
+  const double Mp = kRoundMagic - ymax;
+  const double Beps = (double)B * 1e-12;
+  double np[3] = {0.0, 0.0, 0.0}, ntt = 0.0, nww = 0.0;
+  auto fetch = [&](int it2) {
+    const int64_t j = chunk0 + (int64_t)it2 * 256 + wv * 64 + lane;
+    np[0] = 0.0; np[1] = 0.0; np[2] = 0.0; ntt = 0.0; nww = 0.0;
+    if (j < n_cap && j < n_sel) {
+      const int64_t i = j * stride;
+      np[0] = pts_raw[3 * i]; np[1] = pts_raw[3 * i + 1]; np[2] = pts_raw[3 * i + 2];
+      ntt = t_raw[i];
+      nww = PRE ? A.w_win[j] : w_raw[i];
+    }
+  };
+  np[0] = ta.np[0]; np[1] = ta.np[1]; np[2] = ta.np[2]; ntt = ta.ntt; nww = ta.nww;
+  unsigned next = 0;
+  // this lane's bin set for the quad form: bins NQ c .. NQ c + NQ - 1 (c = lane & 3), pre-scaled by
+  // ysc, in registers for the whole task (ragged B: the bins past B read as bin B - 1, masked below)
+  constexpr int NQ = NB / 4;
+  const int cq = lane & 3;
+  double bq[NQ][3];
+#pragma unroll
+  for (int k = 0; k < NQ; ++k) {
+    const int b = min(NQ * cq + k, B - 1);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) bq[k][r] = A.bins[3 * b + r] * ysc;
+  }
+  auto run_iters = [&](auto pad_tag) {
+    constexpr bool PAD = decltype(pad_tag)::value;
+    for (int it = 0; it < iters; ++it) {
+      const int64_t wbase = chunk0 + (int64_t)it * 256 + wv * 64;
+      if (ctr && !late_next && it == iters - 1 && threadIdx.x == 0) next = atomicAdd(ctr, 1u);
+      // ---- phase A (lane = point): the point's features (w folded in) into the wave's feature rows
+      double d[3];
+      {
+        const bool inr = !PAD || wbase + lane < n_cap;
+        double p[3] = {np[0], np[1], np[2]};
+        const double tt = ntt, ww = nww * scale;
+        if (it + 1 < iters) fetch(it + 1);
+        const double al = (tt - t0) * inv_denom;
+        const double ph[3] = {al * xr[3], al * xr[4], al * xr[5]};
+        double q[3];
+        if (__all(dot3(ph, ph) <= kDeskewShortTs)) deskew_point_cross<true>(p, al, xr, q);
+        else deskew_point_cross<false>(p, al, xr, q);
+        const double wd = inr ? (PRE ? ww : ww * window_weight2(tt, t0, t1, inv_sig, Tx)) : 0.0;
+        direction_fast(q, o, 1e-12, d);
+        sumw += wd;
+        double f[NF];
+        point_features_w(q, d, wd, f);
+#pragma unroll
+        for (int k = 0; k < NF; ++k)
+          if (k != DF) F[(k < DF ? k : k - 1) * FS + lane] = f[k];
+      }
+      // ---- four sub-iterations of 16 points: B1 with lane = (point p = l >> 2, bin quarter c = l & 3),
+      // then B2 over the sub-iteration's 4 MFMA steps
+#pragma unroll
+      for (int sk = 0; sk < 4; ++sk) {
+        const int pt = 16 * sk + (lane >> 2);  // the wave's point (its phase-A lane)
+        const double dx = __shfl(d[0], pt), dy = __shfl(d[1], pt), dz = __shfl(d[2], pt);
+        const double vf = (!PAD || wbase + pt < n_cap) ? 1.0 : 0.0;  // padding: no entropy / max / Π Z
+        // B1: this lane's NQ logits, exps and partial Z, Σ e x, max e (groups of 4: all NQ table reads in
+        // flight at once measured slower, profiles/r06/ab_bins_point_major.txt)
+        double e[NQ];
+        double Zl = 0.0, sl = 0.0, em = 0.0;
+#pragma unroll
+        for (int k0 = 0; k0 < NQ; k0 += 4) {
+          double x[4], ex[4];
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int k = k0 + kk;
+            x[kk] = fma(dz, bq[k][2], fma(dy, bq[k][1], dx * bq[k][0]));
+          }
+          exp2s_shift_tab_n<4, TAB>(x, Mp, ex);
+#pragma unroll
+          for (int kk = 0; kk < 4; ++kk) {
+            const int k = k0 + kk;
+            e[k] = (FULL || NQ * cq + k < B) ? ex[kk] : 0.0;
+            Zl += e[k];
+            sl = fma(e[k], x[kk], sl);
+            em = fmax(em, e[k]);
+          }
+        }
+        // Z over the point's quad (two DPP rounds: the four lanes end bit-identical)
+        double Z = Zl + dpp_f64<kDppXor1>(Zl);
+        Z = Z + dpp_f64<kDppXor2>(Z);
+        const double rZ = recip1(Z);
+        entq = fma(sl * rZ, vf, entq);  // this lane's share of Σ R x
+        mxr = fmax(mxr, em * rZ * vf);
+        if (cq == 0) zst *= PAD ? fma(Z - 1.0, vf, 1.0) : Z;  // Π Z once per point
+        // the responsibilities into the exp slab: row = the point within the sub-iteration
+        {
+          double* er = E + (lane >> 2) * ES + NQ * cq;
+#pragma unroll
+          for (int k = 0; k < NQ; k += 2) *reinterpret_cast<dvec2*>(er + k) = dvec2{e[k] * rZ, e[k + 1] * rZ};
+        }
+        lds_wave_sync();
+        // B2 (lanes = 4 points x 16 bins): the sub-iteration's 4 MFMA steps
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int ss = 4 * sk + s;
+          const int pl = 4 * ss + g;
+          const double fb = F[bl * FS + pl];
+          double fk[NX];
+#pragma unroll
+          for (int t = 0; t < NX; ++t) fk[t] = F[(16 + t) * FS + pl];
+#pragma unroll
+          for (int j = 0; j < BPL; ++j) {
+            const double a = E[(4 * s + g) * ES + 16 * j + bl];
+            acc4[ss % NACC][j] = __builtin_amdgcn_mfma_f64_16x16x4f64(a, fb, acc4[ss % NACC][j], 0, 0, 0);
+#pragma unroll
+            for (int t = 0; t < NX; ++t) accx[j][t] = fma(a, fk[t], accx[j][t]);
+          }
+        }
+        lds_wave_sync();
+      }
+      int e8;
+      zst = frexp(zst, &e8);
+      zex += e8;
+    }
+  };
+  if (chunk0 + (int64_t)iters * 256 <= n_cap) run_iters(std::false_type{});
+  else run_iters(std::true_type{});
+  int64_t npts = n_cap - chunk0;
+  npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
+  // entropy over the chunk's valid points: Σ log Z' - Σ R x (x in units of ln2 / 2048) + ymax per valid
+  // point - B ε per point; every lane holds its own points' Π Z (lane 0 of each wave adds the constants)
+  const double logacc = log(zst) + (double)zex * 0.69314718055994530942;
+  const double ent = logacc - entq * kExp2C1 + ((lane == 0) ? (ymax * kExp2C1 - Beps) * (double)npts * 0.25 : 0.0);
+#pragma unroll
+  for (int j = 0; j < BPL; ++j)
+    if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
+  if (ahead) ahead->valid = false;
+  if (ctr && late_next && threadIdx.x == 0) *late_next = atomicAdd(ctr, 1u);
+  const auto pre = [&]() {
+    if (ctr && !late_next && threadIdx.x == 0) *task_slot = next;
+  };
+  const auto mid = [&]() {
+    if (!ctr || late_next) return;
+    const unsigned tn = *task_slot;
+    ahead->t = tn;
+    if (tn < T) task_operands<PRE>(A, (int)(tn % (unsigned)Hl), (int64_t)(tn / (unsigned)Hl), *ahead);
+  };
+  write_partial_record_mfma<BPL, NX, DF>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec, pre, mid);
+  __syncthreads();
+}
+
 // One task: hypothesis h, chunk c (its points: the tiers of FusedArgs) of the budgeted scan,
 // its partial record written to rec. Ends with the workgroup synchronised (LDS free for the next task).
 // Persistent form (ctr, task_slot, ahead non-null): the next task's ticket is taken by thread 0 at the
@@ -1061,6 +1331,10 @@ template <int BPL, bool FULL, bool PRE>
 GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec, unsigned* ctr = nullptr,
                       unsigned* task_slot = nullptr, TaskAhead* ahead = nullptr, unsigned T = 0, int Hl = 1,
                       unsigned* late_next = nullptr) {
+  if constexpr (bins_lp(BPL)) {
+    bins_task_lp<BPL, FULL, PRE>(A, h, c, lds, rec, ctr, task_slot, ahead, T, Hl, late_next);
+    return;
+  }
   constexpr int NF = NF_BASE;
   // features 0..8 and 10..16 on the matrix core, 17..18 on the VALU; feature 9 (w d_z²) is the trace
   // complement N − w d_x² − w d_y² (write_partial_record_mfma<.., 9>): one VALU feature fewer per step
@@ -1188,7 +1462,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
         double zl = e[0];
   #pragma unroll
         for (int j = 1; j < BPL; ++j) zl += e[j];
-        const double Z = group16_sum(zl);
+        const double Z = group16_sum_bins(zl);
         const double rZ = recip1(Z);
         double r[BPL];
   #pragma unroll
@@ -1289,7 +1563,7 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
 #endif
     return;
   }
-  bins_prologue(A, lds);
+  bins_prologue<BPL>(A, lds);
 #ifdef GC_BINS_TIMING
   bt1 = GC_BT_NOW();
 #endif
@@ -1346,7 +1620,7 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
 template <int BPL, bool FULL>
 __global__ void __launch_bounds__(256, kFusedOcc) k_bins_fused(FusedArgs A) {
   extern __shared__ double lds[];
-  bins_prologue(A, lds);
+  bins_prologue<BPL>(A, lds);
   const int RL = A.B * NF_BASE + REC_EXTRA;
   bins_task<BPL, FULL, false>(A, blockIdx.y, blockIdx.x, lds,
                        A.partials + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * RL);
