@@ -814,7 +814,7 @@ def cpu_leg(n_az, H_total, budget_s):
     # leg (i)
     with threadpool_limits(limits=cores):
         for k in range(3):
-            _cpu_hyp(k)
+            _cpu_hyp(k % H_total)
         ts, outs = [], []
         for k in range(20):
             t0 = time.perf_counter()
@@ -832,7 +832,7 @@ def cpu_leg(n_az, H_total, budget_s):
     pctx = mproc.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
     scans = []
     with pctx.Pool(cores, initializer=_cpu_init, initargs=(n_az, H_total)) as pool:
-        pool.map(_cpu_hyp, range(cores))  # workers built and warm
+        pool.map(_cpu_hyp, [k % H_total for k in range(cores)])  # workers built and warm
         t_start = time.perf_counter()
         n = 0
         while n < 6 and (n < 2 or time.perf_counter() - t_start < budget_s):
@@ -848,9 +848,10 @@ def cpu_leg(n_az, H_total, budget_s):
             "sample": "%d whole %d-hypothesis scans after 1 warm-up (median)" % (len(scans), H_total)}
     best = max(leg1["scans_per_s"], leg2["scans_per_s"])
     return {"value": best, "unit": "scans/s", "cores": cores, "kind": "port",
-            "sample": "oracle (NumPy restatement) on the C3 scan, %d points x %d hypotheses, a1-a16 incl. the "
+            "sample": "oracle (NumPy restatement) on the %s scan, %d points x %d hypotheses, a1-a16 incl. the "
                       "IMU/odom branch, combine, IW apply and map update; value = the faster of leg (i) %s and "
-                      "leg (ii) Pool(%d) %s" % (_CPU["case"]["n"], H_total, leg1["sample"], cores, leg2["sample"]),
+                      "leg (ii) Pool(%d) %s" % (workload_label(H_total, _CPU["case"]["n"], 1).split(" ")[0].rstrip(","),
+                                                _CPU["case"]["n"], H_total, leg1["sample"], cores, leg2["sample"]),
             "legs": {"single_process": leg1, "pool": leg2}, **info}
 
 
