@@ -358,6 +358,11 @@ int stage_slot(gc_ctx* ctx, uint64_t bytes, char** out) {
     for (hipEvent_t& e : ctx->stage_ev) {
       const hipError_t er = hipEventCreateWithFlags(&e, hipEventDisableTiming);
       if (er != hipSuccess) {
+        for (hipEvent_t& d : ctx->stage_ev)  // the ones created so far (the ring stays unset: a retry starts over)
+          if (d) {
+            (void)hipEventDestroy(d);
+            d = nullptr;
+          }
         (void)hipHostFree(h);
         gc::set_error(ctx, std::string("HIP error ") + hipGetErrorString(er) + " creating the staging events");
         return GC_ERR_RUNTIME;
