@@ -937,13 +937,21 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
 struct NoHook {
   GC_DEV void operator()() const {}
 };
-// pre() runs before the first barrier, mid() after it (the persistent bins form's next-task broadcast)
-template <int BPL, int NX, int DF = -1, typename Pre = NoHook, typename Mid = NoHook>
+// pre() runs before the barrier, mid() after it (the persistent bins form's next-task broadcast). Each wave
+// stages its tiles, its two VALU features and its three certificate partials in its OWN slab (WS doubles
+// from lds + wv WS: no other wave reads it during a task, so no barrier is needed before the writes),
+// and computes its log-product and wave sums before the barrier: every latency-bound step of the
+// epilogue runs before mid() issues the next task's loads (a later wait on scratch or on the staged
+// values would otherwise wait for those loads' HBM round trip as well). One barrier, the 4-wave sum in
+// a fixed order, and the caller's closing barrier.
+template <int BPL, int NX, int DF = -1, bool FULL = false, int WS = 0, typename Pre = NoHook, typename Mid = NoHook>
 GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL][NX], double ent, double mxr,
-                                      double sumw, double npts, int B, double* lds, double* rec,
+                                      double sumw, double npts, int B_, double* lds, double* rec,
                                       const Pre& pre = Pre(), const Mid& mid = Mid()) {
+  const int B = FULL ? 16 * BPL : B_;  // FULL: a compile-time bin count (immediate LDS offsets, no bounds branches)
   constexpr int ND = DF >= 0 ? 1 : 0;
   constexpr int NF = ND + 16 + NX;
+  static_assert(WS >= 16 * BPL * NF + 3, "a wave's slab holds its record tiles");
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, g = lane >> 4, bl = lane & 15;
   const int fcol = (DF >= 0 && bl >= DF) ? bl + 1 : bl;  // the feature of MFMA column bl
 #pragma unroll
@@ -955,38 +963,38 @@ GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL
       v += __shfl_xor(v, 32, 64);
       accx[j][t] = v;
     }
-  pre();
-  __syncthreads();
-  mid();
+  const double e = wave_sum(ent), m = wave_max(mxr), s = wave_sum(sumw);
+  double* W = lds + wv * WS;
 #pragma unroll
   for (int j = 0; j < BPL; ++j) {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       const int b = 16 * j + g + 4 * r;
-      if (b < B) lds[(wv * B + b) * NF + fcol] = acc4[j][r];
+      if (b < B) W[b * NF + fcol] = acc4[j][r];
     }
     const int b = 16 * j + bl;
     if (g == 0 && b < B)
 #pragma unroll
-      for (int t = 0; t < NX; ++t) lds[(wv * B + b) * NF + ND + 16 + t] = accx[j][t];
+      for (int t = 0; t < NX; ++t) W[b * NF + ND + 16 + t] = accx[j][t];
   }
-  double e = wave_sum(ent), m = wave_max(mxr), s = wave_sum(sumw);
   if (lane == 0) {
-    lds[4 * B * NF + wv * 3 + 0] = e;
-    lds[4 * B * NF + wv * 3 + 1] = m;
-    lds[4 * B * NF + wv * 3 + 2] = s;
+    W[B * NF + 0] = e;
+    W[B * NF + 1] = m;
+    W[B * NF + 2] = s;
   }
+  pre();
   __syncthreads();
+  mid();
   for (int i = threadIdx.x; i < B * NF; i += kWG) {
-    const auto sum4 = [&](int e) { return (lds[e] + lds[B * NF + e]) + (lds[2 * B * NF + e] + lds[3 * B * NF + e]); };
+    const auto sum4 = [&](int e) { return (lds[e] + lds[WS + e]) + (lds[2 * WS + e] + lds[3 * WS + e]); };
     if (DF >= 0 && i % NF == DF) rec[i] = (sum4(i - DF) - sum4(i - DF + 4)) - sum4(i - DF + 7);  // N − xx − yy
     else rec[i] = sum4(i);
   }
   if (threadIdx.x == 0) {
-    const double* ex = lds + 4 * B * NF;
-    rec[B * NF + 0] = (ex[0] + ex[3]) + (ex[6] + ex[9]);
-    rec[B * NF + 1] = fmax(fmax(ex[1], ex[4]), fmax(ex[7], ex[10]));
-    rec[B * NF + 2] = (ex[2] + ex[5]) + (ex[8] + ex[11]);
+    const double* ex = lds + B * NF;
+    rec[B * NF + 0] = (ex[0] + ex[WS]) + (ex[2 * WS] + ex[3 * WS]);
+    rec[B * NF + 1] = fmax(fmax(ex[1], ex[WS + 1]), fmax(ex[2 * WS + 1], ex[3 * WS + 1]));
+    rec[B * NF + 2] = (ex[2] + ex[WS + 2]) + (ex[2 * WS + 2] + ex[3 * WS + 2]);
     rec[B * NF + 3] = npts;
   }
 }
@@ -1090,26 +1098,42 @@ struct TaskAhead {
   double np[3], ntt, nww;
   unsigned t;   // the next task's ticket (all lanes), read back from the workgroup's task slot
   bool valid;
+  bool ok;      // the lane's point is selected (np / ntt / nww are then the point's; zeroed at use otherwise)
 };
+// n_sel / stride: the a1 selection's count and stride (budget scalars), read once per launch. The raw point
+// is loaded unconditionally from a clamped index, its validity applied where the next task uses it: no
+// branch merge right behind the loads, so the epilogue issuing them never waits for their HBM round trip.
 template <bool PRE>
-GC_DEV void task_operands(const FusedArgs& A, int h, int64_t c, TaskAhead& ta) {
+GC_DEV void task_operands(const FusedArgs& A, int h, int64_t c, int64_t n_sel, int64_t stride, TaskAhead& ta) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   int it_unused;
   const int64_t chunk0 = chunk_first(A, c, &it_unused);
 #pragma unroll
   for (int k = 0; k < 6; ++k) ta.xr[k] = A.xi[6 * h + k];
-  const int64_t n_sel = (int64_t)A.bscal[5], stride = (int64_t)A.bscal[6];
   const int64_t j = chunk0 + wv * 64 + lane;
-  ta.np[0] = 0.0; ta.np[1] = 0.0; ta.np[2] = 0.0; ta.ntt = 0.0; ta.nww = 0.0;
-  if (j < A.n_cap && j < n_sel) {
-    const int64_t i = j * stride;
-    ta.np[0] = A.pts_raw[3 * i]; ta.np[1] = A.pts_raw[3 * i + 1]; ta.np[2] = A.pts_raw[3 * i + 2];
-    ta.ntt = A.t_raw[i];
-    ta.nww = PRE ? A.w_win[j] : A.w_raw[i];
-  }
+  const bool ok = j < A.n_cap && j < n_sel;
+  const int64_t jc = ok ? j : 0, i = jc * stride;
+  ta.np[0] = A.pts_raw[3 * i]; ta.np[1] = A.pts_raw[3 * i + 1]; ta.np[2] = A.pts_raw[3 * i + 2];
+  ta.ntt = A.t_raw[i];
+  ta.nww = PRE ? A.w_win[jc] : A.w_raw[i];
+  ta.ok = ok;
   ta.valid = true;
 }
+// the budget scalars a launch's tasks share (read once per workgroup)
+GC_DEV void selection_of(const FusedArgs& A, int64_t* n_sel, int64_t* stride) {
+  *n_sel = (int64_t)A.bscal[5];
+  *stride = (int64_t)A.bscal[6];
+}
 
+#ifdef GC_BINS_TIMING
+// dev instrumentation: per workgroup of the last k_bins_io launch [start, prologue end, end, tasks] in
+// device real-time ticks (100 MHz, one clock for every XCD); tasks = -1 for a branch workgroup
+__device__ double g_bins_trace[4 * 8192];
+__device__ double g_task_trace[4 * 16384];  // per task [start, end, puller, XCD id]
+__device__ double g_task_ep[2 * 16384];  // per task [end of its first iteration, start of its epilogue] (wave 0)
+__device__ double g_task_wv[4 * 16384];  // per task and wave: the end of its iterations
+#define GC_BT_NOW() ((double)__builtin_amdgcn_s_memrealtime())
+#endif
 // bins_task in the point-major softmax form (bins_lp): the same task, records and ticket protocol.
 // Per iteration of 64 points per wave:
 //  phase A (lane = point): budget selection, deskew, direction, window weight and the 18 features,
@@ -1121,7 +1145,8 @@ GC_DEV void task_operands(const FusedArgs& A, int h, int64_t c, TaskAhead& ta) {
 //       bin 16 j + l, from the slab; B = feature l of that point) and the two VALU features.
 template <int BPL, bool FULL, bool PRE>
 GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, double* rec, unsigned* ctr,
-                         unsigned* task_slot, TaskAhead* ahead, unsigned T, int Hl, unsigned* late_next) {
+                         unsigned* task_slot, TaskAhead* ahead, unsigned T, int Hl, unsigned* late_next,
+                         int64_t n_sel, int64_t stride) {
   typedef double dvec2 __attribute__((ext_vector_type(2)));
   constexpr int NF = NF_BASE;
   constexpr int DF = 9;
@@ -1140,7 +1165,7 @@ GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, doub
   const double o[3] = {A.o0, A.o1, A.o2};
   TaskAhead ta_local;
   TaskAhead& ta = ahead ? *ahead : ta_local;
-  if (!ahead || !ahead->valid) task_operands<PRE>(A, h, c, ta);
+  if (!ahead || !ahead->valid) task_operands<PRE>(A, h, c, n_sel, stride, ta);
   double xr[6];  // the hypothesis's twist: wave-uniform, held in SGPRs
 #pragma unroll
   for (int k = 0; k < 6; ++k) {
@@ -1153,8 +1178,6 @@ GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, doub
   const double* __restrict__ w_raw = A.w_raw;
   const double t0 = A.t0, t1 = A.t1;
   const double scale = A.bscal[2];
-  const int64_t n_sel = (int64_t)A.bscal[5];
-  const int64_t stride = (int64_t)A.bscal[6];
   const double denom = fmax(t1 - t0, 1e-12);
   const double inv_denom = 1.0 / denom;
   const double inv_sig = 1.0 / fmax(0.1 * denom, 1e-6);
@@ -1189,7 +1212,11 @@ GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, doub
       nww = PRE ? A.w_win[j] : w_raw[i];
     }
   };
-  np[0] = ta.np[0]; np[1] = ta.np[1]; np[2] = ta.np[2]; ntt = ta.ntt; nww = ta.nww;
+  {
+    const bool ok = ta.ok;  // applied here, a task after the loads were issued
+    np[0] = ok ? ta.np[0] : 0.0; np[1] = ok ? ta.np[1] : 0.0; np[2] = ok ? ta.np[2] : 0.0;
+    ntt = ok ? ta.ntt : 0.0; nww = ok ? ta.nww : 0.0;
+  }
   unsigned next = 0;
   // this lane's bin set for the quad form: bins NQ c .. NQ c + NQ - 1 (c = lane & 3), pre-scaled by
   // ysc, in registers for the whole task (ragged B: the bins past B read as bin B - 1, masked below)
@@ -1315,9 +1342,9 @@ GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, doub
     if (!ctr || late_next) return;
     const unsigned tn = *task_slot;
     ahead->t = tn;
-    if (tn < T) task_operands<PRE>(A, (int)(tn % (unsigned)Hl), (int64_t)(tn / (unsigned)Hl), *ahead);
+    if (tn < T) task_operands<PRE>(A, (int)(tn % (unsigned)Hl), (int64_t)(tn / (unsigned)Hl), n_sel, stride, *ahead);
   };
-  write_partial_record_mfma<BPL, NX, DF>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec, pre, mid);
+  write_partial_record_mfma<BPL, NX, DF, FULL, WD>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec, pre, mid);
   __syncthreads();
 }
 
@@ -1330,9 +1357,11 @@ GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, doub
 template <int BPL, bool FULL, bool PRE>
 GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec, unsigned* ctr = nullptr,
                       unsigned* task_slot = nullptr, TaskAhead* ahead = nullptr, unsigned T = 0, int Hl = 1,
-                      unsigned* late_next = nullptr) {
+                      unsigned* late_next = nullptr, int bt_task = -1, int64_t n_sel = -1, int64_t stride = 1) {
+  (void)bt_task;
+  if (n_sel < 0) selection_of(A, &n_sel, &stride);
   if constexpr (bins_lp(BPL)) {
-    bins_task_lp<BPL, FULL, PRE>(A, h, c, lds, rec, ctr, task_slot, ahead, T, Hl, late_next);
+    bins_task_lp<BPL, FULL, PRE>(A, h, c, lds, rec, ctr, task_slot, ahead, T, Hl, late_next, n_sel, stride);
     return;
   }
   constexpr int NF = NF_BASE;
@@ -1354,7 +1383,7 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   // here
   TaskAhead ta_local;
   TaskAhead& ta = ahead ? *ahead : ta_local;
-  if (!ahead || !ahead->valid) task_operands<PRE>(A, h, c, ta);
+  if (!ahead || !ahead->valid) task_operands<PRE>(A, h, c, n_sel, stride, ta);
   double xr[6];
 #pragma unroll
   for (int k = 0; k < 6; ++k) xr[k] = ta.xr[k];
@@ -1363,8 +1392,6 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   const double* __restrict__ w_raw = A.w_raw;
   const double t0 = A.t0, t1 = A.t1;
   const double scale = A.bscal[2];
-  const int64_t n_sel = (int64_t)A.bscal[5];
-  const int64_t stride = (int64_t)A.bscal[6];
   const double denom = fmax(t1 - t0, 1e-12);
   const double inv_denom = 1.0 / denom;
   const double inv_sig = 1.0 / fmax(0.1 * denom, 1e-6);
@@ -1405,7 +1432,11 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
       nww = PRE ? A.w_win[j] : w_raw[i];  // PRE: the window is already applied (once per scan)
     }
   };
-  np[0] = ta.np[0]; np[1] = ta.np[1]; np[2] = ta.np[2]; ntt = ta.ntt; nww = ta.nww;
+  {
+    const bool ok = ta.ok;  // applied here, a task after the loads were issued
+    np[0] = ok ? ta.np[0] : 0.0; np[1] = ok ? ta.np[1] : 0.0; np[2] = ok ? ta.np[2] : 0.0;
+    ntt = ok ? ta.ntt : 0.0; nww = ok ? ta.nww : 0.0;
+  }
   unsigned next = 0;
   // A chunk without padding points (all of it below n_cap: every chunk but the last) runs with
   // the valid flag folded to 1.0 — the masking multiplies vanish (x·1 = x, fma(Z−1, 1, 1) = Z
@@ -1492,10 +1523,17 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
         zex += e8;
       }
       lds_wave_sync();
+#ifdef GC_BINS_TIMING
+      if (it == 0 && threadIdx.x == 0 && bt_task >= 0 && bt_task < 16384) g_task_ep[2 * bt_task] = GC_BT_NOW();
+#endif
     }
   };
   if (chunk0 + (int64_t)iters * 256 <= n_cap) run_iters(std::false_type{});
   else run_iters(std::true_type{});
+#ifdef GC_BINS_TIMING
+  if (threadIdx.x == 0 && bt_task >= 0 && bt_task < 16384) g_task_ep[2 * bt_task + 1] = GC_BT_NOW();
+  if ((threadIdx.x & 63) == 0 && bt_task >= 0 && bt_task < 16384) g_task_wv[4 * bt_task + (threadIdx.x >> 6)] = GC_BT_NOW();
+#endif
   // entropy sum over the chunk's valid points: Σ log Z - Σ S/Z - B ε
   int64_t npts = n_cap - chunk0;
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
@@ -1519,9 +1557,9 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
     if (!ctr || late_next) return;
     const unsigned tn = *task_slot;
     ahead->t = tn;
-    if (tn < T) task_operands<PRE>(A, (int)(tn % (unsigned)Hl), (int64_t)(tn / (unsigned)Hl), *ahead);
+    if (tn < T) task_operands<PRE>(A, (int)(tn % (unsigned)Hl), (int64_t)(tn / (unsigned)Hl), n_sel, stride, *ahead);
   };
-  write_partial_record_mfma<BPL, NX, DF>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec, pre, mid);
+  write_partial_record_mfma<BPL, NX, DF, FULL, NS * kFusedFS>(acc4[0], accx, ent, mxr, sumw, (double)npts, B, lds, rec, pre, mid);
   __syncthreads();  // the epilogue's LDS reads are done before the next task writes the slabs
 }
 
@@ -1534,13 +1572,6 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
 // device and shard size: the chunk geometry follows the CU count and H_l). ctr[0] is the task
 // counter; the predict launch that precedes every k_bins_io on the stream zeroes it, so a launch
 // never depends on how the previous one ended. No workgroup waits on another.
-#ifdef GC_BINS_TIMING
-// dev instrumentation: per workgroup of the last k_bins_io launch [start, prologue end, end, tasks] in
-// device real-time ticks (100 MHz, one clock for every XCD); tasks = -1 for a branch workgroup
-__device__ double g_bins_trace[4 * 8192];
-__device__ double g_task_trace[4 * 16384];  // per task [start, end, puller, XCD id]
-#define GC_BT_NOW() ((double)__builtin_amdgcn_s_memrealtime())
-#endif
 template <int BPL, bool FULL, bool AHEAD>
 __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev P, ScanArgs S,
                                                              const double* __restrict__ odom, int n_io, int io_on,
@@ -1578,7 +1609,10 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
   __syncthreads();
   TaskAhead ahead;
   ahead.valid = false;
+  ahead.ok = false;
   ahead.t = task_s;
+  int64_t n_sel, stride;  // the a1 selection, shared by every task of the launch
+  selection_of(A, &n_sel, &stride);
   for (;;) {
     const unsigned t = ahead.t;
     if (t >= T) break;
@@ -1589,11 +1623,12 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
     const double tt0 = GC_BT_NOW();
 #endif
     if constexpr (AHEAD) {
-      bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &task_s, &ahead, T, H);
+      bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &task_s, &ahead, T, H,
+                                 nullptr, (int)t, n_sel, stride);
     } else {
       unsigned next = 0;
       bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &task_s, &ahead, T, H,
-                                 &next);
+                                 &next, (int)t, n_sel, stride);
       if (threadIdx.x == 0) task_s = next;
       __syncthreads();
       ahead.t = task_s;
@@ -2199,6 +2234,16 @@ extern "C" {
 int32_t gc_dev_bins_trace(double* h_out, int64_t n_wg) {
   if (n_wg < 0 || n_wg > 8192) return GC_ERR_RUNTIME;
   return hipMemcpyFromSymbol(h_out, HIP_SYMBOL(gc::g_bins_trace), sizeof(double) * 4 * n_wg) == hipSuccess
+             ? GC_OK : GC_ERR_RUNTIME;
+}
+int32_t gc_dev_task_wv_trace(double* h_out, int64_t n_tasks) {
+  if (n_tasks < 0 || n_tasks > 16384) return GC_ERR_RUNTIME;
+  return hipMemcpyFromSymbol(h_out, HIP_SYMBOL(gc::g_task_wv), sizeof(double) * 4 * n_tasks) == hipSuccess
+             ? GC_OK : GC_ERR_RUNTIME;
+}
+int32_t gc_dev_task_ep_trace(double* h_out, int64_t n_tasks) {
+  if (n_tasks < 0 || n_tasks > 16384) return GC_ERR_RUNTIME;
+  return hipMemcpyFromSymbol(h_out, HIP_SYMBOL(gc::g_task_ep), sizeof(double) * 2 * n_tasks) == hipSuccess
              ? GC_OK : GC_ERR_RUNTIME;
 }
 int32_t gc_dev_task_trace(double* h_out, int64_t n_tasks) {

@@ -67,3 +67,34 @@ print("  per XCD tasks:", [int((xcc == x).sum()) for x in range(8)])
 last = np.argsort(en)[-12:]
 for i in last:
     print(f"   late task {i}: chunk {ch[i]} start {st[i]:.1f} end {en[i]:.1f} dur {du[i]:.1f} puller {int(tk[i, 2])} xcc {xcc[i]}")
+
+# per task [end of its first iteration, start of its epilogue] (wave 0 of the workgroup), when the build
+# exports them: the task's set-up + first iteration, its other iterations, and its epilogue (record
+# reduction + the next task's ticket / operands) up to the next task's start
+if hasattr(L, "gc_dev_task_ep_trace"):
+    eb = (C.c_double * (2 * m))()
+    L.gc_dev_task_ep_trace.argtypes = [C.POINTER(C.c_double), C.c_int64]
+    assert L.gc_dev_task_ep_trace(eb, m) == 0
+    ep = (np.array(eb).reshape(m, 2)[:nT] - t0) / 100.0
+    first, rest, epi = ep[:, 0] - st, ep[:, 1] - ep[:, 0], en - ep[:, 1]
+    for c in range(ch.max() + 1):
+        sel = ch == c
+        print(f"   chunk {c:3d}: first iteration (+ set-up) {np.median(first[sel]):6.2f}  later iterations {np.median(rest[sel]):7.2f}"
+              f"  epilogue {np.median(epi[sel]):5.2f} us (medians)")
+    print(f"  all tasks: epilogue median {np.median(epi):.2f} p90 {np.percentile(epi, 90):.2f} us; first iteration median "
+          f"{np.median(first):.2f} us")
+# per task and wave: the end of the wave's iterations — the waves' skew at the epilogue's first barrier, and
+# the epilogue proper (the last wave's arrival to the task's end)
+if hasattr(L, "gc_dev_task_wv_trace"):
+    wb = (C.c_double * (4 * m))()
+    L.gc_dev_task_wv_trace.argtypes = [C.POINTER(C.c_double), C.c_int64]
+    assert L.gc_dev_task_wv_trace(wb, m) == 0
+    wvt = (np.array(wb).reshape(m, 4)[:nT] - t0) / 100.0
+    skew = wvt.max(axis=1) - wvt.min(axis=1)
+    proper = en - wvt.max(axis=1)
+    for c in range(ch.max() + 1):
+        sel = ch == c
+        print(f"   chunk {c:3d}: wave skew median {np.median(skew[sel]):5.2f} p90 {np.percentile(skew[sel], 90):5.2f}"
+              f"  epilogue after the last wave {np.median(proper[sel]):5.2f} us")
+    print(f"  all tasks: wave skew median {np.median(skew):.2f} p90 {np.percentile(skew, 90):.2f}; epilogue proper median "
+          f"{np.median(proper):.2f} p90 {np.percentile(proper, 90):.2f} us")
