@@ -175,6 +175,47 @@ GC_DEV double recip(double z) {
   e = fma(-z, r, 1.0);
   return fma(r, e, r);
 }
+// A double whose bits the compiler cannot see: two v_mov_b32 at the point of use. In a persistent
+// kernel at 256 VGPRs a plain 64-bit constant is hoisted out of the task loop and spilled, and a
+// polynomial then reloads each coefficient from scratch in a serial chain (the epilogue's log:
+// six dependent scratch round trips per task)
+template <int HI, int LO>
+GC_DEV double vconst() {
+  int h, l;
+  asm volatile("v_mov_b32 %0, %1" : "=v"(l) : "i"(LO));
+  asm volatile("v_mov_b32 %0, %1" : "=v"(h) : "i"(HI));
+  return __hiloint2double(h, l);
+}
+// ln x for a positive normal x (the bins epilogue's log of Π Z): x = 2^k m with m in [√½, √2),
+// f = m − 1, s = f/(2 + f), ln m = f − (f²/2 − s(f²/2 + R(s²))) with R the degree-7 minimax
+// polynomial in s² of the classic fdlibm __ieee754_log; < 1 ulp there, within 2 ulp with the
+// Newton reciprocal for 1/(2 + f). Every coefficient is a vconst.
+GC_DEV double log_pos(double x) {
+  int k;
+  double m = frexp(x, &k);
+  if (m < 0.70710678118654752440) {
+    m *= 2.0;
+    --k;
+  }
+  const double f = m - 1.0;
+  const double s = f * recip(2.0 + f);
+  const double z = s * s, w = z * z;
+  const double t1 = w * (vconst<0x3FD99999, (int)0x9997FA04>() +
+                         w * (vconst<0x3FCC71C5, 0x1D8E78AF>() + w * vconst<0x3FC39A09, (int)0xD078C69F>()));
+  const double t2 = z * (vconst<0x3FE55555, 0x55555593>() +
+                         w * (vconst<0x3FD24924, (int)0x94229359>() +
+                              w * (vconst<0x3FC74664, (int)0x96CB03DE>() + w * vconst<0x3FC2F112, (int)0xDF3E5244>())));
+  const double R = t2 + t1, hfsq = 0.5 * f * f, dk = (double)k;
+  return dk * vconst<0x3FE62E42, (int)0xFEE00000>() -
+         ((hfsq - (s * (hfsq + R) + dk * vconst<0x3DEA39EF, 0x35793C76>())) - f);
+}
+// the per-point entropy shift of the bins epilogue, (ymax ln2/2048 − B ε)/4 with ymax = ceil(2048/(τ ln2)),
+// re-formed from the launch scalars each task (a loop-invariant double here is hoisted and spilled)
+GC_DEV double ent_shift(double inv_tau, int B) {
+  asm volatile("" : "+v"(inv_tau), "+v"(B));
+  const double ymax = ceil(inv_tau * vconst<0x40A71547, 0x652B82FE>());  // 2048 / ln2
+  return (ymax * vconst<0x3F362E42, (int)0xFEFA932F>() - (double)B * 1e-12) * 0.25;  // ln2 / 2048
+}
 // Fused-kernel exp: a 2048-entry table and arguments pre-scaled to y = x·2048/ln2. Entry j holds
 // 2^(j/2048) with (j << 9) subtracted from its high word, so adding (k << 9) to the high word of
 // T[k & 2047] yields 2^(j/2048)·2^(k >> 11) for any k (one integer add instead of a shift and a
@@ -985,16 +1026,49 @@ GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL
   pre();
   __syncthreads();
   mid();
-  for (int i = threadIdx.x; i < B * NF; i += kWG) {
-    const auto sum4 = [&](int e) { return (lds[e] + lds[WS + e]) + (lds[2 * WS + e] + lds[3 * WS + e]); };
-    if (DF >= 0 && i % NF == DF) rec[i] = (sum4(i - DF) - sum4(i - DF + 4)) - sum4(i - DF + 7);  // N − xx − yy
-    else rec[i] = sum4(i);
+  int tid = threadIdx.x;
+  asm volatile("" : "+v"(tid));  // the per-lane addresses formed here, not hoisted out of the task loop and spilled
+  const auto sum4 = [&](int e) { return (lds[e] + lds[WS + e]) + (lds[2 * WS + e] + lds[3 * WS + e]); };
+  if constexpr (FULL) {
+    // a compile-time entry count: every lane's entries summed with their LDS reads issued together (one
+    // LDS round trip instead of one per entry), then stored; the complement entry's three sums are
+    // selected, not branched to
+    constexpr int NE = 16 * BPL * NF, NI = (NE + kWG - 1) / kWG;
+    double v[NI];
+#pragma unroll
+    for (int k = 0; k < NI; ++k) {
+      const int i = min(tid + k * kWG, NE - 1);
+      if constexpr (DF >= 0) {
+        const bool df = i % NF == DF;
+        const int i0 = i - (df ? DF : 0);  // N
+        const double a = sum4(i0), b = sum4(df ? i0 + 4 : i0), c = sum4(df ? i0 + 7 : i0);
+        v[k] = df ? (a - b) - c : a;  // N − xx − yy
+      } else {
+        v[k] = sum4(i);
+      }
+    }
+    // the scheduler otherwise pairs each two reads with a wait for them: every read first
+    __builtin_amdgcn_sched_group_barrier(0x100, (DF >= 0 ? 12 : 4) * NI, 0);
+#pragma unroll
+    for (int k = 0; k < NI; ++k)
+      if (k < NI - 1 || tid + k * kWG < NE) rec[tid + k * kWG] = v[k];
+  } else {
+    for (int i = tid; i < B * NF; i += kWG) {
+      if (DF >= 0 && i % NF == DF) rec[i] = (sum4(i - DF) - sum4(i - DF + 4)) - sum4(i - DF + 7);  // N − xx − yy
+      else rec[i] = sum4(i);
+    }
   }
   if (threadIdx.x == 0) {
     const double* ex = lds + B * NF;
-    rec[B * NF + 0] = (ex[0] + ex[WS]) + (ex[2 * WS] + ex[3 * WS]);
-    rec[B * NF + 1] = fmax(fmax(ex[1], ex[WS + 1]), fmax(ex[2 * WS + 1], ex[3 * WS + 1]));
-    rec[B * NF + 2] = (ex[2] + ex[WS + 2]) + (ex[2 * WS + 2] + ex[3 * WS + 2]);
+    double x[4][3];
+#pragma unroll
+    for (int w = 0; w < 4; ++w)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) x[w][k] = ex[w * WS + k];
+    __builtin_amdgcn_sched_group_barrier(0x100, 12, 0);
+    rec[B * NF + 0] = (x[0][0] + x[1][0]) + (x[2][0] + x[3][0]);
+    rec[B * NF + 1] = fmax(fmax(x[0][1], x[1][1]), fmax(x[2][1], x[3][1]));
+    rec[B * NF + 2] = (x[0][2] + x[1][2]) + (x[2][2] + x[3][2]);
     rec[B * NF + 3] = npts;
   }
 }
@@ -1328,7 +1402,7 @@ GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, doub
   npts = npts < 0 ? 0 : (npts > (int64_t)iters * 256 ? (int64_t)iters * 256 : npts);
   // entropy over the chunk's valid points: Σ log Z' - Σ R x (x in units of ln2 / 2048) + ymax per valid
   // point - B ε per point; every lane holds its own points' Π Z (lane 0 of each wave adds the constants)
-  const double logacc = log(zst) + (double)zex * 0.69314718055994530942;
+  const double logacc = log_pos(zst) + (double)zex * 0.69314718055994530942;
   const double ent = logacc - entq * kExp2C1 + ((lane == 0) ? (ymax * kExp2C1 - Beps) * (double)npts * 0.25 : 0.0);
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
@@ -1418,7 +1492,6 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   // >= ysc (the shift cancels in R and is added back to the entropy below)
   const double ymax = ceil(ysc);
   const double Mp = kRoundMagic - ymax;  // the shift rides in the rounding constant (exp2s_shift_n)
-  const double Beps = (double)B * 1e-12;
   // raw point of the next iteration, loaded one iteration ahead (its HBM latency hides behind
   // this iteration's soft assignment)
   double np[3] = {0.0, 0.0, 0.0}, ntt = 0.0, nww = 0.0;
@@ -1540,9 +1613,9 @@ GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double*
   // the 16 lanes of a point group hold the same product: only bin-lane 0 of each group contributes
   // its log. Σ log Z' (shifted by ymax) - Σ R y + ymax per valid point - B ε per point (lane 0 of
   // each wave)
-  const double logacc = log(zst) + (double)zex * 0.69314718055994530942;
+  const double logacc = log_pos(zst) + (double)zex * 0.69314718055994530942;
   const double ent = (bl == 0 ? logacc : 0.0) - entq * kExp2C1 +
-                     ((lane == 0) ? (ymax * kExp2C1 - Beps) * (double)npts * 0.25 : 0.0);
+                     ((lane == 0) ? ent_shift(A.inv_tau, B) * (double)npts : 0.0);
 #pragma unroll
   for (int j = 0; j < BPL; ++j)
     if (NACC == 2) acc4[0][j] += acc4[NACC - 1][j];
@@ -1614,7 +1687,9 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
   int64_t n_sel, stride;  // the a1 selection, shared by every task of the launch
   selection_of(A, &n_sel, &stride);
   for (;;) {
-    const unsigned t = ahead.t;
+    // uniform: the task's record pointer lives in scalar registers (held in a VGPR it was spilled and
+    // its reload waited on the look-ahead loads issued before it)
+    const unsigned t = __builtin_amdgcn_readfirstlane(ahead.t);
     if (t >= T) break;
     // chunk-major: the workgroups in flight share a chunk's raw points across hypotheses (L2)
     const int64_t c = t / H;
