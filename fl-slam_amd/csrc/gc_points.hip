@@ -978,6 +978,27 @@ __global__ void __launch_bounds__(256, 2) k_moment_partials(int64_t n, int B, in
 struct NoHook {
   GC_DEV void operator()() const {}
 };
+// v + v^16 then + v^32 over the lane index (the value of lane l's column summed over the wave's four
+// 16-lane rows) by gfx950's row and half swaps on the VALU instead of two LDS-routed shuffles; each
+// step adds a lane pair in one order or the other, which is the same double (x + y == y + x)
+GC_DEV double sum_rows4(double v) {
+  const unsigned lo = __double2loint(v), hi = __double2hiint(v);
+  const auto l16 = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+  const auto h16 = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+  const double w = __hiloint2double(h16[0], l16[0]) + __hiloint2double(h16[1], l16[1]);
+  const unsigned wl = __double2loint(w), wh = __double2hiint(w);
+  const auto l32 = __builtin_amdgcn_permlane32_swap(wl, wl, false, false);
+  const auto h32 = __builtin_amdgcn_permlane32_swap(wh, wh, false, false);
+  return __hiloint2double(h32[0], l32[0]) + __hiloint2double(h32[1], l32[1]);
+}
+#ifndef GC_EPI_PERMLANE
+#define GC_EPI_PERMLANE 0
+#endif
+GC_DEV int64_t uniform_i64(int64_t v) {
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)((uint64_t)v >> 32));
+  return (int64_t)(((uint64_t)hi << 32) | lo);
+}
 // pre() runs before the barrier, mid() after it (the persistent bins form's next-task broadcast). Each wave
 // stages its tiles, its two VALU features and its three certificate partials in its OWN slab (WS doubles
 // from lds + wv WS: no other wave reads it during a task, so no barrier is needed before the writes),
@@ -999,10 +1020,14 @@ GC_DEV void write_partial_record_mfma(const v4d (&acc4)[BPL], double (&accx)[BPL
   for (int j = 0; j < BPL; ++j)
 #pragma unroll
     for (int t = 0; t < NX; ++t) {
+#if GC_EPI_PERMLANE
+      accx[j][t] = sum_rows4(accx[j][t]);
+#else
       double v = accx[j][t];
       v += __shfl_xor(v, 16, 64);
       v += __shfl_xor(v, 32, 64);
       accx[j][t] = v;
+#endif
     }
   const double e = wave_sum(ent), m = wave_max(mxr), s = wave_sum(sumw);
   double* W = lds + wv * WS;
@@ -1428,12 +1453,16 @@ GC_DEV void bins_task_lp(const FusedArgs& A, int h, int64_t c, double* lds, doub
 // start of the task's last iteration, broadcast through task_slot at the epilogue's first barrier, and
 // the next task's operands are loaded into ahead during the rest of the epilogue (T tasks, H_l
 // hypotheses: ticket t = chunk t / H_l, hypothesis t % H_l).
-template <int BPL, bool FULL, bool PRE>
-GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec, unsigned* ctr = nullptr,
-                      unsigned* task_slot = nullptr, TaskAhead* ahead = nullptr, unsigned T = 0, int Hl = 1,
-                      unsigned* late_next = nullptr, int bt_task = -1, int64_t n_sel = -1, int64_t stride = 1) {
+// SEL_CHECK: n_sel < 0 asks for the selection here (the non-look-ahead persistent form, which measured
+// better with the launch's selection left in vector registers and this fallback: H = 256 1.1568 against
+// 1.1592 ms with it scalar and given; profiles/r06/ab_bins_epilogue.txt)
+template <int BPL, bool FULL, bool PRE, bool SEL_CHECK = false>
+GC_DEV void bins_task(const FusedArgs& A, int h, int64_t c, double* lds, double* rec, unsigned* ctr,
+                      unsigned* task_slot, TaskAhead* ahead, unsigned T, int Hl, unsigned* late_next, int bt_task,
+                      int64_t n_sel, int64_t stride) {  // n_sel, stride: the launch's selection (selection_of)
   (void)bt_task;
-  if (n_sel < 0) selection_of(A, &n_sel, &stride);
+  if constexpr (SEL_CHECK)
+    if (n_sel < 0) selection_of(A, &n_sel, &stride);
   if constexpr (bins_lp(BPL)) {
     bins_task_lp<BPL, FULL, PRE>(A, h, c, lds, rec, ctr, task_slot, ahead, T, Hl, late_next, n_sel, stride);
     return;
@@ -1686,6 +1715,12 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
   ahead.t = task_s;
   int64_t n_sel, stride;  // the a1 selection, shared by every task of the launch
   selection_of(A, &n_sel, &stride);
+  // uniform values in scalar registers: held in VGPRs they were spilled, and each task's reload waited
+  // (in-order vmcnt) on the previous epilogue's look-ahead loads
+  if constexpr (AHEAD) {
+    n_sel = uniform_i64(n_sel);
+    stride = uniform_i64(stride);
+  }
   for (;;) {
     // uniform: the task's record pointer lives in scalar registers (held in a VGPR it was spilled and
     // its reload waited on the look-ahead loads issued before it)
@@ -1702,8 +1737,8 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_io(FusedArgs A, PipeDev
                                  nullptr, (int)t, n_sel, stride);
     } else {
       unsigned next = 0;
-      bins_task<BPL, FULL, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &task_s, &ahead, T, H,
-                                 &next, (int)t, n_sel, stride);
+      bins_task<BPL, FULL, true, true>(A, h, c, lds, A.partials + ((int64_t)h * chunks + c) * RL, ctr, &task_s, &ahead, T,
+                                 H, &next, (int)t, n_sel, stride);
       if (threadIdx.x == 0) task_s = next;
       __syncthreads();
       ahead.t = task_s;
@@ -1732,8 +1767,11 @@ __global__ void __launch_bounds__(256, kFusedOcc) k_bins_fused(FusedArgs A) {
   extern __shared__ double lds[];
   bins_prologue<BPL>(A, lds);
   const int RL = A.B * NF_BASE + REC_EXTRA;
+  int64_t n_sel, stride;
+  selection_of(A, &n_sel, &stride);
   bins_task<BPL, FULL, false>(A, blockIdx.y, blockIdx.x, lds,
-                       A.partials + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * RL);
+                       A.partials + ((int64_t)blockIdx.y * gridDim.x + blockIdx.x) * RL, nullptr, nullptr, nullptr,
+                       0u, 1, nullptr, -1, n_sel, stride);
 }
 
 // ================================================================ finalize (a6 + certs)
