@@ -172,6 +172,22 @@ def test_moment_match_matches_oracle(ctx, B, n, with_cov):
     (4096, 4096, 48, 4, 0.01), (4096, 4096, 48, 2, 1.0), (4096, 4096, 48, 0, 0.003)])
 def test_fused_bins_match_contract_chain(ctx, n_in, cap, B, iters, tau):
     """Fused a1->a4->a5->a6 == oracle chain budget -> deskew -> dirs -> soft assign -> moments."""
+    _fused_vs_chain(ctx, n_in, cap, B, iters, tau, np.array([[0.02, 0.0, 0.0, 0.0, 0.0, 0.03],
+                                                             [0.0, 0.01, 0.0, 0.01, -0.01, -0.02], [0.0] * 6]))
+
+
+@pytest.mark.parametrize("n_in,iters", [(4096, 0), (8192, 2), (5000, 2)])
+def test_fused_bins_fast_rotation_match_contract_chain(ctx, n_in, iters):
+    """The fused kernel's other two deskew forms: rotations past the short series (θ² > 0.04 over
+    the scan: the nine-term series) and past θ² = 1 (the closed form with sin / cos), in waves that
+    mix them with the short form (θ = α|ω| grows with the point's time)."""
+    xis = np.array([[0.3, -0.1, 0.05, 0.3, -0.2, 0.4],      # |ω| 0.54: short, then the series
+                    [0.1, 0.0, 0.2, 1.2, 0.5, -0.9],        # |ω| 1.58: all three forms
+                    [-0.5, 0.4, 0.0, -2.5, 1.0, 2.0]])      # |ω| 3.35: mostly the closed form
+    _fused_vs_chain(ctx, n_in, n_in, 48, iters, 0.1, xis)
+
+
+def _fused_vs_chain(ctx, n_in, cap, B, iters, tau, xis):
     from gcslam import _abi
     from gcslam.synth import make_scan
     s = make_scan(0, n_az=max(1, n_in // 16))
@@ -179,8 +195,6 @@ def test_fused_bins_match_contract_chain(ctx, n_in, cap, B, iters, tau):
     n_in = P.shape[0]
     o = np.array([-0.065447, -0.100474, 0.108987])
     bins = O.fibonacci_atlas(B)
-    xis = np.array([[0.02, 0.0, 0.0, 0.0, 0.0, 0.03], [0.0, 0.01, 0.0, 0.01, -0.01, -0.02],
-                    [0.0] * 6])
     H = xis.shape[0]
     dP, dT, dW = (_abi.DeviceArray.from_host(ctx, a) for a in (P, T, W))
     scal = _abi.DeviceArray(ctx, 8)
